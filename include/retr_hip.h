@@ -1,0 +1,145 @@
+/* C-ABI of libretr_hip.so — the MI355X (gfx950) kernels behind the RE⫶TR hot path.
+ *
+ * The reference (simeonjunker/retr) is pure Python/PyTorch: it has no native FFI of its own.
+ * Each entry point below replaces the implicit PyTorch/cuDNN/cuBLAS work of one reference
+ * call site (cited per function).  The Python host layer
+ * (retr_amd/_lib.py) binds these with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - every pointer is a device pointer owned by the caller (torch caching allocator); kernels
+ *     never allocate, free or synchronise, so every call is hipGraph-capturable;
+ *   - `dtype` selects the operand type: RETR_F32 (exact-f32 MFMA, parity mode) or RETR_BF16;
+ *   - `stream` is a hipStream_t (torch's current stream);
+ *   - return 0 on success, non-zero on error; retr_last_error() returns the message.
+ *   - activations of the ResNet are NHWC; transformer tokens are batch-major rows [B*L][C].
+ */
+#ifndef RETR_HIP_H
+#define RETR_HIP_H
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RETR_DTYPE_F32 0
+#define RETR_DTYPE_BF16 1
+
+const char* retr_last_error(void);
+int retr_abi_version(void);
+
+/* ---- linear layers: nn.Linear / MHA in/out-proj / MLP head / feed_forward --------------------
+ * replaces F.linear at models/transformer_modules.py:6-11, models/caption.py:161-174,
+ * torch/nn/functional.py:5785-5850 (in-proj) and :6601 (out-proj).
+ * y = relu2( residual + dropout( relu1( x W^T + b ) ) ); relu: 0 none, 1 relu1 */
+int retr_linear_fwd(int dtype, const void* x, long ldx, const void* w, long ldw,
+                    const float* bias, void* y, long ldy, int y_f32, int M, int N, int K, int relu,
+                    const float* residual, long ldr, float drop_p, unsigned long long seed,
+                    void* stream);
+/* dx = gate( dy W [+ addend] ), gate(v) = v * (gate_src > 0) */
+int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long ldw, void* dx,
+                      long lddx, int dx_f32, int M, int N, int K, const void* addend,
+                      int addend_f32, long lda, const void* gate, long ldg, void* stream);
+/* dw[N][K] += dy^T x  (fp32) */
+int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long ldx, float* dw,
+                      long lddw, int M, int N, int K, void* stream);
+/* db[N] += column sums of dy[M][N] */
+int retr_bias_grad(int dtype, const void* dy, long lddy, int M, int N, float* db, void* stream);
+
+/* ---- ResNet convolutions (torchvision conv stack via models/backbone.py:65-69, FrozenBN
+ * models/backbone.py:41-51 folded into the weights) --------------------------------------- */
+int retr_conv_pack(int dtype, const float* w, const float* bn_w, const float* bn_b,
+                   const float* bn_rm, const float* bn_rv, const float* conv_bias, int Co, int Ci,
+                   int KH, int KW, int Cp, void* w_out, void* wt_out, float* bias_out,
+                   float* scale_out, void* stream);
+int retr_conv2d_fwd(int dtype, const void* x, int Nb, int H, int W, int C, const void* w,
+                    const float* bias, const void* residual, void* y, int Co, int KH, int KW,
+                    int stride, int pad, int dil, int relu, void* stream);
+int retr_conv2d_dgrad(int dtype, const void* dy, int Nb, int H, int W, int C, const void* wt,
+                      void* dx, int Co, int KH, int KW, int stride, int pad, int dil,
+                      const void* addend, const void* gate, void* stream);
+int retr_conv2d_wgrad(int dtype, const void* dy, const void* x, int Nb, int H, int W, int C,
+                      float* ws, int Co, int KH, int KW, int stride, int pad, int dil,
+                      void* stream);
+int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,
+                           int Cp, int KH, int KW, int accumulate, void* stream);
+/* NCHW fp32 image -> NHWC (channels zero-padded to Cp) */
+int retr_nchw_to_nhwc(int dtype, const float* x, void* y, int N, int C, int H, int W, int Cp,
+                      void* stream);
+/* MaxPool2d(3, 2, 1) on NHWC (torchvision stem) */
+int retr_maxpool3x3s2(int dtype, const void* x, void* y, int N, int H, int W, int C, int OH,
+                      int OW, void* stream);
+/* F.interpolate(mask[None].float(), size=(h,w)) nearest -> bool (models/backbone.py:75) */
+int retr_mask_nearest(const unsigned char* m, unsigned char* out, int N, int H, int W, int h,
+                      int w, void* stream);
+
+/* ---- LayerNorm (nn.LayerNorm in SelfAttResidual/CrossAttResidual/FFResidual, encoder/decoder
+ * final norms: models/transformer_modules.py:31,58,89; models/ConcatTransformer.py:105,146) ---
+ * y = LN(x) (type dtype), y2 = y + pos[row % period] (optional), saves mean/rstd */
+int retr_layernorm_fwd(int dtype, const float* x, long ldx, const float* gamma,
+                       const float* beta, float eps, int M, int C, void* y, long ldy, void* y2,
+                       const float* pos, int period, float* mean, float* rstd, void* stream);
+/* dx = [addend +] LN'(dy [+ dy2]); dgamma/dbeta accumulate (fp32) */
+int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, const float* x,
+                       long ldx, const float* gamma, const float* mean, const float* rstd, int M,
+                       int C, float* dx, long lddx, const float* addend, float* dgamma,
+                       float* dbeta, void* stream);
+
+/* ---- DecoderEmbeddings: word[caps] + pos[t] -> LayerNorm(eps) -> dropout
+ * (models/transformer_modules.py:113-129) ------------------------------------------------- */
+int retr_embed_ln_fwd(const long long* tokens, int B, int T, int C, const float* word,
+                      const float* posw, const float* gamma, const float* beta, float eps,
+                      float drop_p, unsigned long long seed, float* y, float* mean, float* rstd,
+                      void* stream);
+int retr_embed_ln_bwd(const long long* tokens, int B, int T, int C, const float* word,
+                      const float* posw, const float* gamma, const float* mean, const float* rstd,
+                      const float* dy, float drop_p, unsigned long long seed, float* dword,
+                      float* dposw, float* dgamma, float* dbeta, int padding_idx, void* stream);
+
+/* ---- multi-head attention core: softmax(q k^T * hd^-1/2 + mask) -> dropout -> @ v
+ * (torch/nn/functional.py:6576-6606 need_weights path used by models/ConcatTransformer.py:160,
+ * 204,210).  q: row (b*Lq+i) at q + row*ldq + h*hd; k/v likewise with Lk.  kpm: uint8 [B][Lk]
+ * (1 = padded key).  lse: fp32 [B*H][Lq] saved for backward.  probs (optional): fp32
+ * [B][Lq][Lk] head-averaged attention weights (att dicts of Caption.forward). */
+int retr_attention_fwd(int dtype, const void* q, long ldq, const void* k, long ldk,
+                       const void* v, long ldv, void* o, long ldo, int B, int H, int Lq, int Lk,
+                       int hd, const unsigned char* kpm, int causal, float drop_p,
+                       unsigned long long seed, float* lse, float* probs, void* stream);
+int retr_attention_bwd(int dtype, const void* q, long ldq, const void* k, long ldk,
+                       const void* v, long ldv, const void* o, long ldo, const void* dout,
+                       long lddo, const float* lse, void* dq, long lddq, void* dk, long lddk,
+                       void* dv, long lddv, int B, int H, int Lq, int Lk, int hd,
+                       const unsigned char* kpm, int causal, float drop_p,
+                       unsigned long long seed, float* workspace, void* stream);
+size_t retr_attention_bwd_workspace(int B, int H, int Lq);
+/* decode step: q [B][.] one row per batch; k/v caches with Lmax rows per batch, first Lk valid */
+int retr_attention_decode(int dtype, const void* q, long ldq, const void* k, long ldk,
+                          const void* v, long ldv, void* o, long ldo, int B, int H, int Lk,
+                          int Lmax, int hd, const unsigned char* kpm, void* stream);
+
+/* ---- CrossEntropyLoss (models/caption.py:210, engine.py:71) and argmax (decode.py:71) ----- */
+int retr_ce_fwd(int dtype, const void* logits, long ld, int M, int V, const long long* targets,
+                float* lse, float* loss_rows, float* loss, void* stream);
+int retr_ce_bwd(int dtype, const void* logits, long ld, int M, int V, const long long* targets,
+                const float* lse, const float* dloss, float inv_count, void* dlogits, long lddl,
+                void* stream);
+int retr_argmax_rows(int dtype, const void* x, long ld, int M, int V, long long* out,
+                     void* stream);
+
+/* greedy bookkeeping for step i (eval_utils/decode.py:72-79) on device */
+int retr_greedy_update(const long long* pred, int B, int T, int i, long long eos,
+                       long long* caption, unsigned char* finished, int* done, long long* tok,
+                       void* stream);
+
+/* ---- elementwise helpers --------------------------------------------------------------- */
+/* y[m][n] = x[m][n] * keep(seed, m*N+n) * scale   (backward of the branch dropout) */
+int retr_dropout_apply(int dtype_out, const float* x, long ldx, void* y, long ldy, int M, int N,
+                       float drop_p, unsigned long long seed, void* stream);
+/* out (dtype) <- in (fp32), contiguous */
+int retr_cast(int dtype, const float* x, void* y, long n, void* stream);
+/* dpos[p][c] += sum_{m: m % period == p} d[m][c] */
+int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

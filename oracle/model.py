@@ -1,0 +1,269 @@
+"""Functional fp32 CPU restatement of the RE⫶TR hot path (TEST INFRASTRUCTURE ONLY).
+
+Every function cites the reference file:line it restates.  It runs on a plain ``state_dict``
+(same keys as the reference ``Caption`` model) so it needs no reference import at run time and
+travels to the GPU box with the tests.  Dropout is the identity here (parity is defined with
+``dropout=0``/``.eval()``, SURVEY.md §7 hard part (iv)).
+
+Pinned against the reference itself by ``tests/golden/make_golden.py`` (vectors in
+``tests/golden/*.npz``; see ``tests/test_oracle.py``).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+# ---------------------------------------------------------------------------------------------
+# backbone  (models/backbone.py + torchvision resnet semantics)
+# ---------------------------------------------------------------------------------------------
+
+_ARCH = {"resnet18": ("basic", [2, 2, 2, 2]), "resnet34": ("basic", [3, 4, 6, 3]),
+         "resnet50": ("bottleneck", [3, 4, 6, 3]), "resnet101": ("bottleneck", [3, 4, 23, 3])}
+
+
+def resnet_plan(name, dilation):
+    """Per-block (prefix, kind, inplanes, planes, stride, dilation, has_downsample) list.
+    torchvision ``_make_layer`` semantics with ``replace_stride_with_dilation=[F,F,dilation]``
+    (models/backbone.py:89-91)."""
+    kind, layers = _ARCH[name.lower()]
+    exp = 1 if kind == "basic" else 4
+    inplanes, cur_dil, plan = 64, 1, []
+    for li, (planes, nblk, stride, dil_flag) in enumerate(
+            zip([64, 128, 256, 512], layers, [1, 2, 2, 2], [False, False, False, dilation])):
+        prev_dil = cur_dil
+        if dil_flag:
+            cur_dil *= stride
+            stride = 1
+        ds = stride != 1 or inplanes != planes * exp
+        for bi in range(nblk):
+            d = prev_dil if bi == 0 else cur_dil
+            if kind == "basic" and d > 1:
+                raise NotImplementedError("Dilation > 1 not supported in BasicBlock")
+            plan.append((f"layer{li + 1}.{bi}", kind, inplanes, planes,
+                         stride if bi == 0 else 1, d, ds and bi == 0))
+            inplanes = planes * exp
+    return plan
+
+
+def frozen_bn(x, sd, p):
+    """models/backbone.py:41-51 (scale/bias recomputed in fp32 every call, eps 1e-5)."""
+    w = sd[p + ".weight"].reshape(1, -1, 1, 1)
+    b = sd[p + ".bias"].reshape(1, -1, 1, 1)
+    rv = sd[p + ".running_var"].reshape(1, -1, 1, 1)
+    rm = sd[p + ".running_mean"].reshape(1, -1, 1, 1)
+    scale = w * (rv + 1e-5).rsqrt()
+    bias = b - rm * scale
+    return x * scale + bias
+
+
+def resnet_body(x, sd, name, dilation, pre="backbone.body."):
+    """IntermediateLayerGetter(resnet, {'layer4': '0'}) (models/backbone.py:65,69)."""
+    x = F.conv2d(x, sd[pre + "conv1.weight"], stride=2, padding=3)
+    x = F.relu(frozen_bn(x, sd, pre + "bn1"))
+    x = F.max_pool2d(x, 3, 2, 1)
+    for (p, kind, _cin, _planes, stride, dil, ds) in resnet_plan(name, dilation):
+        q = pre + p + "."
+        idt = x
+        if ds:
+            idt = frozen_bn(F.conv2d(x, sd[q + "downsample.0.weight"], stride=stride), sd,
+                            q + "downsample.1")
+        if kind == "basic":
+            o = F.relu(frozen_bn(F.conv2d(x, sd[q + "conv1.weight"], stride=stride, padding=1),
+                                 sd, q + "bn1"))
+            o = frozen_bn(F.conv2d(o, sd[q + "conv2.weight"], padding=1), sd, q + "bn2")
+        else:
+            o = F.relu(frozen_bn(F.conv2d(x, sd[q + "conv1.weight"]), sd, q + "bn1"))
+            o = F.relu(frozen_bn(F.conv2d(o, sd[q + "conv2.weight"], stride=stride, padding=dil,
+                                          dilation=dil), sd, q + "bn2"))
+            o = frozen_bn(F.conv2d(o, sd[q + "conv3.weight"]), sd, q + "bn3")
+        x = F.relu(o + idt)
+    return x
+
+
+def mask_to_features(mask, hw):
+    """models/backbone.py:75 — nearest interpolation of the pixel mask to the feature grid."""
+    return F.interpolate(mask[None].float(), size=hw).to(torch.bool)[0]
+
+
+# ---------------------------------------------------------------------------------------------
+# transformer  (models/ConcatTransformer.py, models/transformer_modules.py, torch MHA)
+# ---------------------------------------------------------------------------------------------
+
+def sine_table(d_model, max_len=1024):
+    """models/position_encoding.py:16-22 -> buffer ``pe`` [max_len, 1, d_model]."""
+    position = torch.arange(max_len).unsqueeze(1)
+    div_term = torch.exp(torch.arange(0, d_model, 2) * (-math.log(10000.0) / d_model))
+    pe = torch.zeros(max_len, 1, d_model)
+    pe[:, 0, 0::2] = torch.sin(position * div_term)
+    pe[:, 0, 1::2] = torch.cos(position * div_term)
+    return pe
+
+
+def causal_mask(sz):
+    """models/utils.py:50-57: float mask, 0 on/below the diagonal, -inf above."""
+    m = (torch.triu(torch.ones(sz, sz)) == 1).transpose(0, 1)
+    return m.float().masked_fill(m == 0, float("-inf")).masked_fill(m == 1, 0.0)
+
+
+def mha(query, key, value, sd, p, nhead, key_padding_mask=None, attn_mask=None):
+    """``nn.MultiheadAttention.forward`` -> ``F.multi_head_attention_forward`` need_weights path
+    (torch/nn/functional.py:5785-5850 in-projection, :6553-6567 mask merge, :6576-6613 core).
+    Inputs are seq-first [L, B, C].  Returns (out [Lq,B,C], head-averaged P [B,Lq,Lk])."""
+    lq, bsz, c = query.shape
+    lk = key.shape[0]
+    hd = c // nhead
+    w, b = sd[p + ".in_proj_weight"], sd[p + ".in_proj_bias"]
+    wq, wk, wv = w.chunk(3)
+    bq, bk, bv = b.chunk(3)
+    q = F.linear(query, wq, bq)
+    k = F.linear(key, wk, bk)
+    v = F.linear(value, wv, bv)
+    q = q.view(lq, bsz * nhead, hd).transpose(0, 1)
+    k = k.view(lk, bsz * nhead, hd).transpose(0, 1)
+    v = v.view(lk, bsz * nhead, hd).transpose(0, 1)
+    mask = None
+    if attn_mask is not None:
+        mask = attn_mask.unsqueeze(0)
+    if key_padding_mask is not None:
+        kpm = torch.zeros(key_padding_mask.shape, dtype=q.dtype).masked_fill_(
+            key_padding_mask, float("-inf"))
+        kpm = kpm.view(bsz, 1, 1, lk).expand(-1, nhead, -1, -1).reshape(bsz * nhead, 1, lk)
+        mask = kpm if mask is None else mask + kpm
+    qs = q * math.sqrt(1.0 / float(hd))
+    if mask is not None:
+        att = torch.baddbmm(mask, qs, k.transpose(-2, -1))
+    else:
+        att = torch.bmm(qs, k.transpose(-2, -1))
+    att = F.softmax(att, dim=-1)
+    out = torch.bmm(att, v)
+    out = out.transpose(0, 1).contiguous().view(lq * bsz, c)
+    out = F.linear(out, sd[p + ".out_proj.weight"], sd[p + ".out_proj.bias"]).view(lq, bsz, c)
+    return out, att.view(bsz, nhead, lq, lk).mean(dim=1)
+
+
+def layer_norm(x, sd, p, eps=1e-5):
+    return F.layer_norm(x, (x.shape[-1],), sd[p + ".weight"], sd[p + ".bias"], eps)
+
+
+def feed_forward(x, sd, p):
+    """models/transformer_modules.py:6-11 (Linear -> ReLU -> Linear)."""
+    return F.linear(F.relu(F.linear(x, sd[p + ".0.weight"], sd[p + ".0.bias"])),
+                    sd[p + ".2.weight"], sd[p + ".2.bias"])
+
+
+def encoder_layer(x, sd, p, nhead, pos, kpm):
+    """TransformerEncoderLayer.forward (models/ConcatTransformer.py:171-194) with
+    SelfAttResidual (transformer_modules.py:22-46) and FFResidual (:77-97)."""
+    n = layer_norm(x, sd, p + ".self_attn.norm")
+    qk = n + pos
+    a, att = mha(qk, qk, n, sd, p + ".self_attn.sublayer", nhead, key_padding_mask=kpm)
+    x = x + a
+    x = x + feed_forward(layer_norm(x, sd, p + ".ff.norm"), sd, p + ".ff.sublayer")
+    return x, att
+
+
+def decoder_layer(y, mem, sd, p, nhead, pos, qpos, tgt_kpm, mem_kpm, tmask):
+    """TransformerDecoderLayer.forward (models/ConcatTransformer.py:220-257)."""
+    n = layer_norm(y, sd, p + ".tgt_self_attn.norm")
+    qk = n + qpos
+    a, att_s = mha(qk, qk, n, sd, p + ".tgt_self_attn.sublayer", nhead,
+                   key_padding_mask=tgt_kpm, attn_mask=tmask)
+    y = y + a
+    n = layer_norm(y, sd, p + ".tgt_src_cross_attn.norm")
+    a, att_x = mha(n + qpos, mem + pos, mem, sd, p + ".tgt_src_cross_attn.sublayer", nhead,
+                   key_padding_mask=mem_kpm)
+    y = y + a
+    y = y + feed_forward(layer_norm(y, sd, p + ".ff.norm"), sd, p + ".ff.sublayer")
+    return y, att_s, att_x
+
+
+def decoder_embeddings(caps, sd, eps, padding_idx=0, p="transformer.embeddings"):
+    """DecoderEmbeddings.forward (models/transformer_modules.py:113-129); the word table is an
+    nn.Embedding with padding_idx=config.pad_token_id (:103-104): no gradient to that row."""
+    t = caps.shape[1]
+    pos_ids = torch.arange(t, dtype=torch.long).unsqueeze(0).expand(caps.shape)
+    e = F.embedding(caps, sd[p + ".word_embeddings.weight"], padding_idx=padding_idx) + \
+        F.embedding(pos_ids, sd[p + ".position_embeddings.weight"])
+    return F.layer_norm(e, (e.shape[-1],), sd[p + ".LayerNorm.weight"],
+                        sd[p + ".LayerNorm.bias"], eps)
+
+
+def caption_forward(sd, cfg, images, img_mask, caps, cap_mask, return_attention=False):
+    """Caption.forward (models/caption.py:23-47) -> ConcatTransformer.forward
+    (models/ConcatTransformer.py:45-74) -> MLP (models/caption.py:161-174).
+    images [B,3,H,W] fp32, img_mask [B,H,W] bool, caps [B,T] int64, cap_mask [B,T] bool."""
+    feats = resnet_body(images, sd, cfg.backbone, cfg.dilation)
+    m = mask_to_features(img_mask, feats.shape[-2:])
+    src = F.conv2d(feats, sd["input_proj.weight"], sd["input_proj.bias"])
+    src = src.flatten(2)            # [B, C, S]
+    m = m.flatten(1)                # [B, S]
+    bsz, c, s = src.shape
+    nhead = cfg.nheads
+    pe = sd["transformer.positional_encoding.pe"]
+    pos = pe[:s].permute(1, 2, 0).repeat(bsz, 1, 1).permute(2, 0, 1)   # [S, B, C]
+    x = src.permute(2, 0, 1)
+    tgt = decoder_embeddings(caps, sd, cfg.layer_norm_eps, cfg.pad_token_id).permute(1, 0, 2)
+    qpos = sd["transformer.embeddings.position_embeddings.weight"].unsqueeze(1).repeat(1, bsz, 1)
+    atts = {"enc_tc_self_att": [], "dec_exp_self_att": [], "dec_exp_tc_cross_att": []}
+    for i in range(cfg.enc_layers):
+        x, a = encoder_layer(x, sd, f"transformer.encoder.layers.{i}", nhead, pos, m)
+        atts["enc_tc_self_att"].append(a)
+    if cfg.pre_norm:
+        x = layer_norm(x, sd, "transformer.encoder.norm")
+    tmask = causal_mask(tgt.shape[0])
+    y = tgt
+    for i in range(cfg.dec_layers):
+        y, a_s, a_x = decoder_layer(y, x, sd, f"transformer.decoder.layers.{i}", nhead, pos, qpos,
+                                    cap_mask, m, tmask)
+        atts["dec_exp_self_att"].append(a_s)
+        atts["dec_exp_tc_cross_att"].append(a_x)
+    hs = layer_norm(y, sd, "transformer.decoder.norm")
+    h = hs.permute(1, 0, 2)
+    for i in range(3):
+        h = F.linear(h, sd[f"mlp.layers.{i}.weight"], sd[f"mlp.layers.{i}.bias"])
+        if i < 2:
+            h = F.relu(h)
+    if return_attention:
+        return h, {k: torch.stack(v) for k, v in atts.items()}
+    return h
+
+
+def caption_loss(logits, caps_out):
+    """CrossEntropyLoss() (models/caption.py:210) as called at engine.py:71 — mean over B*T,
+    no ignore_index (pad id 0 counts)."""
+    return F.cross_entropy(logits.permute(0, 2, 1), caps_out)
+
+
+def greedy(forward, batch, max_len, bos_token=1, eos_token=2):
+    """eval_utils/decode.py:53-81 (with create_caption_and_mask :20-27).  ``forward(caption,
+    cap_mask) -> logits [B, max_len, V]``.  Returns the caption tensor with the reference's
+    exact write / early-exit semantics."""
+    caption = torch.zeros((batch, max_len), dtype=torch.long)
+    cap_mask = torch.ones((batch, max_len), dtype=torch.bool)
+    caption[:, 0] = bos_token
+    cap_mask[:, 0] = False
+    finished = torch.zeros(batch, dtype=torch.bool)
+    for i in range(max_len - 1):
+        pred = forward(caption, cap_mask)[:, i, :]
+        pid = torch.argmax(pred, axis=-1)
+        finished = torch.logical_or(pid == eos_token, finished)
+        if all(finished):
+            return caption
+        caption[:, i + 1] = pid
+        cap_mask[:, i + 1] = False
+    return caption
+
+
+def prune_cap_ids(idx_seqs, clean=True, pad_token=0, bos_token=1, eos_token=2):
+    """eval_utils/decode.py:84-101."""
+    out = []
+    for seq in idx_seqs:
+        pr = []
+        for idx in seq:
+            pr.append(idx)
+            if idx == eos_token:
+                break
+        if clean:
+            pr = [i for i in pr if i not in (pad_token, bos_token, eos_token)]
+        out.append(pr)
+    return out

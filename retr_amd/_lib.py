@@ -1,0 +1,106 @@
+"""ctypes binding of ``libretr_hip.so`` (the gfx950 kernels; C-ABI in ``include/retr_hip.h``).
+
+The product path has no fallback: if the library is missing or a CUDA/HIP device is absent,
+every op raises.  Build the library with ``make`` (or ``__graft_entry__.build()``).
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libretr_hip.so")
+
+F32, BF16 = 0, 1
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+_U64 = ctypes.c_ulonglong
+_SZ = ctypes.c_size_t
+
+# name -> argtypes (all functions return int unless listed in _RESTYPE)
+_SIGS = {
+    "retr_abi_version": [],
+    "retr_last_error": [],
+    "retr_linear_fwd": [_I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _I, _P, _L, _F, _U64, _P],
+    "retr_linear_dgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _L, _P, _L, _P],
+    "retr_linear_wgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _P],
+    "retr_bias_grad": [_I, _P, _L, _I, _I, _P, _P],
+    "retr_conv_pack": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "retr_conv2d_fwd": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "retr_conv2d_dgrad": [_I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P],
+    "retr_conv2d_wgrad": [_I, _P, _P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P],
+    "retr_conv_wgrad_unpack": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "retr_nchw_to_nhwc": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
+    "retr_maxpool3x3s2": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "retr_mask_nearest": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "retr_layernorm_fwd": [_I, _P, _L, _P, _P, _F, _I, _I, _P, _L, _P, _P, _I, _P, _P, _P],
+    "retr_layernorm_bwd": [_I, _P, _P, _L, _P, _L, _P, _P, _P, _I, _I, _P, _L, _P, _P, _P, _P],
+    "retr_embed_ln_fwd": [_P, _I, _I, _I, _P, _P, _P, _P, _F, _F, _U64, _P, _P, _P, _P],
+    "retr_embed_ln_bwd": [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _U64, _P, _P, _P, _P, _I,
+                          _P],
+    "retr_attention_fwd": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _P, _I, _F,
+                           _U64, _P, _P, _P],
+    "retr_attention_bwd": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _P, _L, _P, _L, _P,
+                           _L, _I, _I, _I, _I, _I, _P, _I, _F, _U64, _P, _P],
+    "retr_attention_bwd_workspace": [_I, _I, _I],
+    "retr_attention_decode": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _P, _P],
+    "retr_greedy_update": [_P, _I, _I, _I, ctypes.c_longlong, _P, _P, _P, _P, _P],
+    "retr_ce_fwd": [_I, _P, _L, _I, _I, _P, _P, _P, _P, _P],
+    "retr_ce_bwd": [_I, _P, _L, _I, _I, _P, _P, _P, _F, _P, _L, _P],
+    "retr_argmax_rows": [_I, _P, _L, _I, _I, _P, _P],
+    "retr_dropout_apply": [_I, _P, _L, _P, _L, _I, _I, _F, _U64, _P],
+    "retr_cast": [_I, _P, _P, _L, _P],
+    "retr_pos_grad": [_I, _P, _L, _I, _I, _I, _P, _P],
+}
+_RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ}
+
+_lib = None
+
+
+def load():
+    """Load the kernel library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"retr_amd: native library {LIB_PATH} is missing; build it with `make` "
+                "(there is no CPU fallback)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPE.get(name, ctypes.c_int)
+        _lib = lib
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        msg = load().retr_last_error()
+        raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("retr_amd ops run on the MI355X (HIP) device only; got a "
+                               f"{t.device} tensor (no CPU fallback)")

@@ -1,0 +1,65 @@
+// Shared definitions for the RE⫶TR gfx950 kernels (HIP, CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+#define RETR_DEVICE __device__ __forceinline__
+
+// ---- dtype tags (mirror include/retr_hip.h) --------------------------------------------------
+enum { RETR_F32 = 0, RETR_BF16 = 1 };
+
+// ---- error plumbing ---------------------------------------------------------------------------
+void retr_set_error(const char* fmt, ...);
+int retr_check_launch(const char* what);
+
+#define RETR_REQUIRE(cond, ...)                  \
+  do {                                           \
+    if (!(cond)) {                               \
+      retr_set_error(__VA_ARGS__);               \
+      return 1;                                  \
+    }                                            \
+  } while (0)
+
+// ---- conversions -------------------------------------------------------------------------------
+template <typename T> RETR_DEVICE float to_f(T v) { return (float)v; }
+template <typename T> RETR_DEVICE T from_f(float v) { return (T)v; }
+
+// ---- counter-based dropout RNG -----------------------------------------------------------------
+// keep(seed, idx) is a pure function of (seed, idx) so backward regenerates forward's mask.
+RETR_DEVICE uint32_t retr_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + idx * 0xD1B54A32D192ED03ull + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+// threshold = p * 2^32 (host computes); element kept iff hash >= threshold
+RETR_DEVICE bool retr_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+  return retr_hash(seed, idx) >= thresh;
+}
+
+struct DropoutParams {
+  uint64_t seed;
+  uint32_t thresh;  // 0 => dropout disabled
+  float scale;      // 1/(1-p)
+};
+
+// ---- wave reductions (wave64) ------------------------------------------------------------------
+RETR_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+RETR_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,279 @@
+// ResNet convolutions as implicit GEMMs on the MFMA core (NHWC activations).
+//
+//   forward : Y[n,oh,ow,co] = act( sum_{kh,kw,ci} X[n,ih,iw,ci] Weff[co,kh,kw,ci] + beff[co] [+ R] )
+//             Weff = W * bn_scale (FrozenBatchNorm2d folded, models/backbone.py:41-51)
+//   dgrad   : dX[n,ih,iw,ci] = gate( sum_{kh,kw,co} G[n,oh,ow,co] Weff[co,kh,kw,ci] [+ addend] )
+//             with ih = oh*s - p + kh*d  (stride handled by a divisibility test)
+//   wgrad   : dWeff[co, (kh,kw,ci)] = sum_pixels G[pix,co] X[pix @ (kh,kw), ci]   (split-K)
+//             then dW = dWeff * bn_scale, scattered to the OIHW parameter layout.
+#include "gemm.hpp"
+#include "epilogues.hpp"
+#include "../../include/retr_hip.h"
+
+using namespace retr;
+
+namespace {
+
+struct Geom {
+  int Nb, H, W, C, Co, KH, KW, s, p, d, OH, OW;
+};
+
+template <typename T>
+struct ConvFwdA {  // A(m = n,oh,ow ; k = kh,kw,ci)
+  static constexpr bool kContig = true;
+  const T* x;
+  Geom g;
+  int M, K;
+  struct Ctx { const T* img; int ihb, iwb; bool ok; };
+  RETR_DEVICE Ctx row_ctx(int r) const {
+    Ctx c;
+    c.ok = r < M;
+    int rr = c.ok ? r : 0;
+    int hw = g.OH * g.OW;
+    int n = rr / hw, rem = rr - n * hw;
+    int oh = rem / g.OW, ow = rem - oh * g.OW;
+    c.img = x + (long)n * g.H * g.W * g.C;
+    c.ihb = oh * g.s - g.p;
+    c.iwb = ow * g.s - g.p;
+    return c;
+  }
+  RETR_DEVICE u32x4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero16();
+    int khw = k / g.C, ci = k - khw * g.C;
+    int kh = khw / g.KW, kw = khw - kh * g.KW;
+    int ih = c.ihb + kh * g.d, iw = c.iwb + kw * g.d;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return zero16();
+    return *(const u32x4*)(c.img + ((long)ih * g.W + iw) * g.C + ci);
+  }
+};
+
+template <typename T>
+struct ConvDgradA {  // A(m = n,ih,iw ; k = kh,kw,co) = G[n, (ih+p-kh d)/s, (iw+p-kw d)/s, co]
+  static constexpr bool kContig = true;
+  const T* gr;
+  Geom g;
+  int M, K;
+  struct Ctx { const T* img; int ihp, iwp; bool ok; };
+  RETR_DEVICE Ctx row_ctx(int r) const {
+    Ctx c;
+    c.ok = r < M;
+    int rr = c.ok ? r : 0;
+    int hw = g.H * g.W;
+    int n = rr / hw, rem = rr - n * hw;
+    int ih = rem / g.W, iw = rem - ih * g.W;
+    c.img = gr + (long)n * g.OH * g.OW * g.Co;
+    c.ihp = ih + g.p;
+    c.iwp = iw + g.p;
+    return c;
+  }
+  RETR_DEVICE u32x4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero16();
+    int khw = k / g.Co, co = k - khw * g.Co;
+    int kh = khw / g.KW, kw = khw - kh * g.KW;
+    int th = c.ihp - kh * g.d, tw = c.iwp - kw * g.d;
+    if (th < 0 || tw < 0) return zero16();
+    int oh = th / g.s, ow = tw / g.s;
+    if (oh * g.s != th || ow * g.s != tw || oh >= g.OH || ow >= g.OW) return zero16();
+    return *(const u32x4*)(c.img + ((long)oh * g.OW + ow) * g.Co + co);
+  }
+};
+
+template <typename T>
+struct ConvWgradB {  // B(row = kh,kw,ci ; k = pixel n,oh,ow) = X[n, oh*s-p+kh d, ow*s-p+kw d, ci]
+  static constexpr bool kContig = false;
+  const T* x;
+  Geom g;
+  int rows, M;
+  struct Ctx { int khd, kwd, ci; bool ok; };
+  RETR_DEVICE Ctx row_ctx(int r) const {
+    Ctx c;
+    c.ok = r < rows;
+    int rr = c.ok ? r : 0;
+    int khw = rr / g.C;
+    c.ci = rr - khw * g.C;
+    int kh = khw / g.KW, kw = khw - kh * g.KW;
+    c.khd = kh * g.d - g.p;
+    c.kwd = kw * g.d - g.p;
+    return c;
+  }
+  RETR_DEVICE u32x4 load(const Ctx& c, int m) const {
+    if (!c.ok || m >= M) return zero16();
+    int hw = g.OH * g.OW;
+    int n = m / hw, rem = m - n * hw;
+    int oh = rem / g.OW, ow = rem - oh * g.OW;
+    int ih = oh * g.s + c.khd, iw = ow * g.s + c.kwd;
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return zero16();
+    return *(const u32x4*)(x + (((long)n * g.H + ih) * g.W + iw) * g.C + c.ci);
+  }
+};
+
+template <typename T, class LA, class LB, class EP>
+int launch_auto(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits,
+                hipStream_t st, const char* what) {
+  if (N >= 128 && M >= 4096) return launch_gemm<T, 128, 128>(la, lb, ep, M, N, K, splits, st, what);
+  return launch_gemm<T, 64, 64>(la, lb, ep, M, N, K, splits, st, what);
+}
+
+template <typename T>
+int conv_fwd_t(const void* x, Geom g, const void* w, const float* bias, const void* res, void* y,
+               int relu, hipStream_t st) {
+  int M = g.Nb * g.OH * g.OW, N = g.Co, K = g.KH * g.KW * g.C;
+  DenseK<T> lb{(const T*)w, (long)K, N, K};
+  EpiFwd<T, T> ep{(T*)y, (long)N, bias, (const T*)res, (long)N, relu ? 2 : 0, DropoutParams{0, 0, 1.f}, 0};
+  if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
+    DenseK<T> la{(const T*)x, (long)g.C, M, K};
+    return launch_auto<T>(la, lb, ep, M, N, K, 1, st, "conv_fwd_1x1");
+  }
+  ConvFwdA<T> la{(const T*)x, g, M, K};
+  return launch_auto<T>(la, lb, ep, M, N, K, 1, st, "conv_fwd");
+}
+
+template <typename T>
+int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* addend,
+                 const void* gate, hipStream_t st) {
+  int M = g.Nb * g.H * g.W, N = g.C, K = g.KH * g.KW * g.Co;
+  DenseK<T> lb{(const T*)wt, (long)K, N, K};
+  EpiDgrad<T, T, T> ep{(T*)dx, (long)N, (const T*)addend, (long)N, (const T*)gate, (long)N};
+  if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
+    DenseK<T> la{(const T*)dy, (long)g.Co, M, K};
+    return launch_auto<T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad_1x1");
+  }
+  ConvDgradA<T> la{(const T*)dy, g, M, K};
+  return launch_auto<T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad");
+}
+
+template <typename T>
+int conv_wgrad_t(const void* dy, const void* x, Geom g, float* ws, hipStream_t st) {
+  int Mp = g.Nb * g.OH * g.OW;          // reduction length (pixels)
+  int R = g.Co, Ncols = g.KH * g.KW * g.C;
+  DenseT<T> la{(const T*)dy, (long)g.Co, R, Mp};
+  constexpr int BK = Elem<T>::BK;
+  bool big = R >= 128 && Ncols >= 128;
+  int s = big ? pick_splits(R, Ncols, Mp, 128, 128, BK) : pick_splits(R, Ncols, Mp, 64, 64, BK);
+  EpiAccF32 ep{ws, (long)Ncols, s > 1};
+  if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
+    DenseT<T> lb{(const T*)x, (long)g.C, Ncols, Mp};
+    return big ? launch_gemm<T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad_1x1")
+               : launch_gemm<T, 64, 64>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad_1x1");
+  }
+  ConvWgradB<T> lb{(const T*)x, g, Ncols, Mp};
+  return big ? launch_gemm<T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad")
+             : launch_gemm<T, 64, 64>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad");
+}
+
+// ---- weight packing: fp32 OIHW (+ FrozenBN buffers) -> folded [Co][KH][KW][Cp] and the
+//      dgrad image [Cp][KH][KW][Co]; also beff/scale for the epilogues.
+template <typename T>
+__global__ void conv_pack_kernel(const float* w, const float* bnw, const float* bnb,
+                                 const float* bnrm, const float* bnrv, const float* conv_bias,
+                                 int Co, int Ci, int KH, int KW, int Cp, T* wout, T* wtout,
+                                 float* bias_out, float* scale_out) {
+  long total = (long)Co * KH * KW * Cp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int ci = i % Cp;
+    long t = i / Cp;
+    int kw = t % KW;
+    t /= KW;
+    int kh = t % KH;
+    int co = (int)(t / KH);
+    float scale = 1.f;
+    if (bnw) scale = bnw[co] * (1.0f / sqrtf(bnrv[co] + 1e-5f));
+    float v = ci < Ci ? w[(((long)co * Ci + ci) * KH + kh) * KW + kw] * scale : 0.f;
+    wout[i] = from_f<T>(v);
+    if (wtout) wtout[(((long)ci * KH + kh) * KW + kw) * Co + co] = from_f<T>(v);
+    if (ci == 0 && kh == 0 && kw == 0) {
+      float b;
+      if (bnw) b = bnb[co] - bnrm[co] * scale;
+      else b = conv_bias ? conv_bias[co] : 0.f;
+      if (bias_out) bias_out[co] = b;
+      if (scale_out) scale_out[co] = scale;
+    }
+  }
+}
+
+__global__ void wgrad_unpack_kernel(const float* ws, const float* scale, float* grad, int Co,
+                                    int Ci, int Cp, int KH, int KW, int accumulate) {
+  long total = (long)Co * Ci * KH * KW;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int kw = i % KW;
+    long t = i / KW;
+    int kh = t % KH;
+    t /= KH;
+    int ci = t % Ci;
+    int co = (int)(t / Ci);
+    float v = ws[((long)co * KH * KW + kh * KW + kw) * Cp + ci];
+    if (scale) v *= scale[co];
+    grad[i] = accumulate ? grad[i] + v : v;
+  }
+}
+
+Geom make_geom(int Nb, int H, int W, int C, int Co, int KH, int KW, int s, int p, int d) {
+  Geom g{Nb, H, W, C, Co, KH, KW, s, p, d, 0, 0};
+  g.OH = (H + 2 * p - d * (KH - 1) - 1) / s + 1;
+  g.OW = (W + 2 * p - d * (KW - 1) - 1) / s + 1;
+  return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int retr_conv2d_fwd(int dtype, const void* x, int Nb, int H, int W, int C, const void* w,
+                    const float* bias, const void* residual, void* y, int Co, int KH, int KW,
+                    int stride, int pad, int dil, int relu, void* stream) {
+  Geom g = make_geom(Nb, H, W, C, Co, KH, KW, stride, pad, dil);
+  int epc = dtype == RETR_BF16 ? 8 : 4;
+  RETR_REQUIRE(C % epc == 0, "conv2d_fwd: C=%d must be a multiple of %d", C, epc);
+  RETR_REQUIRE(g.OH > 0 && g.OW > 0, "conv2d_fwd: empty output");
+  if (dtype == RETR_BF16) return conv_fwd_t<bf16>(x, g, w, bias, residual, y, relu, (hipStream_t)stream);
+  return conv_fwd_t<float>(x, g, w, bias, residual, y, relu, (hipStream_t)stream);
+}
+
+int retr_conv2d_dgrad(int dtype, const void* dy, int Nb, int H, int W, int C, const void* wt,
+                      void* dx, int Co, int KH, int KW, int stride, int pad, int dil,
+                      const void* addend, const void* gate, void* stream) {
+  Geom g = make_geom(Nb, H, W, C, Co, KH, KW, stride, pad, dil);
+  int epc = dtype == RETR_BF16 ? 8 : 4;
+  RETR_REQUIRE(C % epc == 0 && Co % epc == 0, "conv2d_dgrad: channels must be %%%d", epc);
+  if (dtype == RETR_BF16) return conv_dgrad_t<bf16>(dy, g, wt, dx, addend, gate, (hipStream_t)stream);
+  return conv_dgrad_t<float>(dy, g, wt, dx, addend, gate, (hipStream_t)stream);
+}
+
+int retr_conv2d_wgrad(int dtype, const void* dy, const void* x, int Nb, int H, int W, int C,
+                      float* ws, int Co, int KH, int KW, int stride, int pad, int dil,
+                      void* stream) {
+  Geom g = make_geom(Nb, H, W, C, Co, KH, KW, stride, pad, dil);
+  int epc = dtype == RETR_BF16 ? 8 : 4;
+  RETR_REQUIRE(C % epc == 0 && Co % epc == 0, "conv2d_wgrad: channels must be %%%d", epc);
+  if (dtype == RETR_BF16) return conv_wgrad_t<bf16>(dy, x, g, ws, (hipStream_t)stream);
+  return conv_wgrad_t<float>(dy, x, g, ws, (hipStream_t)stream);
+}
+
+int retr_conv_pack(int dtype, const float* w, const float* bn_w, const float* bn_b,
+                   const float* bn_rm, const float* bn_rv, const float* conv_bias, int Co, int Ci,
+                   int KH, int KW, int Cp, void* w_out, void* wt_out, float* bias_out,
+                   float* scale_out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  long total = (long)Co * KH * KW * Cp;
+  int grid = (int)(total / 256 + 1 < 4096 ? total / 256 + 1 : 4096);
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(conv_pack_kernel<bf16>, dim3(grid), dim3(256), 0, st, w, bn_w, bn_b, bn_rm,
+                       bn_rv, conv_bias, Co, Ci, KH, KW, Cp, (bf16*)w_out, (bf16*)wt_out, bias_out, scale_out);
+  else
+    hipLaunchKernelGGL(conv_pack_kernel<float>, dim3(grid), dim3(256), 0, st, w, bn_w, bn_b, bn_rm,
+                       bn_rv, conv_bias, Co, Ci, KH, KW, Cp, (float*)w_out, (float*)wt_out, bias_out, scale_out);
+  return retr_check_launch("conv_pack");
+}
+
+int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,
+                           int Cp, int KH, int KW, int accumulate, void* stream) {
+  long total = (long)Co * Ci * KH * KW;
+  int grid = (int)(total / 256 + 1 < 4096 ? total / 256 + 1 : 4096);
+  hipLaunchKernelGGL(wgrad_unpack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, scale,
+                     grad, Co, Ci, Cp, KH, KW, accumulate);
+  return retr_check_launch("conv_wgrad_unpack");
+}
+
+}  // extern "C"

@@ -1,0 +1,259 @@
+// Generic LDS-tiled MFMA GEMM core for gfx950:  C[m][n] = sum_k A(m,k) * B(n,k)
+//
+//  * 256 threads = 4 waves in a 2x2 arrangement; block tile BM x BN, K-step of 128 bytes
+//    (64 bf16 / 32 f32) per LDS row.
+//  * bf16 operands use v_mfma_f32_16x16x32_bf16, f32 operands the exact-f32
+//    v_mfma_f32_16x16x4_f32 (parity mode).  Accumulation is always fp32.
+//  * Operands are produced by "loaders" (implicit GEMM): a loader maps a 16-byte chunk request
+//    to global memory.  Two chunk orientations exist:
+//      - kContig: the chunk holds EPC consecutive K elements of one row (activations/weights in
+//        [row][k] layout, NHWC im2col);
+//      - !kContig: the chunk holds EPC consecutive ROWS at one k (operands stored [k][row], e.g.
+//        the token/pixel-major tensors of a weight-gradient GEMM).  They are transposed while
+//        being written to LDS.
+//  * LDS image: [rows][8 chunks of 16 B], chunk position XOR-swizzled with (row>>1)&7 so the
+//    ds_read_b128 fragment reads of the 16x16x32 operand map are bank-conflict free.
+//  * Register-staged double buffer: tile k+1 is fetched into VGPRs before the MFMAs of tile k
+//    and written to the other LDS buffer after them; one barrier per K-step.
+//  * Split-K over blockIdx.z; the epilogue decides (store vs atomic) from its own state.
+#pragma once
+#include "common.hpp"
+
+namespace retr {
+
+constexpr int kBKBytes = 128;
+
+template <typename T> struct Elem {
+  static constexpr int EPC = 16 / sizeof(T);       // elements per 16-byte chunk
+  static constexpr int BK = kBKBytes / sizeof(T);   // K elements per tile step
+};
+
+RETR_DEVICE int lds_off(int r, int c) { return r * kBKBytes + ((c ^ ((r >> 1) & 7)) << 4); }
+
+RETR_DEVICE u32x4 zero16() { return u32x4{0u, 0u, 0u, 0u}; }
+
+template <typename T>
+RETR_DEVICE void mfma_step(f32x4& acc, const u32x4& a, const u32x4& b);
+
+template <>
+RETR_DEVICE void mfma_step<bf16>(f32x4& acc, const u32x4& a, const u32x4& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+}
+template <>
+RETR_DEVICE void mfma_step<float>(f32x4& acc, const u32x4& a, const u32x4& b) {
+  f32x4 fa = __builtin_bit_cast(f32x4, a), fb = __builtin_bit_cast(f32x4, b);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[0], fb[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[1], fb[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[2], fb[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[3], fb[3], acc, 0, 0, 0);
+}
+
+// Staging of one operand tile (ROWS x BK) through registers into the swizzled LDS image.
+template <typename T, int ROWS, class L>
+struct Stager {
+  static constexpr int EPC = Elem<T>::EPC;
+  static constexpr int BK = Elem<T>::BK;
+  static constexpr int NCH = ROWS / 32;  // chunks per thread (ROWS*128B / 16B / 256 threads)
+  static constexpr int RCH = ROWS / EPC; // row-chunks per k (row-contig orientation)
+  typename L::Ctx ctx[L::kContig ? NCH : 1];
+  u32x4 reg[NCH];
+
+  RETR_DEVICE void init(const L& l, int row0, int tid) {
+    if constexpr (L::kContig) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) ctx[i] = l.row_ctx(row0 + (tid >> 3) + 32 * i);
+    } else {
+      ctx[0] = l.row_ctx(row0 + (tid % RCH) * EPC);
+    }
+  }
+  RETR_DEVICE void fetch(const L& l, int k0, int tid) {
+    if constexpr (L::kContig) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) reg[i] = l.load(ctx[i], k0 + (tid & 7) * EPC);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) reg[i] = l.load(ctx[0], k0 + tid / RCH + (256 / RCH) * i);
+    }
+  }
+  RETR_DEVICE void store(char* lds, int tid) {
+    if constexpr (L::kContig) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        int r = (tid >> 3) + 32 * i, c = tid & 7;
+        *(u32x4*)(lds + lds_off(r, c)) = reg[i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        int k = tid / RCH + (256 / RCH) * i;
+        int r0 = (tid % RCH) * EPC;
+        const T* v = (const T*)&reg[i];
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          int r = r0 + e;
+          *(T*)(lds + lds_off(r, k / EPC) + (k % EPC) * (int)sizeof(T)) = v[e];
+        }
+      }
+    }
+  }
+};
+
+template <typename T, int BM, int BN, class LA, class LB, class EP>
+__global__ void __launch_bounds__(256)
+gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
+  constexpr int BK = Elem<T>::BK;
+  constexpr int TM = BM / 32, TN = BN / 32;  // 16x16 subtiles per wave (2x2 waves)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int kBuf = (BM + BN) * kBKBytes;  // one stage: A tile then B tile
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware tile order: consecutive tile ids that share an A panel land on one XCD.
+  const int nblk = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  const int kb = blockIdx.y * kchunk;
+  const int ke = min(K, kb + kchunk);
+  if (kb >= ke) {
+    ep.empty_split(m0, n0);
+    return;
+  }
+
+  Stager<T, BM, LA> sa;
+  Stager<T, BN, LB> sb;
+  sa.init(la, m0, tid);
+  sb.init(lb, n0, tid);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  sa.fetch(la, kb, tid);
+  sb.fetch(lb, kb, tid);
+  sa.store(smem, tid);
+  sb.store(smem + BM * kBKBytes, tid);
+  __syncthreads();
+
+  int cur = 0;
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    const bool more = k0 + BK < ke;
+    if (more) {
+      sa.fetch(la, k0 + BK, tid);
+      sb.fetch(lb, k0 + BK, tid);
+    }
+    const char* A = smem + cur * kBuf;
+    const char* B = A + BM * kBKBytes;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = (lane >> 4) + 4 * ks;
+      u32x4 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        af[i] = *(const u32x4*)(A + lds_off(wm * (BM / 2) + 16 * i + (lane & 15), c));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = *(const u32x4*)(B + lds_off(wn * (BN / 2) + 16 * j + (lane & 15), c));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mfma_step<T>(acc[i][j], af[i], bfr[j]);
+    }
+    if (more) {
+      sa.store(smem + (cur ^ 1) * kBuf, tid);
+      sb.store(smem + (cur ^ 1) * kBuf + BM * kBKBytes, tid);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * (BN / 2) + 16 * j + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * (BM / 2) + 16 * i + 4 * (lane >> 4) + e;
+        if (m < M && n < N) ep.apply(m, n, acc[i][j][e]);
+      }
+    }
+}
+
+template <typename T, int BM, int BN>
+constexpr size_t gemm_lds_bytes() { return 2 * (BM + BN) * kBKBytes; }
+
+// Host-side launcher: picks split-K so that the grid has enough blocks to fill 256 CUs.
+template <typename T, int BM, int BN, class LA, class LB, class EP>
+int launch_gemm(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits,
+                hipStream_t st, const char* what) {
+  constexpr int BK = Elem<T>::BK;
+  const int tm = cdiv(M, BM), tn = cdiv(N, BN);
+  if (splits < 1) splits = 1;
+  int ksteps = cdiv(K, BK);
+  if (splits > ksteps) splits = ksteps;
+  int kchunk = cdiv(ksteps, splits) * BK;
+  splits = cdiv(K, kchunk);
+  dim3 grid(tm * tn, splits);
+  size_t lds = gemm_lds_bytes<T, BM, BN>();
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, LA, LB, EP>), grid, dim3(256), lds, st, la, lb, ep,
+                     M, N, K, kchunk, tn);
+  return retr_check_launch(what);
+}
+
+// Split-K heuristic: aim for >= ~2 waves of blocks over 256 CUs when the reduction is long.
+static inline int pick_splits(int M, int N, int K, int BM, int BN, int BK, int max_splits = 64) {
+  long tiles = (long)cdiv(M, BM) * cdiv(N, BN);
+  int ksteps = cdiv(K, BK);
+  if (tiles >= 384 || ksteps < 8) return 1;
+  long want = (512 + tiles - 1) / tiles;
+  long by_k = ksteps / 4;  // keep >= 4 K-steps per split
+  long s = want < by_k ? want : by_k;
+  if (s > max_splits) s = max_splits;
+  return s < 1 ? 1 : (int)s;
+}
+
+// ----------------------------------------------------------------------------------------------
+// Common loaders
+// ----------------------------------------------------------------------------------------------
+
+// Row-major [rows][ld] operand, K contiguous (activations X[M][K], weights W[N][K]).
+template <typename T>
+struct DenseK {
+  static constexpr bool kContig = true;
+  static constexpr int EPC = Elem<T>::EPC;
+  const T* p;
+  long ld;
+  int rows, K;
+  struct Ctx { const T* row; bool ok; };
+  RETR_DEVICE Ctx row_ctx(int r) const { return Ctx{p + (long)r * ld, r < rows}; }
+  RETR_DEVICE u32x4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero16();
+    return *(const u32x4*)(c.row + k);
+  }
+};
+
+// Operand stored [k][ld] (rows contiguous): element (r, k) = p[k*ld + r]; chunks along rows.
+// Requires rows % EPC == 0 or zero-padding beyond `rows` inside the chunk's row range.
+template <typename T>
+struct DenseT {
+  static constexpr bool kContig = false;
+  static constexpr int EPC = Elem<T>::EPC;
+  const T* p;
+  long ld;
+  int rows, K;
+  struct Ctx { const T* col; bool ok; };
+  RETR_DEVICE Ctx row_ctx(int r) const { return Ctx{p + r, r < rows}; }
+  RETR_DEVICE u32x4 load(const Ctx& c, int k) const {
+    if (!c.ok || k >= K) return zero16();
+    return *(const u32x4*)(c.col + (long)k * ld);
+  }
+};
+
+}  // namespace retr

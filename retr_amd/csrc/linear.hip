@@ -1,0 +1,140 @@
+// Linear layers (nn.Linear / MHA projections / MLP head) on the MFMA GEMM core.
+//   forward : Y = epi(X W^T + b)           X [M][K], W [N][K]
+//   dgrad   : dX = gate(dY W [+ addend])   dY [M][N]
+//   wgrad   : dW += dY^T X                 (fp32, split-K + atomics)
+//   bias    : db += colsum(dY)
+#include "gemm.hpp"
+#include "epilogues.hpp"
+#include "../../include/retr_hip.h"
+
+using namespace retr;
+
+namespace {
+
+template <typename T, typename TO>
+int linear_fwd_t(const void* x, long ldx, const void* w, long ldw, const float* bias, void* y,
+                 long ldy, int M, int N, int K, int relu, const float* res, long ldr, float p,
+                 unsigned long long seed, hipStream_t st) {
+  DenseK<T> la{(const T*)x, ldx, M, K};
+  DenseK<T> lb{(const T*)w, ldw, N, K};
+  DropoutParams dp{seed, 0u, 1.f};
+  if (p > 0.f) {
+    dp.thresh = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+    dp.scale = 1.f / (1.f - p);
+  }
+  EpiFwd<TO, float> ep{(TO*)y, ldy, bias, res, ldr, relu, dp, (long)N};
+  if (M >= 2048 && N >= 128)
+    return launch_gemm<T, 128, 128>(la, lb, ep, M, N, K, 1, st, "linear_fwd");
+  return launch_gemm<T, 64, 64>(la, lb, ep, M, N, K, 1, st, "linear_fwd");
+}
+
+template <typename T, typename TO, typename TA>
+int linear_dgrad_t(const void* dy, long lddy, const void* w, long ldw, void* dx, long lddx,
+                   int M, int N, int K, const void* addend, long lda, const void* gate, long ldg,
+                   hipStream_t st) {
+  // dX[m][k] = sum_n dY[m][n] W[n][k]:  A = dY (K-dim = N), B(k, n) = W[n][k] -> stored [n][k]
+  DenseK<T> la{(const T*)dy, lddy, M, N};
+  DenseT<T> lb{(const T*)w, ldw, K, N};
+  EpiDgrad<TO, TA, T> ep{(TO*)dx, lddx, (const TA*)addend, lda, (const T*)gate, ldg};
+  if (M >= 2048 && K >= 128)
+    return launch_gemm<T, 128, 128>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
+  return launch_gemm<T, 64, 64>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
+}
+
+template <typename T>
+int linear_wgrad_t(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw,
+                   int M, int N, int K, hipStream_t st) {
+  // dW[n][k] = sum_m dY[m][n] X[m][k]: A(n, m) = dY[m][n], B(k, m) = X[m][k]  (both [m][.])
+  DenseT<T> la{(const T*)dy, lddy, N, M};
+  DenseT<T> lb{(const T*)x, ldx, K, M};
+  constexpr int BK = Elem<T>::BK;
+  if (N >= 512 && K >= 128) {
+    int s = pick_splits(N, K, M, 128, 128, BK);
+    EpiAccF32 ep{dw, lddw, s > 1};
+    return launch_gemm<T, 128, 128>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
+  }
+  int s = pick_splits(N, K, M, 64, 64, BK);
+  EpiAccF32 ep{dw, lddw, s > 1};
+  return launch_gemm<T, 64, 64>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
+}
+
+// db[n] += sum_m dY[m][n]; one thread per column-pair, blocks stride over rows.
+template <typename T>
+__global__ void colsum_kernel(const T* dy, long ld, int M, int N, float* db, int rows_per_blk) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  int r0 = blockIdx.y * rows_per_blk, r1 = min(M, r0 + rows_per_blk);
+  float s = 0.f;
+  for (int m = r0; m < r1; ++m) s += to_f(dy[(long)m * ld + n]);
+  atomicAdd(db + n, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int retr_linear_fwd(int dtype, const void* x, long ldx, const void* w, long ldw,
+                    const float* bias, void* y, long ldy, int y_f32, int M, int N, int K, int relu,
+                    const float* residual, long ldr, float drop_p, unsigned long long seed,
+                    void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RETR_REQUIRE(M >= 0 && N > 0 && K > 0, "linear_fwd: bad shape M=%d N=%d K=%d", M, N, K);
+  if (M == 0) return 0;
+  if (dtype == RETR_BF16) {
+    RETR_REQUIRE(K % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0, "linear_fwd: K/ld must be %%8");
+    return y_f32 ? linear_fwd_t<bf16, float>(x, ldx, w, ldw, bias, y, ldy, M, N, K, relu, residual, ldr, drop_p, seed, st)
+                 : linear_fwd_t<bf16, bf16>(x, ldx, w, ldw, bias, y, ldy, M, N, K, relu, residual, ldr, drop_p, seed, st);
+  }
+  RETR_REQUIRE(K % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0, "linear_fwd: K/ld must be %%4");
+  return linear_fwd_t<float, float>(x, ldx, w, ldw, bias, y, ldy, M, N, K, relu, residual, ldr,
+                                    drop_p, seed, st);
+}
+
+int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long ldw, void* dx,
+                      long lddx, int dx_f32, int M, int N, int K, const void* addend,
+                      int addend_f32, long lda, const void* gate, long ldg, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (M == 0) return 0;
+  if (dtype == RETR_BF16) {
+    RETR_REQUIRE(N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0 && ldw % 8 == 0,
+                 "linear_dgrad: N/K/ld must be %%8");
+    if (dx_f32) {
+      return addend_f32 ? linear_dgrad_t<bf16, float, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, st)
+                        : linear_dgrad_t<bf16, float, bf16>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, st);
+    }
+    return addend_f32 ? linear_dgrad_t<bf16, bf16, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, st)
+                      : linear_dgrad_t<bf16, bf16, bf16>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, st);
+  }
+  RETR_REQUIRE(N % 4 == 0 && K % 4 == 0 && lddy % 4 == 0 && ldw % 4 == 0,
+               "linear_dgrad: N/K/ld must be %%4");
+  return linear_dgrad_t<float, float, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda,
+                                             gate, ldg, st);
+}
+
+int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long ldx, float* dw,
+                      long lddw, int M, int N, int K, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (M == 0) return 0;
+  if (dtype == RETR_BF16) {
+    RETR_REQUIRE(N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0,
+                 "linear_wgrad: N/K/ld must be %%8");
+    return linear_wgrad_t<bf16>(dy, lddy, x, ldx, dw, lddw, M, N, K, st);
+  }
+  RETR_REQUIRE(N % 4 == 0 && K % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0,
+               "linear_wgrad: N/K/ld must be %%4");
+  return linear_wgrad_t<float>(dy, lddy, x, ldx, dw, lddw, M, N, K, st);
+}
+
+int retr_bias_grad(int dtype, const void* dy, long lddy, int M, int N, float* db, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (M == 0) return 0;
+  int rows = 64;
+  dim3 grid(cdiv(N, 256), cdiv(M, rows));
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)dy, lddy, M, N, db, rows);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, (const float*)dy, lddy, M, N, db, rows);
+  return retr_check_launch("bias_grad");
+}
+
+}  // extern "C"

@@ -1,0 +1,190 @@
+// CrossEntropyLoss over the vocabulary head (models/caption.py:210 as called at engine.py:71:
+// mean over B*T rows, no ignore_index) and the greedy argmax (eval_utils/decode.py:71).
+// One 256-thread block per logit row; row statistics by online max/sum + wave shuffles.
+#include "common.hpp"
+#include "../../include/retr_hip.h"
+
+namespace {
+
+RETR_DEVICE void online_merge(float& m, float& s, float m2, float s2) {
+  float mn = fmaxf(m, m2);
+  if (mn == -INFINITY) return;
+  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+  m = mn;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+ce_fwd_kernel(const T* x, long ld, int V, const long long* tgt, float* lse, float* loss_rows) {
+  __shared__ float sm[4], ss[4];
+  const int row = blockIdx.x;
+  const T* xr = x + (long)row * ld;
+  float m = -INFINITY, s = 0.f;
+  for (int j = threadIdx.x; j < V; j += 256) {
+    float v = to_f(xr[j]);
+    if (v > m) {
+      s = s * __expf(m - v) + 1.f;
+      m = v;
+    } else {
+      s += __expf(v - m);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    online_merge(m, s, m2, s2);
+  }
+  int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sm[w] = m, ss[w] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = sm[0], S = ss[0];
+    for (int i = 1; i < 4; ++i) online_merge(M, S, sm[i], ss[i]);
+    float l = M + logf(S);
+    lse[row] = l;
+    loss_rows[row] = l - to_f(xr[tgt[row]]);
+  }
+}
+
+// deterministic mean of per-row losses (single block)
+__global__ void mean_kernel(const float* v, int n, float* out) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += v[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0] / n;
+}
+
+template <typename T, typename TD>
+__global__ void __launch_bounds__(256)
+ce_bwd_kernel(const T* x, long ld, int V, const long long* tgt, const float* lse,
+              const float* dloss, float inv_count, TD* dx, long lddx) {
+  const int row = blockIdx.x;
+  const T* xr = x + (long)row * ld;
+  TD* dr = dx + (long)row * lddx;
+  const float l = lse[row], g = dloss[0] * inv_count;
+  const long long t = tgt[row];
+  for (int j = threadIdx.x; j < lddx; j += 256) {
+    float d = 0.f;
+    if (j < V) d = (__expf(to_f(xr[j]) - l) - (j == t ? 1.f : 0.f)) * g;
+    dr[j] = from_f<TD>(d);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+argmax_kernel(const T* x, long ld, int V, long long* out) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int row = blockIdx.x;
+  const T* xr = x + (long)row * ld;
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int j = threadIdx.x; j < V; j += 256) {
+    float v = to_f(xr[j]);
+    if (v > bv || (v == bv && j < bi) || (v != v && bv == bv)) bv = v, bi = j;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    float v2 = __shfl_xor(bv, o, 64);
+    int i2 = __shfl_xor(bi, o, 64);
+    bool nan2 = v2 != v2, nan1 = bv != bv;
+    if ((nan2 && !nan1) || (nan2 == nan1 && (v2 > bv || (v2 == bv && i2 < bi)))) bv = v2, bi = i2;
+  }
+  int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sv[w] = bv, si[w] = bi;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 4; ++i) {
+      bool nan2 = sv[i] != sv[i], nan1 = bv != bv;
+      if ((nan2 && !nan1) || (nan2 == nan1 && (sv[i] > bv || (sv[i] == bv && si[i] < bi))))
+        bv = sv[i], bi = si[i];
+    }
+    out[row] = bi;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int retr_ce_fwd(int dtype, const void* logits, long ld, int M, int V, const long long* targets,
+                float* lse, float* loss_rows, float* loss, void* stream) {
+  if (M == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(ce_fwd_kernel<bf16>, dim3(M), dim3(256), 0, st, (const bf16*)logits, ld, V,
+                       targets, lse, loss_rows);
+  else
+    hipLaunchKernelGGL(ce_fwd_kernel<float>, dim3(M), dim3(256), 0, st, (const float*)logits, ld,
+                       V, targets, lse, loss_rows);
+  if (retr_check_launch("ce_fwd")) return 1;
+  if (loss) {
+    hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(256), 0, st, loss_rows, M, loss);
+    return retr_check_launch("ce_mean");
+  }
+  return 0;
+}
+
+int retr_ce_bwd(int dtype, const void* logits, long ld, int M, int V, const long long* targets,
+                const float* lse, const float* dloss, float inv_count, void* dlogits, long lddl,
+                void* stream) {
+  if (M == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL((ce_bwd_kernel<bf16, bf16>), dim3(M), dim3(256), 0, st, (const bf16*)logits,
+                       ld, V, targets, lse, dloss, inv_count, (bf16*)dlogits, lddl);
+  else
+    hipLaunchKernelGGL((ce_bwd_kernel<float, float>), dim3(M), dim3(256), 0, st,
+                       (const float*)logits, ld, V, targets, lse, dloss, inv_count,
+                       (float*)dlogits, lddl);
+  return retr_check_launch("ce_bwd");
+}
+
+int retr_argmax_rows(int dtype, const void* x, long ld, int M, int V, long long* out,
+                     void* stream) {
+  if (M == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(argmax_kernel<bf16>, dim3(M), dim3(256), 0, st, (const bf16*)x, ld, V, out);
+  else
+    hipLaunchKernelGGL(argmax_kernel<float>, dim3(M), dim3(256), 0, st, (const float*)x, ld, V, out);
+  return retr_check_launch("argmax_rows");
+}
+
+}  // extern "C"
+
+// Greedy bookkeeping of eval_utils/decode.py:72-79 for step i, on device (no host sync):
+//   finished |= pred == eos; if all finished -> done = i (the reference returns here, so column
+//   i+1 is never written); else caption[:, i+1] = pred.  tok <- pred feeds step i+1.
+__global__ void greedy_update_kernel(const long long* pred, int B, int T, int i, long long eos,
+                                     long long* caption, unsigned char* finished, int* done,
+                                     long long* tok) {
+  __shared__ int all_fin;
+  if (threadIdx.x == 0) all_fin = 1;
+  __syncthreads();
+  const int prev_done = *done;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    unsigned char f = finished[b] | (pred[b] == eos ? 1 : 0);
+    finished[b] = f;
+    if (!f) atomicAnd(&all_fin, 0);
+  }
+  __syncthreads();
+  const bool stop = prev_done >= 0 || all_fin;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    if (!stop) caption[(long)b * T + i + 1] = pred[b];
+    tok[b] = pred[b];
+  }
+  if (threadIdx.x == 0 && prev_done < 0 && all_fin) *done = i;
+}
+
+extern "C" int retr_greedy_update(const long long* pred, int B, int T, int i, long long eos,
+                                  long long* caption, unsigned char* finished, int* done,
+                                  long long* tok, void* stream) {
+  hipLaunchKernelGGL(greedy_update_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, pred, B, T,
+                     i, eos, caption, finished, done, tok);
+  return retr_check_launch("greedy_update");
+}

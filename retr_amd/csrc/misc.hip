@@ -1,0 +1,182 @@
+// Small streaming kernels around the hot path: image layout change, stem max-pool, mask
+// down-sampling, dropout backward, casts and position-embedding gradient reduction.
+#include "common.hpp"
+#include "../../include/retr_hip.h"
+
+namespace {
+
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(const float* x, T* y, int N, int C, int H, int W, int Cp) {
+  long total = (long)N * H * W * Cp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int c = i % Cp;
+    long pix = i / Cp;
+    int w = pix % W;
+    long t = pix / W;
+    int h = t % H;
+    int n = (int)(t / H);
+    float v = c < C ? x[(((long)n * C + c) * H + h) * W + w] : 0.f;
+    y[i] = from_f<T>(v);
+  }
+}
+
+// MaxPool2d(kernel 3, stride 2, padding 1) NHWC; padding acts as -inf.
+template <typename T>
+__global__ void maxpool_kernel(const T* x, T* y, int N, int H, int W, int C, int OH, int OW) {
+  long total = (long)N * OH * OW * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int c = i % C;
+    long pix = i / C;
+    int ow = pix % OW;
+    long t = pix / OW;
+    int oh = t % OH;
+    int n = (int)(t / OH);
+    float m = -INFINITY;
+    for (int kh = 0; kh < 3; ++kh) {
+      int ih = oh * 2 - 1 + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        int iw = ow * 2 - 1 + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        m = fmaxf(m, to_f(x[(((long)n * H + ih) * W + iw) * C + c]));
+      }
+    }
+    y[i] = from_f<T>(m);
+  }
+}
+
+// torch 'nearest' (legacy): src = min(floor(dst * (float)in/out), in-1)
+__global__ void mask_nearest_kernel(const unsigned char* m, unsigned char* out, int N, int H,
+                                    int W, int h, int w) {
+  long total = (long)N * h * w;
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int x = i % w;
+  long t = i / w;
+  int y = t % h;
+  int n = (int)(t / h);
+  float sh = (float)H / (float)h, sw = (float)W / (float)w;
+  int sy = min((int)floorf(y * sh), H - 1), sx = min((int)floorf(x * sw), W - 1);
+  out[i] = m[((long)n * H + sy) * W + sx] ? 1 : 0;
+}
+
+template <typename TO>
+__global__ void dropout_apply_kernel(const float* x, long ldx, TO* y, long ldy, int M, int N,
+                                     DropoutParams dp) {
+  long total = (long)M * N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    int n = i % N;
+    long m = i / N;
+    float v = x[m * ldx + n];
+    if (dp.thresh) v = retr_keep(dp.seed, (uint64_t)m * N + n, dp.thresh) ? v * dp.scale : 0.f;
+    y[m * ldy + n] = from_f<TO>(v);
+  }
+}
+
+template <typename T>
+__global__ void cast_kernel(const float* x, T* y, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x)
+    y[i] = from_f<T>(x[i]);
+}
+
+template <typename T>
+__global__ void pos_grad_kernel(const T* d, long ld, int M, int C, int period, float* dpos) {
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= (long)period * C) return;
+  int c = i % C, p = (int)(i / C);
+  float s = 0.f;
+  for (int m = p; m < M; m += period) s += to_f(d[(long)m * ld + c]);
+  dpos[(long)p * C + c] += s;
+}
+
+int grid_for(long total) {
+  long g = (total + 255) / 256;
+  return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
+}
+
+DropoutParams make_dp(float p, unsigned long long seed) {
+  DropoutParams dp{seed, 0u, 1.f};
+  if (p > 0.f) {
+    dp.thresh = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+    dp.scale = 1.f / (1.f - p);
+  }
+  return dp;
+}
+
+}  // namespace
+
+extern "C" {
+
+int retr_nchw_to_nhwc(int dtype, const float* x, void* y, int N, int C, int H, int W, int Cp,
+                      void* stream) {
+  long total = (long)N * H * W * Cp;
+  if (total == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, x, (bf16*)y, N, C, H, W, Cp);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x, (float*)y, N, C, H, W, Cp);
+  return retr_check_launch("nchw_to_nhwc");
+}
+
+int retr_maxpool3x3s2(int dtype, const void* x, void* y, int N, int H, int W, int C, int OH,
+                      int OW, void* stream) {
+  long total = (long)N * OH * OW * C;
+  if (total == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(maxpool_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, N, H, W, C, OH, OW);
+  else
+    hipLaunchKernelGGL(maxpool_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)x, (float*)y, N, H, W, C, OH, OW);
+  return retr_check_launch("maxpool3x3s2");
+}
+
+int retr_mask_nearest(const unsigned char* m, unsigned char* out, int N, int H, int W, int h,
+                      int w, void* stream) {
+  long total = (long)N * h * w;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(mask_nearest_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, m, out, N, H, W, h, w);
+  return retr_check_launch("mask_nearest");
+}
+
+int retr_dropout_apply(int dtype_out, const float* x, long ldx, void* y, long ldy, int M, int N,
+                       float drop_p, unsigned long long seed, void* stream) {
+  long total = (long)M * N;
+  if (total == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  DropoutParams dp = make_dp(drop_p, seed);
+  if (dtype_out == RETR_BF16)
+    hipLaunchKernelGGL(dropout_apply_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, x, ldx, (bf16*)y, ldy, M, N, dp);
+  else
+    hipLaunchKernelGGL(dropout_apply_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x, ldx, (float*)y, ldy, M, N, dp);
+  return retr_check_launch("dropout_apply");
+}
+
+int retr_cast(int dtype, const float* x, void* y, long n, void* stream) {
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(cast_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, x, (bf16*)y, n);
+  else
+    hipLaunchKernelGGL(cast_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, x, (float*)y, n);
+  return retr_check_launch("cast");
+}
+
+int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
+                  void* stream) {
+  long total = (long)period * C;
+  if (total == 0 || M == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(pos_grad_kernel<bf16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const bf16*)d, ld, M, C, period, dpos);
+  else
+    hipLaunchKernelGGL(pos_grad_kernel<float>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const float*)d, ld, M, C, period, dpos);
+  return retr_check_launch("pos_grad");
+}
+
+}  // extern "C"

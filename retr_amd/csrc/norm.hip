@@ -1,0 +1,292 @@
+// LayerNorm (+ fused position add) and DecoderEmbeddings (gather + LN + dropout), fwd/bwd.
+// One wave64 per row; lanes own C/64 columns; statistics by wave shuffles.
+#include "common.hpp"
+#include "../../include/retr_hip.h"
+
+namespace {
+
+template <typename T, int PER>
+__global__ void __launch_bounds__(256)
+ln_fwd_kernel(const float* x, long ldx, const float* gamma, const float* beta, float eps, int M,
+              int C, T* y, long ldy, T* y2, const float* pos, int period, float* mean_out,
+              float* rstd_out) {
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (long)row * ldx;
+  float v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    v[i] = xr[lane + 64 * i];
+    s += v[i];
+  }
+  float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    float d = v[i] - mean;
+    q += d * d;
+  }
+  float var = wave_sum(q) / C;
+  float rstd = 1.0f / sqrtf(var + eps);
+  const float* pr = pos ? pos + (long)(row % period) * C : nullptr;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    int c = lane + 64 * i;
+    float o = (v[i] - mean) * rstd * gamma[c] + beta[c];
+    if (y) y[(long)row * ldy + c] = from_f<T>(o);
+    if (y2) y2[(long)row * ldy + c] = from_f<T>(o + pr[c]);
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+// rows_per_block rows handled by 4 waves; per-column dgamma/dbeta partials reduced in LDS.
+template <typename T, int PER>
+__global__ void __launch_bounds__(256)
+ln_bwd_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, const float* gamma,
+              const float* mean, const float* rstd, int M, int C, float* dx, long lddx,
+              const float* addend, float* dgamma, float* dbeta, int rows_per_block) {
+  __shared__ float red[2][4][1024];
+  int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float pg[PER], pb[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) pg[i] = pb[i] = 0.f;
+  int r0 = blockIdx.x * rows_per_block;
+  int r1 = min(M, r0 + rows_per_block);
+  for (int row = r0 + wave; row < r1; row += 4) {
+    float mu = mean[row], rs = rstd[row];
+    float g[PER], xh[PER];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int c = lane + 64 * i;
+      float d = dy ? to_f(dy[(long)row * lddy + c]) : 0.f;
+      if (dy2) d += to_f(dy2[(long)row * lddy + c]);
+      xh[i] = (x[(long)row * ldx + c] - mu) * rs;
+      pg[i] += d * xh[i];
+      pb[i] += d;
+      g[i] = d * gamma[c];
+      s1 += g[i];
+      s2 += g[i] * xh[i];
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int c = lane + 64 * i;
+      float o = rs * (g[i] - s1 - xh[i] * s2);
+      if (addend) o += addend[(long)row * ldx + c];
+      dx[(long)row * lddx + c] = o;
+    }
+  }
+  if (!dgamma && !dbeta) return;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    red[0][wave][lane + 64 * i] = pg[i];
+    red[1][wave][lane + 64 * i] = pb[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    float b = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    if (dgamma) atomicAdd(dgamma + c, a);
+    if (dbeta) atomicAdd(dbeta + c, b);
+  }
+}
+
+template <int PER>
+__global__ void __launch_bounds__(256)
+embed_ln_fwd_kernel(const long long* tok, int M, int T, int C, const float* word,
+                    const float* posw, const float* gamma, const float* beta, float eps,
+                    DropoutParams dp, float* y, float* mean_out, float* rstd_out) {
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  long t = tok[row];
+  int p = row % T;
+  float v[PER], s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    int c = lane + 64 * i;
+    v[i] = word[t * C + c] + posw[(long)p * C + c];
+    s += v[i];
+  }
+  float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    float d = v[i] - mean;
+    q += d * d;
+  }
+  float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    int c = lane + 64 * i;
+    float o = (v[i] - mean) * rstd * gamma[c] + beta[c];
+    if (dp.thresh) o = retr_keep(dp.seed, (uint64_t)row * C + c, dp.thresh) ? o * dp.scale : 0.f;
+    y[(long)row * C + c] = o;
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+template <int PER>
+__global__ void __launch_bounds__(256)
+embed_ln_bwd_kernel(const long long* tok, int M, int T, int C, const float* word,
+                    const float* posw, const float* gamma, const float* mean, const float* rstd,
+                    const float* dy, DropoutParams dp, float* dword, float* dposw, float* dgamma,
+                    float* dbeta, int padding_idx, int rows_per_block) {
+  __shared__ float red[2][4][1024];
+  int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float pg[PER], pb[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) pg[i] = pb[i] = 0.f;
+  int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  for (int row = r0 + wave; row < r1; row += 4) {
+    long t = tok[row];
+    int p = row % T;
+    float mu = mean[row], rs = rstd[row];
+    float g[PER], xh[PER], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int c = lane + 64 * i;
+      float d = dy[(long)row * C + c];
+      if (dp.thresh) d = retr_keep(dp.seed, (uint64_t)row * C + c, dp.thresh) ? d * dp.scale : 0.f;
+      xh[i] = (word[t * C + c] + posw[(long)p * C + c] - mu) * rs;
+      pg[i] += d * xh[i];
+      pb[i] += d;
+      g[i] = d * gamma[c];
+      s1 += g[i];
+      s2 += g[i] * xh[i];
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int c = lane + 64 * i;
+      float o = rs * (g[i] - s1 - xh[i] * s2);
+      if (dword && t != padding_idx) atomicAdd(dword + t * C + c, o);
+      if (dposw) atomicAdd(dposw + (long)p * C + c, o);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    red[0][wave][lane + 64 * i] = pg[i];
+    red[1][wave][lane + 64 * i] = pb[i];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    float b = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    if (dgamma) atomicAdd(dgamma + c, a);
+    if (dbeta) atomicAdd(dbeta + c, b);
+  }
+}
+
+DropoutParams make_dp(float p, unsigned long long seed) {
+  DropoutParams dp{seed, 0u, 1.f};
+  if (p > 0.f) {
+    dp.thresh = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+    dp.scale = 1.f / (1.f - p);
+  }
+  return dp;
+}
+
+#define PER_SWITCH(C, MACRO)          \
+  switch ((C) / 64) {                 \
+    case 1: MACRO(1); break;          \
+    case 2: MACRO(2); break;          \
+    case 4: MACRO(4); break;          \
+    case 8: MACRO(8); break;          \
+    case 16: MACRO(16); break;        \
+    default: retr_set_error("C=%d unsupported (64,128,256,512,1024)", (int)(C)); return 1; \
+  }
+
+}  // namespace
+
+extern "C" {
+
+int retr_layernorm_fwd(int dtype, const float* x, long ldx, const float* gamma,
+                       const float* beta, float eps, int M, int C, void* y, long ldy, void* y2,
+                       const float* pos, int period, float* mean, float* rstd, void* stream) {
+  if (M == 0) return 0;
+  RETR_REQUIRE(C % 64 == 0, "layernorm: C=%d must be a multiple of 64", C);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(cdiv(M, 4));
+#define LNF(P)                                                                                   \
+  if (dtype == RETR_BF16)                                                                         \
+    hipLaunchKernelGGL((ln_fwd_kernel<bf16, P>), grid, dim3(256), 0, st, x, ldx, gamma, beta, eps, \
+                       M, C, (bf16*)y, ldy, (bf16*)y2, pos, period, mean, rstd);                   \
+  else                                                                                            \
+    hipLaunchKernelGGL((ln_fwd_kernel<float, P>), grid, dim3(256), 0, st, x, ldx, gamma, beta, eps,\
+                       M, C, (float*)y, ldy, (float*)y2, pos, period, mean, rstd);
+  PER_SWITCH(C, LNF)
+#undef LNF
+  return retr_check_launch("layernorm_fwd");
+}
+
+int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, const float* x,
+                       long ldx, const float* gamma, const float* mean, const float* rstd, int M,
+                       int C, float* dx, long lddx, const float* addend, float* dgamma,
+                       float* dbeta, void* stream) {
+  if (M == 0) return 0;
+  RETR_REQUIRE(C % 64 == 0, "layernorm: C=%d must be a multiple of 64", C);
+  RETR_REQUIRE(dy || dy2, "layernorm_bwd: no incoming gradient");
+  RETR_REQUIRE(mean && rstd && gamma && dx, "layernorm_bwd: missing saved statistics");
+  hipStream_t st = (hipStream_t)stream;
+  int rpb = 64;
+  dim3 grid(cdiv(M, rpb));
+#define LNB(P)                                                                                     \
+  if (dtype == RETR_BF16)                                                                          \
+    hipLaunchKernelGGL((ln_bwd_kernel<bf16, P>), grid, dim3(256), 0, st, (const bf16*)dy,          \
+                       (const bf16*)dy2, lddy, x, ldx, gamma, mean, rstd, M, C, dx, lddx, addend,  \
+                       dgamma, dbeta, rpb);                                                        \
+  else                                                                                             \
+    hipLaunchKernelGGL((ln_bwd_kernel<float, P>), grid, dim3(256), 0, st, (const float*)dy,        \
+                       (const float*)dy2, lddy, x, ldx, gamma, mean, rstd, M, C, dx, lddx, addend, \
+                       dgamma, dbeta, rpb);
+  PER_SWITCH(C, LNB)
+#undef LNB
+  return retr_check_launch("layernorm_bwd");
+}
+
+int retr_embed_ln_fwd(const long long* tokens, int B, int T, int C, const float* word,
+                      const float* posw, const float* gamma, const float* beta, float eps,
+                      float drop_p, unsigned long long seed, float* y, float* mean, float* rstd,
+                      void* stream) {
+  int M = B * T;
+  if (M == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  DropoutParams dp = make_dp(drop_p, seed);
+  dim3 grid(cdiv(M, 4));
+#define EF(P)                                                                                   \
+  hipLaunchKernelGGL((embed_ln_fwd_kernel<P>), grid, dim3(256), 0, st, tokens, M, T, C, word, posw, \
+                     gamma, beta, eps, dp, y, mean, rstd);
+  PER_SWITCH(C, EF)
+#undef EF
+  return retr_check_launch("embed_ln_fwd");
+}
+
+int retr_embed_ln_bwd(const long long* tokens, int B, int T, int C, const float* word,
+                      const float* posw, const float* gamma, const float* mean, const float* rstd,
+                      const float* dy, float drop_p, unsigned long long seed, float* dword,
+                      float* dposw, float* dgamma, float* dbeta, int padding_idx, void* stream) {
+  int M = B * T;
+  if (M == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  DropoutParams dp = make_dp(drop_p, seed);
+  int rpb = 32;
+  dim3 grid(cdiv(M, rpb));
+#define EB(P)                                                                                   \
+  hipLaunchKernelGGL((embed_ln_bwd_kernel<P>), grid, dim3(256), 0, st, tokens, M, T, C, word, posw, \
+                     gamma, mean, rstd, dy, dp, dword, dposw, dgamma, dbeta, padding_idx, rpb);
+  PER_SWITCH(C, EB)
+#undef EB
+  return retr_check_launch("embed_ln_bwd");
+}
+
+}  // extern "C"

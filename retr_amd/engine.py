@@ -1,0 +1,146 @@
+"""Train / eval entry points with the reference signatures (engine.py).
+
+``pack_encoder_inputs`` (:20-48), ``train_one_epoch`` (:52-87), ``evaluate`` (:89-114) and
+``eval_model`` (:125-187) keep their contracts so ``main.py`` / ``eval_model.py`` drop in.
+Differences (all on the MI355X path, none observable in results):
+  * ``nlgeval`` is imported lazily inside ``eval_model`` (the reference imports it at module
+    top, ``engine.py:14-17``, which makes the module unimportable without the submodule);
+  * under data parallelism (``retr_amd.ddp``) gradients are all-reduced before clipping.
+"""
+import math
+import sys
+from collections import defaultdict
+from os.path import abspath, dirname, join
+
+import torch
+import tqdm
+
+from .models.utils import NestedTensor
+from .eval_utils.decode import greedy_decoding
+
+
+def pack_encoder_inputs(encoder_input, global_features, location_features, device="cpu"):
+    if not global_features and not location_features:
+        t_img, t_mask = encoder_input
+        return (NestedTensor(t_img, t_mask).to(device),)
+    if global_features and not location_features:
+        t_img, t_mask, g_img, g_mask = encoder_input
+        return (NestedTensor(t_img, t_mask).to(device), NestedTensor(g_img, g_mask).to(device))
+    if not global_features and location_features:
+        t_img, t_mask, l_feats = encoder_input
+        return (NestedTensor(t_img, t_mask).to(device), l_feats.to(device))
+    t_img, t_mask, g_img, g_mask, l_feats = encoder_input
+    return (NestedTensor(t_img, t_mask).to(device), NestedTensor(g_img, g_mask).to(device),
+            l_feats.to(device))
+
+
+def train_step(model, criterion, samples, caps, cap_masks, optimizer, max_norm, grad_sync=None):
+    """One reference training step (engine.py:70-83) — returns the loss tensor (no host sync)."""
+    outputs = model(*samples, caps[:, :-1], cap_masks[:, :-1])
+    loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
+    optimizer.zero_grad()
+    loss.backward()
+    if grad_sync is not None:
+        grad_sync.synchronize()
+    if max_norm > 0:
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)
+    optimizer.step()
+    return loss
+
+
+def train_one_epoch(model, criterion, data_loader, optimizer, device, epoch, max_norm,
+                    grad_sync=None):
+    model.train()
+    criterion.train()
+    epoch_loss = 0.0
+    total = len(data_loader)
+    global_features = data_loader.dataset.return_global_context
+    location_features = data_loader.dataset.return_location_features
+    with tqdm.tqdm(total=total) as pbar:
+        for ann_ids, *encoder_input, caps, cap_masks in data_loader:
+            samples = pack_encoder_inputs(encoder_input, global_features, location_features,
+                                          device)
+            caps = caps.to(device)
+            cap_masks = cap_masks.to(device)
+            outputs = model(*samples, caps[:, :-1], cap_masks[:, :-1])
+            loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
+            loss_value = loss.item()
+            epoch_loss += loss_value
+            if not math.isfinite(loss_value):
+                print(f"Loss is {loss_value}, stopping training")
+                sys.exit(1)
+            optimizer.zero_grad()
+            loss.backward()
+            if grad_sync is not None:
+                grad_sync.synchronize()
+            if max_norm > 0:
+                torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)
+            optimizer.step()
+            pbar.update(1)
+    return epoch_loss / total
+
+
+@torch.no_grad()
+def evaluate(model, criterion, data_loader, device):
+    model.eval()
+    criterion.eval()
+    validation_loss = 0.0
+    total = len(data_loader)
+    global_features = data_loader.dataset.return_global_context
+    location_features = data_loader.dataset.return_location_features
+    with tqdm.tqdm(total=total) as pbar:
+        for ann_ids, *encoder_input, caps, cap_masks in data_loader:
+            samples = pack_encoder_inputs(encoder_input, global_features, location_features,
+                                          device)
+            caps = caps.to(device)
+            cap_masks = cap_masks.to(device)
+            outputs = model(*samples, caps[:, :-1], cap_masks[:, :-1])
+            loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
+            validation_loss += loss.item()
+            pbar.update(1)
+    return validation_loss / total
+
+
+def normalize_with_tokenizer(sent, tokenizer):
+    return tokenizer.decode(tokenizer.encode(sent), skip_special_tokens=True)
+
+
+def _nlgeval():
+    """Lazy import of the nlgeval submodule (reference engine.py:14-17)."""
+    try:
+        from nlgeval import NLGEval  # noqa
+    except ImportError:
+        sys.path.append(join(dirname(abspath(__file__)), "nlgeval"))
+        from nlgeval import NLGEval  # noqa
+    return NLGEval
+
+
+def eval_model(model, data_loader, tokenizer, config, metrics_to_omit=[], print_samples=False):
+    """Decode the loader with greedy decoding and score with nlgeval (engine.py:125-187)."""
+    model.eval()
+    NLGEval = _nlgeval()
+    nlgeval = NLGEval(no_skipthoughts=True, no_glove=True, metrics_to_omit=metrics_to_omit)
+    annotations = defaultdict(list)
+    for a in data_loader.dataset.annot:
+        annotations[a[0]].append(a[2])
+    hypotheses, ids_hypotheses, references = [], [], []
+    pad_id = tokenizer.convert_tokens_to_ids(tokenizer.pad_token)
+    bos_id = tokenizer.convert_tokens_to_ids(tokenizer.cls_token)
+    eos_id = tokenizer.convert_tokens_to_ids(tokenizer.sep_token)
+    global_features = data_loader.dataset.return_global_context
+    location_features = data_loader.dataset.return_location_features
+    for i, (ann_ids, *encoder_input, caps, cap_masks) in enumerate(tqdm.tqdm(data_loader)):
+        samples = pack_encoder_inputs(encoder_input, global_features, location_features)
+        hyps = greedy_decoding(samples, model, tokenizer, max_len=config.max_position_embeddings,
+                               clean=True, pad_token=pad_id, bos_token=bos_id,
+                               eos_token=eos_id, device="auto")
+        hypotheses += hyps
+        ids_hyps = [{"ann_id": i, "expression": h} for i, h in zip(ann_ids.tolist(), hyps)]
+        ids_hypotheses += ids_hyps
+        if print_samples:
+            print(*ids_hyps, sep="\n")
+        refs = [annotations[i.item()] for i in ann_ids]
+        references += [[normalize_with_tokenizer(r, tokenizer) for r in _refs] for _refs in refs]
+    transposed_references = list(map(list, zip(*references)))
+    metrics_dict = nlgeval.compute_metrics(ref_list=transposed_references, hyp_list=hypotheses)
+    return metrics_dict, ids_hypotheses

@@ -1,0 +1,656 @@
+"""Autograd operators of the RE⫶TR hot path, each a thin host wrapper over libretr_hip.so.
+
+Granularity follows the reference's residual sub-layers so the backward can fuse what the
+reference computes as separate PyTorch ops:
+
+* ``ln_pos``          LayerNorm (+ position add)         transformer_modules.py:31-34,58-62,89
+* ``self_attn_block`` in-proj -> attention -> out-proj -> dropout -> residual   (:22-46)
+* ``cross_attn_block``                                                           (:49-74)
+* ``ffn_block``       Linear -> ReLU -> Linear -> dropout -> residual            (:6-11,77-97)
+* ``embed_ln``        DecoderEmbeddings                                          (:100-129)
+* ``linear``          input_proj (1x1 conv) and plain linears
+* ``mlp_head``        MLP(C, 512, V, 3)                          models/caption.py:161-174
+* ``cross_entropy``   CrossEntropyLoss (mean, no ignore_index)  caption.py:210 / engine.py:71
+* ``backbone``        ResNet body (NHWC implicit-GEMM convs, FrozenBN folded) backbone.py:41-77
+
+Tensors of the residual stream are fp32; GEMM operands are the compute dtype (bf16 or fp32).
+All ops raise on non-HIP tensors (no CPU fallback).
+"""
+import weakref
+
+import torch
+
+from . import _lib
+from ._lib import BF16, F32, call, ptr
+
+# ---------------------------------------------------------------------------------------------
+# runtime helpers
+# ---------------------------------------------------------------------------------------------
+
+_seed_state = {"base": None, "ctr": 0}
+
+
+def next_seed():
+    """Per-op dropout seed: a pure function of torch's initial seed and a call counter."""
+    if _seed_state["base"] is None:
+        _seed_state["base"] = torch.initial_seed() & 0xFFFFFFFFFFFF
+    _seed_state["ctr"] += 1
+    return (_seed_state["base"] * 0x100000001B3 + _seed_state["ctr"] * 0x9E3779B1) & (2**63 - 1)
+
+
+def dcode(dtype):
+    if dtype == torch.bfloat16:
+        return BF16
+    if dtype == torch.float32:
+        return F32
+    raise TypeError(f"unsupported compute dtype {dtype}")
+
+
+def _st():
+    return _lib.stream()
+
+
+class _WeightCache:
+    """Compute-dtype copies of fp32 parameters, refreshed when the parameter changes
+    (``_version`` bump after an optimizer step).  Optional zero-padding of rows."""
+
+    ATTR = "_retr_compute_copies"
+
+    def get(self, p, dtype, rows=None):
+        rows = rows or p.shape[0]
+        if dtype == torch.float32 and rows == p.shape[0] and p.is_contiguous():
+            return p.detach()
+        key = (dtype, rows)
+        ent = getattr(p, self.ATTR, None)   # cache lives on the parameter object itself
+        ver = (p._version, p.data_ptr())
+        if ent is not None and key in ent and ent[key][0] == ver:
+            return ent[key][1]
+        src = p.detach().contiguous()
+        out = torch.zeros((rows,) + tuple(p.shape[1:]), dtype=dtype, device=p.device) \
+            if rows != p.shape[0] else torch.empty(p.shape, dtype=dtype, device=p.device)
+        call("retr_cast", dcode(dtype), ptr(src), ptr(out), src.numel(), _st())
+        if ent is None:
+            ent = {}
+            setattr(p, self.ATTR, ent)
+        ent[key] = (ver, out)
+        return out
+
+
+WEIGHTS = _WeightCache()
+
+
+def _pad_vec(v, n):
+    if v is None:
+        return None
+    if v.shape[0] == n:
+        return v.detach().contiguous()
+    out = torch.zeros(n, dtype=torch.float32, device=v.device)
+    out[: v.shape[0]] = v.detach()
+    return out
+
+
+def _drop_p(module_training, p):
+    return float(p) if module_training and p > 0 else 0.0
+
+
+# ---------------------------------------------------------------------------------------------
+# low-level launch wrappers (no autograd)
+# ---------------------------------------------------------------------------------------------
+
+def k_linear_fwd(x, w, bias, y, relu=0, res=None, drop_p=0.0, seed=0):
+    M, K = x.shape
+    N = w.shape[0]
+    call("retr_linear_fwd", dcode(x.dtype), ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(bias),
+         ptr(y), y.stride(0), int(y.dtype == torch.float32), M, N, K, relu, ptr(res),
+         res.stride(0) if res is not None else 0, drop_p, seed, _st())
+
+
+def k_linear_dgrad(dy, w, dx, addend=None, gate=None, N=None, K=None):
+    M = dy.shape[0]
+    N = N or w.shape[0]
+    K = K or w.shape[1]
+    call("retr_linear_dgrad", dcode(dy.dtype), ptr(dy), dy.stride(0), ptr(w), w.stride(0),
+         ptr(dx), dx.stride(0), int(dx.dtype == torch.float32), M, N, K, ptr(addend),
+         int(addend is not None and addend.dtype == torch.float32),
+         addend.stride(0) if addend is not None else 0, ptr(gate),
+         gate.stride(0) if gate is not None else 0, _st())
+
+
+def k_linear_wgrad(dy, x, dw, N=None):
+    M = dy.shape[0]
+    N = N or dw.shape[0]
+    K = x.shape[1]
+    call("retr_linear_wgrad", dcode(dy.dtype), ptr(dy), dy.stride(0), ptr(x), x.stride(0),
+         ptr(dw), dw.stride(0), M, N, K, _st())
+
+
+def k_bias_grad(dy, db, N=None):
+    call("retr_bias_grad", dcode(dy.dtype), ptr(dy), dy.stride(0), dy.shape[0], N or db.shape[0],
+         ptr(db), _st())
+
+
+def k_dropout_apply(x, y, drop_p, seed):
+    """y = x * keep * 1/(1-p)  (x fp32 [M,N]); plain cast when drop_p == 0."""
+    M, N = x.shape
+    call("retr_dropout_apply", dcode(y.dtype), ptr(x), x.stride(0), ptr(y), y.stride(0), M, N,
+         drop_p, seed, _st())
+
+
+def k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed, lse, probs=None):
+    call("retr_attention_fwd", dcode(q.dtype), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
+         v.stride(0), ptr(o), o.stride(0), B, H, Lq, Lk, hd, ptr(kpm), int(causal), drop_p, seed,
+         ptr(lse), ptr(probs), _st())
+
+
+def k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, causal, drop_p,
+                    seed):
+    ws = torch.empty(B * H * Lq, dtype=torch.float32, device=q.device)
+    call("retr_attention_bwd", dcode(q.dtype), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
+         v.stride(0), ptr(o), o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(dq), dq.stride(0),
+         ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), B, H, Lq, Lk, hd, ptr(kpm), int(causal),
+         drop_p, seed, ptr(ws), _st())
+
+
+def _rows(t):
+    return t.reshape(-1, t.shape[-1]) if t.dim() != 2 else t
+
+
+# ---------------------------------------------------------------------------------------------
+# LayerNorm (+ position add)
+# ---------------------------------------------------------------------------------------------
+
+class _LnPos(torch.autograd.Function):
+    """mode: 'plain' -> LN(x); 'pos' -> LN(x)+pos; 'both' -> (LN(x), LN(x)+pos)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, pos, period, eps, cdtype, mode):
+        _lib.require_device(x)
+        M, C = x.shape
+        dev = x.device
+        y = torch.empty(M, C, dtype=cdtype, device=dev) if mode in ("plain", "both") else None
+        y2 = torch.empty(M, C, dtype=cdtype, device=dev) if mode in ("pos", "both") else None
+        mean = torch.empty(M, dtype=torch.float32, device=dev)
+        rstd = torch.empty_like(mean)
+        posd = pos.detach().contiguous() if pos is not None else None
+        call("retr_layernorm_fwd", dcode(cdtype), ptr(x), x.stride(0), ptr(gamma), ptr(beta),
+             float(eps), M, C, ptr(y), C, ptr(y2), ptr(posd), int(period or 1), ptr(mean),
+             ptr(rstd), _st())
+        ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.period = period
+        ctx.mode = mode
+        ctx.pos_shape = tuple(pos.shape) if pos is not None else None
+        if mode == "both":
+            return y, y2
+        return y if mode == "plain" else y2
+
+    @staticmethod
+    def backward(ctx, *grads):
+        x, gamma, mean, rstd = ctx.saved_tensors
+        mode = ctx.mode
+        if mode == "both":
+            dy, dy2 = grads
+        elif mode == "plain":
+            dy, dy2 = grads[0], None
+        else:
+            dy, dy2 = None, grads[0]
+        M, C = x.shape
+        dx = torch.empty(M, C, dtype=torch.float32, device=x.device)
+        dgamma = torch.zeros(C, dtype=torch.float32, device=x.device)
+        dbeta = torch.zeros_like(dgamma)
+        if dy is not None:
+            dy = dy.contiguous()
+        if dy2 is not None:
+            dy2 = dy2.contiguous()
+            if dy is not None and dy.dtype != dy2.dtype:
+                dy2 = dy2.to(dy.dtype)
+        ref = dy if dy is not None else dy2
+        call("retr_layernorm_bwd", dcode(ref.dtype), ptr(dy), ptr(dy2), C, ptr(x), x.stride(0),
+             ptr(gamma), ptr(mean), ptr(rstd), M, C, ptr(dx), dx.stride(0), None, ptr(dgamma),
+             ptr(dbeta), _st())
+        dpos = None
+        if ctx.pos_shape is not None and ctx.needs_input_grad[3] and dy2 is not None:
+            dpos = torch.zeros(ctx.pos_shape, dtype=torch.float32, device=x.device)
+            call("retr_pos_grad", dcode(dy2.dtype), ptr(dy2), dy2.stride(0), M, C, ctx.period,
+                 ptr(dpos), _st())
+        return dx, dgamma, dbeta, dpos, None, None, None, None
+
+
+def ln_pos(x, norm, cdtype, pos=None, period=None, mode=None, eps=None):
+    """LayerNorm(x) in compute dtype; with ``pos`` also LayerNorm(x) + pos[row % period]."""
+    if mode is None:
+        mode = "plain" if pos is None else "both"
+    return _LnPos.apply(x, norm.weight, norm.bias, pos, period,
+                        norm.eps if eps is None else eps, cdtype, mode)
+
+
+# ---------------------------------------------------------------------------------------------
+# attention sub-layers
+# ---------------------------------------------------------------------------------------------
+
+class _SelfAttnBlock(torch.autograd.Function):
+    """x_new = res + drop(out_proj(MHA(q=k=npos, v=n)))  — SelfAttResidual."""
+
+    @staticmethod
+    def forward(ctx, npos, n, res, w_in, b_in, w_out, b_out, B, L, H, kpm, causal, drop_attn,
+                drop_res, cdtype, want_probs):
+        M, C = n.shape
+        hd = C // H
+        win = WEIGHTS.get(w_in, cdtype)
+        wout = WEIGHTS.get(w_out, cdtype)
+        dev = n.device
+        qk = torch.empty(M, 2 * C, dtype=cdtype, device=dev)
+        v = torch.empty(M, C, dtype=cdtype, device=dev)
+        k_linear_fwd(npos, win[: 2 * C], b_in[: 2 * C].detach(), qk)
+        k_linear_fwd(n, win[2 * C:], b_in[2 * C:].detach(), v)
+        o = torch.empty(M, C, dtype=cdtype, device=dev)
+        lse = torch.empty(B * H * L, dtype=torch.float32, device=dev)
+        s_att, s_res = next_seed(), next_seed()
+        probs = torch.empty(B, L, L, dtype=torch.float32, device=dev) if want_probs else None
+        k_attention_fwd(qk[:, :C], qk[:, C:], v, o, B, H, L, L, hd, kpm, causal, drop_attn,
+                        s_att, lse, probs)
+        out = torch.empty(M, C, dtype=torch.float32, device=dev)
+        k_linear_fwd(o, wout, b_out.detach(), out, res=res, drop_p=drop_res, seed=s_res)
+        ctx.save_for_backward(npos, n, qk, v, o, lse, kpm, w_in, w_out)
+        ctx.cfg = (B, L, H, causal, drop_attn, drop_res, s_att, s_res, cdtype)
+        if want_probs:
+            ctx.mark_non_differentiable(probs)
+            return out, probs
+        return out
+
+    @staticmethod
+    def backward(ctx, dout, dprobs=None):
+        npos, n, qk, v, o, lse, kpm, w_in, w_out = ctx.saved_tensors
+        B, L, H, causal, drop_attn, drop_res, s_att, s_res, cdtype = ctx.cfg
+        M, C = n.shape
+        hd = C // H
+        dev = n.device
+        dout = dout.contiguous()
+        win = WEIGHTS.get(w_in, cdtype)
+        wout = WEIGHTS.get(w_out, cdtype)
+        dbr = torch.empty(M, C, dtype=cdtype, device=dev)
+        k_dropout_apply(dout, dbr, drop_res, s_res)
+        dw_out = torch.zeros(C, C, dtype=torch.float32, device=dev)
+        db_out = torch.zeros(C, dtype=torch.float32, device=dev)
+        k_linear_wgrad(dbr, o, dw_out)
+        k_bias_grad(dbr, db_out)
+        do = torch.empty(M, C, dtype=cdtype, device=dev)
+        k_linear_dgrad(dbr, wout, do)
+        dqk = torch.empty(M, 2 * C, dtype=cdtype, device=dev)
+        dv = torch.empty(M, C, dtype=cdtype, device=dev)
+        k_attention_bwd(qk[:, :C], qk[:, C:], v, o, do, lse, dqk[:, :C], dqk[:, C:], dv, B, H,
+                        L, L, hd, kpm, causal, drop_attn, s_att)
+        dw_in = torch.zeros(3 * C, C, dtype=torch.float32, device=dev)
+        db_in = torch.zeros(3 * C, dtype=torch.float32, device=dev)
+        k_linear_wgrad(dqk, npos, dw_in[: 2 * C])
+        k_linear_wgrad(dv, n, dw_in[2 * C:])
+        k_bias_grad(dqk, db_in[: 2 * C])
+        k_bias_grad(dv, db_in[2 * C:])
+        dnpos = torch.empty(M, C, dtype=cdtype, device=dev)
+        dn = torch.empty(M, C, dtype=cdtype, device=dev)
+        k_linear_dgrad(dqk, win[: 2 * C], dnpos)
+        k_linear_dgrad(dv, win[2 * C:], dn)
+        return (dnpos, dn, dout, dw_in, db_in, dw_out, db_out) + (None,) * 9
+
+
+class _CrossAttnBlock(torch.autograd.Function):
+    """y_new = res + drop(out_proj(MHA(q=qpos, k=mem_pos, v=mem)))  — CrossAttResidual."""
+
+    @staticmethod
+    def forward(ctx, qpos, mem_pos, mem, res, w_in, b_in, w_out, b_out, B, Lq, Lk, H, kpm,
+                drop_attn, drop_res, cdtype, want_probs):
+        Mq, C = qpos.shape
+        Mk = mem.shape[0]
+        hd = C // H
+        win = WEIGHTS.get(w_in, cdtype)
+        wout = WEIGHTS.get(w_out, cdtype)
+        dev = qpos.device
+        q = torch.empty(Mq, C, dtype=cdtype, device=dev)
+        k = torch.empty(Mk, C, dtype=cdtype, device=dev)
+        v = torch.empty(Mk, C, dtype=cdtype, device=dev)
+        k_linear_fwd(qpos, win[:C], b_in[:C].detach(), q)
+        k_linear_fwd(mem_pos, win[C: 2 * C], b_in[C: 2 * C].detach(), k)
+        k_linear_fwd(mem, win[2 * C:], b_in[2 * C:].detach(), v)
+        o = torch.empty(Mq, C, dtype=cdtype, device=dev)
+        lse = torch.empty(B * H * Lq, dtype=torch.float32, device=dev)
+        s_att, s_res = next_seed(), next_seed()
+        probs = torch.empty(B, Lq, Lk, dtype=torch.float32, device=dev) if want_probs else None
+        k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, False, drop_attn, s_att, lse, probs)
+        out = torch.empty(Mq, C, dtype=torch.float32, device=dev)
+        k_linear_fwd(o, wout, b_out.detach(), out, res=res, drop_p=drop_res, seed=s_res)
+        ctx.save_for_backward(qpos, mem_pos, mem, q, k, v, o, lse, kpm, w_in, w_out)
+        ctx.cfg = (B, Lq, Lk, H, drop_attn, drop_res, s_att, s_res, cdtype)
+        if want_probs:
+            ctx.mark_non_differentiable(probs)
+            return out, probs
+        return out
+
+    @staticmethod
+    def backward(ctx, dout, dprobs=None):
+        qpos, mem_pos, mem, q, k, v, o, lse, kpm, w_in, w_out = ctx.saved_tensors
+        B, Lq, Lk, H, drop_attn, drop_res, s_att, s_res, cdtype = ctx.cfg
+        Mq, C = qpos.shape
+        Mk = mem.shape[0]
+        hd = C // H
+        dev = qpos.device
+        dout = dout.contiguous()
+        win = WEIGHTS.get(w_in, cdtype)
+        wout = WEIGHTS.get(w_out, cdtype)
+        dbr = torch.empty(Mq, C, dtype=cdtype, device=dev)
+        k_dropout_apply(dout, dbr, drop_res, s_res)
+        dw_out = torch.zeros(C, C, dtype=torch.float32, device=dev)
+        db_out = torch.zeros(C, dtype=torch.float32, device=dev)
+        k_linear_wgrad(dbr, o, dw_out)
+        k_bias_grad(dbr, db_out)
+        do = torch.empty(Mq, C, dtype=cdtype, device=dev)
+        k_linear_dgrad(dbr, wout, do)
+        dq = torch.empty(Mq, C, dtype=cdtype, device=dev)
+        dk = torch.empty(Mk, C, dtype=cdtype, device=dev)
+        dv = torch.empty(Mk, C, dtype=cdtype, device=dev)
+        k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, False, drop_attn,
+                        s_att)
+        dw_in = torch.zeros(3 * C, C, dtype=torch.float32, device=dev)
+        db_in = torch.zeros(3 * C, dtype=torch.float32, device=dev)
+        k_linear_wgrad(dq, qpos, dw_in[:C])
+        k_linear_wgrad(dk, mem_pos, dw_in[C: 2 * C])
+        k_linear_wgrad(dv, mem, dw_in[2 * C:])
+        k_bias_grad(dq, db_in[:C])
+        k_bias_grad(dk, db_in[C: 2 * C])
+        k_bias_grad(dv, db_in[2 * C:])
+        dqpos = torch.empty(Mq, C, dtype=cdtype, device=dev)
+        dmem_pos = torch.empty(Mk, C, dtype=cdtype, device=dev)
+        dmem = torch.empty(Mk, C, dtype=cdtype, device=dev)
+        k_linear_dgrad(dq, win[:C], dqpos)
+        k_linear_dgrad(dk, win[C: 2 * C], dmem_pos)
+        k_linear_dgrad(dv, win[2 * C:], dmem)
+        return (dqpos, dmem_pos, dmem, dout, dw_in, db_in, dw_out, db_out) + (None,) * 9
+
+
+class _FFNBlock(torch.autograd.Function):
+    """x_new = res + drop(W2 relu(W1 n + b1) + b2)  — FFResidual(feed_forward)."""
+
+    @staticmethod
+    def forward(ctx, n, res, w1, b1, w2, b2, drop_res, cdtype):
+        M, C = n.shape
+        F = w1.shape[0]
+        dev = n.device
+        w1c, w2c = WEIGHTS.get(w1, cdtype), WEIGHTS.get(w2, cdtype)
+        h = torch.empty(M, F, dtype=cdtype, device=dev)
+        k_linear_fwd(n, w1c, b1.detach(), h, relu=1)
+        out = torch.empty(M, C, dtype=torch.float32, device=dev)
+        seed = next_seed()
+        k_linear_fwd(h, w2c, b2.detach(), out, res=res, drop_p=drop_res, seed=seed)
+        ctx.save_for_backward(n, h, w1, w2)
+        ctx.cfg = (drop_res, seed, cdtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        n, h, w1, w2 = ctx.saved_tensors
+        drop_res, seed, cdtype = ctx.cfg
+        M, C = n.shape
+        F = h.shape[1]
+        dev = n.device
+        dout = dout.contiguous()
+        w1c, w2c = WEIGHTS.get(w1, cdtype), WEIGHTS.get(w2, cdtype)
+        dbr = torch.empty(M, C, dtype=cdtype, device=dev)
+        k_dropout_apply(dout, dbr, drop_res, seed)
+        dw2 = torch.zeros(C, F, dtype=torch.float32, device=dev)
+        db2 = torch.zeros(C, dtype=torch.float32, device=dev)
+        k_linear_wgrad(dbr, h, dw2)
+        k_bias_grad(dbr, db2)
+        dh = torch.empty(M, F, dtype=cdtype, device=dev)
+        k_linear_dgrad(dbr, w2c, dh, gate=h)
+        dw1 = torch.zeros(F, C, dtype=torch.float32, device=dev)
+        db1 = torch.zeros(F, dtype=torch.float32, device=dev)
+        k_linear_wgrad(dh, n, dw1)
+        k_bias_grad(dh, db1)
+        dn = torch.empty(M, C, dtype=cdtype, device=dev)
+        k_linear_dgrad(dh, w1c, dn)
+        return dn, dout, dw1, db1, dw2, db2, None, None
+
+
+def self_attn_block(res_mod, npos, n, res, B, L, kpm, causal, training, cdtype,
+                    want_probs=False):
+    """res_mod: SelfAttResidual container (.sublayer = nn.MultiheadAttention, .dropout)."""
+    sub = res_mod.sublayer
+    return _SelfAttnBlock.apply(npos, n, res, sub.in_proj_weight, sub.in_proj_bias,
+                                sub.out_proj.weight, sub.out_proj.bias, B, L, sub.num_heads, kpm,
+                                causal, _drop_p(training, sub.dropout),
+                                _drop_p(training, res_mod.dropout.p), cdtype, want_probs)
+
+
+def cross_attn_block(res_mod, qpos, mem_pos, mem, res, B, Lq, Lk, kpm, training, cdtype,
+                     want_probs=False):
+    """res_mod: CrossAttResidual container."""
+    sub = res_mod.sublayer
+    return _CrossAttnBlock.apply(qpos, mem_pos, mem, res, sub.in_proj_weight, sub.in_proj_bias,
+                                 sub.out_proj.weight, sub.out_proj.bias, B, Lq, Lk,
+                                 sub.num_heads, kpm, _drop_p(training, sub.dropout),
+                                 _drop_p(training, res_mod.dropout.p), cdtype, want_probs)
+
+
+def ffn_block(res_mod, n, res, training, cdtype):
+    """res_mod: FFResidual container (.sublayer = Sequential(Linear, ReLU, Linear))."""
+    seq = res_mod.sublayer
+    return _FFNBlock.apply(n, res, seq[0].weight, seq[0].bias, seq[2].weight, seq[2].bias,
+                           _drop_p(training, res_mod.dropout.p), cdtype)
+
+
+# ---------------------------------------------------------------------------------------------
+# decoder embeddings
+# ---------------------------------------------------------------------------------------------
+
+class _EmbedLN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, caps, word, posw, gamma, beta, eps, drop_p, padding_idx):
+        B, T = caps.shape
+        C = word.shape[1]
+        if T > posw.shape[0]:
+            raise RuntimeError(f"caption length {T} exceeds max_position_embeddings "
+                               f"{posw.shape[0]}")
+        dev = word.device
+        caps = caps.contiguous()
+        y = torch.empty(B * T, C, dtype=torch.float32, device=dev)
+        mean = torch.empty(B * T, dtype=torch.float32, device=dev)
+        rstd = torch.empty_like(mean)
+        seed = next_seed()
+        call("retr_embed_ln_fwd", ptr(caps), B, T, C, ptr(word), ptr(posw), ptr(gamma),
+             ptr(beta), float(eps), drop_p, seed, ptr(y), ptr(mean), ptr(rstd), _st())
+        ctx.save_for_backward(caps, word, posw, gamma, mean, rstd)
+        ctx.cfg = (eps, drop_p, seed, padding_idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        caps, word, posw, gamma, mean, rstd = ctx.saved_tensors
+        eps, drop_p, seed, padding_idx = ctx.cfg
+        B, T = caps.shape
+        C = word.shape[1]
+        dev = word.device
+        dy = dy.contiguous()
+        dword = torch.zeros_like(word, dtype=torch.float32)
+        dposw = torch.zeros_like(posw, dtype=torch.float32)
+        dgamma = torch.zeros(C, dtype=torch.float32, device=dev)
+        dbeta = torch.zeros_like(dgamma)
+        call("retr_embed_ln_bwd", ptr(caps), B, T, C, ptr(word), ptr(posw), ptr(gamma),
+             ptr(mean), ptr(rstd), ptr(dy), drop_p, seed, ptr(dword), ptr(dposw), ptr(dgamma),
+             ptr(dbeta), -1 if padding_idx is None else int(padding_idx), _st())
+        return None, dword, dposw, dgamma, dbeta, None, None, None
+
+
+def embed_ln(emb, caps, training):
+    """emb: DecoderEmbeddings parameter container."""
+    p = _drop_p(training, emb.dropout.p)
+    we = emb.word_embeddings
+    return _EmbedLN.apply(caps, we.weight, emb.position_embeddings.weight, emb.LayerNorm.weight,
+                          emb.LayerNorm.bias, emb.LayerNorm.eps, p, we.padding_idx)
+
+
+# ---------------------------------------------------------------------------------------------
+# plain linear (input_proj) and the MLP head
+# ---------------------------------------------------------------------------------------------
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, out_f32, dgate, cdtype):
+        M, K = x.shape
+        N = w.shape[0]
+        wc = WEIGHTS.get(w, cdtype).view(N, -1)
+        y = torch.empty(M, N, dtype=torch.float32 if out_f32 else cdtype, device=x.device)
+        k_linear_fwd(x, wc, b.detach() if b is not None else None, y)
+        ctx.save_for_backward(x, w, dgate)
+        ctx.cdtype = cdtype
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, dgate = ctx.saved_tensors
+        cdtype = ctx.cdtype
+        M, K = x.shape
+        N = w.shape[0]
+        wshape = w.shape
+        dev = x.device
+        if dy.dtype != cdtype or not dy.is_contiguous():
+            dyc = torch.empty(M, N, dtype=cdtype, device=dev)
+            k_dropout_apply(dy.float().contiguous(), dyc, 0.0, 0)
+            dy = dyc
+        dw = torch.zeros(N, K, dtype=torch.float32, device=dev)
+        k_linear_wgrad(dy, x, dw)
+        db = None
+        if ctx.has_b:
+            db = torch.zeros(N, dtype=torch.float32, device=dev)
+            k_bias_grad(dy, db)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, K, dtype=cdtype, device=dev)
+            k_linear_dgrad(dy, WEIGHTS.get(w, cdtype).view(N, -1), dx, gate=dgate)
+        return dx, dw.view(wshape), db, None, None, None
+
+
+def linear(x, w, b, cdtype, out_f32=False, dgate=None):
+    """y = x W^T + b.  ``dgate``: forward ReLU output feeding x; the data gradient is gated by
+    ``dgate > 0`` inside the dgrad epilogue (fuses the producer's ReLU backward)."""
+    return _Linear.apply(x, w, b, out_f32, dgate, cdtype)
+
+
+def _round_up(n, m):
+    return (n + m - 1) // m * m
+
+
+class _MLPHead(torch.autograd.Function):
+    """logits = L3(relu(L2(relu(L1 hs))))  with the vocabulary dim padded to a multiple of 64
+    in memory; returns the [B, T, V] view."""
+
+    @staticmethod
+    def forward(ctx, hs, w1, b1, w2, b2, w3, b3, B, T, cdtype):
+        M, C = hs.shape
+        V = w3.shape[0]
+        Vp = _round_up(V, 64)
+        dev = hs.device
+        w1c, w2c = WEIGHTS.get(w1, cdtype), WEIGHTS.get(w2, cdtype)
+        w3c = WEIGHTS.get(w3, cdtype, rows=Vp)
+        b3p = _pad_vec(b3, Vp)
+        h1 = torch.empty(M, w1.shape[0], dtype=cdtype, device=dev)
+        k_linear_fwd(hs, w1c, b1.detach(), h1, relu=1)
+        h2 = torch.empty(M, w2.shape[0], dtype=cdtype, device=dev)
+        k_linear_fwd(h1, w2c, b2.detach(), h2, relu=1)
+        logits = torch.empty(M, Vp, dtype=cdtype, device=dev)
+        k_linear_fwd(h2, w3c, b3p, logits)
+        ctx.save_for_backward(hs, h1, h2, w1, w2, w3)
+        ctx.cfg = (B, T, V, Vp, cdtype)
+        return logits[:, :V].view(B, T, V)
+
+    @staticmethod
+    def backward(ctx, dlog):
+        hs, h1, h2, w1, w2, w3 = ctx.saved_tensors
+        B, T, V, Vp, cdtype = ctx.cfg
+        M, C = hs.shape
+        dev = hs.device
+        # fast path: the gradient is a view of a padded [M, Vp] compute-dtype buffer (from
+        # cross_entropy); otherwise materialise one.
+        if (dlog.dtype == cdtype and dlog.stride(2) == 1 and dlog.stride(1) == Vp
+                and dlog.stride(0) == T * Vp):
+            dl = dlog.as_strided((M, Vp), (Vp, 1))
+        else:
+            dl = torch.zeros(M, Vp, dtype=cdtype, device=dev)
+            dl[:, :V] = dlog.reshape(M, V).to(cdtype)
+        w1c, w2c = WEIGHTS.get(w1, cdtype), WEIGHTS.get(w2, cdtype)
+        w3c = WEIGHTS.get(w3, cdtype, rows=Vp)
+        dw3 = torch.zeros(Vp, w3.shape[1], dtype=torch.float32, device=dev)
+        db3 = torch.zeros(Vp, dtype=torch.float32, device=dev)
+        k_linear_wgrad(dl, h2, dw3)
+        k_bias_grad(dl, db3)
+        dh2 = torch.empty_like(h2)
+        k_linear_dgrad(dl, w3c, dh2, gate=h2)
+        dw2 = torch.zeros(w2.shape, dtype=torch.float32, device=dev)
+        db2 = torch.zeros(w2.shape[0], dtype=torch.float32, device=dev)
+        k_linear_wgrad(dh2, h1, dw2)
+        k_bias_grad(dh2, db2)
+        dh1 = torch.empty_like(h1)
+        k_linear_dgrad(dh2, w2c, dh1, gate=h1)
+        dw1 = torch.zeros(w1.shape, dtype=torch.float32, device=dev)
+        db1 = torch.zeros(w1.shape[0], dtype=torch.float32, device=dev)
+        k_linear_wgrad(dh1, hs, dw1)
+        k_bias_grad(dh1, db1)
+        dhs = torch.empty_like(hs)
+        k_linear_dgrad(dh1, w1c, dhs)
+        return dhs, dw1, db1, dw2, db2, dw3[:V], db3[:V], None, None, None
+
+
+def mlp_head(mlp, hs, B, T, cdtype):
+    l1, l2, l3 = mlp.layers
+    return _MLPHead.apply(hs, l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias, B, T,
+                          cdtype)
+
+
+# ---------------------------------------------------------------------------------------------
+# cross entropy (engine.py:71: criterion(outputs.permute(0, 2, 1), caps[:, 1:]))
+# ---------------------------------------------------------------------------------------------
+
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, target):
+        # x: [B, V, T] (permuted view of [B, T, V] logits whose rows may be padded)
+        _lib.require_device(x, target)
+        B, V, T = x.shape
+        if x.stride(1) == 1 and x.stride(0) == T * x.stride(2):
+            base, ld = x, x.stride(2)
+        else:
+            base = x.permute(0, 2, 1).contiguous()
+            ld = V
+        M = B * T
+        dev = x.device
+        tgt = target.reshape(M).contiguous()
+        lse = torch.empty(M, dtype=torch.float32, device=dev)
+        rows = torch.empty(M, dtype=torch.float32, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        call("retr_ce_fwd", dcode(base.dtype), ptr(base), ld, M, V, ptr(tgt), ptr(lse), ptr(rows),
+             ptr(loss), _st())
+        ctx.save_for_backward(base, tgt, lse)
+        ctx.cfg = (B, V, T, ld)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        base, tgt, lse = ctx.saved_tensors
+        B, V, T, ld = ctx.cfg
+        M = B * T
+        Vp = _round_up(V, 64)
+        dl = torch.empty(M, Vp, dtype=base.dtype, device=base.device)
+        dloss = dloss.reshape(1).float().contiguous()
+        call("retr_ce_bwd", dcode(base.dtype), ptr(base), ld, M, V, ptr(tgt), ptr(lse),
+             ptr(dloss), 1.0 / M, ptr(dl), Vp, _st())
+        return dl[:, :V].view(B, T, V).permute(0, 2, 1), None
+
+
+def cross_entropy(x, target):
+    return _CrossEntropy.apply(x, target)
+
+
+def argmax_rows(x2d):
+    """First-index argmax over the last dim of a [M, V] (row-strided) tensor."""
+    M, V = x2d.shape
+    out = torch.empty(M, dtype=torch.long, device=x2d.device)
+    call("retr_argmax_rows", dcode(x2d.dtype), ptr(x2d), x2d.stride(0), M, V, ptr(out), _st())
+    return out

@@ -1,0 +1,239 @@
+"""ResNet body executor: NHWC implicit-GEMM convolutions with FrozenBatchNorm folded into the
+weights, fused bias/residual/ReLU epilogues, and a hand-scheduled backward.
+
+Replaces the torchvision conv stack that ``models/backbone.py:65,69`` runs through
+``IntermediateLayerGetter`` (return layer4 only), with FrozenBatchNorm2d
+(``models/backbone.py:41-51``: scale = w * rsqrt(rv + 1e-5), bias = b - rm * scale) folded:
+``conv(x, W) * scale + bias == conv(x, W * scale) + bias``.
+
+Backward (only blocks whose parameters require grad — the reference freezes stem + layer1,
+``models/backbone.py:58-60``):
+  G3 = dOut * (out > 0)                          (gate fused into the consumer's dgrad epilogue)
+  dW3 = wgrad(G3, h2) * s3 ;  G2 = dgrad(G3, W3eff) * (h2 > 0)
+  dW2 = wgrad(G2, h1) * s2 ;  G1 = dgrad(G2, W2eff) * (h1 > 0)
+  dW1 = wgrad(G1, x)  * s1 ;  dWds = wgrad(G3, x) * sds
+  G3_prev = (dgrad(G1, W1eff) + [G3 | dgrad(G3, Wdseff)]) * (x > 0)
+"""
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+from .ops import dcode, _st
+
+
+class ConvSpec:
+    __slots__ = ("conv", "bn", "k", "s", "p", "d", "cin", "cout", "cp")
+
+    def __init__(self, conv, bn, stride=1, padding=0, dilation=1):
+        self.conv, self.bn = conv, bn
+        self.k = conv.weight.shape[2]
+        self.s, self.p, self.d = stride, padding, dilation
+        self.cout, self.cin = conv.weight.shape[0], conv.weight.shape[1]
+        self.cp = max(8, (self.cin + 7) // 8 * 8)
+
+    def out_hw(self, h, w):
+        oh = (h + 2 * self.p - self.d * (self.k - 1) - 1) // self.s + 1
+        ow = (w + 2 * self.p - self.d * (self.k - 1) - 1) // self.s + 1
+        return oh, ow
+
+
+class BlockSpec:
+    __slots__ = ("kind", "convs", "ds", "name")
+
+    def __init__(self, name, kind, convs, ds):
+        self.name, self.kind, self.convs, self.ds = name, kind, convs, ds
+
+    def params(self):
+        ps = [c.conv.weight for c in self.convs]
+        if self.ds is not None:
+            ps.append(self.ds.conv.weight)
+        return ps
+
+    def trainable(self):
+        return any(p.requires_grad for p in self.params())
+
+
+def build_plan(body):
+    """body: the IntermediateLayerGetter-equivalent ModuleDict (conv1, bn1, layer1..layer4)."""
+    stem = ConvSpec(body.conv1, body.bn1, 2, 3, 1)
+    blocks = []
+    for li in range(1, 5):
+        layer = getattr(body, f"layer{li}")
+        for bi, blk in enumerate(layer):
+            ds = None
+            if blk.downsample is not None:
+                ds = ConvSpec(blk.downsample[0], blk.downsample[1], blk.downsample[0].stride[0])
+            if hasattr(blk, "conv3"):
+                c2 = blk.conv2
+                convs = [ConvSpec(blk.conv1, blk.bn1),
+                         ConvSpec(c2, blk.bn2, c2.stride[0], c2.padding[0], c2.dilation[0]),
+                         ConvSpec(blk.conv3, blk.bn3)]
+                kind = "bottleneck"
+            else:
+                c1 = blk.conv1
+                convs = [ConvSpec(c1, blk.bn1, c1.stride[0], c1.padding[0], c1.dilation[0]),
+                         ConvSpec(blk.conv2, blk.bn2, 1, 1, 1)]
+                kind = "basic"
+            blocks.append(BlockSpec(f"layer{li}.{bi}", kind, convs, ds))
+    return stem, blocks
+
+
+class _PackCache:
+    """Folded compute-dtype weights per conv, refreshed when the weight or a BN buffer changes."""
+
+    def __init__(self):
+        self._d = {}
+
+    def get(self, spec, dtype):
+        w = spec.conv.weight
+        bn = spec.bn
+        ver = (w._version, w.data_ptr(), dtype) + tuple(
+            (b._version, b.data_ptr()) for b in (bn.weight, bn.bias, bn.running_mean,
+                                                 bn.running_var))
+        ent = self._d.get(id(spec))
+        if ent is not None and ent[0] == ver:
+            return ent[1]
+        co, ci, k = spec.cout, spec.cin, spec.k
+        wp = torch.empty(co, k, k, spec.cp, dtype=dtype, device=w.device)
+        wt = torch.empty(spec.cp, k, k, co, dtype=dtype, device=w.device)
+        bias = torch.empty(co, dtype=torch.float32, device=w.device)
+        scale = torch.empty(co, dtype=torch.float32, device=w.device)
+        wd = w.detach().contiguous()
+        call("retr_conv_pack", dcode(dtype), ptr(wd), ptr(bn.weight), ptr(bn.bias),
+             ptr(bn.running_mean), ptr(bn.running_var), None, co, ci, k, k, spec.cp, ptr(wp),
+             ptr(wt), ptr(bias), ptr(scale), _st())
+        out = (wp, wt, bias, scale)
+        self._d[id(spec)] = (ver, out)
+        return out
+
+
+PACKS = _PackCache()
+
+
+def _conv_fwd(spec, x, shape, relu, residual=None):
+    n, h, w, c = shape
+    oh, ow = spec.out_hw(h, w)
+    wp, _, bias, _ = PACKS.get(spec, x.dtype)
+    y = torch.empty(n, oh, ow, spec.cout, dtype=x.dtype, device=x.device)
+    call("retr_conv2d_fwd", dcode(x.dtype), ptr(x), n, h, w, c, ptr(wp), ptr(bias), ptr(residual),
+         ptr(y), spec.cout, spec.k, spec.k, spec.s, spec.p, spec.d, int(relu), _st())
+    return y, (n, oh, ow, spec.cout)
+
+
+def _conv_dgrad(spec, g, in_shape, addend=None, gate=None):
+    n, h, w, c = in_shape
+    _, wt, _, _ = PACKS.get(spec, g.dtype)
+    dx = torch.empty(n, h, w, c, dtype=g.dtype, device=g.device)
+    call("retr_conv2d_dgrad", dcode(g.dtype), ptr(g), n, h, w, c, ptr(wt), ptr(dx), spec.cout,
+         spec.k, spec.k, spec.s, spec.p, spec.d, ptr(addend), ptr(gate), _st())
+    return dx
+
+
+def _conv_wgrad(spec, g, x, in_shape):
+    n, h, w, c = in_shape
+    _, _, _, scale = PACKS.get(spec, g.dtype)
+    ws = torch.zeros(spec.cout, spec.k * spec.k * c, dtype=torch.float32, device=g.device)
+    call("retr_conv2d_wgrad", dcode(g.dtype), ptr(g), ptr(x), n, h, w, c, ptr(ws), spec.cout,
+         spec.k, spec.k, spec.s, spec.p, spec.d, _st())
+    grad = torch.empty(spec.conv.weight.shape, dtype=torch.float32, device=g.device)
+    call("retr_conv_wgrad_unpack", ptr(ws), ptr(scale), ptr(grad), spec.cout, spec.cin, c, spec.k,
+         spec.k, 0, _st())
+    return grad
+
+
+class _Backbone(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, images, runner, *weights):
+        stem, blocks, cdtype = runner.stem, runner.blocks, runner.cdtype
+        _lib.require_device(images)
+        N, C, H, W = images.shape
+        x = torch.empty(N, H, W, stem.cp, dtype=cdtype, device=images.device)
+        img = images.detach().float().contiguous()
+        call("retr_nchw_to_nhwc", dcode(cdtype), ptr(img), ptr(x), N, C, H, W, stem.cp, _st())
+        s, sh = _conv_fwd(stem, x, (N, H, W, stem.cp), relu=True)
+        ph, pw = (sh[1] + 2 - 3) // 2 + 1, (sh[2] + 2 - 3) // 2 + 1
+        x = torch.empty(N, ph, pw, sh[3], dtype=cdtype, device=images.device)
+        call("retr_maxpool3x3s2", dcode(cdtype), ptr(s), ptr(x), N, sh[1], sh[2], sh[3], ph, pw,
+             _st())
+        shape = (N, ph, pw, sh[3])
+        del s
+        saved = []
+        grad_on = runner.save
+        for blk in blocks:
+            inp, ishape = x, shape
+            if blk.kind == "bottleneck":
+                c1, c2, c3 = blk.convs
+                h1, s1 = _conv_fwd(c1, inp, ishape, True)
+                h2, s2 = _conv_fwd(c2, h1, s1, True)
+                idt = _conv_fwd(blk.ds, inp, ishape, False)[0] if blk.ds is not None else inp
+                out, oshape = _conv_fwd(c3, h2, s2, True, residual=idt)
+                acts = (inp, ishape, h1, s1, h2, s2)
+            else:
+                c1, c2 = blk.convs
+                h1, s1 = _conv_fwd(c1, inp, ishape, True)
+                idt = _conv_fwd(blk.ds, inp, ishape, False)[0] if blk.ds is not None else inp
+                out, oshape = _conv_fwd(c2, h1, s1, True, residual=idt)
+                acts = (inp, ishape, h1, s1, None, None)
+            if grad_on and blk.trainable():
+                saved.append((blk, acts))
+            x, shape = out, oshape
+        ctx.runner = runner
+        ctx.saved_acts = saved
+        ctx.n_weights = len(weights)
+        ctx.out_shape = shape
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        runner = ctx.runner
+        grads = {}
+        g = g.contiguous()
+        saved = ctx.saved_acts
+        for idx in range(len(saved) - 1, -1, -1):
+            blk, (inp, ishape, h1, s1, h2, s2) = saved[idx]
+            need_dx = idx > 0 and saved[idx - 1][0] is runner.blocks[runner.blocks.index(blk) - 1]
+            G3 = g
+            if blk.kind == "bottleneck":
+                c1, c2, c3 = blk.convs
+                grads[c3.conv.weight] = _conv_wgrad(c3, G3, h2, s2)
+                G2 = _conv_dgrad(c3, G3, s2, gate=h2)
+                grads[c2.conv.weight] = _conv_wgrad(c2, G2, h1, s1)
+                G1 = _conv_dgrad(c2, G2, s1, gate=h1)
+            else:
+                c1, c2 = blk.convs
+                grads[c2.conv.weight] = _conv_wgrad(c2, G3, h1, s1)
+                G1 = _conv_dgrad(c2, G3, s1, gate=h1)
+            grads[c1.conv.weight] = _conv_wgrad(c1, G1, inp, ishape)
+            if blk.ds is not None:
+                grads[blk.ds.conv.weight] = _conv_wgrad(blk.ds, G3, inp, ishape)
+            if need_dx:
+                if blk.ds is not None:
+                    tmp = _conv_dgrad(c1, G1, ishape)
+                    g = _conv_dgrad(blk.ds, G3, ishape, addend=tmp, gate=inp)
+                else:
+                    g = _conv_dgrad(c1, G1, ishape, addend=G3, gate=inp)
+            else:
+                g = None
+        out = [None, None]
+        for w in runner.weights:
+            gw = grads.get(w)
+            out.append(gw if (gw is not None and w.requires_grad) else None)
+        ctx.saved_acts = None
+        return tuple(out)
+
+
+class BackboneRunner:
+    """Holds the conv plan of a backbone body; call ``run(images)`` -> NHWC features."""
+
+    def __init__(self, body, cdtype):
+        self.stem, self.blocks = build_plan(body)
+        self.cdtype = cdtype
+        ws = [self.stem.conv.weight]
+        for b in self.blocks:
+            ws.extend(b.params())
+        self.weights = ws
+
+    def run(self, images):
+        # activations are only kept when autograd will call backward
+        self.save = torch.is_grad_enabled() and any(w.requires_grad for w in self.weights)
+        return _Backbone.apply(images, self, *self.weights)

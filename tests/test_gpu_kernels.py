@@ -1,0 +1,245 @@
+"""Per-kernel numerics of libretr_hip.so against plain PyTorch fp32 references (GPU box)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from retr_amd import ops, resnet
+from retr_amd._lib import call, ptr
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (200, 96, 136), (2048, 256, 256),
+                                   (4100, 520, 72), (37, 30522, 64)])
+def test_linear_fwd_dgrad_wgrad(dtype, tol, M, N, K):
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV)
+    w = torch.randn(N, K, generator=g).to(DEV) / math.sqrt(K)
+    b = torch.randn(N, generator=g).to(DEV)
+    res = torch.randn(M, N, generator=g).to(DEV)
+    xc, wc = x.to(dtype), w.to(dtype)
+    y = torch.empty(M, N, device=DEV)
+    ops.k_linear_fwd(xc, wc, b, y, relu=1, res=res)
+    ref = torch.relu(xc.float() @ wc.float().t() + b) + res
+    assert rel_err(y, ref) < tol
+    # dgrad with gate and addend
+    Np = (N + 7) // 8 * 8
+    dy = torch.zeros(M, Np, device=DEV)
+    dy[:, :N] = torch.randn(M, N, generator=g).to(DEV)
+    dyc = dy.to(dtype)
+    wpad = torch.zeros(Np, K, device=DEV, dtype=dtype)
+    wpad[:N] = wc
+    gate = torch.randn(M, K, generator=g).to(DEV).to(dtype)
+    add = torch.randn(M, K, generator=g).to(DEV)
+    dx = torch.empty(M, K, device=DEV)
+    ops.k_linear_dgrad(dyc, wpad, dx, addend=add, gate=gate)
+    ref = (dyc.float() @ wpad.float() + add) * (gate.float() > 0)
+    assert rel_err(dx, ref) < tol
+    dw = torch.zeros(Np, K, device=DEV)
+    ops.k_linear_wgrad(dyc, xc, dw)
+    ref = dyc.float().t() @ xc.float()
+    assert rel_err(dw, ref) < tol
+    db = torch.zeros(Np, device=DEV)
+    ops.k_bias_grad(dyc, db)
+    assert rel_err(db, dyc.float().sum(0)) < tol
+
+
+CONVS = [  # (N, Cin, H, Cout, k, stride, pad, dil)
+    (2, 64, 16, 64, 1, 1, 0, 1),
+    (2, 64, 15, 128, 1, 2, 0, 1),
+    (2, 64, 16, 64, 3, 1, 1, 1),
+    (2, 32, 17, 64, 3, 2, 1, 1),
+    (2, 64, 14, 64, 3, 1, 2, 2),
+    (2, 3, 32, 64, 7, 2, 3, 1),
+]
+
+
+def _pack(w, cdtype):
+    co, ci, k, _ = w.shape
+    cp = max(8, (ci + 7) // 8 * 8)
+    wp = torch.empty(co, k, k, cp, dtype=cdtype, device=DEV)
+    wt = torch.empty(cp, k, k, co, dtype=cdtype, device=DEV)
+    bias = torch.empty(co, device=DEV)
+    scale = torch.empty(co, device=DEV)
+    bw = torch.rand(co, device=DEV) + 0.5
+    bb = torch.randn(co, device=DEV) * 0.1
+    rm = torch.randn(co, device=DEV) * 0.1
+    rv = torch.rand(co, device=DEV) + 0.5
+    call("retr_conv_pack", ops.dcode(cdtype), ptr(w), ptr(bw), ptr(bb), ptr(rm), ptr(rv), None,
+         co, ci, k, k, cp, ptr(wp), ptr(wt), ptr(bias), ptr(scale), ops._st())
+    return wp, wt, bias, scale, cp, (bw, bb, rm, rv)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 5e-6), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("cfg", CONVS)
+def test_conv_fwd_dgrad_wgrad(dtype, tol, cfg):
+    N, Ci, H, Co, k, s, p, d = cfg
+    g = torch.Generator(device="cpu").manual_seed(sum(cfg))
+    x = torch.randn(N, Ci, H, H, generator=g)
+    w = torch.randn(Co, Ci, k, k, generator=g) / math.sqrt(Ci * k * k)
+    wd = w.to(DEV)
+    wp, wt, bias, scale, cp, (bw, bb, rm, rv) = _pack(wd, dtype)
+    # reference (CPU fp32) with the folded weights as the kernel sees them
+    weff = (wp.float()[..., :Ci].permute(0, 3, 1, 2)).cpu()
+    xr = x.to(dtype).float()
+    ref = F.conv2d(xr, weff, stride=s, padding=p, dilation=d) + bias.cpu().view(1, -1, 1, 1)
+    ref = torch.relu(ref)
+    xn = torch.zeros(N, H, H, cp, dtype=dtype, device=DEV)
+    xn[..., :Ci] = x.permute(0, 2, 3, 1).to(DEV).to(dtype)
+    OH = (H + 2 * p - d * (k - 1) - 1) // s + 1
+    y = torch.empty(N, OH, OH, Co, dtype=dtype, device=DEV)
+    call("retr_conv2d_fwd", ops.dcode(dtype), ptr(xn), N, H, H, cp, ptr(wp), ptr(bias), None,
+         ptr(y), Co, k, k, s, p, d, 1, ops._st())
+    assert rel_err(y.permute(0, 3, 1, 2), ref) < tol
+    # backward: dgrad and wgrad of the folded conv
+    gy = torch.randn(N, Co, OH, OH, generator=g)
+    gyc = gy.to(dtype).float()
+    xreq = xr.clone().requires_grad_(True)
+    wreq = weff.clone().requires_grad_(True)
+    F.conv2d(xreq, wreq, stride=s, padding=p, dilation=d).backward(gyc)
+    gn = gy.permute(0, 2, 3, 1).contiguous().to(DEV).to(dtype)
+    if Ci % 8 == 0:
+        dx = torch.empty(N, H, H, cp, dtype=dtype, device=DEV)
+        call("retr_conv2d_dgrad", ops.dcode(dtype), ptr(gn), N, H, H, cp, ptr(wt), ptr(dx), Co,
+             k, k, s, p, d, None, None, ops._st())
+        assert rel_err(dx.permute(0, 3, 1, 2), xreq.grad) < tol
+    ws = torch.zeros(Co, k * k * cp, device=DEV)
+    call("retr_conv2d_wgrad", ops.dcode(dtype), ptr(gn), ptr(xn), N, H, H, cp, ptr(ws), Co, k, k,
+         s, p, d, ops._st())
+    grad = torch.empty(Co, Ci, k, k, device=DEV)
+    call("retr_conv_wgrad_unpack", ptr(ws), None, ptr(grad), Co, Ci, cp, k, k, 0, ops._st())
+    assert rel_err(grad, wreq.grad) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("M,C", [(37, 64), (512, 256), (130, 512)])
+def test_layernorm(dtype, tol, M, C):
+    g = torch.Generator(device="cpu").manual_seed(M * C)
+    x = (torch.randn(M, C, generator=g) * 3 + 1).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV)
+    pos = torch.randn(16, C, generator=g).to(DEV)
+    norm = torch.nn.LayerNorm(C).to(DEV)
+    norm.weight.data.copy_(gamma)
+    norm.bias.data.copy_(beta)
+    xr = x.clone().requires_grad_(True)
+    posr = pos.clone().requires_grad_(True)
+    n, npos = ops.ln_pos(xr, norm, dtype, pos=posr, period=16)
+    xt = x.clone().requires_grad_(True)
+    pt = pos.clone().requires_grad_(True)
+    nt = F.layer_norm(xt, (C,), gamma, beta, 1e-5)
+    rows = torch.arange(M, device=DEV) % 16
+    npt = nt + pt[rows]
+    assert rel_err(n, nt) < tol and rel_err(npos, npt) < tol
+    g1 = torch.randn(M, C, generator=g).to(DEV)
+    g2 = torch.randn(M, C, generator=g).to(DEV)
+    (n.float() * g1 + npos.float() * g2).sum().backward()
+    (nt * g1 + npt * g2).sum().backward()
+    assert rel_err(xr.grad, xt.grad) < 5 * tol
+    assert rel_err(posr.grad, pt.grad) < 5 * tol
+    gt = gamma.clone().requires_grad_(True)
+    bt = beta.clone().requires_grad_(True)
+    nt2 = F.layer_norm(x, (C,), gt, bt, 1e-5)
+    (nt2 * g1 + (nt2 + pos[rows]) * g2).sum().backward()
+    assert rel_err(norm.weight.grad, gt.grad) < 5 * tol
+    assert rel_err(norm.bias.grad, bt.grad) < 5 * tol
+
+
+def _attn_ref(q, k, v, H, kpm, causal):
+    B, Lq, C = q.shape
+    Lk = k.shape[1]
+    hd = C // H
+    qh = q.view(B, Lq, H, hd).transpose(1, 2) * (1.0 / math.sqrt(hd))
+    kh = k.view(B, Lk, H, hd).transpose(1, 2)
+    vh = v.view(B, Lk, H, hd).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2)
+    if kpm is not None:
+        s = s.masked_fill(kpm.bool()[:, None, None, :], float("-inf"))
+    if causal:
+        cm = torch.ones(Lq, Lk, dtype=torch.bool, device=q.device).triu(1)
+        s = s.masked_fill(cm, float("-inf"))
+    p = s.softmax(-1)
+    return (p @ vh).transpose(1, 2).reshape(B, Lq, C), p.mean(1)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("B,H,Lq,Lk,hd,causal,masked", [
+    (2, 8, 16, 4, 8, False, True), (2, 8, 128, 128, 16, True, True),
+    (3, 8, 100, 77, 32, False, True), (2, 8, 128, 400, 32, False, False),
+    (2, 4, 70, 70, 64, False, True)])
+def test_attention(dtype, tol, B, H, Lq, Lk, hd, causal, masked):
+    g = torch.Generator(device="cpu").manual_seed(B * Lq + Lk + hd)
+    C = H * hd
+    q = torch.randn(B, Lq, C, generator=g).to(DEV).to(dtype)
+    k = torch.randn(B, Lk, C, generator=g).to(DEV).to(dtype)
+    v = torch.randn(B, Lk, C, generator=g).to(DEV).to(dtype)
+    kpm = None
+    if masked:
+        kpm = torch.zeros(B, Lk, dtype=torch.uint8)
+        kpm[:, Lk - Lk // 4:] = 1
+        kpm = kpm.to(DEV)
+    o = torch.empty(B * Lq, C, dtype=dtype, device=DEV)
+    lse = torch.empty(B * H * Lq, device=DEV)
+    probs = torch.empty(B, Lq, Lk, device=DEV)
+    ops.k_attention_fwd(q.view(-1, C), k.view(-1, C), v.view(-1, C), o, B, H, Lq, Lk, hd, kpm,
+                        causal, 0.0, 0, lse, probs)
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    ref, pref = _attn_ref(qr, kr, vr, H, kpm, causal)
+    assert rel_err(o.view(B, Lq, C), ref) < tol
+    assert rel_err(probs, pref) < tol
+    do = torch.randn(B, Lq, C, generator=g).to(DEV).to(dtype)
+    ref.backward(do.float())
+    dq = torch.empty_like(o)
+    dk = torch.empty(B * Lk, C, dtype=dtype, device=DEV)
+    dv = torch.empty_like(dk)
+    ops.k_attention_bwd(q.view(-1, C), k.view(-1, C), v.view(-1, C), o, do.view(-1, C), lse, dq,
+                        dk, dv, B, H, Lq, Lk, hd, kpm, causal, 0.0, 0)
+    assert rel_err(dq.view(B, Lq, C), qr.grad) < 3 * tol
+    assert rel_err(dk.view(B, Lk, C), kr.grad) < 3 * tol
+    assert rel_err(dv.view(B, Lk, C), vr.grad) < 3 * tol
+
+
+def test_attention_dropout_statistics():
+    B, H, L, hd = 2, 8, 128, 32
+    C = H * hd
+    q = torch.zeros(B * L, C, device=DEV)
+    k = torch.zeros(B * L, C, device=DEV)
+    v = torch.ones(B * L, C, device=DEV)
+    o = torch.empty(B * L, C, device=DEV)
+    lse = torch.empty(B * H * L, device=DEV)
+    ops.k_attention_fwd(q, k, v, o, B, H, L, L, hd, None, False, 0.1, 1234, lse)
+    # each output = mean over keys of keep/(1-p): expectation 1, row-wise mean ~1
+    assert abs(o.mean().item() - 1.0) < 0.02
+    o2 = torch.empty_like(o)
+    ops.k_attention_fwd(q, k, v, o2, B, H, L, L, hd, None, False, 0.1, 1234, lse)
+    assert torch.equal(o, o2)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+def test_cross_entropy_and_argmax(dtype, tol):
+    B, T, V = 3, 16, 30522
+    g = torch.Generator(device="cpu").manual_seed(7)
+    Vp = (V + 63) // 64 * 64
+    buf = torch.zeros(B * T, Vp, device=DEV, dtype=dtype)
+    buf[:, :V] = (torch.randn(B * T, V, generator=g) * 2).to(DEV).to(dtype)
+    logits = buf[:, :V].view(B, T, V).requires_grad_(False)
+    tgt = torch.randint(0, V, (B, T), generator=g).to(DEV)
+    x = logits.clone().float().requires_grad_(True)
+    lref = F.cross_entropy(x.permute(0, 2, 1), tgt)
+    lref.backward()
+    lt = logits.detach().requires_grad_(True)
+    loss = ops.cross_entropy(lt.permute(0, 2, 1), tgt)
+    assert abs(loss.item() - lref.item()) < tol * abs(lref.item())
+    loss.backward()
+    assert rel_err(lt.grad.float(), x.grad) < 5 * tol
+    am = ops.argmax_rows(buf[:, :V])
+    assert torch.equal(am, buf[:, :V].float().argmax(-1))
