@@ -81,11 +81,26 @@ def exported_symbols():
     return list(_SIGS)
 
 
-def call(name, *args):
+_probe = None
+
+
+def set_probe(p):
+    """Install (or remove with None) a retr_amd.probe.Probe that times selected calls."""
+    global _probe
+    _probe = p
+
+
+def _raw_call(name, args):
     rc = getattr(load(), name)(*args)
     if rc != 0:
         msg = load().retr_last_error()
         raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def call(name, *args):
+    if _probe is not None and name in _probe.names:
+        return _probe.wrap(name, args, lambda: _raw_call(name, args))
+    _raw_call(name, args)
 
 
 def ptr(t):

@@ -1,0 +1,94 @@
+"""In-process kernel timing with HIP events (used by bench.py for the roofline figure).
+
+When a ``Probe`` is installed, every C-ABI call whose name it tracks is bracketed by two
+``torch.cuda.Event``s recorded on torch's current stream — the stream every retr kernel is
+launched on — and its algorithmic FLOPs are computed from the call's shape arguments.
+"""
+import torch
+
+from . import _lib
+
+
+def _conv_out(h, k, s, p, d):
+    return (h + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+def _conv_variant(k, s, p):
+    return "1x1s1" if (k == 1 and s == 1 and p == 0) else f"{k}x{k}"
+
+
+def flops_of(name, a):
+    """(family key, algorithmic FLOPs) of one C-ABI call (2 FLOP per MAC)."""
+    if name == "retr_conv2d_fwd":
+        _, _, n, h, w, c, _, _, _, _, co, kh, kw, s, p, d = a[:16]
+        oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
+        return f"conv_fwd_{_conv_variant(kh, s, p)}", 2.0 * n * oh * ow * co * kh * kw * c
+    if name == "retr_conv2d_dgrad":
+        _, _, n, h, w, c, _, _, co, kh, kw, s, p, d = a[:14]
+        oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
+        return f"conv_dgrad_{_conv_variant(kh, s, p)}", 2.0 * n * oh * ow * co * kh * kw * c
+    if name == "retr_conv2d_wgrad":
+        _, _, _, n, h, w, c, _, co, kh, kw, s, p, d = a[:14]
+        oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
+        return f"conv_wgrad_{_conv_variant(kh, s, p)}", 2.0 * n * oh * ow * co * kh * kw * c
+    if name in ("retr_linear_fwd",):
+        m, n, k = a[9], a[10], a[11]
+        return "linear_fwd", 2.0 * m * n * k
+    if name == "retr_linear_dgrad":
+        m, n, k = a[8], a[9], a[10]
+        return "linear_dgrad", 2.0 * m * n * k
+    if name == "retr_linear_wgrad":
+        m, n, k = a[7], a[8], a[9]
+        return "linear_wgrad", 2.0 * m * n * k
+    if name == "retr_attention_fwd":
+        b, h, lq, lk, hd, causal = a[9], a[10], a[11], a[12], a[13], a[15]
+        return "attention_fwd", 4.0 * b * h * lq * lk * hd * (0.5 if causal else 1.0)
+    if name == "retr_attention_bwd":
+        b, h, lq, lk, hd, causal = a[18], a[19], a[20], a[21], a[22], a[24]
+        return "attention_bwd", 10.0 * b * h * lq * lk * hd * (0.5 if causal else 1.0)
+    return name, 0.0
+
+
+TRACKED = ("retr_conv2d_fwd", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
+           "retr_linear_dgrad", "retr_linear_wgrad", "retr_attention_fwd", "retr_attention_bwd")
+
+
+class Probe:
+    def __init__(self, names=TRACKED):
+        self.names = set(names)
+        self.records = []     # (key, flops, ev0, ev1)
+        self.active = False
+
+    def wrap(self, name, args, fn):
+        if not self.active:
+            return fn()
+        key, fl = flops_of(name, args)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        self.records.append((key, fl, e0, e1))
+
+    def summary(self):
+        """{key: {launches, ms_total, ms_avg, tflops}} (call after synchronising)."""
+        out = {}
+        for key, fl, e0, e1 in self.records:
+            ms = e0.elapsed_time(e1)
+            d = out.setdefault(key, {"launches": 0, "ms_total": 0.0, "flops": 0.0})
+            d["launches"] += 1
+            d["ms_total"] += ms
+            d["flops"] += fl
+        for d in out.values():
+            d["ms_avg"] = d["ms_total"] / max(1, d["launches"])
+            d["tflops"] = d["flops"] / (d["ms_total"] * 1e-3) / 1e12 if d["ms_total"] else 0.0
+        return out
+
+    def __enter__(self):
+        _lib.set_probe(self)
+        self.active = True
+        return self
+
+    def __exit__(self, *exc):
+        self.active = False
+        _lib.set_probe(None)
