@@ -34,10 +34,11 @@ int retr_linear_fwd(int dtype, const void* x, long ldx, const void* w, long ldw,
                     const float* bias, void* y, long ldy, int y_f32, int M, int N, int K, int relu,
                     const float* residual, long ldr, float drop_p, unsigned long long seed,
                     void* stream);
-/* dx = gate( dy W [+ addend] ), gate(v) = v * (gate_src > 0) */
+/* dx = gate( dy W [+ addend] ), gate(v) = v * (gate_src > 0); w_trans: w holds W^T [K][N] */
 int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long ldw, void* dx,
                       long lddx, int dx_f32, int M, int N, int K, const void* addend,
-                      int addend_f32, long lda, const void* gate, long ldg, void* stream);
+                      int addend_f32, long lda, const void* gate, long ldg, int w_trans,
+                      void* stream);
 /* dw[N][K] += dy^T x  (fp32) */
 int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long ldx, float* dw,
                       long lddw, int M, int N, int K, void* stream);
@@ -133,6 +134,9 @@ int retr_greedy_update(const long long* pred, int B, int T, int i, long long eos
 /* y[m][n] = x[m][n] * keep(seed, m*N+n) * scale   (backward of the branch dropout) */
 int retr_dropout_apply(int dtype_out, const float* x, long ldx, void* y, long ldy, int M, int N,
                        float drop_p, unsigned long long seed, void* stream);
+/* y[c][r] = x[r][c] (fp32 -> dtype), rows R..R_pad-1 of y's inner dim zero-filled */
+int retr_transpose_cast(int dtype, const float* x, void* y, int R, int C, int R_pad,
+                        void* stream);
 /* out (dtype) <- in (fp32), contiguous */
 int retr_cast(int dtype, const float* x, void* y, long n, void* stream);
 /* dpos[p][c] += sum_{m: m % period == p} d[m][c] */

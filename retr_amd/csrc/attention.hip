@@ -56,29 +56,39 @@ RETR_DEVICE float grp_sum(float v) {
   return v;
 }
 
-// Load `rows` x hd tile (row r at base + (r0+r)*ld) into LDS row-major [64][HDP+PAD] (zero
-// padded), optionally scaled.
+// Load a 64-row x hd tile (row r at base + (r0+r)*ld) into LDS row-major [64][HDP+PAD], zero
+// padded, optionally scaled; 16-byte global loads (hd and ld are multiples of EPC).
 template <typename T, int HDP>
 RETR_DEVICE void load_rows(T* dst, const T* base, long ld, int r0, int nrows, int hd,
                            float scale) {
-  constexpr int S = HDP + AT<T>::PAD;
-  for (int i = threadIdx.x; i < 64 * HDP; i += 256) {
-    int r = i / HDP, d = i - r * HDP;
-    float v = 0.f;
-    if (r0 + r < nrows && d < hd) v = to_f(base[(long)(r0 + r) * ld + d]) * scale;
-    dst[r * S + d] = from_f<T>(v);
+  constexpr int EPC = AT<T>::EPC, S = HDP + AT<T>::PAD, CPR = HDP / EPC;
+  for (int i = threadIdx.x; i < 64 * CPR; i += 256) {
+    const int r = i / CPR, c = (i % CPR) * EPC;
+    u32x4 v = zero16();
+    if (r0 + r < nrows && c < hd) {
+      v = *(const u32x4*)(base + (long)(r0 + r) * ld + c);
+      if (scale != 1.f) {
+        T* e = (T*)&v;
+#pragma unroll
+        for (int j = 0; j < EPC; ++j) e[j] = from_f<T>(to_f(e[j]) * scale);
+      }
+    }
+    *(u32x4*)(dst + r * S + c) = v;
   }
 }
 // Transposed: dst[d][r] (row stride 64+PAD)
 template <typename T, int HDP>
 RETR_DEVICE void load_rows_t(T* dst, const T* base, long ld, int r0, int nrows, int hd,
                              float scale) {
-  constexpr int S = 64 + AT<T>::PAD;
-  for (int i = threadIdx.x; i < 64 * HDP; i += 256) {
-    int r = i / HDP, d = i - r * HDP;
-    float v = 0.f;
-    if (r0 + r < nrows && d < hd) v = to_f(base[(long)(r0 + r) * ld + d]) * scale;
-    dst[d * S + r] = from_f<T>(v);
+  constexpr int EPC = AT<T>::EPC, S = 64 + AT<T>::PAD, CPR = HDP / EPC;
+  for (int i = threadIdx.x; i < 64 * CPR; i += 256) {
+    const int r = i % 64, c = (i / 64) * EPC;   // consecutive threads -> consecutive rows
+    u32x4 v = zero16();
+    if (r0 + r < nrows && c < hd) v = *(const u32x4*)(base + (long)(r0 + r) * ld + c);
+    const T* e = (const T*)&v;
+#pragma unroll
+    for (int j = 0; j < EPC; ++j)
+      dst[(c + j) * S + r] = scale != 1.f ? from_f<T>(to_f(e[j]) * scale) : e[j];
   }
 }
 
@@ -504,7 +514,8 @@ int retr_attention_fwd(int dtype, const void* q, long ldq, const void* k, long l
                        const void* v, long ldv, void* o, long ldo, int B, int H, int Lq, int Lk,
                        int hd, const unsigned char* kpm, int causal, float drop_p,
                        unsigned long long seed, float* lse, float* probs, void* stream) {
-  RETR_REQUIRE(hd >= 1 && hd <= 64, "attention: head dim %d unsupported (<=64)", hd);
+  RETR_REQUIRE(hd >= 8 && hd <= 64 && hd % 8 == 0, "attention: head dim %d unsupported", hd);
+  RETR_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0, "attention: row strides %%8");
   if (B == 0 || Lq == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == RETR_BF16) {
@@ -520,7 +531,7 @@ int retr_attention_fwd(int dtype, const void* q, long ldq, const void* k, long l
 int retr_attention_decode(int dtype, const void* q, long ldq, const void* k, long ldk,
                           const void* v, long ldv, void* o, long ldo, int B, int H, int Lk,
                           int Lmax, int hd, const unsigned char* kpm, void* stream) {
-  RETR_REQUIRE(hd >= 1 && hd <= 64, "attention: head dim %d unsupported (<=64)", hd);
+  RETR_REQUIRE(hd >= 8 && hd <= 64 && hd % 8 == 0, "attention: head dim %d unsupported", hd);
   RETR_REQUIRE(kpm == nullptr || Lmax == Lk, "attention_decode: kpm needs Lmax == Lk");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == RETR_BF16) {
@@ -539,7 +550,9 @@ int retr_attention_bwd(int dtype, const void* q, long ldq, const void* k, long l
                        void* dv, long lddv, int B, int H, int Lq, int Lk, int hd,
                        const unsigned char* kpm, int causal, float drop_p,
                        unsigned long long seed, float* workspace, void* stream) {
-  RETR_REQUIRE(hd >= 1 && hd <= 64, "attention: head dim %d unsupported (<=64)", hd);
+  RETR_REQUIRE(hd >= 8 && hd <= 64 && hd % 8 == 0, "attention: head dim %d unsupported", hd);
+  RETR_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && lddo % 8 == 0,
+               "attention: row strides %%8");
   if (B == 0 || Lq == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == RETR_BF16) {

@@ -18,6 +18,37 @@ struct Geom {
   int Nb, H, W, C, Co, KH, KW, s, p, d, OH, OW;
 };
 
+// k cursor over (kh, kw, channel) for a K dimension laid out as [KH][KW][Cc]: advancing by
+// the tile depth needs no division (Cc >= 8; at most a few wraps per step).
+struct TapCur {
+  int k, c, kw, khd, kwd;  // flat k, channel in tap, kw index, kh*dil, kw*dil
+};
+RETR_DEVICE TapCur tap_cur(int k, int Cc, int KW, int dil) {
+  TapCur t;
+  t.k = k;
+  int khw = k / Cc;
+  t.c = k - khw * Cc;
+  int kh = khw / KW;
+  t.kw = khw - kh * KW;
+  t.khd = kh * dil;
+  t.kwd = t.kw * dil;
+  return t;
+}
+RETR_DEVICE void tap_advance(TapCur& t, int d, int Cc, int KW, int dil) {
+  t.k += d;
+  t.c += d;
+  while (t.c >= Cc) {
+    t.c -= Cc;
+    if (++t.kw == KW) {
+      t.kw = 0;
+      t.kwd = 0;
+      t.khd += dil;
+    } else {
+      t.kwd += dil;
+    }
+  }
+}
+
 template <typename T>
 struct ConvFwdA {  // A(m = n,oh,ow ; k = kh,kw,ci)
   static constexpr bool kContig = true;
@@ -25,6 +56,7 @@ struct ConvFwdA {  // A(m = n,oh,ow ; k = kh,kw,ci)
   Geom g;
   int M, K;
   struct Ctx { const T* img; int ihb, iwb; bool ok; };
+  using KCur = TapCur;
   RETR_DEVICE Ctx row_ctx(int r) const {
     Ctx c;
     c.ok = r < M;
@@ -37,13 +69,13 @@ struct ConvFwdA {  // A(m = n,oh,ow ; k = kh,kw,ci)
     c.iwb = ow * g.s - g.p;
     return c;
   }
-  RETR_DEVICE u32x4 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero16();
-    int khw = k / g.C, ci = k - khw * g.C;
-    int kh = khw / g.KW, kw = khw - kh * g.KW;
-    int ih = c.ihb + kh * g.d, iw = c.iwb + kw * g.d;
+  RETR_DEVICE KCur kcur(int k) const { return tap_cur(k, g.C, g.KW, g.d); }
+  RETR_DEVICE void advance(KCur& t, int d) const { tap_advance(t, d, g.C, g.KW, g.d); }
+  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& t) const {
+    if (!c.ok || t.k >= K) return zero16();
+    int ih = c.ihb + t.khd, iw = c.iwb + t.kwd;
     if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return zero16();
-    return *(const u32x4*)(c.img + ((long)ih * g.W + iw) * g.C + ci);
+    return *(const u32x4*)(c.img + ((long)ih * g.W + iw) * g.C + t.c);
   }
 };
 
@@ -54,6 +86,7 @@ struct ConvDgradA {  // A(m = n,ih,iw ; k = kh,kw,co) = G[n, (ih+p-kh d)/s, (iw+
   Geom g;
   int M, K;
   struct Ctx { const T* img; int ihp, iwp; bool ok; };
+  using KCur = TapCur;
   RETR_DEVICE Ctx row_ctx(int r) const {
     Ctx c;
     c.ok = r < M;
@@ -66,15 +99,20 @@ struct ConvDgradA {  // A(m = n,ih,iw ; k = kh,kw,co) = G[n, (ih+p-kh d)/s, (iw+
     c.iwp = iw + g.p;
     return c;
   }
-  RETR_DEVICE u32x4 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero16();
-    int khw = k / g.Co, co = k - khw * g.Co;
-    int kh = khw / g.KW, kw = khw - kh * g.KW;
-    int th = c.ihp - kh * g.d, tw = c.iwp - kw * g.d;
+  RETR_DEVICE KCur kcur(int k) const { return tap_cur(k, g.Co, g.KW, g.d); }
+  RETR_DEVICE void advance(KCur& t, int d) const { tap_advance(t, d, g.Co, g.KW, g.d); }
+  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& t) const {
+    if (!c.ok || t.k >= K) return zero16();
+    int th = c.ihp - t.khd, tw = c.iwp - t.kwd;
     if (th < 0 || tw < 0) return zero16();
-    int oh = th / g.s, ow = tw / g.s;
-    if (oh * g.s != th || ow * g.s != tw || oh >= g.OH || ow >= g.OW) return zero16();
-    return *(const u32x4*)(c.img + ((long)oh * g.OW + ow) * g.Co + co);
+    int oh = th, ow = tw;
+    if (g.s != 1) {
+      oh = th / g.s;
+      ow = tw / g.s;
+      if (oh * g.s != th || ow * g.s != tw) return zero16();
+    }
+    if (oh >= g.OH || ow >= g.OW) return zero16();
+    return *(const u32x4*)(c.img + ((long)oh * g.OW + ow) * g.Co + t.c);
   }
 };
 
@@ -85,6 +123,7 @@ struct ConvWgradB {  // B(row = kh,kw,ci ; k = pixel n,oh,ow) = X[n, oh*s-p+kh d
   Geom g;
   int rows, M;
   struct Ctx { int khd, kwd, ci; bool ok; };
+  struct KCur { int m, n, oh, ow; };
   RETR_DEVICE Ctx row_ctx(int r) const {
     Ctx c;
     c.ok = r < rows;
@@ -96,14 +135,35 @@ struct ConvWgradB {  // B(row = kh,kw,ci ; k = pixel n,oh,ow) = X[n, oh*s-p+kh d
     c.kwd = kw * g.d - g.p;
     return c;
   }
-  RETR_DEVICE u32x4 load(const Ctx& c, int m) const {
-    if (!c.ok || m >= M) return zero16();
+  RETR_DEVICE KCur kcur(int m) const {
+    KCur k;
+    k.m = m;
     int hw = g.OH * g.OW;
-    int n = m / hw, rem = m - n * hw;
-    int oh = rem / g.OW, ow = rem - oh * g.OW;
-    int ih = oh * g.s + c.khd, iw = ow * g.s + c.kwd;
+    k.n = m / hw;
+    int rem = m - k.n * hw;
+    k.oh = rem / g.OW;
+    k.ow = rem - k.oh * g.OW;
+    return k;
+  }
+  RETR_DEVICE void advance(KCur& k, int d) const {
+    k.m += d;
+    k.ow += d;
+    if (k.ow >= g.OW) {
+      int q = k.ow / g.OW;
+      k.ow -= q * g.OW;
+      k.oh += q;
+      if (k.oh >= g.OH) {
+        int q2 = k.oh / g.OH;
+        k.oh -= q2 * g.OH;
+        k.n += q2;
+      }
+    }
+  }
+  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& k) const {
+    if (!c.ok || k.m >= M) return zero16();
+    int ih = k.oh * g.s + c.khd, iw = k.ow * g.s + c.kwd;
     if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return zero16();
-    return *(const u32x4*)(x + (((long)n * g.H + ih) * g.W + iw) * g.C + c.ci);
+    return *(const u32x4*)(x + (((long)k.n * g.H + ih) * g.W + iw) * g.C + c.ci);
   }
 };
 
@@ -120,6 +180,7 @@ int conv_fwd_t(const void* x, Geom g, const void* w, const float* bias, const vo
   int M = g.Nb * g.OH * g.OW, N = g.Co, K = g.KH * g.KW * g.C;
   DenseK<T> lb{(const T*)w, (long)K, N, K};
   EpiFwd<T, T> ep{(T*)y, (long)N, bias, (const T*)res, (long)N, relu ? 2 : 0, DropoutParams{0, 0, 1.f}, 0};
+  ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseK<T> la{(const T*)x, (long)g.C, M, K};
     return launch_auto<T>(la, lb, ep, M, N, K, 1, st, "conv_fwd_1x1");
@@ -134,6 +195,7 @@ int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* a
   int M = g.Nb * g.H * g.W, N = g.C, K = g.KH * g.KW * g.Co;
   DenseK<T> lb{(const T*)wt, (long)K, N, K};
   EpiDgrad<T, T, T> ep{(T*)dx, (long)N, (const T*)addend, (long)N, (const T*)gate, (long)N};
+  ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseK<T> la{(const T*)dy, (long)g.Co, M, K};
     return launch_auto<T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad_1x1");
@@ -151,6 +213,7 @@ int conv_wgrad_t(const void* dy, const void* x, Geom g, float* ws, hipStream_t s
   bool big = R >= 128 && Ncols >= 128;
   int s = big ? pick_splits(R, Ncols, Mp, 128, 128, BK) : pick_splits(R, Ncols, Mp, 64, 64, BK);
   EpiAccF32 ep{ws, (long)Ncols, s > 1};
+  ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseT<T> lb{(const T*)x, (long)g.C, Ncols, Mp};
     return big ? launch_gemm<T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad_1x1")

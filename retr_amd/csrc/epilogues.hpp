@@ -1,8 +1,41 @@
-// GEMM epilogues (per-element functors, fused into the MFMA GEMM store).
+// GEMM epilogues.  The GEMM core hands each thread 8 consecutive output columns of one row
+// (apply8, n % 8 == 0, n + 8 <= N) or single elements at a ragged right edge (apply).  All
+// vector accesses are 16-byte (bf16 x 8) or 2 x 16-byte (f32 x 8); an epilogue falls back to
+// scalar accesses when one of its row strides / base pointers is not 8-element aligned.
 #pragma once
 #include "common.hpp"
 
 namespace retr {
+
+template <typename T> RETR_DEVICE void load8(const T* p, float (&v)[8]);
+template <> RETR_DEVICE void load8<bf16>(const bf16* p, float (&v)[8]) {
+  bf16x8 x = *(const bf16x8*)p;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (float)x[e];
+}
+template <> RETR_DEVICE void load8<float>(const float* p, float (&v)[8]) {
+  f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+  v[0] = a[0], v[1] = a[1], v[2] = a[2], v[3] = a[3];
+  v[4] = b[0], v[5] = b[1], v[6] = b[2], v[7] = b[3];
+}
+template <typename T> RETR_DEVICE void store8(T* p, const float (&v)[8]);
+template <> RETR_DEVICE void store8<bf16>(bf16* p, const float (&v)[8]) {
+  bf16x8 x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = (bf16)v[e];
+  *(bf16x8*)p = x;
+}
+template <> RETR_DEVICE void store8<float>(float* p, const float (&v)[8]) {
+  *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+
+// host helper: can rows of `ld` elements starting at `p` be accessed 8-wide?
+template <typename T>
+inline bool vec8_ok(const void* p, long ld) {
+  return p == nullptr || (((uintptr_t)p % (8 * sizeof(T) < 16 ? 8 * sizeof(T) : 16)) == 0 &&
+                          ld % 8 == 0);
+}
 
 // out = relu2( [res +] drop( relu1( acc + bias ) ) )     (linear / conv forward)
 template <typename TO, typename TR>
@@ -15,6 +48,7 @@ struct EpiFwd {
   int relu;           // 0 none, 1 before the residual add (Linear->ReLU), 2 after it (ResNet block)
   DropoutParams dp;   // dropout applied to the branch before the residual add
   long drop_ld;       // logical row length used for the dropout counter
+  int vec;            // 8-wide accesses allowed (set by the host from alignment)
   RETR_DEVICE void apply(int m, int n, float v) const {
     if (bias) v += bias[n];
     if (relu == 1) v = fmaxf(v, 0.f);
@@ -23,7 +57,44 @@ struct EpiFwd {
     if (relu == 2) v = fmaxf(v, 0.f);
     out[(long)m * ldo + n] = from_f<TO>(v);
   }
+  RETR_DEVICE void apply8(int m, int n, float (&v)[8]) const {
+    if (!vec) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) apply(m, n + e, v[e]);
+      return;
+    }
+    if (bias) {
+      float b[8];
+      load8<float>(bias + n, b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += b[e];
+    }
+    if (relu == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (dp.thresh) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = retr_keep(dp.seed, (uint64_t)m * drop_ld + n + e, dp.thresh) ? v[e] * dp.scale : 0.f;
+    }
+    if (res) {
+      float r[8];
+      load8<TR>(res + (long)m * ldr + n, r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += r[e];
+    }
+    if (relu == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    store8<TO>(out + (long)m * ldo + n, v);
+  }
   RETR_DEVICE void empty_split(int, int) const {}
+  RETR_DEVICE bool lane_contiguous() const { return false; }
+  void set_vec() {
+    vec = vec8_ok<TO>(out, ldo) && vec8_ok<TR>(res, ldr) && vec8_ok<float>(bias, 8);
+  }
 };
 
 // out = ( acc [+ addend] ) * (gate > 0 ? 1 : 0)     (data-gradient GEMMs; gate = forward ReLU output)
@@ -35,12 +106,35 @@ struct EpiDgrad {
   long lda;
   const TG* gate;    // or null
   long ldg;
+  int vec;
   RETR_DEVICE void apply(int m, int n, float v) const {
     if (addend) v += to_f(addend[(long)m * lda + n]);
     if (gate && !(to_f(gate[(long)m * ldg + n]) > 0.f)) v = 0.f;
     out[(long)m * ldo + n] = from_f<TO>(v);
   }
+  RETR_DEVICE void apply8(int m, int n, float (&v)[8]) const {
+    if (!vec) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) apply(m, n + e, v[e]);
+      return;
+    }
+    if (addend) {
+      float a[8];
+      load8<TA>(addend + (long)m * lda + n, a);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += a[e];
+    }
+    if (gate) {
+      float g[8];
+      load8<TG>(gate + (long)m * ldg + n, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = g[e] > 0.f ? v[e] : 0.f;
+    }
+    store8<TO>(out + (long)m * ldo + n, v);
+  }
   RETR_DEVICE void empty_split(int, int) const {}
+  RETR_DEVICE bool lane_contiguous() const { return false; }
+  void set_vec() { vec = vec8_ok<TO>(out, ldo) && vec8_ok<TA>(addend, lda) && vec8_ok<TG>(gate, ldg); }
 };
 
 // fp32 accumulation target (weight gradients): atomic when the GEMM is split over K.
@@ -48,12 +142,28 @@ struct EpiAccF32 {
   float* out;
   long ldo;
   int atomic;
+  int vec;
   RETR_DEVICE void apply(int m, int n, float v) const {
     float* p = out + (long)m * ldo + n;
     if (atomic) atomicAdd(p, v);
     else *p += v;
   }
+  RETR_DEVICE void apply8(int m, int n, float (&v)[8]) const {
+    float* p = out + (long)m * ldo + n;
+    if (atomic || !vec) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) apply(m, n + e, v[e]);
+      return;
+    }
+    float o[8];
+    load8<float>(p, o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] += v[e];
+    store8<float>(p, o);
+  }
   RETR_DEVICE void empty_split(int, int) const {}
+  RETR_DEVICE bool lane_contiguous() const { return atomic != 0; }
+  void set_vec() { vec = vec8_ok<float>(out, ldo); }
 };
 
 }  // namespace retr

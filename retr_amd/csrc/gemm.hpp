@@ -56,24 +56,35 @@ struct Stager {
   static constexpr int BK = Elem<T>::BK;
   static constexpr int NCH = ROWS / 32;  // chunks per thread (ROWS*128B / 16B / 256 threads)
   static constexpr int RCH = ROWS / EPC; // row-chunks per k (row-contig orientation)
+  // Each thread owns fixed (row, k-offset) slots of the tile; the loader keeps a k cursor per
+  // slot that advances by BK per tile (no per-load index divisions in the implicit GEMMs).
   typename L::Ctx ctx[L::kContig ? NCH : 1];
+  typename L::KCur kc[L::kContig ? 1 : NCH];
   u32x4 reg[NCH];
 
-  RETR_DEVICE void init(const L& l, int row0, int tid) {
+  RETR_DEVICE void init(const L& l, int row0, int tid, int kb) {
     if constexpr (L::kContig) {
 #pragma unroll
       for (int i = 0; i < NCH; ++i) ctx[i] = l.row_ctx(row0 + (tid >> 3) + 32 * i);
+      kc[0] = l.kcur(kb + (tid & 7) * EPC);
     } else {
       ctx[0] = l.row_ctx(row0 + (tid % RCH) * EPC);
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) kc[i] = l.kcur(kb + tid / RCH + (256 / RCH) * i);
     }
   }
-  RETR_DEVICE void fetch(const L& l, int k0, int tid) {
+  // loads the tile at the cursors, then advances them to the next tile
+  RETR_DEVICE void fetch(const L& l) {
     if constexpr (L::kContig) {
 #pragma unroll
-      for (int i = 0; i < NCH; ++i) reg[i] = l.load(ctx[i], k0 + (tid & 7) * EPC);
+      for (int i = 0; i < NCH; ++i) reg[i] = l.load(ctx[i], kc[0]);
+      l.advance(kc[0], BK);
     } else {
 #pragma unroll
-      for (int i = 0; i < NCH; ++i) reg[i] = l.load(ctx[0], k0 + tid / RCH + (256 / RCH) * i);
+      for (int i = 0; i < NCH; ++i) {
+        reg[i] = l.load(ctx[0], kc[i]);
+        l.advance(kc[i], BK);
+      }
     }
   }
   RETR_DEVICE void store(char* lds, int tid) {
@@ -126,8 +137,8 @@ gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
 
   Stager<T, BM, LA> sa;
   Stager<T, BN, LB> sb;
-  sa.init(la, m0, tid);
-  sb.init(lb, n0, tid);
+  sa.init(la, m0, tid, kb);
+  sb.init(lb, n0, tid, kb);
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -135,8 +146,8 @@ gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  sa.fetch(la, kb, tid);
-  sb.fetch(lb, kb, tid);
+  sa.fetch(la);
+  sb.fetch(lb);
   sa.store(smem, tid);
   sb.store(smem + BM * kBKBytes, tid);
   __syncthreads();
@@ -145,8 +156,8 @@ gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
   for (int k0 = kb; k0 < ke; k0 += BK) {
     const bool more = k0 + BK < ke;
     if (more) {
-      sa.fetch(la, k0 + BK, tid);
-      sb.fetch(lb, k0 + BK, tid);
+      sa.fetch(la);
+      sb.fetch(lb);
     }
     const char* A = smem + cur * kBuf;
     const char* B = A + BM * kBKBytes;
@@ -173,21 +184,53 @@ gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
     cur ^= 1;
   }
 
+  // ---- epilogue through LDS: the accumulator tile (MFMA C layout: 4 rows x 1 column per lane)
+  // is re-laid as fp32 [BM][BN+4] so each thread owns 8 consecutive columns of a row and the
+  // epilogue issues 16-byte loads/stores (rows of 16 threads = 256 contiguous bf16 bytes).
+  constexpr int CS = BN + 4;
+  float* ct = (float*)smem;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * (BN / 2) + 16 * j + (lane & 15);
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = m0 + wm * (BM / 2) + 16 * i + 4 * (lane >> 4) + e;
-        if (m < M && n < N) ep.apply(m, n, acc[i][j][e]);
-      }
+      for (int e = 0; e < 4; ++e)
+        ct[(wm * (BM / 2) + 16 * i + 4 * (lane >> 4) + e) * CS + wn * (BN / 2) + 16 * j +
+           (lane & 15)] = acc[i][j][e];
+  __syncthreads();
+  if (ep.lane_contiguous()) {
+    // float atomics: one wave instruction = 64 consecutive columns of a row (256 contiguous
+    // bytes, the full-rate atomic shape; an 8-column-per-lane layout would be ~8x slower)
+    for (int q = tid; q < BM * BN; q += 256) {
+      const int r = q / BN, c = q % BN;
+      const int m = m0 + r, n = n0 + c;
+      if (m < M && n < N) ep.apply(m, n, ct[r * CS + c]);
     }
+    return;
+  }
+  constexpr int CH = BN / 8;
+#pragma unroll 2
+  for (int q = tid; q < BM * CH; q += 256) {
+    const int r = q / CH, c = (q % CH) * 8;
+    const int m = m0 + r, n = n0 + c;
+    if (m >= M || n >= N) continue;
+    const f32x4 lo = *(const f32x4*)(ct + r * CS + c);
+    const f32x4 hi = *(const f32x4*)(ct + r * CS + c + 4);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if (n + 8 <= N) {
+      ep.apply8(m, n, v);
+    } else {
+      for (int e = 0; e < 8 && n + e < N; ++e) ep.apply(m, n + e, v[e]);
+    }
+  }
 }
 
 template <typename T, int BM, int BN>
-constexpr size_t gemm_lds_bytes() { return 2 * (BM + BN) * kBKBytes; }
+constexpr size_t gemm_lds_bytes() {
+  constexpr size_t stage = 2 * (BM + BN) * kBKBytes;
+  constexpr size_t epi = (size_t)BM * (BN + 4) * 4;
+  return stage > epi ? stage : epi;
+}
 
 // Host-side launcher: picks split-K so that the grid has enough blocks to fill 256 CUs.
 template <typename T, int BM, int BN, class LA, class LB, class EP>
@@ -201,7 +244,15 @@ int launch_gemm(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, i
   int kchunk = cdiv(ksteps, splits) * BK;
   splits = cdiv(K, kchunk);
   dim3 grid(tm * tn, splits);
-  size_t lds = gemm_lds_bytes<T, BM, BN>();
+  constexpr size_t lds = gemm_lds_bytes<T, BM, BN>();
+  if constexpr (lds > 65536) {
+    static bool attr_set = false;   // once per instantiation (host attribute, capture-safe)
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)gemm_kernel<T, BM, BN, LA, LB, EP>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      attr_set = true;
+    }
+  }
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, LA, LB, EP>), grid, dim3(256), lds, st, la, lb, ep,
                      M, N, K, kchunk, tn);
   return retr_check_launch(what);
@@ -232,10 +283,13 @@ struct DenseK {
   long ld;
   int rows, K;
   struct Ctx { const T* row; bool ok; };
+  struct KCur { int k; };
   RETR_DEVICE Ctx row_ctx(int r) const { return Ctx{p + (long)r * ld, r < rows}; }
-  RETR_DEVICE u32x4 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero16();
-    return *(const u32x4*)(c.row + k);
+  RETR_DEVICE KCur kcur(int k) const { return KCur{k}; }
+  RETR_DEVICE void advance(KCur& c, int d) const { c.k += d; }
+  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& k) const {
+    if (!c.ok || k.k >= K) return zero16();
+    return *(const u32x4*)(c.row + k.k);
   }
 };
 
@@ -249,10 +303,13 @@ struct DenseT {
   long ld;
   int rows, K;
   struct Ctx { const T* col; bool ok; };
+  struct KCur { int k; long off; };
   RETR_DEVICE Ctx row_ctx(int r) const { return Ctx{p + r, r < rows}; }
-  RETR_DEVICE u32x4 load(const Ctx& c, int k) const {
-    if (!c.ok || k >= K) return zero16();
-    return *(const u32x4*)(c.col + (long)k * ld);
+  RETR_DEVICE KCur kcur(int k) const { return KCur{k, (long)k * ld}; }
+  RETR_DEVICE void advance(KCur& c, int d) const { c.k += d; c.off += (long)d * ld; }
+  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& k) const {
+    if (!c.ok || k.k >= K) return zero16();
+    return *(const u32x4*)(c.col + k.off);
   }
 };
 

@@ -23,6 +23,7 @@ int linear_fwd_t(const void* x, long ldx, const void* w, long ldw, const float* 
     dp.scale = 1.f / (1.f - p);
   }
   EpiFwd<TO, float> ep{(TO*)y, ldy, bias, res, ldr, relu, dp, (long)N};
+  ep.set_vec();
   if (M >= 2048 && N >= 128)
     return launch_gemm<T, 128, 128>(la, lb, ep, M, N, K, 1, st, "linear_fwd");
   return launch_gemm<T, 64, 64>(la, lb, ep, M, N, K, 1, st, "linear_fwd");
@@ -31,11 +32,19 @@ int linear_fwd_t(const void* x, long ldx, const void* w, long ldw, const float* 
 template <typename T, typename TO, typename TA>
 int linear_dgrad_t(const void* dy, long lddy, const void* w, long ldw, void* dx, long lddx,
                    int M, int N, int K, const void* addend, long lda, const void* gate, long ldg,
-                   hipStream_t st) {
-  // dX[m][k] = sum_n dY[m][n] W[n][k]:  A = dY (K-dim = N), B(k, n) = W[n][k] -> stored [n][k]
+                   int w_trans, hipStream_t st) {
+  // dX[m][k] = sum_n dY[m][n] W[n][k]:  A = dY (K-dim = N), B(k, n) = W[n][k].
+  // w_trans: the caller passes W^T stored [K][N] (K-contiguous B operand, no LDS transpose).
   DenseK<T> la{(const T*)dy, lddy, M, N};
-  DenseT<T> lb{(const T*)w, ldw, K, N};
   EpiDgrad<TO, TA, T> ep{(TO*)dx, lddx, (const TA*)addend, lda, (const T*)gate, ldg};
+  ep.set_vec();
+  if (w_trans) {
+    DenseK<T> lb{(const T*)w, ldw, K, N};
+    if (M >= 2048 && K >= 128)
+      return launch_gemm<T, 128, 128>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
+    return launch_gemm<T, 64, 64>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
+  }
+  DenseT<T> lb{(const T*)w, ldw, K, N};
   if (M >= 2048 && K >= 128)
     return launch_gemm<T, 128, 128>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
   return launch_gemm<T, 64, 64>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
@@ -51,10 +60,12 @@ int linear_wgrad_t(const void* dy, long lddy, const void* x, long ldx, float* dw
   if (N >= 512 && K >= 128) {
     int s = pick_splits(N, K, M, 128, 128, BK);
     EpiAccF32 ep{dw, lddw, s > 1};
+    ep.set_vec();
     return launch_gemm<T, 128, 128>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
   }
   int s = pick_splits(N, K, M, 64, 64, BK);
   EpiAccF32 ep{dw, lddw, s > 1};
+  ep.set_vec();
   return launch_gemm<T, 64, 64>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
 }
 
@@ -92,23 +103,24 @@ int retr_linear_fwd(int dtype, const void* x, long ldx, const void* w, long ldw,
 
 int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long ldw, void* dx,
                       long lddx, int dx_f32, int M, int N, int K, const void* addend,
-                      int addend_f32, long lda, const void* gate, long ldg, void* stream) {
+                      int addend_f32, long lda, const void* gate, long ldg, int w_trans,
+                      void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) return 0;
   if (dtype == RETR_BF16) {
     RETR_REQUIRE(N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0 && ldw % 8 == 0,
                  "linear_dgrad: N/K/ld must be %%8");
     if (dx_f32) {
-      return addend_f32 ? linear_dgrad_t<bf16, float, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, st)
-                        : linear_dgrad_t<bf16, float, bf16>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, st);
+      return addend_f32 ? linear_dgrad_t<bf16, float, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, w_trans, st)
+                        : linear_dgrad_t<bf16, float, bf16>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, w_trans, st);
     }
-    return addend_f32 ? linear_dgrad_t<bf16, bf16, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, st)
-                      : linear_dgrad_t<bf16, bf16, bf16>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, st);
+    return addend_f32 ? linear_dgrad_t<bf16, bf16, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, w_trans, st)
+                      : linear_dgrad_t<bf16, bf16, bf16>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, w_trans, st);
   }
   RETR_REQUIRE(N % 4 == 0 && K % 4 == 0 && lddy % 4 == 0 && ldw % 4 == 0,
                "linear_dgrad: N/K/ld must be %%4");
   return linear_dgrad_t<float, float, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda,
-                                             gate, ldg, st);
+                                             gate, ldg, w_trans, st);
 }
 
 int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long ldx, float* dw,

@@ -180,3 +180,30 @@ int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, f
 }
 
 }  // extern "C"
+
+// y[c][r] = x[r][c] through a 32x33 LDS tile (coalesced both ways); r in [R, R_pad) -> 0.
+template <typename T>
+__global__ void transpose_cast_kernel(const float* x, T* y, int R, int C, int R_pad) {
+  __shared__ float tile[32][33];
+  int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    int r = r0 + i, c = c0 + threadIdx.x;
+    tile[i][threadIdx.x] = (r < R && c < C) ? x[(long)r * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    int c = c0 + i, r = r0 + threadIdx.x;
+    if (c < C && r < R_pad) y[(long)c * R_pad + r] = from_f<T>(tile[threadIdx.x][i]);
+  }
+}
+
+extern "C" int retr_transpose_cast(int dtype, const float* x, void* y, int R, int C, int R_pad,
+                                   void* stream) {
+  dim3 grid((C + 31) / 32, (R_pad + 31) / 32), block(32, 8);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(transpose_cast_kernel<bf16>, grid, block, 0, st, x, (bf16*)y, R, C, R_pad);
+  else
+    hipLaunchKernelGGL(transpose_cast_kernel<float>, grid, block, 0, st, x, (float*)y, R, C, R_pad);
+  return retr_check_launch("transpose_cast");
+}

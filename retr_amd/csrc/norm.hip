@@ -238,7 +238,7 @@ int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, co
   RETR_REQUIRE(dy || dy2, "layernorm_bwd: no incoming gradient");
   RETR_REQUIRE(mean && rstd && gamma && dx, "layernorm_bwd: missing saved statistics");
   hipStream_t st = (hipStream_t)stream;
-  int rpb = 64;
+  int rpb = 16;  // 4 rows per wave: enough blocks to fill 256 CUs at M ~ 2k-6k rows
   dim3 grid(cdiv(M, rpb));
 #define LNB(P)                                                                                     \
   if (dtype == RETR_BF16)                                                                          \

@@ -75,6 +75,26 @@ class _WeightCache:
         ent[key] = (ver, out)
         return out
 
+    def get_t(self, p, dtype, rows=None):
+        """W^T [K][rows] (compute dtype) of a [N][K...] parameter, rows >= N zero-padded: the
+        K-contiguous B operand of the data-gradient GEMM dX = dY W."""
+        n = p.shape[0]
+        rows = rows or n
+        key = ("T", dtype, rows)
+        ent = getattr(p, self.ATTR, None)
+        ver = (p._version, p.data_ptr())
+        if ent is not None and key in ent and ent[key][0] == ver:
+            return ent[key][1]
+        src = p.detach().reshape(n, -1).contiguous()
+        k = src.shape[1]
+        out = torch.empty(k, rows, dtype=dtype, device=p.device)
+        call("retr_transpose_cast", dcode(dtype), ptr(src), ptr(out), n, k, rows, _st())
+        if ent is None:
+            ent = {}
+            setattr(p, self.ATTR, ent)
+        ent[key] = (ver, out)
+        return out
+
 
 WEIGHTS = _WeightCache()
 
@@ -105,15 +125,15 @@ def k_linear_fwd(x, w, bias, y, relu=0, res=None, drop_p=0.0, seed=0):
          res.stride(0) if res is not None else 0, drop_p, seed, _st())
 
 
-def k_linear_dgrad(dy, w, dx, addend=None, gate=None, N=None, K=None):
+def k_linear_dgrad(dy, wt, dx, addend=None, gate=None):
+    """dx = gate(dy W [+ addend]) with ``wt`` = W^T [K][N] (see _WeightCache.get_t)."""
     M = dy.shape[0]
-    N = N or w.shape[0]
-    K = K or w.shape[1]
-    call("retr_linear_dgrad", dcode(dy.dtype), ptr(dy), dy.stride(0), ptr(w), w.stride(0),
+    K, N = wt.shape
+    call("retr_linear_dgrad", dcode(dy.dtype), ptr(dy), dy.stride(0), ptr(wt), wt.stride(0),
          ptr(dx), dx.stride(0), int(dx.dtype == torch.float32), M, N, K, ptr(addend),
          int(addend is not None and addend.dtype == torch.float32),
          addend.stride(0) if addend is not None else 0, ptr(gate),
-         gate.stride(0) if gate is not None else 0, _st())
+         gate.stride(0) if gate is not None else 0, 1, _st())
 
 
 def k_linear_wgrad(dy, x, dw, N=None):
@@ -265,8 +285,8 @@ class _SelfAttnBlock(torch.autograd.Function):
         hd = C // H
         dev = n.device
         dout = dout.contiguous()
-        win = WEIGHTS.get(w_in, cdtype)
-        wout = WEIGHTS.get(w_out, cdtype)
+        wint = WEIGHTS.get_t(w_in, cdtype)
+        woutt = WEIGHTS.get_t(w_out, cdtype)
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
         dw_out = torch.zeros(C, C, dtype=torch.float32, device=dev)
@@ -274,7 +294,7 @@ class _SelfAttnBlock(torch.autograd.Function):
         k_linear_wgrad(dbr, o, dw_out)
         k_bias_grad(dbr, db_out)
         do = torch.empty(M, C, dtype=cdtype, device=dev)
-        k_linear_dgrad(dbr, wout, do)
+        k_linear_dgrad(dbr, woutt, do)
         dqk = torch.empty(M, 2 * C, dtype=cdtype, device=dev)
         dv = torch.empty(M, C, dtype=cdtype, device=dev)
         k_attention_bwd(qk[:, :C], qk[:, C:], v, o, do, lse, dqk[:, :C], dqk[:, C:], dv, B, H,
@@ -287,8 +307,8 @@ class _SelfAttnBlock(torch.autograd.Function):
         k_bias_grad(dv, db_in[2 * C:])
         dnpos = torch.empty(M, C, dtype=cdtype, device=dev)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
-        k_linear_dgrad(dqk, win[: 2 * C], dnpos)
-        k_linear_dgrad(dv, win[2 * C:], dn)
+        k_linear_dgrad(dqk, wint[:, : 2 * C], dnpos)
+        k_linear_dgrad(dv, wint[:, 2 * C:], dn)
         return (dnpos, dn, dout, dw_in, db_in, dw_out, db_out) + (None,) * 9
 
 
@@ -333,8 +353,8 @@ class _CrossAttnBlock(torch.autograd.Function):
         hd = C // H
         dev = qpos.device
         dout = dout.contiguous()
-        win = WEIGHTS.get(w_in, cdtype)
-        wout = WEIGHTS.get(w_out, cdtype)
+        wint = WEIGHTS.get_t(w_in, cdtype)
+        woutt = WEIGHTS.get_t(w_out, cdtype)
         dbr = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
         dw_out = torch.zeros(C, C, dtype=torch.float32, device=dev)
@@ -342,7 +362,7 @@ class _CrossAttnBlock(torch.autograd.Function):
         k_linear_wgrad(dbr, o, dw_out)
         k_bias_grad(dbr, db_out)
         do = torch.empty(Mq, C, dtype=cdtype, device=dev)
-        k_linear_dgrad(dbr, wout, do)
+        k_linear_dgrad(dbr, woutt, do)
         dq = torch.empty(Mq, C, dtype=cdtype, device=dev)
         dk = torch.empty(Mk, C, dtype=cdtype, device=dev)
         dv = torch.empty(Mk, C, dtype=cdtype, device=dev)
@@ -359,9 +379,9 @@ class _CrossAttnBlock(torch.autograd.Function):
         dqpos = torch.empty(Mq, C, dtype=cdtype, device=dev)
         dmem_pos = torch.empty(Mk, C, dtype=cdtype, device=dev)
         dmem = torch.empty(Mk, C, dtype=cdtype, device=dev)
-        k_linear_dgrad(dq, win[:C], dqpos)
-        k_linear_dgrad(dk, win[C: 2 * C], dmem_pos)
-        k_linear_dgrad(dv, win[2 * C:], dmem)
+        k_linear_dgrad(dq, wint[:, :C], dqpos)
+        k_linear_dgrad(dk, wint[:, C: 2 * C], dmem_pos)
+        k_linear_dgrad(dv, wint[:, 2 * C:], dmem)
         return (dqpos, dmem_pos, dmem, dout, dw_in, db_in, dw_out, db_out) + (None,) * 9
 
 
@@ -391,7 +411,7 @@ class _FFNBlock(torch.autograd.Function):
         F = h.shape[1]
         dev = n.device
         dout = dout.contiguous()
-        w1c, w2c = WEIGHTS.get(w1, cdtype), WEIGHTS.get(w2, cdtype)
+        w1t, w2t = WEIGHTS.get_t(w1, cdtype), WEIGHTS.get_t(w2, cdtype)
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, seed)
         dw2 = torch.zeros(C, F, dtype=torch.float32, device=dev)
@@ -399,13 +419,13 @@ class _FFNBlock(torch.autograd.Function):
         k_linear_wgrad(dbr, h, dw2)
         k_bias_grad(dbr, db2)
         dh = torch.empty(M, F, dtype=cdtype, device=dev)
-        k_linear_dgrad(dbr, w2c, dh, gate=h)
+        k_linear_dgrad(dbr, w2t, dh, gate=h)
         dw1 = torch.zeros(F, C, dtype=torch.float32, device=dev)
         db1 = torch.zeros(F, dtype=torch.float32, device=dev)
         k_linear_wgrad(dh, n, dw1)
         k_bias_grad(dh, db1)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
-        k_linear_dgrad(dh, w1c, dn)
+        k_linear_dgrad(dh, w1t, dn)
         return dn, dout, dw1, db1, dw2, db2, None, None
 
 
@@ -524,7 +544,7 @@ class _Linear(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, dtype=cdtype, device=dev)
-            k_linear_dgrad(dy, WEIGHTS.get(w, cdtype).view(N, -1), dx, gate=dgate)
+            k_linear_dgrad(dy, WEIGHTS.get_t(w, cdtype), dx, gate=dgate)
         return dx, dw.view(wshape), db, None, None, None
 
 
@@ -575,26 +595,26 @@ class _MLPHead(torch.autograd.Function):
         else:
             dl = torch.zeros(M, Vp, dtype=cdtype, device=dev)
             dl[:, :V] = dlog.reshape(M, V).to(cdtype)
-        w1c, w2c = WEIGHTS.get(w1, cdtype), WEIGHTS.get(w2, cdtype)
-        w3c = WEIGHTS.get(w3, cdtype, rows=Vp)
+        w1t, w2t = WEIGHTS.get_t(w1, cdtype), WEIGHTS.get_t(w2, cdtype)
+        w3t = WEIGHTS.get_t(w3, cdtype, rows=Vp)
         dw3 = torch.zeros(Vp, w3.shape[1], dtype=torch.float32, device=dev)
         db3 = torch.zeros(Vp, dtype=torch.float32, device=dev)
         k_linear_wgrad(dl, h2, dw3)
         k_bias_grad(dl, db3)
         dh2 = torch.empty_like(h2)
-        k_linear_dgrad(dl, w3c, dh2, gate=h2)
+        k_linear_dgrad(dl, w3t, dh2, gate=h2)
         dw2 = torch.zeros(w2.shape, dtype=torch.float32, device=dev)
         db2 = torch.zeros(w2.shape[0], dtype=torch.float32, device=dev)
         k_linear_wgrad(dh2, h1, dw2)
         k_bias_grad(dh2, db2)
         dh1 = torch.empty_like(h1)
-        k_linear_dgrad(dh2, w2c, dh1, gate=h1)
+        k_linear_dgrad(dh2, w2t, dh1, gate=h1)
         dw1 = torch.zeros(w1.shape, dtype=torch.float32, device=dev)
         db1 = torch.zeros(w1.shape[0], dtype=torch.float32, device=dev)
         k_linear_wgrad(dh1, hs, dw1)
         k_bias_grad(dh1, db1)
         dhs = torch.empty_like(hs)
-        k_linear_dgrad(dh1, w1c, dhs)
+        k_linear_dgrad(dh1, w1t, dhs)
         return dhs, dw1, db1, dw2, db2, dw3[:V], db3[:V], None, None, None
 
 

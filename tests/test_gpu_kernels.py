@@ -41,7 +41,7 @@ def test_linear_fwd_dgrad_wgrad(dtype, tol, M, N, K):
     gate = torch.randn(M, K, generator=g).to(DEV).to(dtype)
     add = torch.randn(M, K, generator=g).to(DEV)
     dx = torch.empty(M, K, device=DEV)
-    ops.k_linear_dgrad(dyc, wpad, dx, addend=add, gate=gate)
+    ops.k_linear_dgrad(dyc, wpad.t().contiguous(), dx, addend=add, gate=gate)
     ref = (dyc.float() @ wpad.float() + add) * (gate.float() > 0)
     assert rel_err(dx, ref) < tol
     dw = torch.zeros(Np, K, device=DEV)
