@@ -32,6 +32,25 @@ RETR_DEVICE int lds_off(int r, int c) { return r * kBKBytes + ((c ^ ((r >> 1) & 
 
 RETR_DEVICE u32x4 zero16() { return u32x4{0u, 0u, 0u, 0u}; }
 
+// k-major LDS image [BK][ROWS] (bf16) of an operand whose global chunks run along rows: written
+// with 16-byte stores, read as MFMA fragments with ds_read_b64_tr_b16 (gfx950 transposing LDS
+// read).  The 8-byte column unit is XOR-swizzled by k so the 8 k-rows touched by one 32-lane
+// half of a transposed read land on distinct banks.
+template <int ROWS>
+RETR_DEVICE int kmaj_off(int k, int r) {  // r multiple of 4
+  constexpr int RB = ROWS * 2;
+  int f;
+  if constexpr (ROWS >= 128) f = 4 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else f = 4 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+  return k * RB + (((r >> 2) ^ f) << 3);
+}
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+RETR_DEVICE s16x4 ds_read_tr16(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(p));
+}
+
 template <typename T>
 RETR_DEVICE void mfma_step(f32x4& acc, const u32x4& a, const u32x4& b);
 
@@ -56,6 +75,8 @@ struct Stager {
   static constexpr int BK = Elem<T>::BK;
   static constexpr int NCH = ROWS / 32;  // chunks per thread (ROWS*128B / 16B / 256 threads)
   static constexpr int RCH = ROWS / EPC; // row-chunks per k (row-contig orientation)
+  // row-contig bf16 operands use the k-major image + transposing reads
+  static constexpr bool kTr = !L::kContig && sizeof(T) == 2;
   // Each thread owns fixed (row, k-offset) slots of the tile; the loader keeps a k cursor per
   // slot that advances by BK per tile (no per-load index divisions in the implicit GEMMs).
   typename L::Ctx ctx[L::kContig ? NCH : 1];
@@ -94,6 +115,12 @@ struct Stager {
         int r = (tid >> 3) + 32 * i, c = tid & 7;
         *(u32x4*)(lds + lds_off(r, c)) = reg[i];
       }
+    } else if constexpr (kTr) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        int k = tid / RCH + (256 / RCH) * i;
+        *(u32x4*)(lds + kmaj_off<ROWS>(k, (tid % RCH) * EPC)) = reg[i];
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
@@ -106,6 +133,22 @@ struct Stager {
           *(T*)(lds + lds_off(r, k / EPC) + (k % EPC) * (int)sizeof(T)) = v[e];
         }
       }
+    }
+  }
+  // MFMA operand fragment of rows [r0, r0+16) for k sub-step ks (32 bf16 / 16 f32 of K):
+  // lane l holds row r0 + (l&15), k chunk (l>>4) + 4 ks.
+  RETR_DEVICE static u32x4 frag(const char* lds, int r0, int ks, int lane) {
+    if constexpr (kTr) {
+      const int k = 32 * ks + 8 * (lane >> 4) + ((lane & 15) >> 2);
+      const int r = r0 + 4 * (lane & 3);
+      s16x4 lo = ds_read_tr16(lds + kmaj_off<ROWS>(k, r));
+      s16x4 hi = ds_read_tr16(lds + kmaj_off<ROWS>(k + 4, r));
+      return u32x4{(unsigned)(unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16),
+                   (unsigned)(unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16),
+                   (unsigned)(unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16),
+                   (unsigned)(unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16)};
+    } else {
+      return *(const u32x4*)(lds + lds_off(r0 + (lane & 15), (lane >> 4) + 4 * ks));
     }
   }
 };
@@ -163,14 +206,13 @@ gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
     const char* B = A + BM * kBKBytes;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int c = (lane >> 4) + 4 * ks;
       u32x4 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
-        af[i] = *(const u32x4*)(A + lds_off(wm * (BM / 2) + 16 * i + (lane & 15), c));
+        af[i] = Stager<T, BM, LA>::frag(A, wm * (BM / 2) + 16 * i, ks, lane);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        bfr[j] = *(const u32x4*)(B + lds_off(wn * (BN / 2) + 16 * j + (lane & 15), c));
+        bfr[j] = Stager<T, BN, LB>::frag(B, wn * (BN / 2) + 16 * j, ks, lane);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
