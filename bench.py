@@ -57,20 +57,22 @@ def build(cfg, device, seed=42):
     return model.to(device), crit
 
 
-def make_optimizer(model, cfg):
+def make_optimizer(model, cfg, capturable=False):
     """main.py:30-39: two param groups (backbone at lr_backbone), AdamW."""
     groups = [{"params": [p for n, p in model.named_parameters()
                           if "backbone" not in n and p.requires_grad]},
               {"params": [p for n, p in model.named_parameters()
                           if "backbone" in n and p.requires_grad], "lr": cfg.lr_backbone}]
-    return torch.optim.AdamW(groups, lr=cfg.lr, weight_decay=cfg.weight_decay)
+    return torch.optim.AdamW(groups, lr=cfg.lr, weight_decay=cfg.weight_decay,
+                             capturable=capturable)
 
 
 def train_bench(args, rank, world, device):
-    from retr_amd.engine import train_step
+    from retr_amd.engine import GraphedTrainStep, train_step
     cfg = cfg2()
     model, crit = build(cfg, device)
-    opt = make_optimizer(model, cfg)
+    graphed = world == 1 and not args.eager
+    opt = make_optimizer(model, cfg, capturable=graphed)
     sync = None
     if world > 1:
         from retr_amd.ddp import GradSync, broadcast_parameters
@@ -85,8 +87,15 @@ def train_bench(args, rank, world, device):
     caps, cap_mask = caps.to(device), cap_mask.to(device)
     model.train()
 
-    def step():
+    def eager_step():
         return train_step(model, crit, samples, caps, cap_mask, opt, cfg.clip_max_norm, sync)
+
+    graph_step = GraphedTrainStep(model, crit, opt, cfg.clip_max_norm, sync) if graphed else None
+
+    def step():
+        if graph_step is not None:
+            return graph_step(samples, caps, cap_mask)
+        return eager_step()
 
     for _ in range(args.warmup):
         loss = step()
@@ -97,7 +106,7 @@ def train_bench(args, rank, world, device):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    with pr:
+    with pr:   # records only eager launches; graph replays bypass the host entirely
         for _ in range(args.steps):
             loss = step()
     torch.cuda.synchronize()
@@ -108,8 +117,18 @@ def train_bench(args, rank, world, device):
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
+    loss_v = float(loss.item())
+    if graphed:
+        # per-kernel HIP-event timing needs host-side launches: re-run the identical step
+        # eagerly (same weights/inputs/stream) with the probe on
+        pr = probe_mod.Probe()
+        with pr:
+            for _ in range(args.probe_steps):
+                eager_step()
+        torch.cuda.synchronize()
     fam = pr.summary()
-    return dt, float(loss.item()), fam
+    nsteps = args.probe_steps if graphed else args.steps
+    return dt, loss_v, fam, nsteps
 
 
 def decode_bench(args, rank, world, device):
@@ -181,6 +200,8 @@ def main():
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
+    ap.add_argument("--probe-steps", type=int, default=2)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -193,7 +214,7 @@ def main():
     device = torch.device("cuda", local)
     torch.manual_seed(42 + rank)
 
-    dt, loss, fam = train_bench(args, rank, world, device)
+    dt, loss, fam, psteps = train_bench(args, rank, world, device)
     imgs = world * args.batch * args.steps
     value = imgs / dt
     dom_key = max(fam, key=lambda k: fam[k]["ms_total"]) if fam else None
@@ -206,9 +227,9 @@ def main():
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
                 "launches": d["launches"], "avg_launch_ms": round(d["ms_avg"], 4),
                 "flops_per_launch": d["flops"] / max(1, d["launches"])}
-    families = {k: {"ms_per_step": round(v["ms_total"] / args.steps, 3),
+    families = {k: {"ms_per_step": round(v["ms_total"] / psteps, 3),
                     "tflops": round(v["tflops"], 1), "launches_per_step":
-                    v["launches"] // args.steps} for k, v in sorted(
+                    v["launches"] // psteps} for k, v in sorted(
                         fam.items(), key=lambda kv: -kv[1]["ms_total"])}
     decode = None
     if not args.no_decode:
@@ -232,6 +253,7 @@ def main():
                           "global_batch": world * args.batch, "seq_len": 128,
                           "parallelism": f"dp{world}"},
                "loss": round(loss, 4), "roofline": roof, "cpu_baseline": cpu,
+               "launch": "eager" if (args.eager or world > 1) else "hipGraph (whole step)",
                "decode": decode, "kernel_families": families}
         print(json.dumps(out), flush=True)
     if world > 1:

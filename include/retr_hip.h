@@ -25,6 +25,11 @@ extern "C" {
 
 const char* retr_last_error(void);
 int retr_abi_version(void);
+/* Dropout masks are keep(seed_op + *seed_base, index): seed_base is a device uint64 that the
+ * training loop advances once per step (retr_seed_bump), so a captured hipGraph replays with
+ * fresh masks.  NULL (default) -> the per-op seed alone. */
+void retr_set_seed_base(const unsigned long long* device_ptr);
+int retr_seed_bump(unsigned long long* device_ptr, unsigned long long delta, void* stream);
 
 /* ---- linear layers: nn.Linear / MHA in/out-proj / MLP head / feed_forward --------------------
  * replaces F.linear at models/transformer_modules.py:6-11, models/caption.py:161-174,
@@ -39,9 +44,10 @@ int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long 
                       long lddx, int dx_f32, int M, int N, int K, const void* addend,
                       int addend_f32, long lda, const void* gate, long ldg, int w_trans,
                       void* stream);
-/* dw[N][K] += dy^T x  (fp32) */
+/* dw[N][K] (=|+=) dy^T x (fp32); db[N] (=|+=) column sums of dy (fused; db may be NULL).
+ * accumulate = 0: dw/db are overwritten (no pre-zeroing needed); 1: added to. */
 int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long ldx, float* dw,
-                      long lddw, int M, int N, int K, void* stream);
+                      long lddw, int M, int N, int K, float* db, int accumulate, void* stream);
 /* db[N] += column sums of dy[M][N] */
 int retr_bias_grad(int dtype, const void* dy, long lddy, int M, int N, float* db, void* stream);
 
@@ -57,6 +63,7 @@ int retr_conv2d_fwd(int dtype, const void* x, int Nb, int H, int W, int C, const
 int retr_conv2d_dgrad(int dtype, const void* dy, int Nb, int H, int W, int C, const void* wt,
                       void* dx, int Co, int KH, int KW, int stride, int pad, int dil,
                       const void* addend, const void* gate, void* stream);
+/* ws[Co][KH*KW*C] = dWeff (fp32, overwritten; NHWC tap order) */
 int retr_conv2d_wgrad(int dtype, const void* dy, const void* x, int Nb, int H, int W, int C,
                       float* ws, int Co, int KH, int KW, int stride, int pad, int dil,
                       void* stream);

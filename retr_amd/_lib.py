@@ -24,11 +24,13 @@ _SZ = ctypes.c_size_t
 _SIGS = {
     "retr_abi_version": [],
     "retr_last_error": [],
+    "retr_set_seed_base": [_P],
+    "retr_seed_bump": [_P, _U64, _P],
     "retr_linear_fwd": [_I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _I, _P, _L, _F, _U64, _P],
     "retr_linear_dgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _L, _P, _L, _I,
                           _P],
     "retr_transpose_cast": [_I, _P, _P, _I, _I, _I, _P],
-    "retr_linear_wgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _P],
+    "retr_linear_wgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _I, _P],
     "retr_bias_grad": [_I, _P, _L, _I, _I, _P, _P],
     "retr_conv_pack": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "retr_conv2d_fwd": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
@@ -57,7 +59,8 @@ _SIGS = {
     "retr_cast": [_I, _P, _P, _L, _P],
     "retr_pos_grad": [_I, _P, _L, _I, _I, _I, _P, _P],
 }
-_RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ}
+_RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
+            "retr_set_seed_base": None}
 
 _lib = None
 
@@ -94,7 +97,7 @@ def set_probe(p):
 
 def _raw_call(name, args):
     rc = getattr(load(), name)(*args)
-    if rc != 0:
+    if rc is not None and rc != 0:   # void functions return None
         msg = load().retr_last_error()
         raise RuntimeError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")
 

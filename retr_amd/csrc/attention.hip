@@ -159,7 +159,7 @@ attn_fwd_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, long ldv
         if (dp.thresh) {
           int key = k0 + 16 * j + c16;
           uint64_t idx = (((uint64_t)b * H + h) * Lq + qrow) * (uint64_t)Lk + key;
-          p = retr_keep(dp.seed, idx, dp.thresh) ? p * dp.scale : 0.f;
+          p = retr_keep(dp_seed(dp), idx, dp.thresh) ? p * dp.scale : 0.f;
         }
         Pw[(4 * g + e) * TS + 16 * j + c16] = from_f<T>(p);
       }
@@ -266,7 +266,7 @@ attn_bwd_dq_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, long 
           float dpv = dP[j][e];
           if (dp.thresh) {
             uint64_t idx = (((uint64_t)b * H + h) * Lq + qrow) * (uint64_t)Lk + key;
-            dpv = retr_keep(dp.seed, idx, dp.thresh) ? dpv * dp.scale : 0.f;
+            dpv = retr_keep(dp_seed(dp), idx, dp.thresh) ? dpv * dp.scale : 0.f;
           }
           ds = p * (dpv - D_[e]);
         }
@@ -355,7 +355,7 @@ attn_bwd_dkdv_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, lon
         bool kp = true;
         if (dp.thresh && valid) {
           uint64_t idx = (((uint64_t)b * H + h) * Lq + qrow) * (uint64_t)Lk + key;
-          kp = retr_keep(dp.seed, idx, dp.thresh);
+          kp = retr_keep(dp_seed(dp), idx, dp.thresh);
         }
         P[e][j] = p;
         keep[e][j] = kp;
@@ -423,15 +423,6 @@ __global__ void attn_probs_kernel(const T* q, long ldq, const T* k, long ldk, in
     acc += p;
   }
   probs[((long)b * Lq + i) * Lk + j] = acc / H;
-}
-
-DropoutParams make_dp(float p, unsigned long long seed) {
-  DropoutParams dp{seed, 0u, 1.f};
-  if (p > 0.f) {
-    dp.thresh = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
-    dp.scale = 1.f / (1.f - p);
-  }
-  return dp;
 }
 
 template <typename T, int HDP> size_t fwd_lds() {

@@ -25,3 +25,14 @@ int retr_check_launch(const char* what) {
 
 extern "C" const char* retr_last_error(void) { return g_err; }
 extern "C" int retr_abi_version(void) { return 1; }
+
+// device-resident step seed used by every dropout mask (see common.hpp make_dp)
+static const unsigned long long* g_seed_base = nullptr;
+const unsigned long long* retr_seed_base() { return g_seed_base; }
+extern "C" void retr_set_seed_base(const unsigned long long* p) { g_seed_base = p; }
+
+__global__ void seed_bump_kernel(unsigned long long* p, unsigned long long d) { *p += d; }
+extern "C" int retr_seed_bump(unsigned long long* p, unsigned long long delta, void* stream) {
+  hipLaunchKernelGGL(seed_bump_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, p, delta);
+  return retr_check_launch("seed_bump");
+}

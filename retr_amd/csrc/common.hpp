@@ -48,7 +48,23 @@ struct DropoutParams {
   uint64_t seed;
   uint32_t thresh;  // 0 => dropout disabled
   float scale;      // 1/(1-p)
+  const unsigned long long* base = nullptr;  // device-side step seed (graph replays advance it)
 };
+// effective seed: per-op constant + the device-resident step seed (so a captured hipGraph draws
+// fresh masks on every replay while backward still regenerates forward's mask)
+RETR_DEVICE uint64_t dp_seed(const DropoutParams& dp) {
+  return dp.base ? dp.seed + *dp.base : dp.seed;
+}
+const unsigned long long* retr_seed_base();
+inline DropoutParams make_dp(float p, unsigned long long seed) {
+  DropoutParams dp{seed, 0u, 1.f, nullptr};
+  if (p > 0.f) {
+    dp.thresh = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
+    dp.scale = 1.f / (1.f - p);
+    dp.base = retr_seed_base();
+  }
+  return dp;
+}
 
 // ---- wave reductions (wave64) ------------------------------------------------------------------
 RETR_DEVICE float wave_sum(float v) {

@@ -212,7 +212,13 @@ int conv_wgrad_t(const void* dy, const void* x, Geom g, float* ws, hipStream_t s
   constexpr int BK = Elem<T>::BK;
   bool big = R >= 128 && Ncols >= 128;
   int s = big ? pick_splits(R, Ncols, Mp, 128, 128, BK) : pick_splits(R, Ncols, Mp, 64, 64, BK);
-  EpiAccF32 ep{ws, (long)Ncols, s > 1};
+  if (s > 1) {  // ws is an output (overwritten): zero it only when split-K adds atomically
+    if (hipMemsetAsync(ws, 0, sizeof(float) * (size_t)R * Ncols, st) != hipSuccess) {
+      retr_set_error("conv_wgrad: memset failed");
+      return 1;
+    }
+  }
+  EpiAccF32 ep{ws, (long)Ncols, s > 1, 0, s == 1, nullptr};
   ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseT<T> lb{(const T*)x, (long)g.C, Ncols, Mp};

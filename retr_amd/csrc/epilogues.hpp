@@ -52,7 +52,7 @@ struct EpiFwd {
   RETR_DEVICE void apply(int m, int n, float v) const {
     if (bias) v += bias[n];
     if (relu == 1) v = fmaxf(v, 0.f);
-    if (dp.thresh) v = retr_keep(dp.seed, (uint64_t)m * drop_ld + n, dp.thresh) ? v * dp.scale : 0.f;
+    if (dp.thresh) v = retr_keep(dp_seed(dp), (uint64_t)m * drop_ld + n, dp.thresh) ? v * dp.scale : 0.f;
     if (res) v += to_f(res[(long)m * ldr + n]);
     if (relu == 2) v = fmaxf(v, 0.f);
     out[(long)m * ldo + n] = from_f<TO>(v);
@@ -76,7 +76,7 @@ struct EpiFwd {
     if (dp.thresh) {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        v[e] = retr_keep(dp.seed, (uint64_t)m * drop_ld + n + e, dp.thresh) ? v[e] * dp.scale : 0.f;
+        v[e] = retr_keep(dp_seed(dp), (uint64_t)m * drop_ld + n + e, dp.thresh) ? v[e] * dp.scale : 0.f;
     }
     if (res) {
       float r[8];
@@ -92,6 +92,8 @@ struct EpiFwd {
   }
   RETR_DEVICE void empty_split(int, int) const {}
   RETR_DEVICE bool lane_contiguous() const { return false; }
+  static constexpr bool kRowSum = false;
+  float* rowsum = nullptr;
   void set_vec() {
     vec = vec8_ok<TO>(out, ldo) && vec8_ok<TR>(res, ldr) && vec8_ok<float>(bias, 8);
   }
@@ -134,18 +136,27 @@ struct EpiDgrad {
   }
   RETR_DEVICE void empty_split(int, int) const {}
   RETR_DEVICE bool lane_contiguous() const { return false; }
+  static constexpr bool kRowSum = false;
+  float* rowsum = nullptr;
   void set_vec() { vec = vec8_ok<TO>(out, ldo) && vec8_ok<TA>(addend, lda) && vec8_ok<TG>(gate, ldg); }
 };
 
-// fp32 accumulation target (weight gradients): atomic when the GEMM is split over K.
+// fp32 weight-gradient target: atomic when the GEMM is split over K (target pre-zeroed or
+// accumulating), else plain store (overwrite) or read-add-write (accumulate).  ``rowsum``:
+// optional fp32 [M] that receives the row sums of the A operand (the bias gradient of a
+// linear layer, fused into its weight-gradient GEMM — no separate column-sum pass over dY).
 struct EpiAccF32 {
   float* out;
   long ldo;
   int atomic;
   int vec;
+  int overwrite;
+  float* rowsum;
+  static constexpr bool kRowSum = true;
   RETR_DEVICE void apply(int m, int n, float v) const {
     float* p = out + (long)m * ldo + n;
     if (atomic) atomicAdd(p, v);
+    else if (overwrite) *p = v;
     else *p += v;
   }
   RETR_DEVICE void apply8(int m, int n, float (&v)[8]) const {
@@ -153,6 +164,10 @@ struct EpiAccF32 {
     if (atomic || !vec) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) apply(m, n + e, v[e]);
+      return;
+    }
+    if (overwrite) {
+      store8<float>(p, v);
       return;
     }
     float o[8];

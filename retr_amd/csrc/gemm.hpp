@@ -135,6 +135,17 @@ struct Stager {
       }
     }
   }
+  // row sums of the staged chunks (row-contig orientation: the thread's EPC rows are fixed)
+  RETR_DEVICE void add_rowsum(float (&s)[EPC]) const {
+    if constexpr (!L::kContig) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const T* v = (const T*)&reg[i];
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) s[e] += to_f(v[e]);
+      }
+    }
+  }
   // MFMA operand fragment of rows [r0, r0+16) for k sub-step ks (32 bf16 / 16 f32 of K):
   // lane l holds row r0 + (l&15), k chunk (l>>4) + 4 ks.
   RETR_DEVICE static u32x4 frag(const char* lds, int r0, int ks, int lane) {
@@ -189,8 +200,16 @@ gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // fused row sums of A (bias gradient) in the blocks of the first column tile
+  constexpr int EPCA = Stager<T, BM, LA>::EPC;
+  const bool do_rs = EP::kRowSum && !LA::kContig && ep.rowsum != nullptr && (bid % tiles_n) == 0;
+  float rs[EPCA];
+#pragma unroll
+  for (int e = 0; e < EPCA; ++e) rs[e] = 0.f;
+
   sa.fetch(la);
   sb.fetch(lb);
+  if (do_rs) sa.add_rowsum(rs);
   sa.store(smem, tid);
   sb.store(smem + BM * kBKBytes, tid);
   __syncthreads();
@@ -201,6 +220,7 @@ gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
     if (more) {
       sa.fetch(la);
       sb.fetch(lb);
+      if (do_rs) sa.add_rowsum(rs);
     }
     const char* A = smem + cur * kBuf;
     const char* B = A + BM * kBKBytes;
@@ -224,6 +244,21 @@ gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
     }
     __syncthreads();
     cur ^= 1;
+  }
+
+  if constexpr (EP::kRowSum && !LA::kContig) {
+    if (do_rs) {  // block-uniform
+      float* red = (float*)smem;
+      for (int i = tid; i < BM; i += 256) red[i] = 0.f;
+      __syncthreads();
+      const int r0 = (tid % (BM / EPCA)) * EPCA;
+#pragma unroll
+      for (int e = 0; e < EPCA; ++e) atomicAdd(red + r0 + e, rs[e]);
+      __syncthreads();
+      for (int i = tid; i < BM; i += 256)
+        if (m0 + i < M) atomicAdd(ep.rowsum + m0 + i, red[i]);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue through LDS: the accumulator tile (MFMA C layout: 4 rows x 1 column per lane)

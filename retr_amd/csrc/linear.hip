@@ -17,11 +17,7 @@ int linear_fwd_t(const void* x, long ldx, const void* w, long ldw, const float* 
                  unsigned long long seed, hipStream_t st) {
   DenseK<T> la{(const T*)x, ldx, M, K};
   DenseK<T> lb{(const T*)w, ldw, N, K};
-  DropoutParams dp{seed, 0u, 1.f};
-  if (p > 0.f) {
-    dp.thresh = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
-    dp.scale = 1.f / (1.f - p);
-  }
+  DropoutParams dp = make_dp(p, seed);
   EpiFwd<TO, float> ep{(TO*)y, ldy, bias, res, ldr, relu, dp, (long)N};
   ep.set_vec();
   if (M >= 2048 && N >= 128)
@@ -50,22 +46,34 @@ int linear_dgrad_t(const void* dy, long lddy, const void* w, long ldw, void* dx,
   return launch_gemm<T, 64, 64>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
 }
 
+// zero an fp32 [rows][cols] region with row stride ld (stream-ordered, graph-capturable)
+int zero_f32(float* p, long ld, int rows, int cols, hipStream_t st) {
+  hipError_t e = (ld == cols) ? hipMemsetAsync(p, 0, sizeof(float) * (size_t)rows * cols, st)
+                              : hipMemset2DAsync(p, sizeof(float) * ld, 0, sizeof(float) * cols,
+                                                 rows, st);
+  if (e != hipSuccess) {
+    retr_set_error("memset: %s", hipGetErrorString(e));
+    return 1;
+  }
+  return 0;
+}
+
 template <typename T>
 int linear_wgrad_t(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw,
-                   int M, int N, int K, hipStream_t st) {
+                   int M, int N, int K, float* db, int accumulate, hipStream_t st) {
   // dW[n][k] = sum_m dY[m][n] X[m][k]: A(n, m) = dY[m][n], B(k, m) = X[m][k]  (both [m][.])
   DenseT<T> la{(const T*)dy, lddy, N, M};
   DenseT<T> lb{(const T*)x, ldx, K, M};
   constexpr int BK = Elem<T>::BK;
-  if (N >= 512 && K >= 128) {
-    int s = pick_splits(N, K, M, 128, 128, BK);
-    EpiAccF32 ep{dw, lddw, s > 1};
-    ep.set_vec();
-    return launch_gemm<T, 128, 128>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
+  const bool big = N >= 512 && K >= 128;
+  int s = big ? pick_splits(N, K, M, 128, 128, BK) : pick_splits(N, K, M, 64, 64, BK);
+  if (!accumulate) {
+    if (s > 1 && zero_f32(dw, lddw, N, K, st)) return 1;
+    if (db && zero_f32(db, N, 1, N, st)) return 1;
   }
-  int s = pick_splits(N, K, M, 64, 64, BK);
-  EpiAccF32 ep{dw, lddw, s > 1};
+  EpiAccF32 ep{dw, lddw, s > 1, 0, !accumulate && s == 1, db};
   ep.set_vec();
+  if (big) return launch_gemm<T, 128, 128>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
   return launch_gemm<T, 64, 64>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
 }
 
@@ -124,17 +132,17 @@ int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long 
 }
 
 int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long ldx, float* dw,
-                      long lddw, int M, int N, int K, void* stream) {
+                      long lddw, int M, int N, int K, float* db, int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) return 0;
   if (dtype == RETR_BF16) {
     RETR_REQUIRE(N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0,
                  "linear_wgrad: N/K/ld must be %%8");
-    return linear_wgrad_t<bf16>(dy, lddy, x, ldx, dw, lddw, M, N, K, st);
+    return linear_wgrad_t<bf16>(dy, lddy, x, ldx, dw, lddw, M, N, K, db, accumulate, st);
   }
   RETR_REQUIRE(N % 4 == 0 && K % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0,
                "linear_wgrad: N/K/ld must be %%4");
-  return linear_wgrad_t<float>(dy, lddy, x, ldx, dw, lddw, M, N, K, st);
+  return linear_wgrad_t<float>(dy, lddy, x, ldx, dw, lddw, M, N, K, db, accumulate, st);
 }
 
 int retr_bias_grad(int dtype, const void* dy, long lddy, int M, int N, float* db, void* stream) {

@@ -71,7 +71,7 @@ __global__ void dropout_apply_kernel(const float* x, long ldx, TO* y, long ldy, 
     int n = i % N;
     long m = i / N;
     float v = x[m * ldx + n];
-    if (dp.thresh) v = retr_keep(dp.seed, (uint64_t)m * N + n, dp.thresh) ? v * dp.scale : 0.f;
+    if (dp.thresh) v = retr_keep(dp_seed(dp), (uint64_t)m * N + n, dp.thresh) ? v * dp.scale : 0.f;
     y[m * ldy + n] = from_f<TO>(v);
   }
 }
@@ -96,15 +96,6 @@ __global__ void pos_grad_kernel(const T* d, long ld, int M, int C, int period, f
 int grid_for(long total) {
   long g = (total + 255) / 256;
   return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
-}
-
-DropoutParams make_dp(float p, unsigned long long seed) {
-  DropoutParams dp{seed, 0u, 1.f};
-  if (p > 0.f) {
-    dp.thresh = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
-    dp.scale = 1.f / (1.f - p);
-  }
-  return dp;
 }
 
 }  // namespace

@@ -125,7 +125,7 @@ embed_ln_fwd_kernel(const long long* tok, int M, int T, int C, const float* word
   for (int i = 0; i < PER; ++i) {
     int c = lane + 64 * i;
     float o = (v[i] - mean) * rstd * gamma[c] + beta[c];
-    if (dp.thresh) o = retr_keep(dp.seed, (uint64_t)row * C + c, dp.thresh) ? o * dp.scale : 0.f;
+    if (dp.thresh) o = retr_keep(dp_seed(dp), (uint64_t)row * C + c, dp.thresh) ? o * dp.scale : 0.f;
     y[(long)row * C + c] = o;
   }
   if (lane == 0) {
@@ -155,7 +155,7 @@ embed_ln_bwd_kernel(const long long* tok, int M, int T, int C, const float* word
     for (int i = 0; i < PER; ++i) {
       int c = lane + 64 * i;
       float d = dy[(long)row * C + c];
-      if (dp.thresh) d = retr_keep(dp.seed, (uint64_t)row * C + c, dp.thresh) ? d * dp.scale : 0.f;
+      if (dp.thresh) d = retr_keep(dp_seed(dp), (uint64_t)row * C + c, dp.thresh) ? d * dp.scale : 0.f;
       xh[i] = (word[t * C + c] + posw[(long)p * C + c] - mu) * rs;
       pg[i] += d * xh[i];
       pb[i] += d;
@@ -185,15 +185,6 @@ embed_ln_bwd_kernel(const long long* tok, int M, int T, int C, const float* word
     if (dgamma) atomicAdd(dgamma + c, a);
     if (dbeta) atomicAdd(dbeta + c, b);
   }
-}
-
-DropoutParams make_dp(float p, unsigned long long seed) {
-  DropoutParams dp{seed, 0u, 1.f};
-  if (p > 0.f) {
-    dp.thresh = (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f);
-    dp.scale = 1.f / (1.f - p);
-  }
-  return dp;
 }
 
 #define PER_SWITCH(C, MACRO)          \

@@ -36,6 +36,8 @@ def pack_encoder_inputs(encoder_input, global_features, location_features, devic
 
 def train_step(model, criterion, samples, caps, cap_masks, optimizer, max_norm, grad_sync=None):
     """One reference training step (engine.py:70-83) — returns the loss tensor (no host sync)."""
+    from . import ops
+    ops.bump_seed()
     outputs = model(*samples, caps[:, :-1], cap_masks[:, :-1])
     loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
     optimizer.zero_grad()
@@ -46,6 +48,51 @@ def train_step(model, criterion, samples, caps, cap_masks, optimizer, max_norm, 
         torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)
     optimizer.step()
     return loss
+
+
+class GraphedTrainStep:
+    """The training step of ``train_step`` captured once into a hipGraph and replayed.
+
+    Every kernel of the step (forward, CE, backward, gradient clipping and the optimizer) is
+    stream-ordered and allocation-free inside the capture (torch's graph memory pool), so one
+    ``hipGraphLaunch`` replaces ~1.2k individual launches and the Python/ctypes host work.
+    Inputs are copied into static device buffers before each replay; dropout masks change
+    every replay through the device-side step seed (ops.bump_seed inside the graph).
+    Requirements: ``optimizer`` built with ``capturable=True``; fixed batch shapes.
+    """
+
+    def __init__(self, model, criterion, optimizer, max_norm, grad_sync=None, warmup=2):
+        self.model, self.criterion, self.optimizer = model, criterion, optimizer
+        self.max_norm, self.grad_sync, self.warmup = max_norm, grad_sync, warmup
+        self.graph = None
+        self.static = None
+        self.loss = None
+
+    def _step(self):
+        s_img, s_mask, s_caps, s_cm = self.static
+        return train_step(self.model, self.criterion, (NestedTensor(s_img, s_mask),), s_caps,
+                          s_cm, self.optimizer, self.max_norm, self.grad_sync)
+
+    def __call__(self, samples, caps, cap_masks):
+        nt = samples[0]
+        if self.static is None:
+            self.static = (nt.tensors.clone(), nt.mask.clone(), caps.clone(), cap_masks.clone())
+        else:
+            for dst, src in zip(self.static, (nt.tensors, nt.mask, caps, cap_masks)):
+                dst.copy_(src, non_blocking=True)
+        if self.graph is None:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(self.warmup):
+                    self.loss = self._step()
+            torch.cuda.current_stream().wait_stream(side)
+            self.optimizer.zero_grad(set_to_none=True)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.loss = self._step()
+        self.graph.replay()
+        return self.loss
 
 
 def train_one_epoch(model, criterion, data_loader, optimizer, device, epoch, max_norm,

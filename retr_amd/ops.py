@@ -16,8 +16,6 @@ reference computes as separate PyTorch ops:
 Tensors of the residual stream are fp32; GEMM operands are the compute dtype (bf16 or fp32).
 All ops raise on non-HIP tensors (no CPU fallback).
 """
-import weakref
-
 import torch
 
 from . import _lib
@@ -36,6 +34,26 @@ def next_seed():
         _seed_state["base"] = torch.initial_seed() & 0xFFFFFFFFFFFF
     _seed_state["ctr"] += 1
     return (_seed_state["base"] * 0x100000001B3 + _seed_state["ctr"] * 0x9E3779B1) & (2**63 - 1)
+
+
+_seed_base = {}
+
+
+def seed_base(device=None):
+    """Device-resident step seed shared by every dropout mask (see retr_set_seed_base)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    t = _seed_base.get(dev)
+    if t is None:
+        t = torch.full((1,), (torch.initial_seed() * 0x9E3779B97F4A7C15) & (2 ** 62 - 1),
+                       dtype=torch.int64, device=dev)
+        _seed_base[dev] = t
+        call("retr_set_seed_base", ptr(t))
+    return t
+
+
+def bump_seed(delta=0x9E3779B97F4A7C1):
+    """Advance the step seed on the device (stream-ordered; captured into training graphs)."""
+    call("retr_seed_bump", ptr(seed_base()), delta, _st())
 
 
 def dcode(dtype):
@@ -136,12 +154,17 @@ def k_linear_dgrad(dy, wt, dx, addend=None, gate=None):
          gate.stride(0) if gate is not None else 0, 1, _st())
 
 
-def k_linear_wgrad(dy, x, dw, N=None):
+def k_linear_wgrad(dy, x, dw, db=None, accumulate=False):
+    """dw (=|+=) dy^T x and, fused, db (=|+=) colsum(dy); overwrite needs no pre-zeroing."""
     M = dy.shape[0]
-    N = N or dw.shape[0]
+    N = dw.shape[0]
     K = x.shape[1]
     call("retr_linear_wgrad", dcode(dy.dtype), ptr(dy), dy.stride(0), ptr(x), x.stride(0),
-         ptr(dw), dw.stride(0), M, N, K, _st())
+         ptr(dw), dw.stride(0), M, N, K, ptr(db), int(accumulate), _st())
+
+
+def _empty(*shape, dev):
+    return torch.empty(shape, dtype=torch.float32, device=dev)
 
 
 def k_bias_grad(dy, db, N=None):
@@ -289,22 +312,17 @@ class _SelfAttnBlock(torch.autograd.Function):
         woutt = WEIGHTS.get_t(w_out, cdtype)
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
-        dw_out = torch.zeros(C, C, dtype=torch.float32, device=dev)
-        db_out = torch.zeros(C, dtype=torch.float32, device=dev)
-        k_linear_wgrad(dbr, o, dw_out)
-        k_bias_grad(dbr, db_out)
+        dw_out, db_out = _empty(C, C, dev=dev), _empty(C, dev=dev)
+        k_linear_wgrad(dbr, o, dw_out, db_out)
         do = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
         dqk = torch.empty(M, 2 * C, dtype=cdtype, device=dev)
         dv = torch.empty(M, C, dtype=cdtype, device=dev)
         k_attention_bwd(qk[:, :C], qk[:, C:], v, o, do, lse, dqk[:, :C], dqk[:, C:], dv, B, H,
                         L, L, hd, kpm, causal, drop_attn, s_att)
-        dw_in = torch.zeros(3 * C, C, dtype=torch.float32, device=dev)
-        db_in = torch.zeros(3 * C, dtype=torch.float32, device=dev)
-        k_linear_wgrad(dqk, npos, dw_in[: 2 * C])
-        k_linear_wgrad(dv, n, dw_in[2 * C:])
-        k_bias_grad(dqk, db_in[: 2 * C])
-        k_bias_grad(dv, db_in[2 * C:])
+        dw_in, db_in = _empty(3 * C, C, dev=dev), _empty(3 * C, dev=dev)
+        k_linear_wgrad(dqk, npos, dw_in[: 2 * C], db_in[: 2 * C])
+        k_linear_wgrad(dv, n, dw_in[2 * C:], db_in[2 * C:])
         dnpos = torch.empty(M, C, dtype=cdtype, device=dev)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dqk, wint[:, : 2 * C], dnpos)
@@ -357,10 +375,8 @@ class _CrossAttnBlock(torch.autograd.Function):
         woutt = WEIGHTS.get_t(w_out, cdtype)
         dbr = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
-        dw_out = torch.zeros(C, C, dtype=torch.float32, device=dev)
-        db_out = torch.zeros(C, dtype=torch.float32, device=dev)
-        k_linear_wgrad(dbr, o, dw_out)
-        k_bias_grad(dbr, db_out)
+        dw_out, db_out = _empty(C, C, dev=dev), _empty(C, dev=dev)
+        k_linear_wgrad(dbr, o, dw_out, db_out)
         do = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
         dq = torch.empty(Mq, C, dtype=cdtype, device=dev)
@@ -368,14 +384,10 @@ class _CrossAttnBlock(torch.autograd.Function):
         dv = torch.empty(Mk, C, dtype=cdtype, device=dev)
         k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, False, drop_attn,
                         s_att)
-        dw_in = torch.zeros(3 * C, C, dtype=torch.float32, device=dev)
-        db_in = torch.zeros(3 * C, dtype=torch.float32, device=dev)
-        k_linear_wgrad(dq, qpos, dw_in[:C])
-        k_linear_wgrad(dk, mem_pos, dw_in[C: 2 * C])
-        k_linear_wgrad(dv, mem, dw_in[2 * C:])
-        k_bias_grad(dq, db_in[:C])
-        k_bias_grad(dk, db_in[C: 2 * C])
-        k_bias_grad(dv, db_in[2 * C:])
+        dw_in, db_in = _empty(3 * C, C, dev=dev), _empty(3 * C, dev=dev)
+        k_linear_wgrad(dq, qpos, dw_in[:C], db_in[:C])
+        k_linear_wgrad(dk, mem_pos, dw_in[C: 2 * C], db_in[C: 2 * C])
+        k_linear_wgrad(dv, mem, dw_in[2 * C:], db_in[2 * C:])
         dqpos = torch.empty(Mq, C, dtype=cdtype, device=dev)
         dmem_pos = torch.empty(Mk, C, dtype=cdtype, device=dev)
         dmem = torch.empty(Mk, C, dtype=cdtype, device=dev)
@@ -414,16 +426,12 @@ class _FFNBlock(torch.autograd.Function):
         w1t, w2t = WEIGHTS.get_t(w1, cdtype), WEIGHTS.get_t(w2, cdtype)
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, seed)
-        dw2 = torch.zeros(C, F, dtype=torch.float32, device=dev)
-        db2 = torch.zeros(C, dtype=torch.float32, device=dev)
-        k_linear_wgrad(dbr, h, dw2)
-        k_bias_grad(dbr, db2)
+        dw2, db2 = _empty(C, F, dev=dev), _empty(C, dev=dev)
+        k_linear_wgrad(dbr, h, dw2, db2)
         dh = torch.empty(M, F, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, w2t, dh, gate=h)
-        dw1 = torch.zeros(F, C, dtype=torch.float32, device=dev)
-        db1 = torch.zeros(F, dtype=torch.float32, device=dev)
-        k_linear_wgrad(dh, n, dw1)
-        k_bias_grad(dh, db1)
+        dw1, db1 = _empty(F, C, dev=dev), _empty(F, dev=dev)
+        k_linear_wgrad(dh, n, dw1, db1)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dh, w1t, dn)
         return dn, dout, dw1, db1, dw2, db2, None, None
@@ -535,12 +543,9 @@ class _Linear(torch.autograd.Function):
             dyc = torch.empty(M, N, dtype=cdtype, device=dev)
             k_dropout_apply(dy.float().contiguous(), dyc, 0.0, 0)
             dy = dyc
-        dw = torch.zeros(N, K, dtype=torch.float32, device=dev)
-        k_linear_wgrad(dy, x, dw)
-        db = None
-        if ctx.has_b:
-            db = torch.zeros(N, dtype=torch.float32, device=dev)
-            k_bias_grad(dy, db)
+        dw = _empty(N, K, dev=dev)
+        db = _empty(N, dev=dev) if ctx.has_b else None
+        k_linear_wgrad(dy, x, dw, db)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, dtype=cdtype, device=dev)
@@ -597,22 +602,16 @@ class _MLPHead(torch.autograd.Function):
             dl[:, :V] = dlog.reshape(M, V).to(cdtype)
         w1t, w2t = WEIGHTS.get_t(w1, cdtype), WEIGHTS.get_t(w2, cdtype)
         w3t = WEIGHTS.get_t(w3, cdtype, rows=Vp)
-        dw3 = torch.zeros(Vp, w3.shape[1], dtype=torch.float32, device=dev)
-        db3 = torch.zeros(Vp, dtype=torch.float32, device=dev)
-        k_linear_wgrad(dl, h2, dw3)
-        k_bias_grad(dl, db3)
+        dw3, db3 = _empty(Vp, w3.shape[1], dev=dev), _empty(Vp, dev=dev)
+        k_linear_wgrad(dl, h2, dw3, db3)
         dh2 = torch.empty_like(h2)
         k_linear_dgrad(dl, w3t, dh2, gate=h2)
-        dw2 = torch.zeros(w2.shape, dtype=torch.float32, device=dev)
-        db2 = torch.zeros(w2.shape[0], dtype=torch.float32, device=dev)
-        k_linear_wgrad(dh2, h1, dw2)
-        k_bias_grad(dh2, db2)
+        dw2, db2 = _empty(*w2.shape, dev=dev), _empty(w2.shape[0], dev=dev)
+        k_linear_wgrad(dh2, h1, dw2, db2)
         dh1 = torch.empty_like(h1)
         k_linear_dgrad(dh2, w2t, dh1, gate=h1)
-        dw1 = torch.zeros(w1.shape, dtype=torch.float32, device=dev)
-        db1 = torch.zeros(w1.shape[0], dtype=torch.float32, device=dev)
-        k_linear_wgrad(dh1, hs, dw1)
-        k_bias_grad(dh1, db1)
+        dw1, db1 = _empty(*w1.shape, dev=dev), _empty(w1.shape[0], dev=dev)
+        k_linear_wgrad(dh1, hs, dw1, db1)
         dhs = torch.empty_like(hs)
         k_linear_dgrad(dh1, w1t, dhs)
         return dhs, dw1, db1, dw2, db2, dw3[:V], db3[:V], None, None, None

@@ -132,7 +132,7 @@ def _conv_dgrad(spec, g, in_shape, addend=None, gate=None):
 def _conv_wgrad(spec, g, x, in_shape):
     n, h, w, c = in_shape
     _, _, _, scale = PACKS.get(spec, g.dtype)
-    ws = torch.zeros(spec.cout, spec.k * spec.k * c, dtype=torch.float32, device=g.device)
+    ws = torch.empty(spec.cout, spec.k * spec.k * c, dtype=torch.float32, device=g.device)
     call("retr_conv2d_wgrad", dcode(g.dtype), ptr(g), ptr(x), n, h, w, c, ptr(ws), spec.cout,
          spec.k, spec.k, spec.s, spec.p, spec.d, _st())
     grad = torch.empty(spec.conv.weight.shape, dtype=torch.float32, device=g.device)

@@ -51,6 +51,16 @@ def test_linear_fwd_dgrad_wgrad(dtype, tol, M, N, K):
     db = torch.zeros(Np, device=DEV)
     ops.k_bias_grad(dyc, db)
     assert rel_err(db, dyc.float().sum(0)) < tol
+    # fused bias gradient + accumulate mode
+    dw2 = torch.ones(Np, K, device=DEV)
+    db2 = torch.ones(Np, device=DEV)
+    ops.k_linear_wgrad(dyc, xc, dw2, db2, accumulate=True)
+    assert rel_err(dw2, ref + 1) < tol
+    assert rel_err(db2, dyc.float().sum(0) + 1) < tol
+    dw3 = torch.full((Np, K), float("nan"), device=DEV)
+    db3 = torch.full((Np,), float("nan"), device=DEV)
+    ops.k_linear_wgrad(dyc, xc, dw3, db3)           # overwrite mode: no pre-zeroing needed
+    assert rel_err(dw3, ref) < tol and rel_err(db3, dyc.float().sum(0)) < tol
 
 
 CONVS = [  # (N, Cin, H, Cout, k, stride, pad, dil)
