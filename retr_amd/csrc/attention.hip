@@ -425,6 +425,66 @@ __global__ void attn_probs_kernel(const T* q, long ldq, const T* k, long ldk, in
   probs[((long)b * Lq + i) * Lk + j] = acc / H;
 }
 
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+attn_decode_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, long ldv, T* o, long ldo,
+                   int H, int Lk, int Lmax, int hd, const unsigned char* kpm, float scale) {
+  extern __shared__ float sm[];
+  float* sc = sm;            // [Lk] scores -> probabilities
+  float* qs = sc + Lk;       // [64] scaled query (rounded to T like the tiled kernel)
+  float* red = qs + 64;      // [256] reduction scratch
+  const int tid = threadIdx.x, b = blockIdx.x / H, h = blockIdx.x % H;
+  constexpr int EPC = 16 / sizeof(T);
+  for (int d = tid; d < hd; d += 256) qs[d] = to_f(from_f<T>(to_f(q[(long)b * ldq + h * hd + d]) * scale));
+  __syncthreads();
+  const T* kb = k + (long)b * Lmax * ldk + h * hd;
+  const T* vb = v + (long)b * Lmax * ldv + h * hd;
+  float mx = -INFINITY;
+  for (int j = tid; j < Lk; j += 256) {
+    float s = -INFINITY;
+    if (!(kpm && kpm[(long)b * Lk + j])) {
+      s = 0.f;
+      const T* kr = kb + (long)j * ldk;
+      for (int d0 = 0; d0 < hd; d0 += EPC) {
+        u32x4 raw = *(const u32x4*)(kr + d0);
+        const T* e = (const T*)&raw;
+#pragma unroll
+        for (int t = 0; t < EPC; ++t) s += qs[d0 + t] * to_f(e[t]);
+      }
+    }
+    sc[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  if ((tid & 63) == 0) red[tid >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int j = tid; j < Lk; j += 256) {
+    float p = mx == -INFINITY ? 0.f : __expf(sc[j] - mx);
+    sc[j] = p;
+    sum += p;
+  }
+  sum = wave_sum(sum);
+  if ((tid & 63) == 0) red[4 + (tid >> 6)] = sum;
+  __syncthreads();
+  const float inv = 1.f / (red[4] + red[5] + red[6] + red[7]);
+  __syncthreads();
+  const int nc = 256 / hd, d = tid % hd, c = tid / hd;
+  float acc = 0.f;
+  if (c < nc)
+    for (int j = c; j < Lk; j += nc) acc += sc[j] * to_f(vb[(long)j * ldv + d]);
+  red[tid] = acc;
+  __syncthreads();
+  if (tid < hd) {
+    float s = 0.f;
+    for (int cc = 0; cc < nc; ++cc) s += red[cc * hd + tid];
+    o[(long)b * ldo + h * hd + tid] = from_f<T>(s * inv);
+  }
+}
+
 template <typename T, int HDP> size_t fwd_lds() {
   constexpr int RS = HDP + AT<T>::PAD, TS = 64 + AT<T>::PAD;
   return sizeof(T) * (2 * 64 * RS + HDP * TS + 4 * 16 * TS);
@@ -517,20 +577,29 @@ int retr_attention_fwd(int dtype, const void* q, long ldq, const void* k, long l
   return fwd_t<float, 64>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed, lse, probs, st);
 }
 
-// Decode step: one query row per batch against the first Lk rows of a key/value cache whose
-// batch stride is Lmax rows (KV-cache incremental greedy decode, eval_utils/decode.py:68-79).
+// Decode step: one query row per (batch, head) against the first Lk rows of a key/value cache
+// whose batch stride is Lmax rows (KV-cache incremental greedy decode, decode.py:68-79).
+// One 256-thread block per (b, h): scores in LDS (16-byte K loads), block max/sum, then
+// P.V with threads split over (head dim, key stripe) and an LDS reduction.
 int retr_attention_decode(int dtype, const void* q, long ldq, const void* k, long ldk,
                           const void* v, long ldv, void* o, long ldo, int B, int H, int Lk,
                           int Lmax, int hd, const unsigned char* kpm, void* stream) {
   RETR_REQUIRE(hd >= 8 && hd <= 64 && hd % 8 == 0, "attention: head dim %d unsupported", hd);
   RETR_REQUIRE(kpm == nullptr || Lmax == Lk, "attention_decode: kpm needs Lmax == Lk");
+  RETR_REQUIRE(Lk >= 1 && Lk <= 4096, "attention_decode: Lk=%d out of range", Lk);
+  RETR_REQUIRE(ldk % 8 == 0 && ldv % 8 == 0, "attention_decode: row strides %%8");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == RETR_BF16) {
-    if (hd <= 32) return fwd_t<bf16, 32>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, 1, Lk, hd, kpm, 0, 0.f, 0, nullptr, nullptr, st, Lmax);
-    return fwd_t<bf16, 64>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, 1, Lk, hd, kpm, 0, 0.f, 0, nullptr, nullptr, st, Lmax);
-  }
-  if (hd <= 32) return fwd_t<float, 32>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, 1, Lk, hd, kpm, 0, 0.f, 0, nullptr, nullptr, st, Lmax);
-  return fwd_t<float, 64>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, 1, Lk, hd, kpm, 0, 0.f, 0, nullptr, nullptr, st, Lmax);
+  const float scale = 1.0f / sqrtf((float)hd);
+  const size_t lds = sizeof(float) * (Lk + 64 + 256 + 8);
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(attn_decode_kernel<bf16>, dim3(B * H), dim3(256), lds, st, (const bf16*)q, ldq,
+                       (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, H, Lk, Lmax, hd, kpm,
+                       scale);
+  else
+    hipLaunchKernelGGL(attn_decode_kernel<float>, dim3(B * H), dim3(256), lds, st, (const float*)q,
+                       ldq, (const float*)k, ldk, (const float*)v, ldv, (float*)o, ldo, H, Lk, Lmax,
+                       hd, kpm, scale);
+  return retr_check_launch("attention_decode");
 }
 
 size_t retr_attention_bwd_workspace(int B, int H, int Lq) { return sizeof(float) * (size_t)B * H * Lq; }

@@ -13,8 +13,11 @@ positions have exactly zero influence, rows are independent):
     the final LayerNorm, the MLP head and a first-index argmax;
   * the finished/early-exit bookkeeping runs on the device (retr_greedy_update) and the host
     polls it every ``poll`` steps, so no per-step synchronisation.
-The attention kernel processes the cached keys in the same 64-key tiles as the full causal
-forward, so the logits of a row are bit-identical to the full recompute on the same device.
+The T-1 per-step launch sequences are captured once per (shape, weights) as hipGraphs and
+replayed, so a step costs its kernels' device time, not ~100 host launches.  The single-query
+attention (retr_attention_decode) reduces keys in a different order than the tiled training
+kernel, so logits agree with the full recompute to rounding, and the token ids agree with the
+reference algorithm run by the CPU oracle (tests/test_gpu_model.py).
 """
 import torch
 
@@ -40,13 +43,52 @@ def prepare_tokenizer():
     return tokenizer, start_token, end_token
 
 
-class IncrementalGreedy:
-    """KV-cache greedy decoder over a ``Caption`` model (eval mode semantics)."""
+class _DecodeState:
+    """Static device buffers (and captured per-step hipGraphs) for one (B, S, T) shape."""
 
-    def __init__(self, model):
+    def __init__(self, B, S, T, C, F, n_layers, V, cd, dev):
+        f32 = torch.float32
+        self.B, self.S, self.T = B, S, T
+        self.kx = [torch.empty(B * S, C, dtype=cd, device=dev) for _ in range(n_layers)]
+        self.vx = [torch.empty(B * S, C, dtype=cd, device=dev) for _ in range(n_layers)]
+        self.kc = [torch.zeros(B * T, C, dtype=cd, device=dev) for _ in range(n_layers)]
+        self.vc = [torch.zeros(B * T, C, dtype=cd, device=dev) for _ in range(n_layers)]
+        self.kpm = torch.zeros(B, S, dtype=torch.uint8, device=dev)
+        self.caption = torch.zeros(B, T, dtype=torch.long, device=dev)
+        self.tok = torch.zeros(B, dtype=torch.long, device=dev)
+        self.finished = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.done = torch.full((1,), -1, dtype=torch.int32, device=dev)
+        self.y = torch.empty(B, C, dtype=f32, device=dev)
+        self.y2 = torch.empty_like(self.y)
+        self.n = torch.empty(B, C, dtype=cd, device=dev)
+        self.npos = torch.empty_like(self.n)
+        self.q = torch.empty_like(self.n)
+        self.o = torch.empty_like(self.n)
+        self.mean = torch.empty(B, dtype=f32, device=dev)
+        self.rstd = torch.empty_like(self.mean)
+        self.ffh = torch.empty(B, F, dtype=cd, device=dev)
+        self.h1 = torch.empty(B, 512, dtype=cd, device=dev)
+        self.h2 = torch.empty(B, 512, dtype=cd, device=dev)
+        self.Vp = (V + 63) // 64 * 64
+        self.logits = torch.empty(B, self.Vp, dtype=cd, device=dev)
+        self.pred = torch.empty(B, dtype=torch.long, device=dev)
+        self.head_bias = None
+        self.graphs = None
+        self.signature = None
+
+
+class IncrementalGreedy:
+    """KV-cache greedy decoder over a ``Caption`` model (eval mode semantics).  The T-1 decode
+    steps are captured once per (shape, weights) as hipGraphs and replayed per batch."""
+
+    def __init__(self, model, use_graphs=True):
         self.model = model
         self.tr = model.transformer
         self.cdtype = model.cdtype
+        self.use_graphs = use_graphs
+        if not hasattr(model, "_retr_decode_states"):
+            model._retr_decode_states = {}
+        self.states = model._retr_decode_states
 
     def _ln(self, x, norm, y=None, y2=None, pos=None):
         M, C = x.shape
@@ -54,110 +96,131 @@ class IncrementalGreedy:
              ptr(norm.bias), float(norm.eps), M, C, ptr(y), C, ptr(y2), ptr(pos), 1, None, None,
              _st())
 
+    def _signature(self):
+        return tuple((p._version, p.data_ptr()) for p in self.model.parameters())
+
+    def _step(self, st, i, eos_token):
+        """Kernels of decode step i (reads token i, writes caption column i+1)."""
+        model, tr, cd = self.model, self.tr, self.cdtype
+        B, S, T = st.B, st.S, st.T
+        C = st.n.shape[1]
+        layers = list(tr.decoder.layers)
+        H = layers[0].tgt_self_attn.sublayer.num_heads
+        hd = C // H
+        emb = tr.embeddings
+        qp = emb.position_embeddings.weight.detach()[i]
+        s = _st()
+        y, y2 = st.y, st.y2
+        call("retr_embed_ln_fwd", ptr(st.tok), B, 1, C, ptr(emb.word_embeddings.weight), ptr(qp),
+             ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias), float(emb.LayerNorm.eps), 0.0, 0,
+             ptr(y), ptr(st.mean), ptr(st.rstd), s)
+        for li, layer in enumerate(layers):
+            sa = layer.tgt_self_attn
+            sub = sa.sublayer
+            w = ops.WEIGHTS.get(sub.in_proj_weight, cd)
+            b = sub.in_proj_bias.detach()
+            self._ln(y, sa.norm, y=st.n, y2=st.npos, pos=qp)
+            k_linear_fwd(st.npos, w[:C], b[:C], st.q)
+            k_linear_fwd(st.npos, w[C:2 * C], b[C:2 * C], st.kc[li][i::T])
+            k_linear_fwd(st.n, w[2 * C:], b[2 * C:], st.vc[li][i::T])
+            call("retr_attention_decode", dcode(cd), ptr(st.q), C, ptr(st.kc[li]), C,
+                 ptr(st.vc[li]), C, ptr(st.o), C, B, H, i + 1, T, hd, None, s)
+            k_linear_fwd(st.o, ops.WEIGHTS.get(sub.out_proj.weight, cd),
+                         sub.out_proj.bias.detach(), y2, res=y)
+            y, y2 = y2, y
+            ca = layer.tgt_src_cross_attn
+            sub = ca.sublayer
+            w = ops.WEIGHTS.get(sub.in_proj_weight, cd)
+            b = sub.in_proj_bias.detach()
+            self._ln(y, ca.norm, y2=st.npos, pos=qp)
+            k_linear_fwd(st.npos, w[:C], b[:C], st.q)
+            call("retr_attention_decode", dcode(cd), ptr(st.q), C, ptr(st.kx[li]), C,
+                 ptr(st.vx[li]), C, ptr(st.o), C, B, H, S, S, hd, ptr(st.kpm), s)
+            k_linear_fwd(st.o, ops.WEIGHTS.get(sub.out_proj.weight, cd),
+                         sub.out_proj.bias.detach(), y2, res=y)
+            y, y2 = y2, y
+            ff = layer.ff
+            self._ln(y, ff.norm, y=st.n)
+            f0, f2 = ff.sublayer[0], ff.sublayer[2]
+            k_linear_fwd(st.n, ops.WEIGHTS.get(f0.weight, cd), f0.bias.detach(), st.ffh, relu=1)
+            k_linear_fwd(st.ffh, ops.WEIGHTS.get(f2.weight, cd), f2.bias.detach(), y2, res=y)
+            y, y2 = y2, y
+        l1, l2, l3 = model.mlp.layers
+        V = l3.weight.shape[0]
+        self._ln(y, tr.decoder.norm, y=st.n)
+        k_linear_fwd(st.n, ops.WEIGHTS.get(l1.weight, cd), l1.bias.detach(), st.h1, relu=1)
+        k_linear_fwd(st.h1, ops.WEIGHTS.get(l2.weight, cd), l2.bias.detach(), st.h2, relu=1)
+        k_linear_fwd(st.h2, ops.WEIGHTS.get(l3.weight, cd, rows=st.Vp),
+                     st.head_bias, st.logits)
+        call("retr_argmax_rows", dcode(cd), ptr(st.logits), st.Vp, B, V, ptr(st.pred), s)
+        call("retr_greedy_update", ptr(st.pred), B, T, i, int(eos_token), ptr(st.caption),
+             ptr(st.finished), ptr(st.done), ptr(st.tok), s)
+
     @torch.no_grad()
     def __call__(self, samples, max_len, bos_token, eos_token, poll=8):
         model, tr, cd = self.model, self.tr, self.cdtype
         src, mask, B, S = model.encode_image(samples)
         kpm = mask.reshape(B, S).contiguous().view(torch.uint8)
         mem, mem_pos, _ = tr.encode(src, B, S, kpm, cd)
-        qpos_w = tr.embeddings.position_embeddings.weight.detach()
+        qpos_w = tr.embeddings.position_embeddings.weight
         T = max_len
         if T != qpos_w.shape[0]:
             raise RuntimeError(f"The size of tensor a ({T}) must match the size of tensor b "
                                f"({qpos_w.shape[0]}) at non-singleton dimension 0")
         C = mem.shape[1]
-        dev = mem.device
         layers = list(tr.decoder.layers)
-        H = layers[0].tgt_self_attn.sublayer.num_heads
-        hd = C // H
-        # cross-attention K/V once per batch
-        cross = []
-        for layer in layers:
+        key = (B, S, T, cd, int(eos_token))
+        st = self.states.get(key)
+        if st is None:
+            st = _DecodeState(B, S, T, C, layers[0].ff.sublayer[0].weight.shape[0], len(layers),
+                              model.mlp.layers[2].weight.shape[0], cd, mem.device)
+            self.states[key] = st
+        # cross-attention K/V of every decoder layer, once per batch, into the static buffers
+        for li, layer in enumerate(layers):
             sub = layer.tgt_src_cross_attn.sublayer
             w = ops.WEIGHTS.get(sub.in_proj_weight, cd)
             b = sub.in_proj_bias.detach()
-            kx = torch.empty(B * S, C, dtype=cd, device=dev)
-            vx = torch.empty(B * S, C, dtype=cd, device=dev)
-            k_linear_fwd(mem_pos, w[C:2 * C], b[C:2 * C], kx)
-            k_linear_fwd(mem, w[2 * C:], b[2 * C:], vx)
-            cross.append((kx, vx))
-        kc = [torch.zeros(B * T, C, dtype=cd, device=dev) for _ in layers]
-        vc = [torch.zeros(B * T, C, dtype=cd, device=dev) for _ in layers]
-        caption = torch.zeros(B, T, dtype=torch.long, device=dev)
-        caption[:, 0] = bos_token
-        tok = torch.full((B,), bos_token, dtype=torch.long, device=dev)
-        finished = torch.zeros(B, dtype=torch.uint8, device=dev)
-        done = torch.full((1,), -1, dtype=torch.int32, device=dev)
-        # step buffers
-        y = torch.empty(B, C, dtype=torch.float32, device=dev)
-        y2 = torch.empty_like(y)
-        n = torch.empty(B, C, dtype=cd, device=dev)
-        npos = torch.empty_like(n)
-        q = torch.empty_like(n)
-        o = torch.empty_like(n)
-        emb = tr.embeddings
-        mean = torch.empty(B, dtype=torch.float32, device=dev)
-        rstd = torch.empty_like(mean)
-        l1, l2, l3 = model.mlp.layers
-        V = l3.weight.shape[0]
-        Vp = (V + 63) // 64 * 64
-        w1, w2 = ops.WEIGHTS.get(l1.weight, cd), ops.WEIGHTS.get(l2.weight, cd)
-        w3 = ops.WEIGHTS.get(l3.weight, cd, rows=Vp)
-        b3 = ops._pad_vec(l3.bias, Vp)
-        h1 = torch.empty(B, l1.weight.shape[0], dtype=cd, device=dev)
-        h2 = torch.empty(B, l2.weight.shape[0], dtype=cd, device=dev)
-        logits = torch.empty(B, Vp, dtype=cd, device=dev)
-        pred = torch.empty(B, dtype=torch.long, device=dev)
-        ffh = torch.empty(B, layers[0].ff.sublayer[0].weight.shape[0], dtype=cd, device=dev)
-        st = _st()
+            k_linear_fwd(mem_pos, w[C:2 * C], b[C:2 * C], st.kx[li])
+            k_linear_fwd(mem, w[2 * C:], b[2 * C:], st.vx[li])
+        st.kpm.copy_(kpm)
+        st.caption.zero_()
+        st.caption[:, 0] = bos_token
+        st.tok.fill_(bos_token)
+        st.finished.zero_()
+        st.done.fill_(-1)
+        sig = self._signature()
+        if st.signature != sig:
+            st.head_bias = ops._pad_vec(model.mlp.layers[2].bias, st.Vp)
+            st.graphs = None
+        if self.use_graphs and st.graphs is None:
+            # warm once eagerly (kernel attributes, weight copies), then capture every step
+            self._step(st, 0, eos_token)
+            torch.cuda.synchronize()
+            st.caption.zero_()
+            st.caption[:, 0] = bos_token
+            st.tok.fill_(bos_token)
+            st.finished.zero_()
+            st.done.fill_(-1)
+            graphs = []
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for i in range(T - 1):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=side):
+                        self._step(st, i, eos_token)
+                    graphs.append(g)
+            torch.cuda.current_stream().wait_stream(side)
+            st.graphs = graphs
+        st.signature = sig
         for i in range(T - 1):
-            qp = qpos_w[i]
-            call("retr_embed_ln_fwd", ptr(tok), B, 1, C, ptr(emb.word_embeddings.weight),
-                 ptr(qp), ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias),
-                 float(emb.LayerNorm.eps), 0.0, 0, ptr(y), ptr(mean), ptr(rstd), st)
-            for li, layer in enumerate(layers):
-                sa = layer.tgt_self_attn
-                sub = sa.sublayer
-                w = ops.WEIGHTS.get(sub.in_proj_weight, cd)
-                b = sub.in_proj_bias.detach()
-                self._ln(y, sa.norm, y=n, y2=npos, pos=qp)
-                k_linear_fwd(npos, w[:C], b[:C], q)
-                kci, vci = kc[li][i::T], vc[li][i::T]     # row b*T + i of the caches
-                k_linear_fwd(npos, w[C:2 * C], b[C:2 * C], kci)
-                k_linear_fwd(n, w[2 * C:], b[2 * C:], vci)
-                call("retr_attention_decode", dcode(cd), ptr(q), C, ptr(kc[li]), C, ptr(vc[li]),
-                     C, ptr(o), C, B, H, i + 1, T, hd, None, st)
-                k_linear_fwd(o, ops.WEIGHTS.get(sub.out_proj.weight, cd),
-                             sub.out_proj.bias.detach(), y2, res=y)
-                y, y2 = y2, y
-                ca = layer.tgt_src_cross_attn
-                sub = ca.sublayer
-                w = ops.WEIGHTS.get(sub.in_proj_weight, cd)
-                b = sub.in_proj_bias.detach()
-                self._ln(y, ca.norm, y2=npos, pos=qp)
-                k_linear_fwd(npos, w[:C], b[:C], q)
-                kx, vx = cross[li]
-                call("retr_attention_decode", dcode(cd), ptr(q), C, ptr(kx), C, ptr(vx), C,
-                     ptr(o), C, B, H, S, S, hd, ptr(kpm), st)
-                k_linear_fwd(o, ops.WEIGHTS.get(sub.out_proj.weight, cd),
-                             sub.out_proj.bias.detach(), y2, res=y)
-                y, y2 = y2, y
-                ff = layer.ff
-                self._ln(y, ff.norm, y=n)
-                f0, f2 = ff.sublayer[0], ff.sublayer[2]
-                k_linear_fwd(n, ops.WEIGHTS.get(f0.weight, cd), f0.bias.detach(), ffh, relu=1)
-                k_linear_fwd(ffh, ops.WEIGHTS.get(f2.weight, cd), f2.bias.detach(), y2, res=y)
-                y, y2 = y2, y
-            self._ln(y, tr.decoder.norm, y=n)
-            k_linear_fwd(n, w1, l1.bias.detach(), h1, relu=1)
-            k_linear_fwd(h1, w2, l2.bias.detach(), h2, relu=1)
-            k_linear_fwd(h2, w3, b3, logits)
-            call("retr_argmax_rows", dcode(cd), ptr(logits), Vp, B, V, ptr(pred), st)
-            call("retr_greedy_update", ptr(pred), B, T, i, int(eos_token), ptr(caption),
-                 ptr(finished), ptr(done), ptr(tok), st)
-            if (i + 1) % poll == 0 and int(done.item()) >= 0:
+            if self.use_graphs:
+                st.graphs[i].replay()
+            else:
+                self._step(st, i, eos_token)
+            if (i + 1) % poll == 0 and int(st.done.item()) >= 0:
                 break
-        return caption
+        return st.caption.clone()
 
 
 def _full_forward_greedy(samples, model, max_len, bos_token, eos_token, device):

@@ -218,6 +218,29 @@ def test_attention(dtype, tol, B, H, Lq, Lk, hd, causal, masked):
     assert rel_err(dv.view(B, Lk, C), vr.grad) < 3 * tol
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("B,H,Lk,Lmax,hd,masked", [
+    (2, 8, 1, 128, 32, False), (3, 8, 77, 128, 32, False), (2, 8, 400, 400, 32, True),
+    (4, 4, 128, 128, 64, True), (2, 8, 19, 20, 8, False)])
+def test_attention_decode(dtype, tol, B, H, Lk, Lmax, hd, masked):
+    """Single-query attention over a [B][Lmax] key cache (first Lk rows valid)."""
+    g = torch.Generator(device="cpu").manual_seed(B * Lk + hd)
+    C = H * hd
+    q = torch.randn(B, 1, C, generator=g).to(DEV).to(dtype)
+    kc = torch.randn(B, Lmax, C, generator=g).to(DEV).to(dtype)
+    vc = torch.randn(B, Lmax, C, generator=g).to(DEV).to(dtype)
+    kpm = None
+    if masked:
+        kpm = torch.zeros(B, Lk, dtype=torch.uint8)
+        kpm[:, Lk - Lk // 4:] = 1
+        kpm = kpm.to(DEV)
+    o = torch.empty(B, C, dtype=dtype, device=DEV)
+    call("retr_attention_decode", ops.dcode(dtype), ptr(q), C, ptr(kc), C, ptr(vc), C, ptr(o), C,
+         B, H, Lk, Lmax, hd, ptr(kpm), ops._st())
+    ref, _ = _attn_ref(q.float(), kc[:, :Lk].float(), vc[:, :Lk].float(), H, kpm, False)
+    assert rel_err(o.view(B, 1, C), ref) < tol
+
+
 def test_attention_dropout_statistics():
     B, H, L, hd = 2, 8, 128, 32
     C = H * hd

@@ -8,7 +8,8 @@ import pytest
 import torch
 
 from oracle import model as orc
-from retr_amd.eval_utils.decode import greedy, greedy_reference_algorithm
+from retr_amd.eval_utils.decode import (IncrementalGreedy, greedy,
+                                        greedy_reference_algorithm)
 from retr_amd.models.caption import build_model
 from retr_amd.models.utils import NestedTensor
 from retr_amd.synthetic import synthetic_captions, synthetic_images, synthetic_state_dict
@@ -99,9 +100,11 @@ def test_greedy_ids_bit_exact(case):
     # EOS choices: never emitted / emitted by row 0 mid-sequence (early finish of one row) /
     # the token row 0 emits at step 1 for every row that also emits it (full early return)
     for eos in (-1, int(ids_never[0, 6]), int(ids_never[0, 1])):
-        ids = greedy(samples, model, max_len=T, bos_token=101, eos_token=eos)
+        ids = greedy(samples, model, max_len=T, bos_token=101, eos_token=eos)   # hipGraphs
+        ids_eager = IncrementalGreedy(model, use_graphs=False)(samples[0], T, 101, eos)
+        assert torch.equal(ids, ids_eager), (case, eos)       # graph replay == eager launches
         ids_full = greedy_reference_algorithm(samples, model, T, 101, eos)
-        assert torch.equal(ids, ids_full), (case, eos)        # incremental == full recompute
+        assert torch.equal(ids, ids_full), (case, eos)        # KV cache == full recompute ids
         ids_o = _oracle_greedy(cfg, sd, images, mask, eos)
         assert torch.equal(ids.cpu(), ids_o), (case, eos)      # == reference algorithm on CPU
 
