@@ -57,12 +57,16 @@ def build(cfg, device, seed=42):
     return model.to(device), crit
 
 
-def make_optimizer(model, cfg, capturable=False):
-    """main.py:30-39: two param groups (backbone at lr_backbone), AdamW."""
+def make_optimizer(model, cfg, capturable=False, fused=True):
+    """main.py:30-39: two param groups (backbone at lr_backbone), AdamW — by default the
+    MI355X FusedAdamW (clip + AdamW in two kernels over flat arenas, retr_amd/optim.py)."""
     groups = [{"params": [p for n, p in model.named_parameters()
                           if "backbone" not in n and p.requires_grad]},
               {"params": [p for n, p in model.named_parameters()
                           if "backbone" in n and p.requires_grad], "lr": cfg.lr_backbone}]
+    if fused:
+        from retr_amd.optim import FusedAdamW
+        return FusedAdamW(groups, lr=cfg.lr, weight_decay=cfg.weight_decay)
     return torch.optim.AdamW(groups, lr=cfg.lr, weight_decay=cfg.weight_decay,
                              capturable=capturable)
 
@@ -72,7 +76,7 @@ def train_bench(args, rank, world, device):
     cfg = cfg2()
     model, crit = build(cfg, device)
     graphed = world == 1 and not args.eager
-    opt = make_optimizer(model, cfg, capturable=graphed)
+    opt = make_optimizer(model, cfg, capturable=graphed, fused=not args.torch_adamw)
     sync = None
     if world > 1:
         from retr_amd.ddp import GradSync, broadcast_parameters
@@ -121,12 +125,27 @@ def train_bench(args, rank, world, device):
     if graphed:
         # per-kernel HIP-event timing needs host-side launches: re-run the identical step
         # eagerly (same weights/inputs/stream) with the probe on
-        pr = probe_mod.Probe()
+        pr = probe_mod.Probe(detail=bool(args.probe_detail))
         with pr:
             for _ in range(args.probe_steps):
                 eager_step()
         torch.cuda.synchronize()
     fam = pr.summary()
+    if args.probe_detail and rank == 0:
+        nst = args.probe_steps if graphed else args.steps
+        with open(args.probe_detail, "w") as f:
+            for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms_total"]):
+                f.write(f"{v['ms_total'] / nst:8.3f} ms/step {v['launches'] // nst:4d}x "
+                        f"{v['ms_avg'] * 1e3:8.1f} us {v['tflops']:7.1f} TF/s  {k}\n")
+        fam = {}
+        for k, v in pr.summary().items():
+            d = fam.setdefault(k.split(" | ")[0], {"launches": 0, "ms_total": 0.0,
+                                                   "flops": 0.0})
+            for f in ("launches", "ms_total", "flops"):
+                d[f] += v[f]
+        for d in fam.values():
+            d["ms_avg"] = d["ms_total"] / max(1, d["launches"])
+            d["tflops"] = d["flops"] / (d["ms_total"] * 1e-3) / 1e12 if d["ms_total"] else 0.0
     nsteps = args.probe_steps if graphed else args.steps
     return dt, loss_v, fam, nsteps
 
@@ -202,6 +221,9 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     ap.add_argument("--probe-steps", type=int, default=2)
+    ap.add_argument("--torch-adamw", action="store_true",
+                    help="torch.optim.AdamW + clip_grad_norm_ instead of the fused kernels")
+    ap.add_argument("--probe-detail", default="", help="write a per-shape kernel table here")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -45,7 +45,8 @@ int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long 
                       int addend_f32, long lda, const void* gate, long ldg, int w_trans,
                       void* stream);
 /* dw[N][K] (=|+=) dy^T x (fp32); db[N] (=|+=) column sums of dy (fused; db may be NULL).
- * accumulate = 0: dw/db are overwritten (no pre-zeroing needed); 1: added to. */
+ * accumulate = 0: dw/db are overwritten (no pre-zeroing needed); 1: added to.
+ * N may be ragged when lddy covers N rounded up to the 16-byte vector (padded dy rows). */
 int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long ldx, float* dw,
                       long lddw, int M, int N, int K, float* db, int accumulate, void* stream);
 /* db[N] += column sums of dy[M][N] */
@@ -149,6 +150,23 @@ int retr_cast(int dtype, const float* x, void* y, long n, void* stream);
 /* dpos[p][c] += sum_{m: m % period == p} d[m][c] */
 int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
                   void* stream);
+
+/* ---- fused clip_grad_norm_ + AdamW over flat fp32 arenas --------------------------------
+ * Replaces engine.py:80-83 (torch.nn.utils.clip_grad_norm_ + optimizer.step()) with the
+ * optimizer built at main.py:39-41 (torch.optim.AdamW, two param groups).
+ * retr_adamw_sumsq: partials[b] = sum of grad^2 over a grid-stride slice (b < nparts; grad may
+ *   be NULL -> zeros); if step != NULL, *step += 1 (device-side step counter).
+ * retr_adamw_update: coef = min(max_norm / (sqrt(sum partials) + 1e-6), 1) when max_norm > 0;
+ *   g *= coef (written back only when coef < 1); AdamW (amsgrad=False, maximize=False) with
+ *   hyper = {lr, weight_decay} read from device memory and bias corrections from the step count
+ *   *step + step_offset (the offset covers parameters that skipped steps without a gradient).
+ *   n % 4 == 0, all arrays 16-byte aligned. */
+int retr_adamw_sumsq(const float* grad, long n, float* partials, int nparts, float* step,
+                     void* stream);
+int retr_adamw_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n,
+                      const float* hyper, double beta1, double beta2, float eps,
+                      const float* step, float step_offset, const float* partials, int nparts,
+                      float max_norm, void* stream);
 
 #ifdef __cplusplus
 }

@@ -17,6 +17,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_long
 _F = ctypes.c_float
+_D = ctypes.c_double
 _U64 = ctypes.c_ulonglong
 _SZ = ctypes.c_size_t
 
@@ -58,6 +59,8 @@ _SIGS = {
     "retr_dropout_apply": [_I, _P, _L, _P, _L, _I, _I, _F, _U64, _P],
     "retr_cast": [_I, _P, _P, _L, _P],
     "retr_pos_grad": [_I, _P, _L, _I, _I, _I, _P, _P],
+    "retr_adamw_sumsq": [_P, _L, _P, _I, _P, _P],
+    "retr_adamw_update": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P],
 }
 _RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
             "retr_set_seed_base": None}

@@ -136,12 +136,13 @@ int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long 
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) return 0;
   if (dtype == RETR_BF16) {
-    RETR_REQUIRE(N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0,
-                 "linear_wgrad: N/K/ld must be %%8");
+    // a ragged N reads the 16-byte group past row N-1 of dY: the row stride must cover it
+    RETR_REQUIRE(lddy >= (N + 7) / 8 * 8 && K % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0,
+                 "linear_wgrad: K/ld must be %%8 and ld(dy) >= N rounded up to 8");
     return linear_wgrad_t<bf16>(dy, lddy, x, ldx, dw, lddw, M, N, K, db, accumulate, st);
   }
-  RETR_REQUIRE(N % 4 == 0 && K % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0,
-               "linear_wgrad: N/K/ld must be %%4");
+  RETR_REQUIRE(lddy >= (N + 3) / 4 * 4 && K % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0,
+               "linear_wgrad: K/ld must be %%4 and ld(dy) >= N rounded up to 4");
   return linear_wgrad_t<float>(dy, lddy, x, ldx, dw, lddw, M, N, K, db, accumulate, st);
 }
 

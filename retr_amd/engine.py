@@ -34,6 +34,18 @@ def pack_encoder_inputs(encoder_input, global_features, location_features, devic
             l_feats.to(device))
 
 
+def clip_and_step(model, optimizer, max_norm):
+    """engine.py:80-83: clip_grad_norm_(model.parameters(), max_norm) + optimizer.step().
+    With a FusedAdamW that manages every trainable parameter both run as two fused kernels."""
+    from .optim import FusedAdamW
+    if isinstance(optimizer, FusedAdamW) and optimizer.covers(model.parameters()):
+        optimizer.step(max_norm=max_norm if max_norm > 0 else 0.0)
+        return
+    if max_norm > 0:
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)
+    optimizer.step()
+
+
 def train_step(model, criterion, samples, caps, cap_masks, optimizer, max_norm, grad_sync=None):
     """One reference training step (engine.py:70-83) — returns the loss tensor (no host sync)."""
     from . import ops
@@ -44,9 +56,7 @@ def train_step(model, criterion, samples, caps, cap_masks, optimizer, max_norm, 
     loss.backward()
     if grad_sync is not None:
         grad_sync.synchronize()
-    if max_norm > 0:
-        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)
-    optimizer.step()
+    clip_and_step(model, optimizer, max_norm)
     return loss
 
 
@@ -58,7 +68,8 @@ class GraphedTrainStep:
     ``hipGraphLaunch`` replaces ~1.2k individual launches and the Python/ctypes host work.
     Inputs are copied into static device buffers before each replay; dropout masks change
     every replay through the device-side step seed (ops.bump_seed inside the graph).
-    Requirements: ``optimizer`` built with ``capturable=True``; fixed batch shapes.
+    Requirements: ``optimizer`` built with ``capturable=True`` (or a retr_amd FusedAdamW, whose
+    step counter and lr live on the device); fixed batch shapes.
     """
 
     def __init__(self, model, criterion, optimizer, max_norm, grad_sync=None, warmup=2):
@@ -91,6 +102,8 @@ class GraphedTrainStep:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self.loss = self._step()
+        if hasattr(self.optimizer, "sync_hyper"):
+            self.optimizer.sync_hyper()      # lr schedule changes reach the captured kernels
         self.graph.replay()
         return self.loss
 
@@ -120,9 +133,7 @@ def train_one_epoch(model, criterion, data_loader, optimizer, device, epoch, max
             loss.backward()
             if grad_sync is not None:
                 grad_sync.synchronize()
-            if max_norm > 0:
-                torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)
-            optimizer.step()
+            clip_and_step(model, optimizer, max_norm)
             pbar.update(1)
     return epoch_loss / total
 

@@ -19,6 +19,7 @@ All ops raise on non-HIP tensors (no CPU fallback).
 import torch
 
 from . import _lib
+from .optim import grad_buffer
 from ._lib import BF16, F32, call, ptr
 
 # ---------------------------------------------------------------------------------------------
@@ -219,6 +220,7 @@ class _LnPos(torch.autograd.Function):
              float(eps), M, C, ptr(y), C, ptr(y2), ptr(posd), int(period or 1), ptr(mean),
              ptr(rstd), _st())
         ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.gparams = (gamma, beta, pos)
         ctx.period = period
         ctx.mode = mode
         ctx.pos_shape = tuple(pos.shape) if pos is not None else None
@@ -238,8 +240,9 @@ class _LnPos(torch.autograd.Function):
             dy, dy2 = None, grads[0]
         M, C = x.shape
         dx = torch.empty(M, C, dtype=torch.float32, device=x.device)
-        dgamma = torch.zeros(C, dtype=torch.float32, device=x.device)
-        dbeta = torch.zeros_like(dgamma)
+        gp, bp, pp = ctx.gparams
+        dgamma, _ = grad_buffer(gp)
+        dbeta, _ = grad_buffer(bp)
         if dy is not None:
             dy = dy.contiguous()
         if dy2 is not None:
@@ -252,7 +255,7 @@ class _LnPos(torch.autograd.Function):
              ptr(dbeta), _st())
         dpos = None
         if ctx.pos_shape is not None and ctx.needs_input_grad[3] and dy2 is not None:
-            dpos = torch.zeros(ctx.pos_shape, dtype=torch.float32, device=x.device)
+            dpos, _ = grad_buffer(pp)
             call("retr_pos_grad", dcode(dy2.dtype), ptr(dy2), dy2.stride(0), M, C, ctx.period,
                  ptr(dpos), _st())
         return dx, dgamma, dbeta, dpos, None, None, None, None
@@ -294,6 +297,7 @@ class _SelfAttnBlock(torch.autograd.Function):
         out = torch.empty(M, C, dtype=torch.float32, device=dev)
         k_linear_fwd(o, wout, b_out.detach(), out, res=res, drop_p=drop_res, seed=s_res)
         ctx.save_for_backward(npos, n, qk, v, o, lse, kpm, w_in, w_out)
+        ctx.gparams = (w_in, b_in, w_out, b_out)
         ctx.cfg = (B, L, H, causal, drop_attn, drop_res, s_att, s_res, cdtype)
         if want_probs:
             ctx.mark_non_differentiable(probs)
@@ -312,17 +316,16 @@ class _SelfAttnBlock(torch.autograd.Function):
         woutt = WEIGHTS.get_t(w_out, cdtype)
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
-        dw_out, db_out = _empty(C, C, dev=dev), _empty(C, dev=dev)
-        k_linear_wgrad(dbr, o, dw_out, db_out)
+        (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
+        k_linear_wgrad(dbr, o, dw_out, db_out, accumulate=True)
         do = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
         dqk = torch.empty(M, 2 * C, dtype=cdtype, device=dev)
         dv = torch.empty(M, C, dtype=cdtype, device=dev)
         k_attention_bwd(qk[:, :C], qk[:, C:], v, o, do, lse, dqk[:, :C], dqk[:, C:], dv, B, H,
                         L, L, hd, kpm, causal, drop_attn, s_att)
-        dw_in, db_in = _empty(3 * C, C, dev=dev), _empty(3 * C, dev=dev)
-        k_linear_wgrad(dqk, npos, dw_in[: 2 * C], db_in[: 2 * C])
-        k_linear_wgrad(dv, n, dw_in[2 * C:], db_in[2 * C:])
+        k_linear_wgrad(dqk, npos, dw_in[: 2 * C], db_in[: 2 * C], accumulate=True)
+        k_linear_wgrad(dv, n, dw_in[2 * C:], db_in[2 * C:], accumulate=True)
         dnpos = torch.empty(M, C, dtype=cdtype, device=dev)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dqk, wint[:, : 2 * C], dnpos)
@@ -356,6 +359,7 @@ class _CrossAttnBlock(torch.autograd.Function):
         out = torch.empty(Mq, C, dtype=torch.float32, device=dev)
         k_linear_fwd(o, wout, b_out.detach(), out, res=res, drop_p=drop_res, seed=s_res)
         ctx.save_for_backward(qpos, mem_pos, mem, q, k, v, o, lse, kpm, w_in, w_out)
+        ctx.gparams = (w_in, b_in, w_out, b_out)
         ctx.cfg = (B, Lq, Lk, H, drop_attn, drop_res, s_att, s_res, cdtype)
         if want_probs:
             ctx.mark_non_differentiable(probs)
@@ -375,8 +379,8 @@ class _CrossAttnBlock(torch.autograd.Function):
         woutt = WEIGHTS.get_t(w_out, cdtype)
         dbr = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
-        dw_out, db_out = _empty(C, C, dev=dev), _empty(C, dev=dev)
-        k_linear_wgrad(dbr, o, dw_out, db_out)
+        (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
+        k_linear_wgrad(dbr, o, dw_out, db_out, accumulate=True)
         do = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
         dq = torch.empty(Mq, C, dtype=cdtype, device=dev)
@@ -384,10 +388,9 @@ class _CrossAttnBlock(torch.autograd.Function):
         dv = torch.empty(Mk, C, dtype=cdtype, device=dev)
         k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, False, drop_attn,
                         s_att)
-        dw_in, db_in = _empty(3 * C, C, dev=dev), _empty(3 * C, dev=dev)
-        k_linear_wgrad(dq, qpos, dw_in[:C], db_in[:C])
-        k_linear_wgrad(dk, mem_pos, dw_in[C: 2 * C], db_in[C: 2 * C])
-        k_linear_wgrad(dv, mem, dw_in[2 * C:], db_in[2 * C:])
+        k_linear_wgrad(dq, qpos, dw_in[:C], db_in[:C], accumulate=True)
+        k_linear_wgrad(dk, mem_pos, dw_in[C: 2 * C], db_in[C: 2 * C], accumulate=True)
+        k_linear_wgrad(dv, mem, dw_in[2 * C:], db_in[2 * C:], accumulate=True)
         dqpos = torch.empty(Mq, C, dtype=cdtype, device=dev)
         dmem_pos = torch.empty(Mk, C, dtype=cdtype, device=dev)
         dmem = torch.empty(Mk, C, dtype=cdtype, device=dev)
@@ -412,6 +415,7 @@ class _FFNBlock(torch.autograd.Function):
         seed = next_seed()
         k_linear_fwd(h, w2c, b2.detach(), out, res=res, drop_p=drop_res, seed=seed)
         ctx.save_for_backward(n, h, w1, w2)
+        ctx.gparams = (w1, b1, w2, b2)
         ctx.cfg = (drop_res, seed, cdtype)
         return out
 
@@ -426,12 +430,11 @@ class _FFNBlock(torch.autograd.Function):
         w1t, w2t = WEIGHTS.get_t(w1, cdtype), WEIGHTS.get_t(w2, cdtype)
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, seed)
-        dw2, db2 = _empty(C, F, dev=dev), _empty(C, dev=dev)
-        k_linear_wgrad(dbr, h, dw2, db2)
+        (dw1, _), (db1, _), (dw2, _), (db2, _) = map(grad_buffer, ctx.gparams)
+        k_linear_wgrad(dbr, h, dw2, db2, accumulate=True)
         dh = torch.empty(M, F, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, w2t, dh, gate=h)
-        dw1, db1 = _empty(F, C, dev=dev), _empty(F, dev=dev)
-        k_linear_wgrad(dh, n, dw1, db1)
+        k_linear_wgrad(dh, n, dw1, db1, accumulate=True)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dh, w1t, dn)
         return dn, dout, dw1, db1, dw2, db2, None, None
@@ -485,6 +488,7 @@ class _EmbedLN(torch.autograd.Function):
         call("retr_embed_ln_fwd", ptr(caps), B, T, C, ptr(word), ptr(posw), ptr(gamma),
              ptr(beta), float(eps), drop_p, seed, ptr(y), ptr(mean), ptr(rstd), _st())
         ctx.save_for_backward(caps, word, posw, gamma, mean, rstd)
+        ctx.gparams = (word, posw, gamma, beta)
         ctx.cfg = (eps, drop_p, seed, padding_idx)
         return y
 
@@ -496,10 +500,7 @@ class _EmbedLN(torch.autograd.Function):
         C = word.shape[1]
         dev = word.device
         dy = dy.contiguous()
-        dword = torch.zeros_like(word, dtype=torch.float32)
-        dposw = torch.zeros_like(posw, dtype=torch.float32)
-        dgamma = torch.zeros(C, dtype=torch.float32, device=dev)
-        dbeta = torch.zeros_like(dgamma)
+        (dword, _), (dposw, _), (dgamma, _), (dbeta, _) = map(grad_buffer, ctx.gparams)
         call("retr_embed_ln_bwd", ptr(caps), B, T, C, ptr(word), ptr(posw), ptr(gamma),
              ptr(mean), ptr(rstd), ptr(dy), drop_p, seed, ptr(dword), ptr(dposw), ptr(dgamma),
              ptr(dbeta), -1 if padding_idx is None else int(padding_idx), _st())
@@ -527,6 +528,7 @@ class _Linear(torch.autograd.Function):
         y = torch.empty(M, N, dtype=torch.float32 if out_f32 else cdtype, device=x.device)
         k_linear_fwd(x, wc, b.detach() if b is not None else None, y)
         ctx.save_for_backward(x, w, dgate)
+        ctx.gparams = (w, b)
         ctx.cdtype = cdtype
         ctx.has_b = b is not None
         return y
@@ -537,20 +539,19 @@ class _Linear(torch.autograd.Function):
         cdtype = ctx.cdtype
         M, K = x.shape
         N = w.shape[0]
-        wshape = w.shape
         dev = x.device
         if dy.dtype != cdtype or not dy.is_contiguous():
             dyc = torch.empty(M, N, dtype=cdtype, device=dev)
             k_dropout_apply(dy.float().contiguous(), dyc, 0.0, 0)
             dy = dyc
-        dw = _empty(N, K, dev=dev)
-        db = _empty(N, dev=dev) if ctx.has_b else None
-        k_linear_wgrad(dy, x, dw, db)
+        dw, _ = grad_buffer(w)
+        db = grad_buffer(ctx.gparams[1])[0] if ctx.has_b else None
+        k_linear_wgrad(dy, x, dw.view(N, K), db, accumulate=True)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(M, K, dtype=cdtype, device=dev)
             k_linear_dgrad(dy, WEIGHTS.get_t(w, cdtype), dx, gate=dgate)
-        return dx, dw.view(wshape), db, None, None, None
+        return dx, dw, db, None, None, None
 
 
 def linear(x, w, b, cdtype, out_f32=False, dgate=None):
@@ -583,6 +584,7 @@ class _MLPHead(torch.autograd.Function):
         logits = torch.empty(M, Vp, dtype=cdtype, device=dev)
         k_linear_fwd(h2, w3c, b3p, logits)
         ctx.save_for_backward(hs, h1, h2, w1, w2, w3)
+        ctx.gparams = (w1, b1, w2, b2, w3, b3)
         ctx.cfg = (B, T, V, Vp, cdtype)
         return logits[:, :V].view(B, T, V)
 
@@ -602,19 +604,18 @@ class _MLPHead(torch.autograd.Function):
             dl[:, :V] = dlog.reshape(M, V).to(cdtype)
         w1t, w2t = WEIGHTS.get_t(w1, cdtype), WEIGHTS.get_t(w2, cdtype)
         w3t = WEIGHTS.get_t(w3, cdtype, rows=Vp)
-        dw3, db3 = _empty(Vp, w3.shape[1], dev=dev), _empty(Vp, dev=dev)
-        k_linear_wgrad(dl, h2, dw3, db3)
+        (dw1, _), (db1, _), (dw2, _), (db2, _), (dw3, _), (db3, _) = map(grad_buffer,
+                                                                         ctx.gparams)
+        k_linear_wgrad(dl, h2, dw3, db3, accumulate=True)     # N = V rows of the padded dl
         dh2 = torch.empty_like(h2)
         k_linear_dgrad(dl, w3t, dh2, gate=h2)
-        dw2, db2 = _empty(*w2.shape, dev=dev), _empty(w2.shape[0], dev=dev)
-        k_linear_wgrad(dh2, h1, dw2, db2)
+        k_linear_wgrad(dh2, h1, dw2, db2, accumulate=True)
         dh1 = torch.empty_like(h1)
         k_linear_dgrad(dh2, w2t, dh1, gate=h1)
-        dw1, db1 = _empty(*w1.shape, dev=dev), _empty(w1.shape[0], dev=dev)
-        k_linear_wgrad(dh1, hs, dw1, db1)
+        k_linear_wgrad(dh1, hs, dw1, db1, accumulate=True)
         dhs = torch.empty_like(hs)
         k_linear_dgrad(dh1, w1t, dhs)
-        return dhs, dw1, db1, dw2, db2, dw3[:V], db3[:V], None, None, None
+        return dhs, dw1, db1, dw2, db2, dw3, db3, None, None, None
 
 
 def mlp_head(mlp, hs, B, T, cdtype):

@@ -1,0 +1,276 @@
+"""Fused gradient clipping + AdamW over flat parameter / gradient arenas (MI355X).
+
+Drop-in for the reference's optimizer step (main.py:39-41 builds ``torch.optim.AdamW`` over two
+param groups; engine.py:80-83 runs ``clip_grad_norm_`` then ``optimizer.step()``):
+
+    optimizer = FusedAdamW(param_dicts, lr=config.lr, weight_decay=config.weight_decay)
+    ...
+    optimizer.step(max_norm=max_norm)      # == clip_grad_norm_(params, max_norm); step()
+
+Layout.  At construction every parameter of every group is moved into one fp32 arena ``P``
+(group after group, each parameter 64-byte aligned; ``p.data`` becomes a view), with matching
+arenas ``G`` (gradients), ``M`` / ``V`` (moments).  The HIP kernels (retr_amd/csrc/optim.hip)
+then update a whole group in one streaming pass.  The gradient arena is also where the
+backward kernels write: ``grad_slot(p)`` (used by every retr_amd autograd Function) hands out
+the zeroed ``G`` view of a parameter the first time it receives a gradient after a reset, so
+AccumulateGrad adopts it without a copy and no per-parameter zero-fill is needed.  Gradients
+that arrive elsewhere (a second contributor, a non-retr op, user code) are copied in before
+the update, so results never depend on who produced them.
+
+Semantics match torch.optim.AdamW (amsgrad=False, maximize=False) + clip_grad_norm_ up to
+fp32 rounding; parameters whose ``.grad`` is None are skipped (no decay, no moment update).
+The step counter and the hyper-parameters (lr, weight_decay per group) live on the device so
+a hipGraph-captured step replays correctly; ``sync_hyper()`` pushes host-side lr changes
+(e.g. from a StepLR scheduler) before a replay.
+"""
+import torch
+
+from ._lib import call, ptr, stream
+
+_ALIGN = 16          # floats per arena slot alignment (64 B)
+_NPARTS = 512        # norm partials per contiguous segment
+
+
+def _round(n, a=_ALIGN):
+    return (n + a - 1) // a * a
+
+
+class _GradArena:
+    """Bookkeeping for handing out zeroed gradient views (see module docstring)."""
+
+    def __init__(self, G):
+        self.G = G
+        self.handed = set()
+        self.dirty = False
+
+    def hand_out(self, p):
+        if p.grad is not None or id(p) in self.handed:
+            return None
+        self.handed.add(id(p))
+        self.dirty = True
+        # a new view object: AccumulateGrad adopts a returned gradient only when nothing else
+        # references its TensorImpl (``p._retr_grad_view`` itself would force a copy)
+        return p._retr_grad_view.view(p.shape)
+
+    def reset(self):
+        if self.dirty:
+            self.G.zero_()
+        self.handed.clear()
+        self.dirty = False
+
+
+def grad_slot(p):
+    """Zeroed fp32 gradient buffer for parameter ``p`` to accumulate into and return from an
+    autograd Function, or None (caller allocates a zeroed buffer of its own)."""
+    a = getattr(p, "_retr_arena", None)
+    if a is None:
+        return None
+    return a.hand_out(p)
+
+
+def grad_buffer(p, shape=None):
+    """(buffer, from_arena): a zeroed fp32 buffer shaped like ``p`` (or ``shape``)."""
+    v = grad_slot(p)
+    if v is not None:
+        return (v if shape is None else v.view(shape)), True
+    return torch.zeros(shape if shape is not None else p.shape, dtype=torch.float32,
+                       device=p.device), False
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
+                 amsgrad=False, maximize=False, **unused):
+        if amsgrad or maximize:
+            raise NotImplementedError("FusedAdamW: amsgrad / maximize are not supported")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        maximize=False, foreach=None, capturable=True, differentiable=False,
+                        fused=None)
+        super().__init__(params, defaults)
+        self._build()
+
+    # -- arena construction ----------------------------------------------------------------
+    def _build(self):
+        plist = [p for g in self.param_groups for p in g["params"]]
+        if len({id(p) for p in plist}) != len(plist):
+            raise ValueError("FusedAdamW: a parameter appears in more than one group")
+        dev = plist[0].device
+        for p in plist:
+            if p.dtype != torch.float32 or not p.is_cuda or p.is_sparse:
+                raise TypeError("FusedAdamW: fp32 dense device parameters only")
+            if p.device != dev:
+                raise ValueError("FusedAdamW: all parameters must be on one device")
+        self._slots = {}
+        self._groups = []         # (lo, hi) element range of each group
+        off = 0
+        for g in self.param_groups:
+            lo = off
+            for p in g["params"]:
+                self._slots[id(p)] = (off, p.numel())
+                off += _round(p.numel())
+            self._groups.append((lo, off))
+        total = max(off, _ALIGN)
+        self.P = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.G = torch.zeros_like(self.P)
+        self.M = torch.zeros_like(self.P)
+        self.V = torch.zeros_like(self.P)
+        self.arena = _GradArena(self.G)
+        self._step_t = torch.zeros(1, dtype=torch.float32, device=dev)   # device step count
+        self._global = 0                                  # host mirror of _step_t
+        self._counts = {id(p): 0 for p in plist}          # per-parameter step (torch semantics)
+        self._hyper = torch.zeros(len(self.param_groups), 2, dtype=torch.float32, device=dev)
+        self._hyper_host = None
+        self._partials = torch.zeros(_NPARTS * 2 * len(self.param_groups) + _NPARTS,
+                                     dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p in plist:
+                o, n = self._slots[id(p)]
+                view = self.P[o:o + n].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+                p._retr_grad_view = self.G[o:o + n].view_as(p)
+                p._retr_arena = self.arena
+                self.state[p] = {"exp_avg": self.M[o:o + n].view_as(p),
+                                 "exp_avg_sq": self.V[o:o + n].view_as(p)}
+        self.sync_hyper()
+
+    def sync_hyper(self):
+        """Copy (lr, weight_decay) of every group to the device if they changed."""
+        h = [(float(g["lr"]), float(g["weight_decay"])) for g in self.param_groups]
+        if h != self._hyper_host:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("FusedAdamW: hyper-parameters changed during graph capture")
+            self._hyper.copy_(torch.tensor(h, dtype=torch.float32))
+            self._hyper_host = h
+
+    def covers(self, params):
+        """True if every parameter in ``params`` that requires grad is managed here."""
+        return all(id(p) in self._slots for p in params if p.requires_grad)
+
+    # -- optimizer API ---------------------------------------------------------------------
+    def zero_grad(self, set_to_none=True):
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                if set_to_none:
+                    p.grad = None
+                elif p.grad.data_ptr() != p._retr_grad_view.data_ptr():
+                    p.grad.zero_()
+        self.arena.reset()
+        if not set_to_none:
+            # gradients stay allocated (views of G or foreign tensors) and autograd adds into
+            # them: never hand out slots, and zero G again at the next reset
+            self.arena.handed.update(id(p) for g in self.param_groups for p in g["params"])
+            self.arena.dirty = True
+
+    def _segments(self):
+        """Maximal runs of consecutive parameters (within one group, same step count) that
+        have gradients; gradients living outside the arena are copied in."""
+        segs, foreign, active = [], [], []
+        for gi, g in enumerate(self.param_groups):
+            run = None
+            for p in g["params"]:
+                o, n = self._slots[id(p)]
+                off = self._counts[id(p)] - self._global
+                if p.grad is None or (run is not None and run[3] != off):
+                    if run is not None:
+                        segs.append(run)
+                        run = None
+                    if p.grad is None:
+                        continue
+                if p.grad.is_sparse:
+                    raise RuntimeError("FusedAdamW does not support sparse gradients")
+                if p.grad.data_ptr() != p._retr_grad_view.data_ptr():
+                    p._retr_grad_view.copy_(p.grad)
+                    foreign.append(p)
+                    self.arena.dirty = True
+                active.append(p)
+                if run is None:
+                    run = [gi, o, o + _round(n), off]
+                else:
+                    run[2] = o + _round(n)
+            if run is not None:
+                segs.append(run)
+        return segs, foreign, active
+
+    @torch.no_grad()
+    def step(self, closure=None, max_norm=0.0):
+        """AdamW step; with ``max_norm > 0`` first clip the global gradient 2-norm (exactly
+        ``torch.nn.utils.clip_grad_norm_(params, max_norm)`` over this optimizer's params)."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        if not torch.cuda.is_current_stream_capturing():
+            self.sync_hyper()
+        segs, foreign, active = self._segments()
+        if not segs:
+            return loss
+        nparts = _NPARTS * len(segs)
+        if nparts > self._partials.numel():
+            self._partials = torch.zeros(nparts, dtype=torch.float32, device=self.P.device)
+        st = stream()
+        clip = float(max_norm) > 0
+        for k, (gi, lo, hi, _) in enumerate(segs):
+            call("retr_adamw_sumsq", ptr(self.G) + 4 * lo if clip else None, hi - lo,
+                 ptr(self._partials) + 4 * _NPARTS * k, _NPARTS,
+                 ptr(self._step_t) if k == 0 else None, st)
+        b1, b2 = self.param_groups[0]["betas"]
+        eps = self.param_groups[0]["eps"]
+        for gi, lo, hi, off in segs:
+            g = self.param_groups[gi]
+            if tuple(g["betas"]) != (b1, b2) or g["eps"] != eps:
+                b1, b2 = g["betas"]
+                eps = g["eps"]
+            call("retr_adamw_update", ptr(self.P) + 4 * lo, ptr(self.G) + 4 * lo,
+                 ptr(self.M) + 4 * lo, ptr(self.V) + 4 * lo, hi - lo, ptr(self._hyper) + 8 * gi,
+                 float(b1), float(b2), float(eps), ptr(self._step_t), float(off),
+                 ptr(self._partials), nparts, float(max_norm) if clip else 0.0, st)
+        self._global += 1
+        for p in active:
+            self._counts[id(p)] += 1
+        for p in foreign:          # clipped values back into gradients living elsewhere
+            if clip:
+                p.grad.copy_(p._retr_grad_view)
+        _bump_versions(self.param_groups)
+        return loss
+
+    def state_dict(self):
+        """torch.optim.AdamW layout: per-parameter 'step' (CPU float tensor) + moments."""
+        sd = super().state_dict()
+        idx = [i for g in sd["param_groups"] for i in g["params"]]
+        plist = [p for g in self.param_groups for p in g["params"]]
+        for i, p in zip(idx, plist):
+            st = dict(sd["state"].get(i, {}))
+            st["step"] = torch.tensor(float(self._counts[id(p)]))
+            sd["state"][i] = st
+        return sd
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        # re-seat the loaded moments into the arenas; step counts back to host + device
+        with torch.no_grad():
+            for g in self.param_groups:
+                for p in g["params"]:
+                    o, n = self._slots[id(p)]
+                    s = self.state.get(p, {})
+                    m, v = self.M[o:o + n].view_as(p), self.V[o:o + n].view_as(p)
+                    if "exp_avg" in s:
+                        m.copy_(s["exp_avg"])
+                        v.copy_(s["exp_avg_sq"])
+                    self._counts[id(p)] = int(float(s["step"])) if "step" in s else 0
+                    self.state[p] = {"exp_avg": m, "exp_avg_sq": v}
+            self._global = max(self._counts.values(), default=0)
+            self._step_t.fill_(float(self._global))
+        self._hyper_host = None
+        self.sync_hyper()
+
+
+def _bump_versions(groups):
+    """The kernels write parameters through raw pointers; tell autograd / the compute-copy
+    caches (ops._WeightCache keys on ``_version``) that they changed."""
+    inc = torch.autograd.graph.increment_version
+    for g in groups:
+        for p in g["params"]:
+            if p.grad is not None:
+                inc(p)

@@ -49,13 +49,35 @@ def flops_of(name, a):
     return name, 0.0
 
 
+def shape_of(name, a):
+    """Short shape tag of a call (for the per-shape breakdown)."""
+    if name == "retr_conv2d_fwd":
+        return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} ->{a[10]} k{a[11]} s{a[13]} d{a[15]}"
+    if name == "retr_conv2d_dgrad":
+        return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} <-{a[8]} k{a[9]} s{a[11]} d{a[13]}"
+    if name == "retr_conv2d_wgrad":
+        return f"N{a[3]} {a[4]}x{a[5]}x{a[6]} ->{a[8]} k{a[9]} s{a[11]} d{a[13]}"
+    if name == "retr_linear_fwd":
+        return f"M{a[9]} N{a[10]} K{a[11]} relu{a[12]} res{int(bool(a[13]))}"
+    if name == "retr_linear_dgrad":
+        return f"M{a[8]} N{a[9]} K{a[10]} add{int(bool(a[11]))} gate{int(bool(a[14]))}"
+    if name == "retr_linear_wgrad":
+        return f"M{a[7]} N{a[8]} K{a[9]} db{int(bool(a[10]))} acc{a[11]}"
+    if name == "retr_attention_fwd":
+        return f"B{a[9]} H{a[10]} Lq{a[11]} Lk{a[12]} hd{a[13]} c{a[15]}"
+    if name == "retr_attention_bwd":
+        return f"B{a[18]} H{a[19]} Lq{a[20]} Lk{a[21]} hd{a[22]} c{a[24]}"
+    return ""
+
+
 TRACKED = ("retr_conv2d_fwd", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
            "retr_linear_dgrad", "retr_linear_wgrad", "retr_attention_fwd", "retr_attention_bwd")
 
 
 class Probe:
-    def __init__(self, names=TRACKED):
+    def __init__(self, names=TRACKED, detail=False):
         self.names = set(names)
+        self.detail = detail
         self.records = []     # (key, flops, ev0, ev1)
         self.active = False
 
@@ -63,6 +85,8 @@ class Probe:
         if not self.active:
             return fn()
         key, fl = flops_of(name, args)
+        if self.detail:
+            key = f"{key} | {shape_of(name, args)}"
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()

@@ -18,6 +18,7 @@ import torch
 
 from . import _lib
 from ._lib import call, ptr
+from .optim import grad_buffer
 from .ops import dcode, _st
 
 
@@ -135,7 +136,7 @@ def _conv_wgrad(spec, g, x, in_shape):
     ws = torch.empty(spec.cout, spec.k * spec.k * c, dtype=torch.float32, device=g.device)
     call("retr_conv2d_wgrad", dcode(g.dtype), ptr(g), ptr(x), n, h, w, c, ptr(ws), spec.cout,
          spec.k, spec.k, spec.s, spec.p, spec.d, _st())
-    grad = torch.empty(spec.conv.weight.shape, dtype=torch.float32, device=g.device)
+    grad, _ = grad_buffer(spec.conv.weight)     # sole writer: overwrite mode below
     call("retr_conv_wgrad_unpack", ptr(ws), ptr(scale), ptr(grad), spec.cout, spec.cin, c, spec.k,
          spec.k, 0, _st())
     return grad

@@ -61,6 +61,11 @@ def test_linear_fwd_dgrad_wgrad(dtype, tol, M, N, K):
     db3 = torch.full((Np,), float("nan"), device=DEV)
     ops.k_linear_wgrad(dyc, xc, dw3, db3)           # overwrite mode: no pre-zeroing needed
     assert rel_err(dw3, ref) < tol and rel_err(db3, dyc.float().sum(0)) < tol
+    # exactly N output rows from the column-padded dy (the MLP head's vocab gradient)
+    dw4 = torch.zeros(N, K, device=DEV)
+    db4 = torch.zeros(N, device=DEV)
+    ops.k_linear_wgrad(dyc, xc, dw4, db4, accumulate=True)
+    assert rel_err(dw4, ref[:N]) < tol and rel_err(db4, dyc.float().sum(0)[:N]) < tol
 
 
 CONVS = [  # (N, Cin, H, Cout, k, stride, pad, dil)

@@ -1,0 +1,149 @@
+"""FusedAdamW (retr_amd/optim.py + csrc/optim.hip) against torch.optim.AdamW + clip_grad_norm_
+(the reference's optimizer step, main.py:39-41 / engine.py:80-83), and the gradient arena that
+the backward Functions write into."""
+import copy
+
+import pytest
+import torch
+
+from retr_amd.models.utils import NestedTensor
+from retr_amd.optim import FusedAdamW
+from tests.helpers import make_config
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def _params(seed):
+    g = torch.Generator().manual_seed(seed)
+    shapes = [(7, 13), (256,), (3, 5, 2), (1,), (1000,), (64, 33)]
+    return [torch.nn.Parameter(torch.randn(s, generator=g).to(DEV)) for s in shapes]
+
+
+@pytest.mark.parametrize("max_norm", [0.0, 0.5, 1e6])
+def test_fused_adamw_matches_torch(max_norm):
+    ref = _params(0)
+    mine = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+
+    def groups(ps):
+        return [{"params": ps[:3]}, {"params": ps[3:], "lr": 3e-3, "weight_decay": 0.0}]
+    opt_r = torch.optim.AdamW(groups(ref), lr=1e-2, weight_decay=1e-2, foreach=False)
+    opt_m = FusedAdamW(groups(mine), lr=1e-2, weight_decay=1e-2)
+    g = torch.Generator().manual_seed(1)
+    for it in range(4):
+        grads = [torch.randn(p.shape, generator=g).to(DEV) * (it + 1) for p in ref]
+        for k, (pr, pm, gr) in enumerate(zip(ref, mine, grads)):
+            skip = it == 2 and k in (1, 4)          # parameters without a gradient this step
+            pr.grad = None if skip else gr.clone()
+            pm.grad = None if skip else gr.clone()  # foreign gradients: copied into the arena
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_([p for p in ref if p.grad is not None], max_norm,
+                                           foreach=False)
+        opt_r.step()
+        opt_m.step(max_norm=max_norm)
+        if it == 1:                                  # lr schedule change between steps
+            for o in (opt_r, opt_m):
+                o.param_groups[0]["lr"] *= 0.5
+        for pr, pm in zip(ref, mine):
+            assert _rel(pm.detach(), pr.detach()) < 2e-6
+            if pr.grad is not None:
+                assert _rel(pm.grad, pr.grad) < 2e-6     # clipped gradients written back
+            sr, sm = opt_r.state[pr], opt_m.state[pm]
+            if sr:
+                assert _rel(sm["exp_avg"], sr["exp_avg"]) < 2e-6
+                assert _rel(sm["exp_avg_sq"], sr["exp_avg_sq"]) < 2e-6
+
+
+def test_fused_adamw_state_dict_roundtrip():
+    ps = _params(2)
+    opt = FusedAdamW([{"params": ps}], lr=1e-3)
+    for p in ps:
+        p.grad = torch.ones_like(p)
+    opt.step()
+    sd = copy.deepcopy(opt.state_dict())
+    ps2 = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt2 = FusedAdamW([{"params": ps2}], lr=1e-3)
+    opt2.load_state_dict(sd)
+    for p, q in ((p, q) for p, q in zip(ps, ps2)):
+        assert torch.equal(opt.state[p]["exp_avg"], opt2.state[q]["exp_avg"])
+        p.grad = torch.full_like(p, 0.5)
+        q.grad = torch.full_like(q, 0.5)
+    opt.step()
+    opt2.step()
+    for p, q in zip(ps, ps2):
+        assert torch.equal(p, q)
+
+
+def _micro_model():
+    from bench import build
+    cfg = make_config()
+    model, crit = build(cfg, DEV)
+    return cfg, model, crit
+
+
+def _batch(cfg):
+    from retr_amd.synthetic import synthetic_captions, synthetic_images
+    img, mask = synthetic_images(2, 64, seed=5)
+    caps, cm = synthetic_captions(2, cfg.max_position_embeddings, cfg.vocab_size, seed=6)
+    return (NestedTensor(img.to(DEV), mask.to(DEV)),), caps.to(DEV), cm.to(DEV)
+
+
+def _groups(model, cfg):
+    return [{"params": [p for n, p in model.named_parameters()
+                        if "backbone" not in n and p.requires_grad]},
+            {"params": [p for n, p in model.named_parameters()
+                        if "backbone" in n and p.requires_grad], "lr": cfg.lr_backbone}]
+
+
+def test_train_steps_fused_vs_torch_optimizer():
+    """Three engine.train_step's with FusedAdamW (gradients written straight into the arena)
+    against the same model with torch.optim.AdamW + clip_grad_norm_."""
+    from retr_amd.engine import train_step
+    cfg, m1, crit = _micro_model()
+    _, m2, _ = _micro_model()
+    o1 = FusedAdamW(_groups(m1, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    o2 = torch.optim.AdamW(_groups(m2, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay,
+                           foreach=False)
+    samples, caps, cm = _batch(cfg)
+    m1.train()
+    m2.train()
+    for _ in range(3):
+        l1 = train_step(m1, crit, samples, caps, cm, o1, 0.1)
+        l2 = train_step(m2, crit, samples, caps, cm, o2, 0.1)
+        assert abs(l1.item() - l2.item()) <= 1e-5 * abs(l2.item())
+    # gradients are written straight into the arena; only parameters with several
+    # contributors (the learned query positions, shared by the decoder layers) are summed by
+    # autograd outside it and copied in
+    ps = [q for g in o1.param_groups for q in g["params"]]
+    in_arena = sum(p.grad.data_ptr() == p._retr_grad_view.data_ptr() for p in ps)
+    assert in_arena >= len(ps) - 2, (in_arena, len(ps))
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert _rel(a.detach(), b.detach()) < 1e-5, n
+
+
+def test_gradient_accumulation_with_arena():
+    """Two backward passes without zero_grad accumulate exactly like autograd's default."""
+    cfg, model, crit = _micro_model()
+    opt = FusedAdamW(_groups(model, cfg), lr=cfg.lr)
+    samples, caps, cm = _batch(cfg)
+    model.train()
+
+    def loss():
+        out = model(*samples, caps[:, :-1], cm[:, :-1])
+        return crit(out.permute(0, 2, 1), caps[:, 1:])
+    opt.zero_grad()
+    loss().backward()
+    g1 = {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}
+    loss().backward()
+    for n, p in model.named_parameters():
+        if n in g1:
+            assert _rel(p.grad, 2 * g1[n]) < 1e-6, n
+    opt.zero_grad()
+    loss().backward()
+    for n, p in model.named_parameters():
+        if n in g1:
+            assert _rel(p.grad, g1[n]) < 1e-6, n
