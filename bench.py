@@ -260,7 +260,8 @@ def main():
                                                                      / ddt, 2),
                   "unit": "refs/s", "batch_per_gpu": args.decode_batch, "steps": steps,
                   "config": "cfg5: ResNet-50 dilation=True 224x224, 6/6 d256, bf16, "
-                            "KV-cache greedy (bit-exact to the reference algorithm)"}
+                            "KV-cache greedy, per-step hipGraphs (token ids equal to the "
+                            "reference algorithm)"}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
