@@ -57,9 +57,9 @@ def build(cfg, device, seed=42):
     return model.to(device), crit
 
 
-def make_optimizer(model, cfg, capturable=False, fused=True):
-    """main.py:30-39: two param groups (backbone at lr_backbone), AdamW — by default the
-    MI355X FusedAdamW (clip + AdamW in two kernels over flat arenas, retr_amd/optim.py)."""
+def make_optimizer(model, cfg, capturable=False, fused=False):
+    """main.py:30-39: two param groups (backbone at lr_backbone), AdamW — torch's, or with
+    ``fused`` the MI355X FusedAdamW (clip + AdamW in two kernels over flat arenas)."""
     groups = [{"params": [p for n, p in model.named_parameters()
                           if "backbone" not in n and p.requires_grad]},
               {"params": [p for n, p in model.named_parameters()
@@ -76,7 +76,7 @@ def train_bench(args, rank, world, device):
     cfg = cfg2()
     model, crit = build(cfg, device)
     graphed = world == 1 and not args.eager
-    opt = make_optimizer(model, cfg, capturable=graphed, fused=not args.torch_adamw)
+    opt = make_optimizer(model, cfg, capturable=graphed, fused=args.fused_adamw)
     sync = None
     if world > 1:
         from retr_amd.ddp import GradSync, broadcast_parameters
@@ -221,8 +221,9 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     ap.add_argument("--probe-steps", type=int, default=2)
-    ap.add_argument("--torch-adamw", action="store_true",
-                    help="torch.optim.AdamW + clip_grad_norm_ instead of the fused kernels")
+    ap.add_argument("--fused-adamw", action="store_true",
+                    help="retr_amd FusedAdamW (clip + AdamW kernels over flat arenas) instead of "
+                         "torch.optim.AdamW + clip_grad_norm_")
     ap.add_argument("--probe-detail", default="", help="write a per-shape kernel table here")
     args = ap.parse_args()
 
@@ -277,6 +278,7 @@ def main():
                           "parallelism": f"dp{world}"},
                "loss": round(loss, 4), "roofline": roof, "cpu_baseline": cpu,
                "launch": "eager" if (args.eager or world > 1) else "hipGraph (whole step)",
+               "optimizer": "FusedAdamW" if args.fused_adamw else "torch.optim.AdamW",
                "decode": decode, "kernel_families": families}
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -156,6 +156,10 @@ class FusedAdamW(torch.optim.Optimizer):
                     p.grad = None
                 elif p.grad.data_ptr() != p._retr_grad_view.data_ptr():
                     p.grad.zero_()
+        if torch.cuda.is_current_stream_capturing():
+            # a captured step must clear G on every replay, whatever the host-side dirty flag
+            # says at capture time (the memset before capture leaves it False)
+            self.arena.dirty = True
         self.arena.reset()
         if not set_to_none:
             # gradients stay allocated (views of G or foreign tensors) and autograd adds into

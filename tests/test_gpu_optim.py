@@ -147,3 +147,25 @@ def test_gradient_accumulation_with_arena():
     for n, p in model.named_parameters():
         if n in g1:
             assert _rel(p.grad, g1[n]) < 1e-6, n
+
+
+def test_graphed_step_with_fused_adamw_matches_eager():
+    """engine.GraphedTrainStep (whole step in one hipGraph, FusedAdamW inside) against the same
+    steps run eagerly: the gradient arena must be cleared on every replay."""
+    from retr_amd.engine import GraphedTrainStep, train_step
+    cfg, m1, crit = _micro_model()
+    _, m2, _ = _micro_model()
+    o1 = FusedAdamW(_groups(m1, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    o2 = FusedAdamW(_groups(m2, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    samples, caps, cm = _batch(cfg)
+    m1.train()
+    m2.train()
+    graphed = GraphedTrainStep(m1, crit, o1, 0.1, warmup=2)
+    # first call: 2 eager warm-up steps, capture, 1 replay; then one replay per call -> 7 steps
+    for _ in range(5):
+        lg = graphed(samples, caps, cm).item()
+    for _ in range(7):
+        le = train_step(m2, crit, samples, caps, cm, o2, 0.1).item()
+    assert abs(lg - le) <= 1e-5 * abs(le), (lg, le)
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert _rel(a.detach(), b.detach()) < 1e-5, n
