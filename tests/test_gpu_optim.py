@@ -122,7 +122,7 @@ def test_train_steps_fused_vs_torch_optimizer():
     in_arena = sum(p.grad.data_ptr() == p._retr_grad_view.data_ptr() for p in ps)
     assert in_arena >= len(ps) - 2, (in_arena, len(ps))
     for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
-        assert _rel(a.detach(), b.detach()) < 1e-5, n
+        assert _rel(a.detach(), b.detach()) < 5e-5, n
 
 
 def test_gradient_accumulation_with_arena():
@@ -141,12 +141,12 @@ def test_gradient_accumulation_with_arena():
     loss().backward()
     for n, p in model.named_parameters():
         if n in g1:
-            assert _rel(p.grad, 2 * g1[n]) < 1e-6, n
+            assert _rel(p.grad, 2 * g1[n]) < 1e-5, n     # fp32 atomics: order may differ
     opt.zero_grad()
     loss().backward()
     for n, p in model.named_parameters():
         if n in g1:
-            assert _rel(p.grad, g1[n]) < 1e-6, n
+            assert _rel(p.grad, g1[n]) < 1e-5, n
 
 
 def test_graphed_step_with_fused_adamw_matches_eager():
@@ -168,4 +168,4 @@ def test_graphed_step_with_fused_adamw_matches_eager():
         le = train_step(m2, crit, samples, caps, cm, o2, 0.1).item()
     assert abs(lg - le) <= 1e-5 * abs(le), (lg, le)
     for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
-        assert _rel(a.detach(), b.detach()) < 1e-5, n
+        assert _rel(a.detach(), b.detach()) < 5e-5, n
