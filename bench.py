@@ -52,7 +52,9 @@ def cfg5(dtype="bf16"):
 
 
 def build(cfg, device, seed=42):
-    model, crit = build_model(cfg)
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):    # build_model's prints (caption.py:204,211)
+        model, crit = build_model(cfg)
     model.load_state_dict(synthetic_state_dict(model, seed=seed))
     return model.to(device), crit
 
@@ -76,7 +78,7 @@ def train_bench(args, rank, world, device):
     cfg = cfg2()
     model, crit = build(cfg, device)
     graphed = world == 1 and not args.eager
-    opt = make_optimizer(model, cfg, capturable=graphed, fused=args.fused_adamw)
+    opt = make_optimizer(model, cfg, capturable=graphed, fused=not args.torch_adamw)
     sync = None
     if world > 1:
         from retr_amd.ddp import GradSync, broadcast_parameters
@@ -105,14 +107,12 @@ def train_bench(args, rank, world, device):
         loss = step()
     torch.cuda.synchronize()
     assert torch.isfinite(loss).item(), "non-finite loss in warmup"
-    pr = probe_mod.Probe()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    with pr:   # records only eager launches; graph replays bypass the host entirely
-        for _ in range(args.steps):
-            loss = step()
+    for _ in range(args.steps):
+        loss = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -122,17 +122,16 @@ def train_bench(args, rank, world, device):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     loss_v = float(loss.item())
-    if graphed:
-        # per-kernel HIP-event timing needs host-side launches: re-run the identical step
-        # eagerly (same weights/inputs/stream) with the probe on
-        pr = probe_mod.Probe(detail=bool(args.probe_detail))
-        with pr:
-            for _ in range(args.probe_steps):
-                eager_step()
-        torch.cuda.synchronize()
+    # per-kernel HIP-event timing needs host-side launches: after the timed region, re-run the
+    # identical step eagerly (same weights / inputs / stream) with the probe on
+    pr = probe_mod.Probe(detail=bool(args.probe_detail))
+    with pr:
+        for _ in range(args.probe_steps):
+            eager_step()
+    torch.cuda.synchronize()
     fam = pr.summary()
     if args.probe_detail and rank == 0:
-        nst = args.probe_steps if graphed else args.steps
+        nst = max(1, args.probe_steps)
         with open(args.probe_detail, "w") as f:
             for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms_total"]):
                 f.write(f"{v['ms_total'] / nst:8.3f} ms/step {v['launches'] // nst:4d}x "
@@ -146,8 +145,7 @@ def train_bench(args, rank, world, device):
         for d in fam.values():
             d["ms_avg"] = d["ms_total"] / max(1, d["launches"])
             d["tflops"] = d["flops"] / (d["ms_total"] * 1e-3) / 1e12 if d["ms_total"] else 0.0
-    nsteps = args.probe_steps if graphed else args.steps
-    return dt, loss_v, fam, nsteps
+    return dt, loss_v, fam, max(1, args.probe_steps)
 
 
 def decode_bench(args, rank, world, device):
@@ -175,15 +173,29 @@ def decode_bench(args, rank, world, device):
     return dt, steps
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args):
-    """CPU oracle (oracle/model.py, fp32 eager torch, reference op order) on this host:
-    fwd + CE + backward of config 2 on a bounded sample (batch 2, 640x640)."""
+    """CPU oracle (oracle/model.py: fp32 eager torch in the reference's op order, pinned to the
+    reference by tests/golden) on this host: fwd + CE + backward of config 2 on a bounded
+    sample (batch 2, 640x640), timed steps until ``--cpu-seconds`` have elapsed."""
     from oracle import model as orc
     cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(cores)
     cfg = cfg2("fp32")
     cfg.dropout = 0.0
-    model, _ = build_model(cfg)
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):
+        model, _ = build_model(cfg)
     sd = synthetic_state_dict(model, seed=42)
     trainable = {n for n, p in model.named_parameters() if p.requires_grad}
     sd = {k: (v.requires_grad_(True) if k in trainable else v) for k, v in sd.items()}
@@ -198,14 +210,35 @@ def cpu_baseline(args):
         orc.caption_loss(lo, caps[:, 1:]).backward()
 
     step()
-    n = args.cpu_steps
+    n = 0
     t0 = time.perf_counter()
-    for _ in range(n):
+    while True:
         step()
-    dt = time.perf_counter() - t0
+        n += 1
+        dt = time.perf_counter() - t0
+        if (n >= 2 and dt >= args.cpu_seconds) or n >= 50:
+            break
     return {"value": round(B * n / dt, 4), "unit": "images/s", "cores": cores, "kind": "port",
+            "cpu": _cpu_model(), "seconds": round(dt, 2),
             "sample": f"config 2 shapes (R50 6/6 d256 {args.size}x{args.size}), batch {B}, "
-                      f"{n} timed fwd+CE+bwd steps after 1 warm-up, fp32 oracle/model.py"}
+                      f"{n} timed fwd+CE+bwd steps after 1 warm-up, fp32 oracle/model.py, "
+                      f"{cores} threads"}
+
+
+def _traffic(family):
+    """Per-launch HBM bytes of ``family`` from the committed rocprofv3 --pmc pass
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py with the gfx950 FETCH_SIZE x2
+    correction), or None when no counter pass covers it."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    ent = d.get("families", {}).get(family)
+    if not ent:
+        return None, None
+    return ent.get("bytes_per_launch"), d.get("source")
 
 
 def main():
@@ -218,12 +251,13 @@ def main():
     ap.add_argument("--decode-batch", type=int, default=64)
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU-baseline sample: timed oracle steps until this much CPU time")
     ap.add_argument("--eager", action="store_true", help="no hipGraph capture of the step")
     ap.add_argument("--probe-steps", type=int, default=2)
-    ap.add_argument("--fused-adamw", action="store_true",
-                    help="retr_amd FusedAdamW (clip + AdamW kernels over flat arenas) instead of "
-                         "torch.optim.AdamW + clip_grad_norm_")
+    ap.add_argument("--torch-adamw", action="store_true",
+                    help="torch.optim.AdamW(capturable) + clip_grad_norm_ instead of the default "
+                         "retr_amd FusedAdamW (clip + AdamW kernels over flat arenas)")
     ap.add_argument("--probe-detail", default="", help="write a per-shape kernel table here")
     args = ap.parse_args()
 
@@ -245,11 +279,18 @@ def main():
     if dom_key:
         d = fam[dom_key]
         achieved = d["tflops"]
-        roof = {"bound": "mfma", "kernel": dom_key, "achieved": round(achieved, 2),
-                "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                "launches": d["launches"], "avg_launch_ms": round(d["ms_avg"], 4),
-                "flops_per_launch": d["flops"] / max(1, d["launches"])}
+        traffic, tsrc = _traffic(dom_key)
+        roof = {"bound": "mfma", "kernel": dom_key,
+                "kernel_symbol": probe_mod.FAMILY_SYMBOL.get(dom_key, dom_key),
+                "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                "traffic_source": tsrc,
+                "launches_per_step": d["launches"] // max(1, psteps),
+                "avg_launch_us": round(d["ms_avg"] * 1e3, 2),
+                "flops_per_launch": round(d["flops"] / max(1, d["launches"]), 1),
+                "timing": "HIP events around each launch on torch's current stream (the "
+                          "stream every retr kernel runs on), device spin in front so the "
+                          "events bracket device time only; eager re-run of the step"}
     families = {k: {"ms_per_step": round(v["ms_total"] / psteps, 3),
                     "tflops": round(v["tflops"], 1), "launches_per_step":
                     v["launches"] // psteps} for k, v in sorted(
@@ -278,7 +319,7 @@ def main():
                           "parallelism": f"dp{world}"},
                "loss": round(loss, 4), "roofline": roof, "cpu_baseline": cpu,
                "launch": "eager" if (args.eager or world > 1) else "hipGraph (whole step)",
-               "optimizer": "FusedAdamW" if args.fused_adamw else "torch.optim.AdamW",
+               "optimizer": "torch.optim.AdamW" if args.torch_adamw else "FusedAdamW",
                "decode": decode, "kernel_families": families}
         print(json.dumps(out), flush=True)
     if world > 1:

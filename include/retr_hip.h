@@ -30,6 +30,10 @@ int retr_abi_version(void);
  * fresh masks.  NULL (default) -> the per-op seed alone. */
 void retr_set_seed_base(const unsigned long long* device_ptr);
 int retr_seed_bump(unsigned long long* device_ptr, unsigned long long delta, void* stream);
+/* Measurement only (bench.py kernel probe; no reference counterpart): one wave busy-waits
+ * `us` microseconds on the device clock, so a following event pair times device execution
+ * without the host launch gap. */
+int retr_spin_us(float us, void* stream);
 
 /* ---- linear layers: nn.Linear / MHA in/out-proj / MLP head / feed_forward --------------------
  * replaces F.linear at models/transformer_modules.py:6-11, models/caption.py:161-174,
@@ -139,6 +143,12 @@ int retr_greedy_update(const long long* pred, int B, int T, int i, long long eos
                        void* stream);
 
 /* ---- elementwise helpers --------------------------------------------------------------- */
+/* Encoder output without a final LayerNorm (pre_norm=False; models/ConcatTransformer.py:24,
+ * 105-106): y = cast(x), y2 = cast(x + pos[row % period]) (either output may be NULL) */
+int retr_add_pos_fwd(int dtype, const float* x, long ldx, int M, int C, const float* pos,
+                     int period, void* y, void* y2, long ldy, void* stream);
+/* out[i] (fp32) = a[i] + b[i] (either input may be NULL): gradient of retr_add_pos_fwd */
+int retr_sum2(int dtype, const void* a, const void* b, long n, float* out, void* stream);
 /* y[m][n] = x[m][n] * keep(seed, m*N+n) * scale   (backward of the branch dropout) */
 int retr_dropout_apply(int dtype_out, const float* x, long ldx, void* y, long ldy, int M, int N,
                        float drop_p, unsigned long long seed, void* stream);

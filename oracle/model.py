@@ -188,19 +188,27 @@ def decoder_embeddings(caps, sd, eps, padding_idx=0, p="transformer.embeddings")
                         sd[p + ".LayerNorm.bias"], eps)
 
 
-def caption_forward(sd, cfg, images, img_mask, caps, cap_mask, return_attention=False):
-    """Caption.forward (models/caption.py:23-47) -> ConcatTransformer.forward
-    (models/ConcatTransformer.py:45-74) -> MLP (models/caption.py:161-174).
-    images [B,3,H,W] fp32, img_mask [B,H,W] bool, caps [B,T] int64, cap_mask [B,T] bool."""
-    feats = resnet_body(images, sd, cfg.backbone, cfg.dilation)
-    m = mask_to_features(img_mask, feats.shape[-2:])
-    src = F.conv2d(feats, sd["input_proj.weight"], sd["input_proj.bias"])
-    src = src.flatten(2)            # [B, C, S]
-    m = m.flatten(1)                # [B, S]
+def position_table(sd, cfg, s):
+    """ConcatTransformer.positional_encoding(src) (models/ConcatTransformer.py:55) as [S, C]
+    before the batch repeat: the sine table slice (models/position_encoding.py:24-35) or, for
+    'learned'/'v3', LayerNorm(pos_embed(arange(S))) (position_encoding.py:50-63; its dropout is
+    the identity in the parity setting, like every dropout here)."""
+    if cfg.position_embedding in ("v3", "learned"):
+        p = "transformer.positional_encoding"
+        e = sd[p + ".pos_embed.weight"][:s]
+        return F.layer_norm(e, (e.shape[-1],), sd[p + ".LayerNorm.weight"],
+                            sd[p + ".LayerNorm.bias"], 1e-5)
+    if s > sd["transformer.positional_encoding.pe"].shape[0]:
+        raise RuntimeError(f"sequence length {s} exceeds the sine table")
+    return sd["transformer.positional_encoding.pe"][:s, 0]
+
+
+def transformer_forward(sd, cfg, src, m, caps, cap_mask):
+    """ConcatTransformer.forward (models/ConcatTransformer.py:45-74) on already concatenated
+    src [B, C, S] / mask [B, S].  Returns (hs [T, B, C], attention lists)."""
     bsz, c, s = src.shape
     nhead = cfg.nheads
-    pe = sd["transformer.positional_encoding.pe"]
-    pos = pe[:s].permute(1, 2, 0).repeat(bsz, 1, 1).permute(2, 0, 1)   # [S, B, C]
+    pos = position_table(sd, cfg, s).t().unsqueeze(0).repeat(bsz, 1, 1).permute(2, 0, 1)
     x = src.permute(2, 0, 1)
     tgt = decoder_embeddings(caps, sd, cfg.layer_norm_eps, cfg.pad_token_id).permute(1, 0, 2)
     qpos = sd["transformer.embeddings.position_embeddings.weight"].unsqueeze(1).repeat(1, bsz, 1)
@@ -208,7 +216,7 @@ def caption_forward(sd, cfg, images, img_mask, caps, cap_mask, return_attention=
     for i in range(cfg.enc_layers):
         x, a = encoder_layer(x, sd, f"transformer.encoder.layers.{i}", nhead, pos, m)
         atts["enc_tc_self_att"].append(a)
-    if cfg.pre_norm:
+    if cfg.pre_norm:           # encoder norm exists only with normalize_before (:23-24)
         x = layer_norm(x, sd, "transformer.encoder.norm")
     tmask = causal_mask(tgt.shape[0])
     y = tgt
@@ -217,15 +225,74 @@ def caption_forward(sd, cfg, images, img_mask, caps, cap_mask, return_attention=
                                     cap_mask, m, tmask)
         atts["dec_exp_self_att"].append(a_s)
         atts["dec_exp_tc_cross_att"].append(a_x)
-    hs = layer_norm(y, sd, "transformer.decoder.norm")
+    return layer_norm(y, sd, "transformer.decoder.norm"), atts
+
+
+def mlp_head(hs, sd):
+    """MLP(C, 512, V, 3) (models/caption.py:161-174) on hs [T, B, C] -> logits [B, T, V]."""
     h = hs.permute(1, 0, 2)
     for i in range(3):
         h = F.linear(h, sd[f"mlp.layers.{i}.weight"], sd[f"mlp.layers.{i}.bias"])
         if i < 2:
             h = F.relu(h)
+    return h
+
+
+def image_tokens(sd, cfg, images, img_mask):
+    """Backbone + mask interpolation + input_proj + flatten (models/caption.py:29-36)."""
+    feats = resnet_body(images, sd, cfg.backbone, cfg.dilation)
+    m = mask_to_features(img_mask, feats.shape[-2:])
+    src = F.conv2d(feats, sd["input_proj.weight"], sd["input_proj.bias"])
+    return src.flatten(2), m.flatten(1), m
+
+
+def _finish(hs, atts, sd, return_attention):
+    h = mlp_head(hs, sd)
     if return_attention:
         return h, {k: torch.stack(v) for k, v in atts.items()}
     return h
+
+
+def caption_forward(sd, cfg, images, img_mask, caps, cap_mask, return_attention=False):
+    """Caption.forward (models/caption.py:23-47) -> ConcatTransformer.forward
+    (models/ConcatTransformer.py:45-74) -> MLP (models/caption.py:161-174).
+    images [B,3,H,W] fp32, img_mask [B,H,W] bool, caps [B,T] int64, cap_mask [B,T] bool."""
+    src, m, _ = image_tokens(sd, cfg, images, img_mask)
+    hs, atts = transformer_forward(sd, cfg, src, m, caps, cap_mask)
+    return _finish(hs, atts, sd, return_attention)
+
+
+def caption_loc_forward(sd, cfg, images, img_mask, loc_feats, caps, cap_mask,
+                        return_attention=False):
+    """CaptionLoc.forward (models/caption.py:64-95): one extra memory token
+    loc_proj(loc_feats) (Linear(7, C), :60) appended unmasked after the image tokens."""
+    src, m, _ = image_tokens(sd, cfg, images, img_mask)
+    loc = F.linear(loc_feats, sd["loc_proj.weight"], sd["loc_proj.bias"]).unsqueeze(-1)
+    src = torch.concat([src, loc], 2)
+    m = torch.concat([m, torch.zeros((loc_feats.shape[0], 1)).bool()], 1)
+    hs, atts = transformer_forward(sd, cfg, src, m, caps, cap_mask)
+    return _finish(hs, atts, sd, return_attention)
+
+
+def caption_globalloc_forward(sd, cfg, t_images, t_mask, g_images, g_mask, loc_feats, caps,
+                              cap_mask, return_attention=False):
+    """CaptionGlobalLoc.forward (models/caption.py:113-158): target tokens, then one token per
+    location feature (loc_proj = Linear(1, C) on loc_feats[..., None], :110), then the global
+    context image's tokens (second backbone pass); ensure_unmasked_values (models/utils.py:
+    60-89) is the identity unless a context mask is entirely True."""
+    t_src, t_m, _ = image_tokens(sd, cfg, t_images, t_mask)
+    loc = F.linear(loc_feats.unsqueeze(2), sd["loc_proj.weight"], sd["loc_proj.bias"])
+    loc = loc.permute(0, 2, 1)
+    src = torch.concat([t_src, loc], 2)
+    m = torch.concat([t_m, torch.zeros((loc.shape[0], loc.shape[2])).bool()], 1)
+    g_src, _, g_m = image_tokens(sd, cfg, g_images, g_mask)
+    if not bool(torch.any(g_m.reshape(g_m.shape[0], -1) == False, dim=1).all()):  # noqa: E712
+        raise ValueError("oracle: a fully masked context mask needs the reference's random "
+                         "ensure_unmasked_values filler (not restated)")
+    src = torch.concat([src, g_src], 2)
+    m = torch.concat([m, g_m.flatten(1)], 1)
+    hs, atts = transformer_forward(sd, cfg, src, m, caps, cap_mask)
+    return _finish(hs, atts, sd, return_attention)
 
 
 def caption_loss(logits, caps_out):

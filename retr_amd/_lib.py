@@ -27,6 +27,7 @@ _SIGS = {
     "retr_last_error": [],
     "retr_set_seed_base": [_P],
     "retr_seed_bump": [_P, _U64, _P],
+    "retr_spin_us": [_F, _P],
     "retr_linear_fwd": [_I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _I, _P, _L, _F, _U64, _P],
     "retr_linear_dgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _L, _P, _L, _I,
                           _P],
@@ -58,6 +59,8 @@ _SIGS = {
     "retr_argmax_rows": [_I, _P, _L, _I, _I, _P, _P],
     "retr_dropout_apply": [_I, _P, _L, _P, _L, _I, _I, _F, _U64, _P],
     "retr_cast": [_I, _P, _P, _L, _P],
+    "retr_add_pos_fwd": [_I, _P, _L, _I, _I, _P, _I, _P, _P, _L, _P],
+    "retr_sum2": [_I, _P, _P, _L, _P, _P],
     "retr_pos_grad": [_I, _P, _L, _I, _I, _I, _P, _P],
     "retr_adamw_sumsq": [_P, _L, _P, _I, _P, _P],
     "retr_adamw_update": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P],

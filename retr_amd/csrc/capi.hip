@@ -36,3 +36,18 @@ extern "C" int retr_seed_bump(unsigned long long* p, unsigned long long delta, v
   hipLaunchKernelGGL(seed_bump_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, p, delta);
   return retr_check_launch("seed_bump");
 }
+
+// Measurement helper (bench.py probe): one wave that busy-waits `us` microseconds on the device
+// clock (s_memrealtime, 100 MHz).  Launched just before a probe's start event so the host has
+// already queued the timed kernel when the event executes: the event pair then brackets only
+// device execution, not host launch latency.
+__global__ void spin_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+extern "C" int retr_spin_us(float us, void* stream) {
+  unsigned long long ticks = us > 0.f ? (unsigned long long)(us * 100.f) : 0ull;
+  if (ticks > 100000000ull) ticks = 100000000ull;   // <= 1 s
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ticks);
+  return retr_check_launch("spin");
+}

@@ -167,11 +167,11 @@ struct ConvWgradB {  // B(row = kh,kw,ci ; k = pixel n,oh,ow) = X[n, oh*s-p+kh d
   }
 };
 
-template <typename T, class LA, class LB, class EP>
+template <int FAM, typename T, class LA, class LB, class EP>
 int launch_auto(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits,
                 hipStream_t st, const char* what) {
-  if (N >= 128 && M >= 4096) return launch_gemm<T, 128, 128>(la, lb, ep, M, N, K, splits, st, what);
-  return launch_gemm<T, 64, 64>(la, lb, ep, M, N, K, splits, st, what);
+  if (N >= 128 && M >= 4096) return launch_gemm<FAM, T, 128, 128>(la, lb, ep, M, N, K, splits, st, what);
+  return launch_gemm<FAM, T, 64, 64>(la, lb, ep, M, N, K, splits, st, what);
 }
 
 template <typename T>
@@ -183,10 +183,10 @@ int conv_fwd_t(const void* x, Geom g, const void* w, const float* bias, const vo
   ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseK<T> la{(const T*)x, (long)g.C, M, K};
-    return launch_auto<T>(la, lb, ep, M, N, K, 1, st, "conv_fwd_1x1");
+    return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd_1x1");
   }
   ConvFwdA<T> la{(const T*)x, g, M, K};
-  return launch_auto<T>(la, lb, ep, M, N, K, 1, st, "conv_fwd");
+  return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd");
 }
 
 template <typename T>
@@ -198,10 +198,10 @@ int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* a
   ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseK<T> la{(const T*)dy, (long)g.Co, M, K};
-    return launch_auto<T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad_1x1");
+    return launch_auto<kFamConvDgrad, T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad_1x1");
   }
   ConvDgradA<T> la{(const T*)dy, g, M, K};
-  return launch_auto<T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad");
+  return launch_auto<kFamConvDgrad, T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad");
 }
 
 template <typename T>
@@ -222,12 +222,12 @@ int conv_wgrad_t(const void* dy, const void* x, Geom g, float* ws, hipStream_t s
   ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseT<T> lb{(const T*)x, (long)g.C, Ncols, Mp};
-    return big ? launch_gemm<T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad_1x1")
-               : launch_gemm<T, 64, 64>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad_1x1");
+    return big ? launch_gemm<kFamConvWgrad, T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad_1x1")
+               : launch_gemm<kFamConvWgrad, T, 64, 64>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad_1x1");
   }
   ConvWgradB<T> lb{(const T*)x, g, Ncols, Mp};
-  return big ? launch_gemm<T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad")
-             : launch_gemm<T, 64, 64>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad");
+  return big ? launch_gemm<kFamConvWgrad, T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad")
+             : launch_gemm<kFamConvWgrad, T, 64, 64>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad");
 }
 
 // ---- weight packing: fp32 OIHW (+ FrozenBN buffers) -> folded [Co][KH][KW][Cp] and the

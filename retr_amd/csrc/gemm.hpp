@@ -164,7 +164,12 @@ struct Stager {
   }
 };
 
-template <typename T, int BM, int BN, class LA, class LB, class EP>
+// FAM: call-site family tag (kFam* below); it only makes every family's instantiations
+// distinct kernel symbols, so rocprof summaries group by family (gemm_kernel<FAM, ...>).
+enum { kFamLinearFwd = 0, kFamLinearDgrad = 1, kFamLinearWgrad = 2, kFamConvFwd = 3,
+       kFamConvDgrad = 4, kFamConvWgrad = 5 };
+
+template <int FAM, typename T, int BM, int BN, class LA, class LB, class EP>
 __global__ void __launch_bounds__(256)
 gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
   constexpr int BK = Elem<T>::BK;
@@ -310,7 +315,7 @@ constexpr size_t gemm_lds_bytes() {
 }
 
 // Host-side launcher: picks split-K so that the grid has enough blocks to fill 256 CUs.
-template <typename T, int BM, int BN, class LA, class LB, class EP>
+template <int FAM, typename T, int BM, int BN, class LA, class LB, class EP>
 int launch_gemm(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits,
                 hipStream_t st, const char* what) {
   constexpr int BK = Elem<T>::BK;
@@ -325,12 +330,12 @@ int launch_gemm(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, i
   if constexpr (lds > 65536) {
     static bool attr_set = false;   // once per instantiation (host attribute, capture-safe)
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)gemm_kernel<T, BM, BN, LA, LB, EP>,
+      (void)hipFuncSetAttribute((const void*)gemm_kernel<FAM, T, BM, BN, LA, LB, EP>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       attr_set = true;
     }
   }
-  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, LA, LB, EP>), grid, dim3(256), lds, st, la, lb, ep,
+  hipLaunchKernelGGL((gemm_kernel<FAM, T, BM, BN, LA, LB, EP>), grid, dim3(256), lds, st, la, lb, ep,
                      M, N, K, kchunk, tn);
   return retr_check_launch(what);
 }

@@ -21,8 +21,8 @@ int linear_fwd_t(const void* x, long ldx, const void* w, long ldw, const float* 
   EpiFwd<TO, float> ep{(TO*)y, ldy, bias, res, ldr, relu, dp, (long)N};
   ep.set_vec();
   if (M >= 2048 && N >= 128)
-    return launch_gemm<T, 128, 128>(la, lb, ep, M, N, K, 1, st, "linear_fwd");
-  return launch_gemm<T, 64, 64>(la, lb, ep, M, N, K, 1, st, "linear_fwd");
+    return launch_gemm<kFamLinearFwd, T, 128, 128>(la, lb, ep, M, N, K, 1, st, "linear_fwd");
+  return launch_gemm<kFamLinearFwd, T, 64, 64>(la, lb, ep, M, N, K, 1, st, "linear_fwd");
 }
 
 template <typename T, typename TO, typename TA>
@@ -37,13 +37,13 @@ int linear_dgrad_t(const void* dy, long lddy, const void* w, long ldw, void* dx,
   if (w_trans) {
     DenseK<T> lb{(const T*)w, ldw, K, N};
     if (M >= 2048 && K >= 128)
-      return launch_gemm<T, 128, 128>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
-    return launch_gemm<T, 64, 64>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
+      return launch_gemm<kFamLinearDgrad, T, 128, 128>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
+    return launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
   }
   DenseT<T> lb{(const T*)w, ldw, K, N};
   if (M >= 2048 && K >= 128)
-    return launch_gemm<T, 128, 128>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
-  return launch_gemm<T, 64, 64>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
+    return launch_gemm<kFamLinearDgrad, T, 128, 128>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
+  return launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
 }
 
 // zero an fp32 [rows][cols] region with row stride ld (stream-ordered, graph-capturable)
@@ -73,8 +73,8 @@ int linear_wgrad_t(const void* dy, long lddy, const void* x, long ldx, float* dw
   }
   EpiAccF32 ep{dw, lddw, s > 1, 0, !accumulate && s == 1, db};
   ep.set_vec();
-  if (big) return launch_gemm<T, 128, 128>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
-  return launch_gemm<T, 64, 64>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
+  if (big) return launch_gemm<kFamLinearWgrad, T, 128, 128>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
+  return launch_gemm<kFamLinearWgrad, T, 64, 64>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
 }
 
 // db[n] += sum_m dY[m][n]; one thread per column-pair, blocks stride over rows.

@@ -197,6 +197,33 @@ embed_ln_bwd_kernel(const long long* tok, int M, int T, int C, const float* word
     default: retr_set_error("C=%d unsupported (64,128,256,512,1024)", (int)(C)); return 1; \
   }
 
+
+// y = cast(x), y2 = cast(x + pos[row % period]): the encoder output when there is no final
+// encoder LayerNorm (pre_norm=False, models/ConcatTransformer.py:24,105-106): the decoder then
+// reads memory = x and memory + pos directly.  One thread per 4 consecutive columns.
+template <typename T>
+__global__ void add_pos_kernel(const float* x, long ldx, int M, int C, const float* pos,
+                               int period, T* y, T* y2, long ldy) {
+  const long i = (blockIdx.x * (long)blockDim.x + threadIdx.x) * 4;
+  if (i >= (long)M * C) return;
+  const int row = (int)(i / C), c = (int)(i % C);
+  const float4 v = *(const float4*)(x + (long)row * ldx + c);
+  const float a[4] = {v.x, v.y, v.z, v.w};
+  const float* pr = pos ? pos + (long)(row % period) * C + c : nullptr;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (y) y[(long)row * ldy + c + e] = from_f<T>(a[e]);
+    if (y2) y2[(long)row * ldy + c + e] = from_f<T>(a[e] + (pr ? pr[e] : 0.f));
+  }
+}
+
+// out (fp32) = a + b (either may be null): the gradient of add_pos w.r.t. x
+template <typename T>
+__global__ void sum2_kernel(const T* a, const T* b, long n, float* out) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = (a ? to_f(a[i]) : 0.f) + (b ? to_f(b[i]) : 0.f);
+}
 }  // namespace
 
 extern "C" {
@@ -278,6 +305,39 @@ int retr_embed_ln_bwd(const long long* tokens, int B, int T, int C, const float*
   PER_SWITCH(C, EB)
 #undef EB
   return retr_check_launch("embed_ln_bwd");
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int retr_add_pos_fwd(int dtype, const float* x, long ldx, int M, int C, const float* pos,
+                     int period, void* y, void* y2, long ldy, void* stream) {
+  if (M == 0) return 0;
+  RETR_REQUIRE(C % 4 == 0 && ldx % 4 == 0 && period > 0, "add_pos: C/ld must be %%4");
+  const long n4 = (long)M * C / 4;
+  dim3 grid(cdiv(n4, 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(add_pos_kernel<bf16>, grid, dim3(256), 0, st, x, ldx, M, C, pos, period,
+                       (bf16*)y, (bf16*)y2, ldy);
+  else
+    hipLaunchKernelGGL(add_pos_kernel<float>, grid, dim3(256), 0, st, x, ldx, M, C, pos, period,
+                       (float*)y, (float*)y2, ldy);
+  return retr_check_launch("add_pos_fwd");
+}
+
+int retr_sum2(int dtype, const void* a, const void* b, long n, float* out, void* stream) {
+  if (n == 0) return 0;
+  dim3 grid(cdiv(n, 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(sum2_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)a, (const bf16*)b,
+                       n, out);
+  else
+    hipLaunchKernelGGL(sum2_kernel<float>, grid, dim3(256), 0, st, (const float*)a,
+                       (const float*)b, n, out);
+  return retr_check_launch("sum2");
 }
 
 }  // extern "C"

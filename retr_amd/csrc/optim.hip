@@ -60,7 +60,9 @@ adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const f
     float s = 0.f;
     for (int i = threadIdx.x; i < nparts; i += kThreads) s += partials[i];
     s = block_sum(s, red);
-    coef = fminf(max_norm / (sqrtf(s) + 1e-6f), 1.f);   // clip_grad_norm_: clamp(max=1)
+    // clip_grad_norm_: coef = clamp(max_norm / (norm + 1e-6), max=1); a NaN norm stays NaN
+    // (torch's clamp propagates it and the gradients are always multiplied)
+    coef = (s != s) ? s : fminf(max_norm / (sqrtf(s) + 1e-6f), 1.f);
   }
   const float lr = hyper[0], wd = hyper[1];
   // scalars as torch forms them (python doubles rounded once to fp32)
@@ -69,7 +71,7 @@ adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const f
   const float bc2s = (float)sqrt(1.0 - pow(beta2, t));
   const float step_size = (float)((double)lr / bc1), decay = (float)(1.0 - (double)lr * wd);
   const float omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2), b2f = (float)beta2;
-  const bool scale = coef < 1.f;
+  const bool scale = !(coef >= 1.f);   // also for a NaN coefficient
   for (long i = (long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long)gridDim.x * kThreads) {
     float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
     float* pe = &pp.x; float* ge = &gg.x; float* me = &mm.x; float* ve = &vv.x;

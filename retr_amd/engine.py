@@ -68,6 +68,16 @@ class GraphedTrainStep:
     ``hipGraphLaunch`` replaces ~1.2k individual launches and the Python/ctypes host work.
     Inputs are copied into static device buffers before each replay; dropout masks change
     every replay through the device-side step seed (ops.bump_seed inside the graph).
+
+    First call: ``warmup`` eager steps (kernel attributes, weight copies, optimizer state
+    allocation), then the parameters, optimizer state and step seed are restored to their
+    values before the warm-up, the step is captured and replayed once -- so every call,
+    the first included, applies exactly one update (one reference step) to its batch.
+    After every replay the trainable parameters' autograd versions are bumped (the kernels
+    write them through raw pointers) so version-keyed caches (bf16 weight copies, packed
+    convolution weights, captured decode graphs) never serve values from before the replay,
+    and FusedAdamW's host step counters advance with the device counter.
+
     Requirements: ``optimizer`` built with ``capturable=True`` (or a retr_amd FusedAdamW, whose
     step counter and lr live on the device); fixed batch shapes.
     """
@@ -78,11 +88,60 @@ class GraphedTrainStep:
         self.graph = None
         self.static = None
         self.loss = None
+        self._active = None
 
     def _step(self):
         s_img, s_mask, s_caps, s_cm = self.static
         return train_step(self.model, self.criterion, (NestedTensor(s_img, s_mask),), s_caps,
                           s_cm, self.optimizer, self.max_norm, self.grad_sync)
+
+    def _params(self):
+        return [p for g in self.optimizer.param_groups for p in g["params"]]
+
+    def _snapshot(self):
+        from . import ops
+        from .optim import FusedAdamW
+        opt = self.optimizer
+        seed = ops.seed_base().clone()
+        if isinstance(opt, FusedAdamW):
+            return ("fused", opt.snapshot(), seed)
+        params = [p.detach().clone() for p in self._params()]
+        state = {id(p): {k: (v.clone() if torch.is_tensor(v) else v)
+                         for k, v in opt.state[p].items()} for p in self._params()
+                 if p in opt.state}
+        return ("torch", (params, state), seed)
+
+    @torch.no_grad()
+    def _restore(self, snap):
+        from . import ops
+        kind, data, seed = snap
+        opt = self.optimizer
+        ops.seed_base().copy_(seed)
+        if kind == "fused":
+            opt.restore(data)
+        else:
+            params, state = data
+            for p, v in zip(self._params(), params):
+                p.copy_(v)
+            for p in self._params():
+                st = opt.state.get(p)
+                if not st:
+                    continue
+                old = state.get(id(p))
+                for k, v in st.items():
+                    if not torch.is_tensor(v):
+                        continue
+                    if old is None:           # state created by the warm-up: back to "fresh"
+                        v.zero_()
+                    else:
+                        v.copy_(old[k])
+        self._bump()
+
+    def _bump(self):
+        inc = torch.autograd.graph.increment_version
+        for p in self._params():
+            if p.requires_grad:
+                inc(p)
 
     def __call__(self, samples, caps, cap_masks):
         nt = samples[0]
@@ -92,19 +151,26 @@ class GraphedTrainStep:
             for dst, src in zip(self.static, (nt.tensors, nt.mask, caps, cap_masks)):
                 dst.copy_(src, non_blocking=True)
         if self.graph is None:
+            snap = self._snapshot()
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 for _ in range(self.warmup):
-                    self.loss = self._step()
+                    self._step().detach()
             torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
             self.optimizer.zero_grad(set_to_none=True)
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
-                self.loss = self._step()
+                self.loss = self._step().detach()
+            self._active = list(getattr(self.optimizer, "_last_active", []))
+            self._restore(snap)
         if hasattr(self.optimizer, "sync_hyper"):
             self.optimizer.sync_hyper()      # lr schedule changes reach the captured kernels
         self.graph.replay()
+        if hasattr(self.optimizer, "_advance_host"):
+            self.optimizer._advance_host(self._active)
+        self._bump()
         return self.loss
 
 

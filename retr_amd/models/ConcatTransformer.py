@@ -82,16 +82,29 @@ class ConcatTransformer(nn.Module):
                 nn.init.xavier_uniform_(p)
 
     # ------------------------------------------------------------------------------------------
+    def position_rows(self, B, S):
+        """(table, period): the encoder position encoding as rows consumed by the fused
+        LayerNorm(+pos) kernels — row r of the token matrix uses table[r % period].  Sine
+        (models/position_encoding.py:24-35): the fixed [S, C] slice, period S.  Learned
+        ('learned'/'v3', :50-63): LayerNorm(pos_embed) repeated and dropped out per sample,
+        [B*S, C], period B*S."""
+        from .. import ops
+        from .position_encoding import PositionalEmbedding
+        pe_mod = self.positional_encoding
+        if isinstance(pe_mod, PositionalEmbedding):
+            return ops.learned_pos(pe_mod, B, S, self.training), B * S
+        return pe_mod.table(S), S
+
     def encode(self, src_rows, B, S, kpm_src, cdtype, want_att=False):
         """Encoder stack + final norm.  src_rows: fp32 [B*S, C].  Returns (mem, mem_pos) in the
         compute dtype plus the list of head-averaged self-attention maps if ``want_att``."""
         from .. import ops
-        pe = self.positional_encoding.table(S)
+        pe, period = self.position_rows(B, S)
         x = src_rows
         atts = []
         for layer in self.encoder.layers:
             sa = layer.self_attn
-            n, npos = ops.ln_pos(x, sa.norm, cdtype, pos=pe, period=S)
+            n, npos = ops.ln_pos(x, sa.norm, cdtype, pos=pe, period=period)
             r = ops.self_attn_block(sa, npos, n, x, B, S, kpm_src, False, self.training, cdtype,
                                     want_probs=want_att)
             if want_att:
@@ -102,9 +115,11 @@ class ConcatTransformer(nn.Module):
             ff = layer.ff
             x = ops.ffn_block(ff, ops.ln_pos(x, ff.norm, cdtype), x, self.training, cdtype)
         if self.encoder.norm is None:
-            raise NotImplementedError("pre_norm=False (no encoder final LayerNorm) is not on the "
-                                      "MI355X hot path; the reference template uses pre_norm=True")
-        mem, mem_pos = ops.ln_pos(x, self.encoder.norm, cdtype, pos=pe, period=S)
+            # pre_norm=False: the reference builds no encoder norm (:23-24) and the decoder
+            # reads the raw residual stream as memory
+            mem, mem_pos = ops.add_pos(x, pe, period, cdtype)
+        else:
+            mem, mem_pos = ops.ln_pos(x, self.encoder.norm, cdtype, pos=pe, period=period)
         return mem, mem_pos, atts
 
     def decode(self, mem, mem_pos, B, S, kpm_src, tgt, tgt_mask, cdtype, want_att=False):

@@ -71,29 +71,114 @@ class Caption(nn.Module):
         return out
 
 
-class CaptionLoc(nn.Module):
-    """Parameter container of the location-feature variant (models/caption.py:50-95); its
-    forward is out of the hot-path scope."""
+def _small_linear(x, lin, cdtype):
+    """nn.Linear with a tiny input width (loc_proj: 7 or 1 features) on the MFMA GEMM: the
+    feature dim is zero-padded to the GEMM's 16-byte K granule (the pad contributes exact
+    zeros); the weight gradient flows back through the pad.  x: [M, K] -> fp32 [M, C]."""
+    import torch.nn.functional as F
+    from .. import ops
+    k = lin.in_features
+    if x.shape[-1] != k:       # F.linear's error (the reference's Linear(7) vs 5 features)
+        raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied "
+                           f"({x.shape[0]}x{x.shape[-1]} and {k}x{lin.out_features})")
+    kp = (k + 7) // 8 * 8
+    xp = F.pad(x.float(), (0, kp - k)).to(cdtype).contiguous()
+    wp = F.pad(lin.weight, (0, kp - k))
+    return ops.linear(xp, wp, lin.bias, cdtype, out_f32=True)
+
+
+class _ConcatMixin:
+    """Shared host plumbing of the location / global-context variants: build the memory token
+    rows of ConcatTransformer.forward's concatenation (models/ConcatTransformer.py:47-53) in
+    the batch-major layout of ConcatTransformer.run."""
+
+    def _run(self, parts, target_exp, target_exp_mask, return_attention):
+        from .. import ops
+        b = parts[0][0].shape[0]
+        rows = torch.cat([r for r, _ in parts], 1)            # [B, S_total, C]
+        mask = torch.cat([m for _, m in parts], 1)            # [B, S_total]
+        s = rows.shape[1]
+        hs, att = self.transformer.run(rows.reshape(b * s, -1), b, s, mask, target_exp,
+                                       target_exp_mask, self.cdtype,
+                                       return_attention=return_attention)
+        out = ops.mlp_head(self.mlp, hs, b, target_exp.shape[1], self.cdtype)
+        if return_attention:
+            return out, att
+        return out
+
+    def _image_part(self, samples):
+        src, mask, b, s = self.encode_image(samples)
+        return src.view(b, s, -1), mask
+
+    def set_compute_dtype(self, dtype):
+        self.cdtype = dtype
+        self.transformer.cdtype = dtype
+        self.backbone.cdtype = dtype
+        return self
+
+
+class CaptionLoc(_ConcatMixin, Caption):
+    """Target image + location features (models/caption.py:50-95): ``loc_proj = Linear(7, C)``
+    maps the location vector to one extra, never-masked memory token appended after the image
+    tokens.  The dataset's position features have 5 entries (data_utils/utils.py:200-237), so
+    with the reference's Linear(7) a real batch fails exactly as in the reference (F.linear's
+    shape error); 7-feature inputs run."""
 
     def __init__(self, backbone, transformer, positional_encoding, hidden_dim, vocab_size):
-        super().__init__()
+        nn.Module.__init__(self)          # registration order = reference (parameter order)
         self.backbone = backbone
         self.positional_encoding = positional_encoding
         self.input_proj = nn.Conv2d(backbone.num_channels, hidden_dim, kernel_size=1)
         self.loc_proj = nn.Linear(7, hidden_dim)
         self.transformer = transformer
         self.mlp = MLP(hidden_dim, 512, vocab_size, 3)
+        self.cdtype = torch.bfloat16
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("CaptionLoc is not on the MI355X hot path (SURVEY.md §8 f3)")
+    def forward(self, t_samples, loc_feats, target_exp, target_exp_mask, return_attention=False):
+        t_rows, t_mask = self._image_part(t_samples)
+        b = t_rows.shape[0]
+        loc = _small_linear(loc_feats.reshape(b, -1), self.loc_proj, self.cdtype)   # [B, C]
+        loc_mask = torch.zeros((b, 1), dtype=torch.bool, device=t_mask.device)
+        return self._run([(t_rows, t_mask), (loc.view(b, 1, -1), loc_mask)], target_exp,
+                         target_exp_mask, return_attention)
 
 
-class CaptionGlobalLoc(CaptionLoc):
-    """Parameter container of models/caption.py:98-158 (``loc_proj = Linear(1, C)``)."""
+class CaptionGlobalLoc(_ConcatMixin, Caption):
+    """Target image + location features + global context image (models/caption.py:98-158):
+    memory = [target tokens, one token per location feature (``loc_proj = Linear(1, C)`` on
+    each scalar), context-image tokens (second backbone pass, its mask passed through
+    ensure_unmasked_values)]."""
 
     def __init__(self, backbone, transformer, positional_encoding, hidden_dim, vocab_size):
-        super().__init__(backbone, transformer, positional_encoding, hidden_dim, vocab_size)
+        nn.Module.__init__(self)          # registration order = reference (parameter order)
+        self.backbone = backbone
+        self.positional_encoding = positional_encoding
+        self.input_proj = nn.Conv2d(backbone.num_channels, hidden_dim, kernel_size=1)
         self.loc_proj = nn.Linear(1, hidden_dim)
+        self.transformer = transformer
+        self.mlp = MLP(hidden_dim, 512, vocab_size, 3)
+        self.cdtype = torch.bfloat16
+
+    def forward(self, t_samples, g_samples, loc_feats, target_exp, target_exp_mask,
+                return_attention=False):
+        from .utils import ensure_unmasked_values
+        t_rows, t_mask = self._image_part(t_samples)
+        b = t_rows.shape[0]
+        nf = loc_feats.shape[1]
+        loc = _small_linear(loc_feats.reshape(b * nf, 1), self.loc_proj, self.cdtype)
+        loc_mask = torch.zeros((b, nf), dtype=torch.bool, device=t_mask.device)
+        if not isinstance(g_samples, NestedTensor):
+            g_samples = nested_tensor_from_tensor_list(g_samples)
+        feats, g_mask = self.backbone.features(g_samples, self.cdtype)
+        gb, gh, gw, cb = feats.shape
+        g_mask = ensure_unmasked_values(g_mask)
+        from .. import ops
+        g_rows = ops.linear(feats.view(gb * gh * gw, cb), self.input_proj.weight,
+                            self.input_proj.bias, self.cdtype, out_f32=True,
+                            dgate=feats.view(gb * gh * gw, cb))
+        return self._run([(t_rows, t_mask), (loc.view(b, nf, -1), loc_mask),
+                          (g_rows.view(gb, gh * gw, -1), g_mask.view(gb, gh * gw))],
+                         target_exp, target_exp_mask, return_attention)
 
 
 class CrossEntropyLoss(nn.CrossEntropyLoss):
@@ -123,8 +208,7 @@ def build_model(config):
     else:
         raise NotImplementedError()
     model = Model(backbone, transformer, None, config.hidden_dim, config.vocab_size)
-    if isinstance(model, Caption):
-        model.set_compute_dtype(compute_dtype(config))
+    model.set_compute_dtype(compute_dtype(config))
     print(f"Built {model.__class__.__name__} model with {transformer.__class__.__name__}")
     criterion = CrossEntropyLoss()
     return model, criterion

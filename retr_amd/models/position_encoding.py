@@ -36,8 +36,10 @@ class PositionalEncoding(nn.Module):
 
 
 class PositionalEmbedding(nn.Module):
-    """Learned variant ('learned'/'v3', models/position_encoding.py:38-63): parameter container
-    kept for state_dict compatibility; the hot path implements the sine variant."""
+    """Learned variant ('learned'/'v3', models/position_encoding.py:38-63): LayerNorm of the
+    first S rows of ``pos_embed``, repeated over the batch, dropout (fixed p=0.1 like the
+    reference).  On the hot path ConcatTransformer.position_rows runs it as ops.learned_pos
+    (HIP LayerNorm + dropout kernels) and feeds the fused LayerNorm+pos kernels."""
 
     def __init__(self, embedding_dim, dropout=0.1, max_position_embeddings=5000):
         super().__init__()
@@ -45,9 +47,12 @@ class PositionalEmbedding(nn.Module):
         self.LayerNorm = nn.LayerNorm(embedding_dim)
         self.dropout = nn.Dropout(dropout)
 
-    def table(self, seq_len):
-        raise NotImplementedError("learned position embeddings are not on the MI355X hot path "
-                                  "(SURVEY.md §8 f4); use position_embedding='sine'")
+    def forward(self, x):
+        """x: [B, C, S] -> embeddings [B, C, S] (reference layout)."""
+        from .. import ops
+        b, _, s = x.shape
+        rows = ops.learned_pos(self, b, s, self.training)
+        return rows.view(b, s, -1).permute(0, 2, 1)
 
 
 def build_position_encoding(config):

@@ -34,6 +34,26 @@ def generate_square_subsequent_mask(sz):
     return mask
 
 
+def ensure_unmasked_values(mask, unmasked_ratio=0.01):
+    """models/utils.py:60-89: a sample whose mask is entirely True (nothing to attend to) gets a
+    random filler mask with ``round(h*w*unmasked_ratio)`` positions unmasked (numpy's global
+    RNG, as the reference); other samples are untouched.  Used on the global-context mask of
+    CaptionGlobalLoc (models/caption.py:140)."""
+    import numpy as np
+    b, h, w = mask.shape
+    flat = mask.reshape((b, -1))
+    has_unmasked = torch.any(flat == False, dim=1)  # noqa: E712
+    if False in has_unmasked:
+        filler = torch.ones((h, w), dtype=bool, device=mask.device.type)
+        ff = filler.flatten()
+        idx = np.indices(ff.shape).flatten()
+        pick = np.random.choice(idx, replace=False, size=round(idx.size * unmasked_ratio))
+        ff[pick] = False
+        filler = ff.reshape((h, w))
+        mask[~has_unmasked] = filler
+    return mask
+
+
 def nested_tensor_from_tensor_list(tensor_list: List[Tensor]):
     """Zero-pad a list of [3,h,w] images to the max size; mask True on padding."""
     if tensor_list[0].ndim != 3:

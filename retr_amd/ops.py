@@ -674,3 +674,108 @@ def argmax_rows(x2d):
     out = torch.empty(M, dtype=torch.long, device=x2d.device)
     call("retr_argmax_rows", dcode(x2d.dtype), ptr(x2d), x2d.stride(0), M, V, ptr(out), _st())
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# encoder output without a final LayerNorm (pre_norm=False) and learned position embeddings
+# ---------------------------------------------------------------------------------------------
+
+class _AddPos(torch.autograd.Function):
+    """(cast(x), cast(x + pos[row % period])): memory and memory+pos for the decoder when the
+    encoder has no final LayerNorm (models/ConcatTransformer.py:24, :105-106 with
+    normalize_before=False; the cross-attention keys add ``pos`` at
+    transformer_modules.py:61-62)."""
+
+    @staticmethod
+    def forward(ctx, x, pos, period, cdtype):
+        _lib.require_device(x)
+        M, C = x.shape
+        y = torch.empty(M, C, dtype=cdtype, device=x.device)
+        y2 = torch.empty_like(y)
+        posd = pos.detach().contiguous()
+        call("retr_add_pos_fwd", dcode(cdtype), ptr(x), x.stride(0), M, C, ptr(posd), int(period),
+             ptr(y), ptr(y2), C, _st())
+        ctx.cfg = (M, C, period, tuple(pos.shape))
+        return y, y2
+
+    @staticmethod
+    def backward(ctx, dy, dy2):
+        M, C, period, pshape = ctx.cfg
+        ref = dy if dy is not None else dy2
+        dev = ref.device
+        dy = dy.contiguous() if dy is not None else None
+        dy2 = dy2.contiguous() if dy2 is not None else None
+        if dy is not None and dy2 is not None and dy.dtype != dy2.dtype:
+            dy2 = dy2.to(dy.dtype)
+        dx = torch.empty(M, C, dtype=torch.float32, device=dev)
+        call("retr_sum2", dcode(ref.dtype), ptr(dy), ptr(dy2), M * C, ptr(dx), _st())
+        dpos = None
+        if ctx.needs_input_grad[1] and dy2 is not None:
+            dpos = torch.zeros(pshape, dtype=torch.float32, device=dev)
+            call("retr_pos_grad", dcode(dy2.dtype), ptr(dy2), C, M, C, period, ptr(dpos), _st())
+        return dx, dpos, None, None
+
+
+def add_pos(x, pos, period, cdtype):
+    return _AddPos.apply(x, pos, period, cdtype)
+
+
+class _LearnedPos(torch.autograd.Function):
+    """PositionalEmbedding.forward (models/position_encoding.py:50-63): the [S, C] table
+    LayerNorm(pos_embed[0:S]) repeated over the batch and dropped out per (b, s, c) (dropout
+    after the repeat, so every sample has its own mask).  Returns batch-major rows
+    [B*S, C] fp32 (consumed by the fused LayerNorm + position kernels with period B*S)."""
+
+    @staticmethod
+    def forward(ctx, weight, gamma, beta, B, S, eps, drop_p):
+        _lib.require_device(weight)
+        C = weight.shape[1]
+        dev = weight.device
+        if S > weight.shape[0]:
+            raise RuntimeError(f"index out of range: position {S - 1} >= num_embeddings "
+                               f"{weight.shape[0]}")
+        tab = torch.empty(S, C, dtype=torch.float32, device=dev)
+        mean = torch.empty(S, dtype=torch.float32, device=dev)
+        rstd = torch.empty_like(mean)
+        wd = weight.detach()
+        call("retr_layernorm_fwd", F32, ptr(wd), wd.stride(0), ptr(gamma), ptr(beta), float(eps),
+             S, C, ptr(tab), C, None, None, 1, ptr(mean), ptr(rstd), _st())
+        rep = tab.repeat(B, 1)
+        seed = next_seed()
+        if drop_p > 0:
+            call("retr_dropout_apply", F32, ptr(rep), C, ptr(rep), C, B * S, C, float(drop_p),
+                 seed, _st())
+        ctx.save_for_backward(weight, gamma, mean, rstd)
+        ctx.cfg = (B, S, C, drop_p, seed)
+        return rep
+
+    @staticmethod
+    def backward(ctx, dout):
+        weight, gamma, mean, rstd = ctx.saved_tensors
+        B, S, C, drop_p, seed = ctx.cfg
+        dev = weight.device
+        d = dout.float().contiguous()
+        if drop_p > 0:
+            dd = torch.empty_like(d)
+            call("retr_dropout_apply", F32, ptr(d), C, ptr(dd), C, B * S, C, float(drop_p), seed,
+                 _st())
+            d = dd
+        dtab = torch.zeros(S, C, dtype=torch.float32, device=dev)
+        call("retr_pos_grad", F32, ptr(d), C, B * S, C, S, ptr(dtab), _st())
+        dw, _ = grad_buffer(weight)
+        dgamma, _ = grad_buffer(gamma)
+        dbeta, _ = grad_buffer(beta)
+        wd = weight.detach()
+        # rows 0..S-1 of the (zeroed) embedding gradient are written directly; rows >= S get
+        # no gradient, as from nn.Embedding with ids arange(S)
+        call("retr_layernorm_bwd", F32, ptr(dtab), None, C, ptr(wd), wd.stride(0), ptr(gamma),
+             ptr(mean), ptr(rstd), S, C, ptr(dw), dw.stride(0), None, ptr(dgamma), ptr(dbeta),
+             _st())
+        return dw, dgamma, dbeta, None, None, None, None
+
+
+def learned_pos(pe_module, B, S, training):
+    """pe_module: PositionalEmbedding container (.pos_embed, .LayerNorm, .dropout)."""
+    return _LearnedPos.apply(pe_module.pos_embed.weight, pe_module.LayerNorm.weight,
+                             pe_module.LayerNorm.bias, B, S, pe_module.LayerNorm.eps,
+                             _drop_p(training, pe_module.dropout.p))

@@ -230,14 +230,36 @@ class FusedAdamW(torch.optim.Optimizer):
                  ptr(self.M) + 4 * lo, ptr(self.V) + 4 * lo, hi - lo, ptr(self._hyper) + 8 * gi,
                  float(b1), float(b2), float(eps), ptr(self._step_t), float(off),
                  ptr(self._partials), nparts, float(max_norm) if clip else 0.0, st)
-        self._global += 1
-        for p in active:
-            self._counts[id(p)] += 1
+        self._advance_host(active)
+        self._last_active = active
         for p in foreign:          # clipped values back into gradients living elsewhere
             if clip:
                 p.grad.copy_(p._retr_grad_view)
         _bump_versions(self.param_groups)
         return loss
+
+    def _advance_host(self, active):
+        """Host mirror of one executed step (called by step(), and by GraphedTrainStep after
+        every replay of a captured step, whose kernels advance only the device counter)."""
+        self._global += 1
+        for p in active:
+            self._counts[id(p)] += 1
+
+    def snapshot(self):
+        """Device copies of parameters / moments / step counter plus the host counters."""
+        return (self.P.clone(), self.M.clone(), self.V.clone(), self._step_t.clone(),
+                self._global, dict(self._counts))
+
+    def restore(self, snap):
+        """In-place restore of ``snapshot()`` (pointers stay valid for captured graphs)."""
+        P, M, V, t, g, counts = snap
+        with torch.no_grad():
+            self.P.copy_(P)
+            self.M.copy_(M)
+            self.V.copy_(V)
+            self._step_t.copy_(t)
+        self._global = g
+        self._counts = dict(counts)
 
     def state_dict(self):
         """torch.optim.AdamW layout: per-parameter 'step' (CPU float tensor) + moments."""

@@ -3,6 +3,14 @@
 When a ``Probe`` is installed, every C-ABI call whose name it tracks is bracketed by two
 ``torch.cuda.Event``s recorded on torch's current stream — the stream every retr kernel is
 launched on — and its algorithmic FLOPs are computed from the call's shape arguments.
+A short device-side spin (``retr_spin_us``) is queued in front of the start event, so by the
+time the event executes the host has already queued the kernel: the event pair brackets the
+kernel's device execution, not the host's launch latency (which a plain eager re-run would
+add to every launch).
+
+Family keys match the GEMM kernel's family tag (``gemm_kernel<FAM, ...>`` in csrc/gemm.hpp:
+0 linear_fwd, 1 linear_dgrad, 2 linear_wgrad, 3 conv_fwd, 4 conv_dgrad, 5 conv_wgrad) and the
+attention kernels, so a family's time here and its rows in a rocprofv3 summary agree.
 """
 import torch
 
@@ -22,15 +30,15 @@ def flops_of(name, a):
     if name == "retr_conv2d_fwd":
         _, _, n, h, w, c, _, _, _, _, co, kh, kw, s, p, d = a[:16]
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
-        return f"conv_fwd_{_conv_variant(kh, s, p)}", 2.0 * n * oh * ow * co * kh * kw * c
+        return "conv_fwd", 2.0 * n * oh * ow * co * kh * kw * c
     if name == "retr_conv2d_dgrad":
         _, _, n, h, w, c, _, _, co, kh, kw, s, p, d = a[:14]
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
-        return f"conv_dgrad_{_conv_variant(kh, s, p)}", 2.0 * n * oh * ow * co * kh * kw * c
+        return "conv_dgrad", 2.0 * n * oh * ow * co * kh * kw * c
     if name == "retr_conv2d_wgrad":
         _, _, _, n, h, w, c, _, co, kh, kw, s, p, d = a[:14]
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
-        return f"conv_wgrad_{_conv_variant(kh, s, p)}", 2.0 * n * oh * ow * co * kh * kw * c
+        return "conv_wgrad", 2.0 * n * oh * ow * co * kh * kw * c
     if name in ("retr_linear_fwd",):
         m, n, k = a[9], a[10], a[11]
         return "linear_fwd", 2.0 * m * n * k
@@ -74,10 +82,33 @@ TRACKED = ("retr_conv2d_fwd", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_li
            "retr_linear_dgrad", "retr_linear_wgrad", "retr_attention_fwd", "retr_attention_bwd")
 
 
+FAMILY_SYMBOL = {"linear_fwd": "gemm_kernel<0,", "linear_dgrad": "gemm_kernel<1,",
+                 "linear_wgrad": "gemm_kernel<2,", "conv_fwd": "gemm_kernel<3,",
+                 "conv_dgrad": "gemm_kernel<4,", "conv_wgrad": "gemm_kernel<5,",
+                 "attention_fwd": "attn_fwd_kernel",
+                 "attention_bwd": "attn_bwd_"}
+
+
+def family_of_symbol(name):
+    """Family key of a rocprof kernel name (mangled ``_ZN4retr11gemm_kernelILi3E...`` or
+    demangled ``retr::gemm_kernel<3, ...>``), or None."""
+    import re
+    m = re.search(r"gemm_kernelILi(\d+)E", name) or re.search(r"gemm_kernel<(\d+),", name)
+    if m:
+        return ("linear_fwd", "linear_dgrad", "linear_wgrad", "conv_fwd", "conv_dgrad",
+                "conv_wgrad")[int(m.group(1))]
+    if "attn_fwd_kernel" in name:
+        return "attention_fwd"
+    if "attn_bwd_" in name:
+        return "attention_bwd"
+    return None
+
+
 class Probe:
-    def __init__(self, names=TRACKED, detail=False):
+    def __init__(self, names=TRACKED, detail=False, spin_us=40.0):
         self.names = set(names)
         self.detail = detail
+        self.spin_us = spin_us
         self.records = []     # (key, flops, ev0, ev1)
         self.active = False
 
@@ -89,6 +120,8 @@ class Probe:
             key = f"{key} | {shape_of(name, args)}"
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
+        if self.spin_us > 0:
+            _lib._raw_call("retr_spin_us", (float(self.spin_us), _lib.stream()))
         e0.record()
         fn()
         e1.record()

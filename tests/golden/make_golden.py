@@ -9,7 +9,7 @@ restatement in ``oracle/tv_resnet.py``; everything else is the reference's code.
 Inputs are fully deterministic (retr_amd.synthetic: numpy PCG64 per state_dict key; images /
 captions from fixed seeds), so the fixtures store only outputs and the tests regenerate inputs.
 
-    python tests/golden/make_golden.py            # writes tests/golden/*.npz
+    python tests/golden/make_golden.py [case ...]   # writes tests/golden/*.npz
 """
 import os
 import sys
@@ -25,7 +25,8 @@ sys.path.insert(0, ROOT)
 from oracle.tv_resnet import install_torchvision_standin  # noqa: E402
 from retr_amd.synthetic import (synthetic_captions, synthetic_images,  # noqa: E402
                                 synthetic_state_dict)
-from tests.helpers import PARITY_CASES, make_config  # noqa: E402
+from tests.helpers import (F2_CASE, PARITY_CASES, VARIANT_CASES, f2_inputs,  # noqa: E402
+                           make_config, variant_config, variant_inputs)
 
 SMALL_GRADS = ("input_proj.bias", "transformer.decoder.norm.weight", "mlp.layers.2.bias",
                "transformer.embeddings.position_embeddings.weight",
@@ -102,10 +103,77 @@ def make_case(name, caption, utils, decode):
     print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB) loss={out['loss']:.6f}")
 
 
+def _grads(model, out):
+    names, norms = [], []
+    for n, p in model.named_parameters():
+        if p.requires_grad and p.grad is not None:
+            names.append(n)
+            norms.append(p.grad.norm().item())
+    out["grad_names"] = np.array(names)
+    out["grad_norms"] = np.array(norms)
+
+
+def make_variant(name, caption, utils):
+    """Non-default reference surfaces (pre_norm=False): CaptionLoc,
+    CaptionGlobalLoc, learned position embeddings, post-norm encoder (no final LayerNorm)."""
+    cfg = variant_config(name)
+    torch.manual_seed(0)
+    model, criterion = caption.build_model(cfg)
+    sd = synthetic_state_dict(model, seed=42)
+    model.load_state_dict(sd)
+    pe = model.transformer.positional_encoding
+    if hasattr(pe, "dropout"):
+        pe.dropout.p = 0.0      # the learned PE's own dropout is fixed at 0.1 in the reference
+    images, mask, extra, caps, cap_mask = variant_inputs(name, cfg)
+    args = [utils.NestedTensor(images, mask)]
+    for e in extra:
+        args.append(utils.NestedTensor(*e) if isinstance(e, tuple) else e)
+    model.train()
+    logits = model(*args, caps[:, :-1], cap_mask[:, :-1])
+    loss = criterion(logits.permute(0, 2, 1), caps[:, 1:])
+    loss.backward()
+    out = {"loss": np.float64(loss.item()), "logits": logits.detach().numpy()}
+    _grads(model, out)
+    path = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB) loss={out['loss']:.6f}")
+
+
+def make_f2(ct_module):
+    """the transformer half at real depth (6/6, d256, nhead 8, S=196, T=128)
+    imported directly from models/ConcatTransformer.py (no torchvision shim involved)."""
+    kw = F2_CASE
+    cfg = make_config(dtype="fp32", **kw)
+    torch.manual_seed(0)
+    tr = ct_module.build_transformer(cfg)
+    sd = synthetic_state_dict(tr, seed=43)
+    tr.load_state_dict(sd)
+    tr.train()
+    src, mask, caps, cap_mask, weight = f2_inputs(cfg)
+    src.requires_grad_(True)
+    hs, atts = tr(src, mask, None, None, caps, cap_mask)
+    (hs * weight).sum().backward()
+    out = {"hs": hs.detach().numpy(), "src_grad": src.grad.numpy()}
+    for k, v in atts.items():
+        out["att/" + k] = v.detach()[:, :, ::7].numpy()       # every 7th query row
+    _grads(tr, out)
+    path = os.path.join(HERE, "f2_transformer.npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e3:.0f} kB)")
+
+
 def main():
     caption, utils, decode = ref_modules()
-    for name in PARITY_CASES:
-        make_case(name, caption, utils, decode)
+    import importlib
+    ct = importlib.import_module("models.ConcatTransformer")
+    which = sys.argv[1:] or (list(PARITY_CASES) + list(VARIANT_CASES) + ["f2"])
+    for name in which:
+        if name in PARITY_CASES:
+            make_case(name, caption, utils, decode)
+        elif name in VARIANT_CASES:
+            make_variant(name, caption, utils)
+        elif name == "f2":
+            make_f2(ct)
 
 
 if __name__ == "__main__":

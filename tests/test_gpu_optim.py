@@ -161,11 +161,94 @@ def test_graphed_step_with_fused_adamw_matches_eager():
     m1.train()
     m2.train()
     graphed = GraphedTrainStep(m1, crit, o1, 0.1, warmup=2)
-    # first call: 2 eager warm-up steps, capture, 1 replay; then one replay per call -> 7 steps
+    # every call applies exactly one update (the warm-up steps are rolled back before capture)
     for _ in range(5):
         lg = graphed(samples, caps, cm).item()
-    for _ in range(7):
+    for _ in range(5):
         le = train_step(m2, crit, samples, caps, cm, o2, 0.1).item()
     assert abs(lg - le) <= 1e-5 * abs(le), (lg, le)
     for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
         assert _rel(a.detach(), b.detach()) < 5e-5, n
+
+
+def _micro_bf16(lr):
+    from bench import build
+    cfg = make_config(dtype="bf16")
+    cfg.lr = lr
+    model, crit = build(cfg, DEV)
+    return cfg, model, crit
+
+
+def _make_opt(kind, model, cfg):
+    if kind == "fused":
+        return FusedAdamW(_groups(model, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    return torch.optim.AdamW(_groups(model, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay,
+                             capturable=True, foreach=False)
+
+
+@pytest.mark.parametrize("kind", ["fused", "torch"])
+def test_graphed_bf16_step_matches_eager_then_eval(kind):
+    """The benchmarked path: GraphedTrainStep in bf16 (bf16 weight copies refreshed inside the
+    replayed graph) == eager train_step, one update per call from the first call on; eager
+    forwards and greedy decodes after replays see the replayed weights (no stale caches)."""
+    from retr_amd.engine import GraphedTrainStep, train_step
+    from retr_amd.eval_utils.decode import greedy
+    lr = 2e-3                      # large enough that stale weights would be obvious
+    cfg, m1, crit = _micro_bf16(lr)
+    _, m2, _ = _micro_bf16(lr)
+    o1, o2 = _make_opt(kind, m1, cfg), _make_opt(kind, m2, cfg)
+    samples, caps, cm = _batch(cfg)
+    graphed = GraphedTrainStep(m1, crit, o1, 0.1, warmup=2)
+
+    def train(n):
+        for _ in range(n):
+            m1.train()
+            m2.train()
+            lg = graphed(samples, caps, cm).item()
+            le = train_step(m2, crit, samples, caps, cm, o2, 0.1).item()
+            assert abs(lg - le) <= 2e-3 * abs(le), (lg, le)
+
+    def compare_eval():
+        m1.eval()
+        m2.eval()
+        with torch.no_grad():
+            a = m1(*samples, caps[:, :-1], cm[:, :-1]).float()
+            b = m2(*samples, caps[:, :-1], cm[:, :-1]).float()
+        assert ((a - b).norm() / b.norm()).item() < 1e-2
+        ia = greedy(list(samples), m1, max_len=cfg.max_position_embeddings, bos_token=101,
+                    eos_token=102)
+        ib = greedy(list(samples), m2, max_len=cfg.max_position_embeddings, bos_token=101,
+                    eos_token=102)
+        assert (ia == ib).float().mean().item() > 0.9
+
+    train(3)
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert _rel(a.detach(), b.detach()) < 2e-3, n
+    compare_eval()
+    train(3)                     # replays after an eager eval (caches refreshed by the eval)
+    compare_eval()
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert _rel(a.detach(), b.detach()) < 2e-3, n
+    if kind == "fused":
+        s1, s2 = o1.state_dict(), o2.state_dict()
+        for i in s2["state"]:
+            assert float(s1["state"][i]["step"]) == float(s2["state"][i]["step"]) == 6.0
+
+
+def test_fused_clip_nonfinite_norm_matches_torch():
+    """A NaN gradient makes torch's clip coefficient NaN and every gradient NaN after
+    clip_grad_norm_; the fused clip propagates it the same way."""
+    ref = _params(3)
+    mine = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+    opt_r = torch.optim.AdamW(ref, lr=1e-3, foreach=False)
+    opt_m = FusedAdamW([{"params": mine}], lr=1e-3)
+    for pr, pm in zip(ref, mine):
+        g = torch.ones_like(pr)
+        pr.grad, pm.grad = g.clone(), g.clone()
+    ref[1].grad[3] = float("nan")
+    mine[1].grad[3] = float("nan")
+    torch.nn.utils.clip_grad_norm_(ref, 0.1, foreach=False)
+    opt_r.step()
+    opt_m.step(max_norm=0.1)
+    for pr, pm in zip(ref, mine):
+        assert torch.isnan(pr.detach()).all() and torch.isnan(pm.detach()).all()

@@ -91,3 +91,44 @@ def test_config_defaults_match_template():
     assert (c.hidden_dim, c.enc_layers, c.dec_layers, c.nheads, c.dim_feedforward) == \
         (256, 6, 6, 8, 2048)
     assert (c.max_position_embeddings, c.vocab_size, c.layer_norm_eps) == (128, 30522, 1e-12)
+
+
+def test_install_as_reference_modules_routes_reference_imports():
+    """main.py / eval_model.py import `models.caption`, `engine`, `eval_utils.decode`,
+    `train_utils.checkpoints` (main.py:1-12, eval_model.py:1-20): after the install those
+    names resolve to the MI355X modules."""
+    import sys
+    import retr_amd
+    names = ("models", "models.caption", "models.utils", "models.backbone",
+             "models.position_encoding", "models.transformer_modules",
+             "models.ConcatTransformer", "engine", "eval_utils", "eval_utils.decode",
+             "train_utils", "train_utils.checkpoints")
+    saved = {n: sys.modules.get(n) for n in names}
+    try:
+        retr_amd.install_as_reference_modules()
+        import models.caption as mc
+        import engine as eng
+        from eval_utils.decode import greedy_decoding
+        from train_utils.checkpoints import save_ckp, load_ckp  # noqa: F401
+        import retr_amd.models.caption
+        import retr_amd.engine
+        import retr_amd.eval_utils.decode as dec
+        assert mc is retr_amd.models.caption and eng is retr_amd.engine
+        assert greedy_decoding is dec.greedy_decoding
+        model, crit = mc.build_model(make_config())
+        assert type(model).__name__ == "Caption"
+    finally:
+        for n, m in saved.items():
+            if m is None:
+                sys.modules.pop(n, None)
+            else:
+                sys.modules[n] = m
+
+
+def test_prune_cap_ids_product_matches_oracle():
+    from oracle import model as orc
+    from retr_amd.eval_utils.decode import prune_cap_ids
+    seqs = [[101, 5, 6, 102, 7, 0], [101, 0, 9, 9], [101, 102, 102], [], [3, 102]]
+    for clean in (True, False):
+        assert prune_cap_ids(seqs, clean, 0, 101, 102) == \
+            orc.prune_cap_ids(seqs, clean, 0, 101, 102)

@@ -9,7 +9,8 @@ import torch
 from oracle import model as orc
 from retr_amd.models.caption import build_model
 from retr_amd.synthetic import synthetic_captions, synthetic_images, synthetic_state_dict
-from tests.helpers import PARITY_CASES, make_config
+from tests.helpers import (F2_CASE, PARITY_CASES, VARIANT_CASES, f2_inputs, make_config,
+                           variant_config, variant_inputs)
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -73,3 +74,56 @@ def test_prune_cap_ids_semantics():
     assert orc.prune_cap_ids(seqs, True, 0, 101, 102) == [[5, 6], [9, 9], []]
     assert orc.prune_cap_ids(seqs, False, 0, 101, 102) == [[101, 5, 6, 102], [101, 0, 9, 9],
                                                             [101, 102]]
+
+
+def _variant_oracle(name, sd, cfg, images, mask, extra, caps, cap_mask, **kw):
+    if cfg.use_global_features:
+        (g_img, g_mask), loc = extra
+        return orc.caption_globalloc_forward(sd, cfg, images, mask, g_img, g_mask, loc,
+                                             caps, cap_mask, **kw)
+    if cfg.use_location_features:
+        return orc.caption_loc_forward(sd, cfg, images, mask, extra[0], caps, cap_mask, **kw)
+    return orc.caption_forward(sd, cfg, images, mask, caps, cap_mask, **kw)
+
+
+@pytest.mark.parametrize("name", list(VARIANT_CASES))
+def test_oracle_variants_match_reference(name):
+    """CaptionLoc / CaptionGlobalLoc / learned PE / post-norm encoder."""
+    g = np.load(os.path.join(GOLD, f"{name}.npz"))
+    cfg = variant_config(name)
+    model, _ = build_model(cfg)
+    sd = synthetic_state_dict(model, seed=42)
+    trainable = [n for n, p in model.named_parameters() if p.requires_grad]
+    assert list(g["grad_names"]) == trainable
+    images, mask, extra, caps, cap_mask = variant_inputs(name, cfg)
+    sdo = {k: (v.clone().requires_grad_(True) if k in trainable else v) for k, v in sd.items()}
+    lo = _variant_oracle(name, sdo, cfg, images, mask, extra, caps[:, :-1], cap_mask[:, :-1])
+    loss = orc.caption_loss(lo, caps[:, 1:])
+    loss.backward()
+    np.testing.assert_allclose(lo.detach().numpy(), g["logits"], rtol=0, atol=2e-5)
+    assert abs(loss.item() - float(g["loss"])) < 1e-5
+    norms = np.array([sdo[n].grad.norm().item() for n in trainable])
+    np.testing.assert_allclose(norms, g["grad_norms"], rtol=1e-4, atol=1e-9)
+
+
+def test_oracle_f2_transformer_matches_reference():
+    """F2: the 6/6 d256 transformer at S=196 (models/ConcatTransformer.py direct import)."""
+    from retr_amd.models.ConcatTransformer import build_transformer
+    g = np.load(os.path.join(GOLD, "f2_transformer.npz"))
+    cfg = make_config(dtype="fp32", **F2_CASE)
+    tr = build_transformer(cfg)
+    sd = {"transformer." + k: v for k, v in synthetic_state_dict(tr, seed=43).items()}
+    names = ["transformer." + n for n, _ in tr.named_parameters()]
+    sdo = {k: (v.clone().requires_grad_(True) if k in names else v) for k, v in sd.items()}
+    src, mask, caps, cap_mask, weight = f2_inputs(cfg)
+    src.requires_grad_(True)
+    hs, att = orc.transformer_forward(sdo, cfg, src, mask, caps, cap_mask)
+    (hs * weight).sum().backward()
+    np.testing.assert_allclose(hs.detach().numpy(), g["hs"], rtol=0, atol=3e-5)
+    np.testing.assert_allclose(src.grad.numpy(), g["src_grad"], rtol=0, atol=1e-4)
+    for k, v in att.items():
+        np.testing.assert_allclose(torch.stack(v).detach()[:, :, ::7].numpy(), g["att/" + k],
+                                   rtol=0, atol=1e-6)
+    assert [n[len("transformer."):] for n in names] == list(g["grad_names"])
+    norms = np.array([sdo[n].grad.norm().item() for n in names])
+    np.testing.assert_allclose(norms, g["grad_norms"], rtol=1e-4, atol=1e-9)
