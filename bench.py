@@ -149,7 +149,9 @@ def train_bench(args, rank, world, device):
 
 
 def decode_bench(args, rank, world, device):
-    from retr_amd.eval_utils.decode import greedy
+    """cfg5 decode: greedy (the reference's algorithm, KV-cache incremental form) and beam
+    search (beam 5; new capability) refs/sec over one batch, hipGraph-replayed steps."""
+    from retr_amd.eval_utils.decode import IncrementalBeam, greedy
     cfg = cfg5()
     model, _ = build(cfg, device)
     model.eval()
@@ -157,20 +159,26 @@ def decode_bench(args, rank, world, device):
     img, mask = synthetic_images(B, 224, seed=3000 + rank)
     samples = [NestedTensor(img.to(device), mask.to(device))]
     T = cfg.max_position_embeddings
-    ids = greedy(samples, model, max_len=T, bos_token=101, eos_token=102)   # warm-up
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    ids = greedy(samples, model, max_len=T, bos_token=101, eos_token=102)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
-    steps = int((ids != 0).sum(1).max().item())
-    return dt, steps
+    out = {}
+    runs = [("greedy", lambda: greedy(samples, model, max_len=T, bos_token=101, eos_token=102))]
+    if args.beam > 1:
+        beam = IncrementalBeam(model, args.beam)
+        runs.append((f"beam{args.beam}", lambda: beam(samples, T, 101, 102)))
+    for name, fn in runs:
+        ids = fn()                                  # warm-up (captures the step graphs)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        ids = fn()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], device=device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = t.item()
+        out[name] = (dt, int((ids != 0).sum(1).max().item()))
+    return out
 
 
 def _cpu_model():
@@ -249,6 +257,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--size", type=int, default=640)
     ap.add_argument("--decode-batch", type=int, default=64)
+    ap.add_argument("--beam", type=int, default=5, help="beam width of the decode block (1: off)")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -297,13 +306,20 @@ def main():
                         fam.items(), key=lambda kv: -kv[1]["ms_total"])}
     decode = None
     if not args.no_decode:
-        ddt, steps = decode_bench(args, rank, world, device)
+        res = decode_bench(args, rank, world, device)
+        ddt, steps = res["greedy"]
         decode = {"metric": "greedy-decode refs/sec", "value": round(world * args.decode_batch
                                                                      / ddt, 2),
                   "unit": "refs/s", "batch_per_gpu": args.decode_batch, "steps": steps,
+                  "ms_per_batch": round(ddt * 1e3, 2),
                   "config": "cfg5: ResNet-50 dilation=True 224x224, 6/6 d256, bf16, "
                             "KV-cache greedy, per-step hipGraphs (token ids equal to the "
                             "reference algorithm)"}
+        for name, (bdt, bsteps) in res.items():
+            if name != "greedy":
+                decode[name] = {"value": round(world * args.decode_batch / bdt, 2),
+                                "unit": "refs/s", "ms_per_batch": round(bdt * 1e3, 2),
+                                "steps": bsteps}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)

@@ -123,10 +123,14 @@ int retr_attention_bwd(int dtype, const void* q, long ldq, const void* k, long l
                        const unsigned char* kpm, int causal, float drop_p,
                        unsigned long long seed, float* workspace, void* stream);
 size_t retr_attention_bwd_workspace(int B, int H, int Lq);
-/* decode step: q [B][.] one row per batch; k/v caches with Lmax rows per batch, first Lk valid */
+/* decode step: q [B][.] one query row per caption (or beam); k/v with Lmax rows per kv batch,
+ * first Lk valid.  Query row r attends kv batch r / kv_group (kv_group = beams per image for
+ * the shared cross-attention memory, else 1); with `anc` (int32 [B][Lmax], beam search) key j
+ * of row r is cache row anc[r][j] * Lmax + j instead. */
 int retr_attention_decode(int dtype, const void* q, long ldq, const void* k, long ldk,
                           const void* v, long ldv, void* o, long ldo, int B, int H, int Lk,
-                          int Lmax, int hd, const unsigned char* kpm, void* stream);
+                          int Lmax, int hd, const unsigned char* kpm, int kv_group,
+                          const int* anc, void* stream);
 
 /* ---- CrossEntropyLoss (models/caption.py:210, engine.py:71) and argmax (decode.py:71) ----- */
 int retr_ce_fwd(int dtype, const void* logits, long ld, int M, int V, const long long* targets,
@@ -138,6 +142,16 @@ int retr_argmax_rows(int dtype, const void* x, long ld, int M, int V, long long*
                      void* stream);
 
 /* greedy bookkeeping for step i (eval_utils/decode.py:72-79) on device */
+/* ---- beam search (new capability; reference decode.py has greedy only) -------------------
+ * per row of x [M][ld]: the K best (index, log-softmax value), first index on ties (K <= 8) */
+int retr_topk_rows(int dtype, const void* x, long ld, int M, int V, int K, int* idx,
+                   float* logprob, void* stream);
+/* one beam step for B images x K beams: select survivors from the retr_topk_rows candidates,
+ * reorder hist [B*K][T] / anc [B*K][T], append step i's token, done = i once all finished */
+int retr_beam_select(const int* cand_tok, const float* cand_lp, int B, int K, int i, int T,
+                     long long eos, float* scores, unsigned char* finished, long long* hist,
+                     int* anc, long long* tok, unsigned char* item_done, int* done,
+                     void* stream);
 int retr_greedy_update(const long long* pred, int B, int T, int i, long long eos,
                        long long* caption, unsigned char* finished, int* done, long long* tok,
                        void* stream);

@@ -334,3 +334,55 @@ def prune_cap_ids(idx_seqs, clean=True, pad_token=0, bos_token=1, eos_token=2):
             pr = [i for i in pr if i not in (pad_token, bos_token, eos_token)]
         out.append(pr)
     return out
+
+
+def beam_search(forward, batch, max_len, beam_size, bos_token=1, eos_token=2):
+    """CPU restatement (full recompute per step) of the MI355X beam search semantics of
+    retr_amd/eval_utils/decode.py IncrementalBeam / csrc/beam.hip.  The reference has NO beam
+    search: this is test infrastructure for the kernels, and its only
+    reference anchor is the bridge beam_size=1 == greedy (eval_utils/decode.py:53-81).
+    ``forward(caption [R, T], cap_mask [R, T]) -> logits [R, T, V]`` over R = batch*beam rows
+    (row b*K + k = beam k of image b).  Returns the caption [batch, T] of each image's best
+    beam in greedy's format (columns after the terminating step zero)."""
+    K, T = beam_size, max_len
+    R = batch * K
+    hist = torch.zeros((R, T), dtype=torch.long)
+    hist[:, 0] = bos_token
+    scores = torch.zeros(R)
+    finished = torch.zeros(R, dtype=torch.bool)
+    done = -1
+    for i in range(T - 1):
+        cm = torch.arange(T).unsqueeze(0).expand(R, T) > i
+        logits = forward(hist, cm)[:, i, :].float()
+        lse = torch.logsumexp(logits, -1, keepdim=True)
+        vals, idx = torch.sort(logits, dim=-1, descending=True, stable=True)   # first index on ties
+        lp = (vals[:, :K] - lse)
+        tok = idx[:, :K]
+        nh, ns, nf = hist.clone(), scores.clone(), finished.clone()
+        for b in range(batch):
+            cands = []                                   # (score, beam, rank-order) stable
+            for k in range(K if i > 0 else 1):
+                r = b * K + k
+                if i > 0 and bool(finished[r]):
+                    cands.append((float(scores[r]), k, int(tok[r, 0])))
+                else:
+                    base = float(scores[r]) if i > 0 else 0.0
+                    for j in range(K):
+                        cands.append((float(torch.tensor(base) + lp[r, j]), k, int(tok[r, j])))
+            order = sorted(range(len(cands)), key=lambda c: (-cands[c][0], c))[:K]
+            for s, c in enumerate(order):
+                sc, k, t = cands[c]
+                src, dst = b * K + k, b * K + s
+                nh[dst] = hist[src]
+                nh[dst, i + 1] = t
+                ns[dst] = sc
+                nf[dst] = (bool(finished[src]) if i > 0 else False) or t == eos_token
+        hist, scores, finished = nh, ns, nf
+        if bool(finished.all()):
+            done = i
+            break
+    best = scores.view(batch, K).argmax(-1)
+    cap = hist.view(batch, K, T)[torch.arange(batch), best].clone()
+    if done >= 0:
+        cap[:, done + 1:] = 0
+    return cap

@@ -52,7 +52,11 @@ _SIGS = {
     "retr_attention_bwd": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _P, _L, _P, _L, _P,
                            _L, _I, _I, _I, _I, _I, _P, _I, _F, _U64, _P, _P],
     "retr_attention_bwd_workspace": [_I, _I, _I],
-    "retr_attention_decode": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _P, _P],
+    "retr_attention_decode": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _P, _I,
+                              _P, _P],
+    "retr_topk_rows": [_I, _P, _L, _I, _I, _I, _P, _P, _P],
+    "retr_beam_select": [_P, _P, _I, _I, _I, _I, ctypes.c_longlong, _P, _P, _P, _P, _P, _P, _P,
+                         _P],
     "retr_greedy_update": [_P, _I, _I, _I, ctypes.c_longlong, _P, _P, _P, _P, _P],
     "retr_ce_fwd": [_I, _P, _L, _I, _I, _P, _P, _P, _P, _P],
     "retr_ce_bwd": [_I, _P, _L, _I, _I, _P, _P, _P, _F, _P, _L, _P],

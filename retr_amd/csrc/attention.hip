@@ -429,7 +429,8 @@ __global__ void attn_probs_kernel(const T* q, long ldq, const T* k, long ldk, in
 template <typename T>
 __global__ void __launch_bounds__(256)
 attn_decode_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, long ldv, T* o, long ldo,
-                   int H, int Lk, int Lmax, int hd, const unsigned char* kpm, float scale) {
+                   int H, int Lk, int Lmax, int hd, const unsigned char* kpm, float scale,
+                   int kv_group, const int* anc) {
   extern __shared__ float sm[];
   float* sc = sm;            // [Lk] scores -> probabilities
   float* qs = sc + Lk;       // [64] scaled query (rounded to T like the tiled kernel)
@@ -438,14 +439,19 @@ attn_decode_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, long 
   constexpr int EPC = 16 / sizeof(T);
   for (int d = tid; d < hd; d += 256) qs[d] = to_f(from_f<T>(to_f(q[(long)b * ldq + h * hd + d]) * scale));
   __syncthreads();
-  const T* kb = k + (long)b * Lmax * ldk + h * hd;
-  const T* vb = v + (long)b * Lmax * ldv + h * hd;
+  // key/value row of key j: the query's kv batch (b / kv_group) or, for beam search, the cache
+  // row named by the ancestry table (beam rows are reordered without moving the cache)
+  const int kvb = b / kv_group;
+  const int* ar = anc ? anc + (long)b * Lmax : nullptr;
+  auto kvrow = [&](int j) -> long { return (ar ? (long)ar[j] : (long)kvb) * Lmax + j; };
+  const T* kb = k + h * hd;
+  const T* vb = v + h * hd;
   float mx = -INFINITY;
   for (int j = tid; j < Lk; j += 256) {
     float s = -INFINITY;
-    if (!(kpm && kpm[(long)b * Lk + j])) {
+    if (!(kpm && kpm[(long)kvb * Lk + j])) {
       s = 0.f;
-      const T* kr = kb + (long)j * ldk;
+      const T* kr = kb + kvrow(j) * ldk;
       for (int d0 = 0; d0 < hd; d0 += EPC) {
         u32x4 raw = *(const u32x4*)(kr + d0);
         const T* e = (const T*)&raw;
@@ -475,7 +481,7 @@ attn_decode_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, long 
   const int nc = 256 / hd, d = tid % hd, c = tid / hd;
   float acc = 0.f;
   if (c < nc)
-    for (int j = c; j < Lk; j += nc) acc += sc[j] * to_f(vb[(long)j * ldv + d]);
+    for (int j = c; j < Lk; j += nc) acc += sc[j] * to_f(vb[kvrow(j) * ldv + d]);
   red[tid] = acc;
   __syncthreads();
   if (tid < hd) {
@@ -583,9 +589,11 @@ int retr_attention_fwd(int dtype, const void* q, long ldq, const void* k, long l
 // P.V with threads split over (head dim, key stripe) and an LDS reduction.
 int retr_attention_decode(int dtype, const void* q, long ldq, const void* k, long ldk,
                           const void* v, long ldv, void* o, long ldo, int B, int H, int Lk,
-                          int Lmax, int hd, const unsigned char* kpm, void* stream) {
+                          int Lmax, int hd, const unsigned char* kpm, int kv_group,
+                          const int* anc, void* stream) {
   RETR_REQUIRE(hd >= 8 && hd <= 64 && hd % 8 == 0, "attention: head dim %d unsupported", hd);
   RETR_REQUIRE(kpm == nullptr || Lmax == Lk, "attention_decode: kpm needs Lmax == Lk");
+  RETR_REQUIRE(kv_group >= 1, "attention_decode: kv_group must be >= 1");
   RETR_REQUIRE(Lk >= 1 && Lk <= 4096, "attention_decode: Lk=%d out of range", Lk);
   RETR_REQUIRE(ldk % 8 == 0 && ldv % 8 == 0, "attention_decode: row strides %%8");
   hipStream_t st = (hipStream_t)stream;
@@ -594,11 +602,11 @@ int retr_attention_decode(int dtype, const void* q, long ldq, const void* k, lon
   if (dtype == RETR_BF16)
     hipLaunchKernelGGL(attn_decode_kernel<bf16>, dim3(B * H), dim3(256), lds, st, (const bf16*)q, ldq,
                        (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, H, Lk, Lmax, hd, kpm,
-                       scale);
+                       scale, kv_group, anc);
   else
     hipLaunchKernelGGL(attn_decode_kernel<float>, dim3(B * H), dim3(256), lds, st, (const float*)q,
                        ldq, (const float*)k, ldk, (const float*)v, ldv, (float*)o, ldo, H, Lk, Lmax,
-                       hd, kpm, scale);
+                       hd, kpm, scale, kv_group, anc);
   return retr_check_launch("attention_decode");
 }
 

@@ -84,10 +84,27 @@ argmax_kernel(const T* x, long ld, int V, long long* out) {
   const T* xr = x + (long)row * ld;
   float bv = -INFINITY;
   int bi = 0x7fffffff;
-  for (int j = threadIdx.x; j < V; j += 256) {
-    float v = to_f(xr[j]);
+  // 16-byte vector loads (bf16 x 8 / f32 x 4 x 2); the (value, first index, NaN-wins) order
+  // makes the result independent of the visiting order (torch.argmax semantics)
+  auto visit = [&](float v, int j) {
     if (v > bv || (v == bv && j < bi) || (v != v && bv == bv)) bv = v, bi = j;
+  };
+  const int V8 = ((ld % 8) == 0) ? V / 8 : 0;
+  for (int c = threadIdx.x; c < V8; c += 256) {
+    float v[8];
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8 x8 = *(const bf16x8*)(xr + 8 * c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (float)x8[e];
+    } else {
+      const f32x4 a = *(const f32x4*)(xr + 8 * c), b = *(const f32x4*)(xr + 8 * c + 4);
+      v[0] = a[0], v[1] = a[1], v[2] = a[2], v[3] = a[3];
+      v[4] = b[0], v[5] = b[1], v[6] = b[2], v[7] = b[3];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) visit(v[e], 8 * c + e);
   }
+  for (int j = 8 * V8 + threadIdx.x; j < V; j += 256) visit(to_f(xr[j]), j);
   for (int o = 32; o > 0; o >>= 1) {
     float v2 = __shfl_xor(bv, o, 64);
     int i2 = __shfl_xor(bi, o, 64);

@@ -44,42 +44,59 @@ def prepare_tokenizer():
 
 
 class _DecodeState:
-    """Static device buffers (and captured per-step hipGraphs) for one (B, S, T) shape."""
+    """Static device buffers (and captured per-step hipGraphs) for one (B, K, S, T) shape;
+    the decoder runs R = B*K rows (K = beams per image, 1 for greedy)."""
 
-    def __init__(self, B, S, T, C, F, n_layers, V, cd, dev):
+    def __init__(self, B, S, T, C, F, n_layers, V, cd, dev, K=1):
         f32 = torch.float32
-        self.B, self.S, self.T = B, S, T
+        R = B * K
+        self.B, self.K, self.R, self.S, self.T = B, K, R, S, T
         self.kx = [torch.empty(B * S, C, dtype=cd, device=dev) for _ in range(n_layers)]
         self.vx = [torch.empty(B * S, C, dtype=cd, device=dev) for _ in range(n_layers)]
-        self.kc = [torch.zeros(B * T, C, dtype=cd, device=dev) for _ in range(n_layers)]
-        self.vc = [torch.zeros(B * T, C, dtype=cd, device=dev) for _ in range(n_layers)]
+        self.kc = [torch.zeros(R * T, C, dtype=cd, device=dev) for _ in range(n_layers)]
+        self.vc = [torch.zeros(R * T, C, dtype=cd, device=dev) for _ in range(n_layers)]
         self.kpm = torch.zeros(B, S, dtype=torch.uint8, device=dev)
         self.caption = torch.zeros(B, T, dtype=torch.long, device=dev)
-        self.tok = torch.zeros(B, dtype=torch.long, device=dev)
-        self.finished = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.tok = torch.zeros(R, dtype=torch.long, device=dev)
+        self.finished = torch.zeros(R, dtype=torch.uint8, device=dev)
         self.done = torch.full((1,), -1, dtype=torch.int32, device=dev)
-        self.y = torch.empty(B, C, dtype=f32, device=dev)
+        self.y = torch.empty(R, C, dtype=f32, device=dev)
         self.y2 = torch.empty_like(self.y)
-        self.n = torch.empty(B, C, dtype=cd, device=dev)
+        self.n = torch.empty(R, C, dtype=cd, device=dev)
         self.npos = torch.empty_like(self.n)
         self.q = torch.empty_like(self.n)
         self.o = torch.empty_like(self.n)
-        self.mean = torch.empty(B, dtype=f32, device=dev)
+        self.mean = torch.empty(R, dtype=f32, device=dev)
         self.rstd = torch.empty_like(self.mean)
-        self.ffh = torch.empty(B, F, dtype=cd, device=dev)
-        self.h1 = torch.empty(B, 512, dtype=cd, device=dev)
-        self.h2 = torch.empty(B, 512, dtype=cd, device=dev)
+        self.ffh = torch.empty(R, F, dtype=cd, device=dev)
+        self.h1 = torch.empty(R, 512, dtype=cd, device=dev)
+        self.h2 = torch.empty(R, 512, dtype=cd, device=dev)
         self.Vp = (V + 63) // 64 * 64
-        self.logits = torch.empty(B, self.Vp, dtype=cd, device=dev)
-        self.pred = torch.empty(B, dtype=torch.long, device=dev)
+        self.logits = torch.empty(R, self.Vp, dtype=cd, device=dev)
+        self.pred = torch.empty(R, dtype=torch.long, device=dev)
+        if K > 1:
+            self.init_beam(dev)
         self.head_bias = None
         self.graphs = None
         self.signature = None
+
+    def init_beam(self, dev):
+        R, K, T = self.R, self.K, self.T
+        self.beam = True
+        self.hist = torch.zeros(R, T, dtype=torch.long, device=dev)
+        self.anc = torch.zeros(R, T, dtype=torch.int32, device=dev)
+        self.scores = torch.zeros(R, dtype=torch.float32, device=dev)
+        self.cand_tok = torch.zeros(R, K, dtype=torch.int32, device=dev)
+        self.cand_lp = torch.zeros(R, K, dtype=torch.float32, device=dev)
+        self.item_done = torch.zeros(self.B, dtype=torch.uint8, device=dev)
 
 
 class IncrementalGreedy:
     """KV-cache greedy decoder over a ``Caption`` model (eval mode semantics).  The T-1 decode
     steps are captured once per (shape, weights) as hipGraphs and replayed per batch."""
+
+    beam = False
+    K = 1
 
     def __init__(self, model, use_graphs=True):
         self.model = model
@@ -102,7 +119,7 @@ class IncrementalGreedy:
     def _step(self, st, i, eos_token):
         """Kernels of decode step i (reads token i, writes caption column i+1)."""
         model, tr, cd = self.model, self.tr, self.cdtype
-        B, S, T = st.B, st.S, st.T
+        B, S, T, R = st.B, st.S, st.T, st.R
         C = st.n.shape[1]
         layers = list(tr.decoder.layers)
         H = layers[0].tgt_self_attn.sublayer.num_heads
@@ -111,7 +128,7 @@ class IncrementalGreedy:
         qp = emb.position_embeddings.weight.detach()[i]
         s = _st()
         y, y2 = st.y, st.y2
-        call("retr_embed_ln_fwd", ptr(st.tok), B, 1, C, ptr(emb.word_embeddings.weight), ptr(qp),
+        call("retr_embed_ln_fwd", ptr(st.tok), R, 1, C, ptr(emb.word_embeddings.weight), ptr(qp),
              ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias), float(emb.LayerNorm.eps), 0.0, 0,
              ptr(y), ptr(st.mean), ptr(st.rstd), s)
         for li, layer in enumerate(layers):
@@ -124,7 +141,8 @@ class IncrementalGreedy:
             k_linear_fwd(st.npos, w[C:2 * C], b[C:2 * C], st.kc[li][i::T])
             k_linear_fwd(st.n, w[2 * C:], b[2 * C:], st.vc[li][i::T])
             call("retr_attention_decode", dcode(cd), ptr(st.q), C, ptr(st.kc[li]), C,
-                 ptr(st.vc[li]), C, ptr(st.o), C, B, H, i + 1, T, hd, None, s)
+                 ptr(st.vc[li]), C, ptr(st.o), C, R, H, i + 1, T, hd, None, 1,
+                 ptr(st.anc) if self.beam else None, s)
             k_linear_fwd(st.o, ops.WEIGHTS.get(sub.out_proj.weight, cd),
                          sub.out_proj.bias.detach(), y2, res=y)
             y, y2 = y2, y
@@ -135,7 +153,7 @@ class IncrementalGreedy:
             self._ln(y, ca.norm, y2=st.npos, pos=qp)
             k_linear_fwd(st.npos, w[:C], b[:C], st.q)
             call("retr_attention_decode", dcode(cd), ptr(st.q), C, ptr(st.kx[li]), C,
-                 ptr(st.vx[li]), C, ptr(st.o), C, B, H, S, S, hd, ptr(st.kpm), s)
+                 ptr(st.vx[li]), C, ptr(st.o), C, R, H, S, S, hd, ptr(st.kpm), st.K, None, s)
             k_linear_fwd(st.o, ops.WEIGHTS.get(sub.out_proj.weight, cd),
                          sub.out_proj.bias.detach(), y2, res=y)
             y, y2 = y2, y
@@ -152,14 +170,37 @@ class IncrementalGreedy:
         k_linear_fwd(st.h1, ops.WEIGHTS.get(l2.weight, cd), l2.bias.detach(), st.h2, relu=1)
         k_linear_fwd(st.h2, ops.WEIGHTS.get(l3.weight, cd, rows=st.Vp),
                      st.head_bias, st.logits)
-        call("retr_argmax_rows", dcode(cd), ptr(st.logits), st.Vp, B, V, ptr(st.pred), s)
-        call("retr_greedy_update", ptr(st.pred), B, T, i, int(eos_token), ptr(st.caption),
+        self._select(st, i, V, eos_token, s)
+
+    def _select(self, st, i, V, eos_token, s):
+        """Greedy: first-index argmax + the reference's finished/early-exit bookkeeping."""
+        cd = self.cdtype
+        call("retr_argmax_rows", dcode(cd), ptr(st.logits), st.Vp, st.B, V, ptr(st.pred), s)
+        call("retr_greedy_update", ptr(st.pred), st.B, st.T, i, int(eos_token), ptr(st.caption),
              ptr(st.finished), ptr(st.done), ptr(st.tok), s)
+
+    # -- state handling (overridden by IncrementalBeam) --------------------------------------
+    def _new_state(self, B, S, T, C, F, L, V, cd, dev):
+        return _DecodeState(B, S, T, C, F, L, V, cd, dev)
+
+    def _reset(self, st, bos_token):
+        st.caption.zero_()
+        st.caption[:, 0] = bos_token
+        st.tok.fill_(bos_token)
+        st.finished.zero_()
+        st.done.fill_(-1)
+
+    def _result(self, st):
+        return st.caption.clone()
 
     @torch.no_grad()
     def __call__(self, samples, max_len, bos_token, eos_token, poll=8):
+        """samples: the model's memory inputs (a NestedTensor for Caption; the argument list of
+        CaptionLoc / CaptionGlobalLoc before the caption), as passed to ``greedy``."""
         model, tr, cd = self.model, self.tr, self.cdtype
-        src, mask, B, S = model.encode_image(samples)
+        if not isinstance(samples, (list, tuple)):
+            samples = [samples]
+        src, mask, B, S = model.memory_tokens(*samples)
         kpm = mask.reshape(B, S).contiguous().view(torch.uint8)
         mem, mem_pos, _ = tr.encode(src, B, S, kpm, cd)
         qpos_w = tr.embeddings.position_embeddings.weight
@@ -169,11 +210,12 @@ class IncrementalGreedy:
                                f"({qpos_w.shape[0]}) at non-singleton dimension 0")
         C = mem.shape[1]
         layers = list(tr.decoder.layers)
-        key = (B, S, T, cd, int(eos_token))
+        key = (type(self).__name__, self.K, B, S, T, cd, int(eos_token))
         st = self.states.get(key)
         if st is None:
-            st = _DecodeState(B, S, T, C, layers[0].ff.sublayer[0].weight.shape[0], len(layers),
-                              model.mlp.layers[2].weight.shape[0], cd, mem.device)
+            st = self._new_state(B, S, T, C, layers[0].ff.sublayer[0].weight.shape[0],
+                                 len(layers), model.mlp.layers[2].weight.shape[0], cd,
+                                 mem.device)
             self.states[key] = st
         # cross-attention K/V of every decoder layer, once per batch, into the static buffers
         for li, layer in enumerate(layers):
@@ -183,11 +225,7 @@ class IncrementalGreedy:
             k_linear_fwd(mem_pos, w[C:2 * C], b[C:2 * C], st.kx[li])
             k_linear_fwd(mem, w[2 * C:], b[2 * C:], st.vx[li])
         st.kpm.copy_(kpm)
-        st.caption.zero_()
-        st.caption[:, 0] = bos_token
-        st.tok.fill_(bos_token)
-        st.finished.zero_()
-        st.done.fill_(-1)
+        self._reset(st, bos_token)
         sig = self._signature()
         if st.signature != sig:
             st.head_bias = ops._pad_vec(model.mlp.layers[2].bias, st.Vp)
@@ -196,11 +234,7 @@ class IncrementalGreedy:
             # warm once eagerly (kernel attributes, weight copies), then capture every step
             self._step(st, 0, eos_token)
             torch.cuda.synchronize()
-            st.caption.zero_()
-            st.caption[:, 0] = bos_token
-            st.tok.fill_(bos_token)
-            st.finished.zero_()
-            st.done.fill_(-1)
+            self._reset(st, bos_token)
             graphs = []
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
@@ -220,9 +254,76 @@ class IncrementalGreedy:
                 self._step(st, i, eos_token)
             if (i + 1) % poll == 0 and int(st.done.item()) >= 0:
                 break
-        return st.caption.clone()
+        return self._result(st)
 
 
+class IncrementalBeam(IncrementalGreedy):
+    """KV-cache beam search (new capability: the reference decodes greedily only,
+    eval_utils/decode.py:53-81).  K beams per image run as B*K decoder rows; per step
+    ``retr_topk_rows`` gives every row its K best tokens and log-softmax values and
+    ``retr_beam_select`` keeps the K best of (finished beams: their score and argmax
+    continuation; others: score + log p of each of their K tokens), reorders the token history
+    and the cache-ancestry table (csrc/beam.hip), so the K/V caches are never copied.  The loop
+    ends like greedy's: at the first step after which every beam of every image has emitted
+    EOS, whose column is not written.  Result: each image's highest-scoring beam (optionally
+    length-normalised), in greedy's caption format.  With K = 1 it is greedy, token for token.
+    """
+
+    beam = True
+
+    def __init__(self, model, beam_size=5, use_graphs=True, length_penalty=0.0):
+        super().__init__(model, use_graphs)
+        if not 1 <= beam_size <= 8:
+            raise ValueError(f"beam_size must be in [1, 8], got {beam_size}")
+        self.K = beam_size
+        self.length_penalty = float(length_penalty)
+        self.last_scores = None
+
+    def _new_state(self, B, S, T, C, F, L, V, cd, dev):
+        st = _DecodeState(B, S, T, C, F, L, V, cd, dev, K=self.K)
+        if self.K == 1:
+            st.init_beam(dev)
+        return st
+
+    def _reset(self, st, bos_token):
+        st.hist.zero_()
+        st.hist[:, 0] = bos_token
+        st.anc.copy_(torch.arange(st.R, dtype=torch.int32, device=st.anc.device)[:, None]
+                     .expand(st.R, st.T))
+        st.scores.zero_()
+        st.tok.fill_(bos_token)
+        st.finished.zero_()
+        st.item_done.zero_()
+        st.done.fill_(-1)
+
+    def __call__(self, samples, max_len, bos_token, eos_token, poll=8):
+        self._eos = int(eos_token)
+        return super().__call__(samples, max_len, bos_token, eos_token, poll)
+
+    def _select(self, st, i, V, eos_token, s):
+        call("retr_topk_rows", dcode(self.cdtype), ptr(st.logits), st.Vp, st.R, V, st.K,
+             ptr(st.cand_tok), ptr(st.cand_lp), s)
+        call("retr_beam_select", ptr(st.cand_tok), ptr(st.cand_lp), st.B, st.K, i, st.T,
+             int(eos_token), ptr(st.scores), ptr(st.finished), ptr(st.hist), ptr(st.anc),
+             ptr(st.tok), ptr(st.item_done), ptr(st.done), s)
+
+    def _result(self, st):
+        B, K, T = st.B, st.K, st.T
+        done = int(st.done.item())
+        hist = st.hist.view(B, K, T)
+        scores = st.scores.view(B, K)
+        if self.length_penalty:
+            # GNMT length normalisation; length = tokens after BOS up to the first EOS
+            is_eos = hist[..., 1:] == self._eos
+            first = is_eos.int().argmax(-1) + 1
+            length = torch.where(is_eos.any(-1), first, torch.full_like(first, T - 1)).float()
+            scores = scores / ((5.0 + length) / 6.0) ** self.length_penalty
+        best = scores.argmax(-1)
+        cap = hist[torch.arange(B, device=hist.device), best].clone()
+        if done >= 0:
+            cap[:, done + 1:] = 0
+        self.last_scores = scores.gather(1, best[:, None])[:, 0]
+        return cap
 def _full_forward_greedy(samples, model, max_len, bos_token, eos_token, device):
     """The reference algorithm (decode.py:59-81) on the MI355X kernels: one full model forward
     per step.  Used when the model is in training mode (dropout active) and for parity tests."""
@@ -247,9 +348,34 @@ def greedy(samples, model, max_len=20, device="auto", bos_token=1, eos_token=2):
     if device == "auto":
         device = "cuda" if torch.cuda.is_available() else "cpu"
     samples = [s.to(device) for s in samples]
-    if model.training or not hasattr(model, "encode_image"):
+    if model.training or not hasattr(model, "memory_tokens"):
         return _full_forward_greedy(samples, model, max_len, bos_token, eos_token, device)
-    return IncrementalGreedy(model)(samples[0], max_len, bos_token, eos_token)
+    return IncrementalGreedy(model)(samples, max_len, bos_token, eos_token)
+
+
+def beam_search(samples, model, max_len=20, beam_size=5, device="auto", bos_token=1,
+                eos_token=2, length_penalty=0.0):
+    """Beam-search decoding for a batch of samples (new; the reference has greedy only).  Same
+    inputs and caption format as ``greedy``; ``beam_size=1`` returns exactly greedy's ids."""
+    if device == "auto":
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    samples = [s.to(device) for s in samples]
+    if model.training:
+        raise RuntimeError("beam_search runs in eval mode (model.eval())")
+    return IncrementalBeam(model, beam_size, length_penalty=length_penalty)(
+        samples, max_len, bos_token, eos_token)
+
+
+def beam_decoding(samples, model, tokenizer, max_len=20, beam_size=5, clean=True, pad_token=0,
+                  bos_token=1, eos_token=2, device="auto", length_penalty=0.0):
+    """greedy_decoding's wrapper (decode.py:112-128) around ``beam_search``."""
+    caption_idx = beam_search(samples, model, max_len=max_len, beam_size=beam_size,
+                              device=device, bos_token=bos_token, eos_token=eos_token,
+                              length_penalty=length_penalty)
+    caption_idx = caption_idx.cpu().detach().numpy().tolist()
+    pruned = prune_cap_ids(caption_idx, clean=clean, pad_token=pad_token, bos_token=bos_token,
+                           eos_token=eos_token)
+    return idx2sents(pruned, tokenizer)
 
 
 def greedy_reference_algorithm(samples, model, max_len, bos_token=1, eos_token=2,

@@ -59,6 +59,10 @@ class Caption(nn.Module):
                          self.cdtype, out_f32=True, dgate=feats.view(b * s, cb))
         return src, mask.view(b, s), b, s
 
+    def memory_tokens(self, samples):
+        """Encoder input rows of this model: (src fp32 [B*S, C], mask [B, S], B, S)."""
+        return self.encode_image(samples)
+
     def forward(self, samples, target_exp, target_exp_mask, return_attention=False):
         from .. import ops
         src, mask, b, s = self.encode_image(samples)
@@ -92,13 +96,18 @@ class _ConcatMixin:
     rows of ConcatTransformer.forward's concatenation (models/ConcatTransformer.py:47-53) in
     the batch-major layout of ConcatTransformer.run."""
 
-    def _run(self, parts, target_exp, target_exp_mask, return_attention):
-        from .. import ops
+    @staticmethod
+    def _concat(parts):
         b = parts[0][0].shape[0]
         rows = torch.cat([r for r, _ in parts], 1)            # [B, S_total, C]
         mask = torch.cat([m for _, m in parts], 1)            # [B, S_total]
         s = rows.shape[1]
-        hs, att = self.transformer.run(rows.reshape(b * s, -1), b, s, mask, target_exp,
+        return rows.reshape(b * s, -1), mask, b, s
+
+    def _run(self, parts, target_exp, target_exp_mask, return_attention):
+        from .. import ops
+        rows, mask, b, s = self._concat(parts)
+        hs, att = self.transformer.run(rows, b, s, mask, target_exp,
                                        target_exp_mask, self.cdtype,
                                        return_attention=return_attention)
         out = ops.mlp_head(self.mlp, hs, b, target_exp.shape[1], self.cdtype)
@@ -134,13 +143,19 @@ class CaptionLoc(_ConcatMixin, Caption):
         self.mlp = MLP(hidden_dim, 512, vocab_size, 3)
         self.cdtype = torch.bfloat16
 
-    def forward(self, t_samples, loc_feats, target_exp, target_exp_mask, return_attention=False):
+    def _parts(self, t_samples, loc_feats):
         t_rows, t_mask = self._image_part(t_samples)
         b = t_rows.shape[0]
         loc = _small_linear(loc_feats.reshape(b, -1), self.loc_proj, self.cdtype)   # [B, C]
         loc_mask = torch.zeros((b, 1), dtype=torch.bool, device=t_mask.device)
-        return self._run([(t_rows, t_mask), (loc.view(b, 1, -1), loc_mask)], target_exp,
-                         target_exp_mask, return_attention)
+        return [(t_rows, t_mask), (loc.view(b, 1, -1), loc_mask)]
+
+    def memory_tokens(self, t_samples, loc_feats):
+        return self._concat(self._parts(t_samples, loc_feats))
+
+    def forward(self, t_samples, loc_feats, target_exp, target_exp_mask, return_attention=False):
+        return self._run(self._parts(t_samples, loc_feats), target_exp, target_exp_mask,
+                         return_attention)
 
 
 class CaptionGlobalLoc(_ConcatMixin, Caption):
@@ -161,6 +176,13 @@ class CaptionGlobalLoc(_ConcatMixin, Caption):
 
     def forward(self, t_samples, g_samples, loc_feats, target_exp, target_exp_mask,
                 return_attention=False):
+        return self._run(self._parts(t_samples, g_samples, loc_feats), target_exp,
+                         target_exp_mask, return_attention)
+
+    def memory_tokens(self, t_samples, g_samples, loc_feats):
+        return self._concat(self._parts(t_samples, g_samples, loc_feats))
+
+    def _parts(self, t_samples, g_samples, loc_feats):
         from .utils import ensure_unmasked_values
         t_rows, t_mask = self._image_part(t_samples)
         b = t_rows.shape[0]
@@ -176,9 +198,8 @@ class CaptionGlobalLoc(_ConcatMixin, Caption):
         g_rows = ops.linear(feats.view(gb * gh * gw, cb), self.input_proj.weight,
                             self.input_proj.bias, self.cdtype, out_f32=True,
                             dgate=feats.view(gb * gh * gw, cb))
-        return self._run([(t_rows, t_mask), (loc.view(b, nf, -1), loc_mask),
-                          (g_rows.view(gb, gh * gw, -1), g_mask.view(gb, gh * gw))],
-                         target_exp, target_exp_mask, return_attention)
+        return [(t_rows, t_mask), (loc.view(b, nf, -1), loc_mask),
+                (g_rows.view(gb, gh * gw, -1), g_mask.view(gb, gh * gw))]
 
 
 class CrossEntropyLoss(nn.CrossEntropyLoss):

@@ -746,6 +746,7 @@ class _LearnedPos(torch.autograd.Function):
             call("retr_dropout_apply", F32, ptr(rep), C, ptr(rep), C, B * S, C, float(drop_p),
                  seed, _st())
         ctx.save_for_backward(weight, gamma, mean, rstd)
+        ctx.beta = beta
         ctx.cfg = (B, S, C, drop_p, seed)
         return rep
 
@@ -764,7 +765,7 @@ class _LearnedPos(torch.autograd.Function):
         call("retr_pos_grad", F32, ptr(d), C, B * S, C, S, ptr(dtab), _st())
         dw, _ = grad_buffer(weight)
         dgamma, _ = grad_buffer(gamma)
-        dbeta, _ = grad_buffer(beta)
+        dbeta, _ = grad_buffer(ctx.beta)
         wd = weight.detach()
         # rows 0..S-1 of the (zeroed) embedding gradient are written directly; rows >= S get
         # no gradient, as from nn.Embedding with ids arange(S)

@@ -1,0 +1,89 @@
+"""Beam-search decode (new capability, the reference decodes greedily only).
+
+Parity: beam_size=1 == greedy, token for token (the reference anchor, eval_utils/decode.py:
+53-81) on the micro configs (three EOS choices incl. early exit) and at cfg5 shape; beam_size>1
+against the CPU oracle's full-recompute restatement of the same semantics (oracle/model.py
+beam_search, itself pinned to the reference's greedy ids at beam 1 in tests/test_oracle.py).
+"""
+import pytest
+import torch
+
+from oracle import model as orc
+from retr_amd.eval_utils.decode import IncrementalBeam, beam_search, greedy
+from retr_amd.models.caption import build_model
+from retr_amd.models.utils import NestedTensor
+from retr_amd.synthetic import synthetic_images, synthetic_state_dict
+from tests.helpers import PARITY_CASES, make_config
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _setup(case, dtype="fp32"):
+    kw, size, B = PARITY_CASES[case]
+    cfg = make_config(dtype=dtype, **kw)
+    model, _ = build_model(cfg)
+    sd = synthetic_state_dict(model, seed=42)
+    model.load_state_dict(sd)
+    model.to(DEV).eval()
+    images, mask = synthetic_images(B, size, seed=1, pad_band=True)
+    return cfg, model, sd, images, mask
+
+
+@pytest.mark.parametrize("case", ["micro_r18", "micro_r50_dil"])
+def test_beam1_equals_greedy(case):
+    cfg, model, sd, images, mask = _setup(case)
+    T = cfg.max_position_embeddings
+    samples = [NestedTensor(images.to(DEV), mask.to(DEV))]
+    never = greedy(samples, model, max_len=T, bos_token=101, eos_token=-1)
+    for eos in (-1, int(never[0, 6]), int(never[0, 1])):
+        g = greedy(samples, model, max_len=T, bos_token=101, eos_token=eos)
+        b = beam_search(samples, model, max_len=T, beam_size=1, bos_token=101, eos_token=eos)
+        assert torch.equal(g, b), (case, eos)
+
+
+@pytest.mark.parametrize("K", [2, 3, 5])
+def test_beam_matches_oracle_restatement(K):
+    cfg, model, sd, images, mask = _setup("micro_r18")
+    T = cfg.max_position_embeddings
+    B = images.shape[0]
+    samples = [NestedTensor(images.to(DEV), mask.to(DEV))]
+    never = greedy(samples, model, max_len=T, bos_token=101, eos_token=-1)
+    img_r = images.repeat_interleave(K, 0)
+    mask_r = mask.repeat_interleave(K, 0)
+    for eos in (-1, int(never[0, 3])):
+        ids = beam_search(samples, model, max_len=T, beam_size=K, bos_token=101, eos_token=eos)
+        ids_e = IncrementalBeam(model, K, use_graphs=False)(samples, T, 101, eos)
+        assert torch.equal(ids, ids_e)                      # graph replay == eager launches
+        with torch.no_grad():
+            ref = orc.beam_search(
+                lambda c, m: orc.caption_forward(sd, cfg, img_r, mask_r, c, m), B, T, K, 101,
+                eos)
+        assert torch.equal(ids.cpu(), ref), (K, eos, ids.cpu(), ref)
+
+
+def test_beam_cfg5_shape_bf16():
+    """cfg5 decode shape (R50 dil 224, 6/6 d256, V 30522, T 128, batch 64) in bf16: beam 1 ==
+    greedy bitwise; beam 5 runs, its hipGraph replays equal eager launches, and its best beam
+    never scores below the greedy path's own log-probability."""
+    kw = dict(backbone="ResNet50", dilation=True, hidden=256, layers=(6, 6), vocab=30522,
+              max_pos=128, ffn=2048)
+    cfg = make_config(dtype="bf16", **kw)
+    model, _ = build_model(cfg)
+    model.load_state_dict(synthetic_state_dict(model, seed=42))
+    model.to(DEV).eval()
+    B, T = 64, 128
+    images, mask = synthetic_images(B, 224, seed=7)
+    samples = [NestedTensor(images.to(DEV), mask.to(DEV))]
+    g = greedy(samples, model, max_len=T, bos_token=101, eos_token=102)
+    b1 = beam_search(samples, model, max_len=T, beam_size=1, bos_token=101, eos_token=102)
+    assert torch.equal(g, b1)
+    dec = IncrementalBeam(model, 5)
+    b5 = dec(samples, T, 101, 102)
+    s5 = dec.last_scores.clone()
+    b5e = IncrementalBeam(model, 5, use_graphs=False)(samples, T, 101, 102)
+    assert torch.equal(b5, b5e)
+    g1 = IncrementalBeam(model, 1)
+    g1(samples, T, 101, 102)
+    assert bool((s5 >= g1.last_scores - 1e-3).all())
+    assert b5.shape == (B, T) and bool((b5[:, 0] == 101).all())

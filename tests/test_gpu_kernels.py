@@ -241,7 +241,7 @@ def test_attention_decode(dtype, tol, B, H, Lk, Lmax, hd, masked):
         kpm = kpm.to(DEV)
     o = torch.empty(B, C, dtype=dtype, device=DEV)
     call("retr_attention_decode", ops.dcode(dtype), ptr(q), C, ptr(kc), C, ptr(vc), C, ptr(o), C,
-         B, H, Lk, Lmax, hd, ptr(kpm), ops._st())
+         B, H, Lk, Lmax, hd, ptr(kpm), 1, None, ops._st())
     ref, _ = _attn_ref(q.float(), kc[:, :Lk].float(), vc[:, :Lk].float(), H, kpm, False)
     assert rel_err(o.view(B, 1, C), ref) < tol
 

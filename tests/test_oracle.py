@@ -127,3 +127,17 @@ def test_oracle_f2_transformer_matches_reference():
     assert [n[len("transformer."):] for n in names] == list(g["grad_names"])
     norms = np.array([sdo[n].grad.norm().item() for n in names])
     np.testing.assert_allclose(norms, g["grad_norms"], rtol=1e-4, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", [n for n in PARITY_CASES if n.startswith("micro")])
+def test_oracle_beam1_is_reference_greedy(name):
+    """The beam-search restatement (no reference implementation exists) is anchored to the
+    reference through beam_size=1 == eval_utils/decode.py greedy, on the reference's own ids."""
+    g = np.load(os.path.join(GOLD, f"{name}.npz"))
+    cfg, sd, images, mask, caps, cap_mask, _ = _case(name)
+    T = cfg.max_position_embeddings
+    for i, eos in enumerate(g["greedy_eos"]):
+        with torch.no_grad():
+            ids = orc.beam_search(lambda c, m: orc.caption_forward(sd, cfg, images, mask, c, m),
+                                  images.shape[0], T, 1, 101, int(eos))
+        np.testing.assert_array_equal(ids.numpy(), g[f"greedy/eos{i}"])
