@@ -15,6 +15,11 @@
 #include "gemm.hpp"
 #include "../../include/retr_hip.h"
 
+int retr_attention_fwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
+                        long ldv, void* o, long ldo, int B, int H, int Lq, int Lk, int hd,
+                        const unsigned char* kpm, int causal, float p, unsigned long long seed,
+                        float* lse, hipStream_t st);
+
 using namespace retr;
 
 namespace {
@@ -92,6 +97,12 @@ RETR_DEVICE void load_rows_t(T* dst, const T* base, long ld, int r0, int nrows, 
   }
 }
 
+// attention dropout keep decision of (query row, key): the fused kernels' RNG (common.hpp)
+RETR_DEVICE bool attn_keep_at(const DropoutParams& dp, uint32_t row, int key) {
+  const uint32_t bits = attn_pair_bits(attn_row_key(dp_seed(dp), row), (uint32_t)key);
+  return attn_keep(bits, (uint32_t)key, (dp.thresh + 0x8000u) >> 16);
+}
+
 RETR_DEVICE bool masked(const unsigned char* kpm, int b, int Lk, int key, int qrow, int causal) {
   if (key >= Lk) return true;
   if (kpm && kpm[(long)b * Lk + key]) return true;
@@ -157,9 +168,8 @@ attn_fwd_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, long ldv
         float p = (mn == -INFINITY) ? 0.f : __expf(S[j][e] - mn);
         rs += p;
         if (dp.thresh) {
-          int key = k0 + 16 * j + c16;
-          uint64_t idx = (((uint64_t)b * H + h) * Lq + qrow) * (uint64_t)Lk + key;
-          p = retr_keep(dp_seed(dp), idx, dp.thresh) ? p * dp.scale : 0.f;
+          const int key = k0 + 16 * j + c16;
+          p = attn_keep_at(dp, ((uint32_t)b * H + h) * Lq + qrow, key) ? p * dp.scale : 0.f;
         }
         Pw[(4 * g + e) * TS + 16 * j + c16] = from_f<T>(p);
       }
@@ -264,10 +274,8 @@ attn_bwd_dq_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, long 
         if (!masked(kpm, b, Lk, key, qrow, causal) && qrow < Lq) {
           float p = __expf(S[j][e] - L_[e]);
           float dpv = dP[j][e];
-          if (dp.thresh) {
-            uint64_t idx = (((uint64_t)b * H + h) * Lq + qrow) * (uint64_t)Lk + key;
-            dpv = retr_keep(dp_seed(dp), idx, dp.thresh) ? dpv * dp.scale : 0.f;
-          }
+          if (dp.thresh)
+            dpv = attn_keep_at(dp, ((uint32_t)b * H + h) * Lq + qrow, key) ? dpv * dp.scale : 0.f;
           ds = p * (dpv - D_[e]);
         }
         Pw[(4 * g + e) * TS + 16 * j + c16] = from_f<T>(ds);
@@ -353,10 +361,7 @@ attn_bwd_dkdv_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, lon
         bool valid = qrow < Lq && !masked(kpm, b, Lk, key, qrow, causal);
         float p = valid ? __expf(S[j][e] - Ls[qi]) : 0.f;
         bool kp = true;
-        if (dp.thresh && valid) {
-          uint64_t idx = (((uint64_t)b * H + h) * Lq + qrow) * (uint64_t)Lk + key;
-          kp = retr_keep(dp_seed(dp), idx, dp.thresh);
-        }
+        if (dp.thresh && valid) kp = attn_keep_at(dp, ((uint32_t)b * H + h) * Lq + qrow, key);
         P[e][j] = p;
         keep[e][j] = kp;
         float pd = dp.thresh ? (kp ? p * dp.scale : 0.f) : p;
@@ -514,6 +519,17 @@ void allow_lds(K kern, size_t bytes) {
   }
 }
 
+template <typename T>
+int launch_probs(const void* q, long ldq, const void* k, long ldk, int B, int H, int Lq, int Lk,
+                 int hd, const unsigned char* kpm, int causal, const float* lse, float* probs,
+                 hipStream_t st) {
+  const float scale = 1.0f / sqrtf((float)hd);
+  dim3 g2(cdiv((long)Lq * Lk, 256), B);
+  hipLaunchKernelGGL((attn_probs_kernel<T>), g2, dim3(256), 0, st, (const T*)q, ldq,
+                     (const T*)k, ldk, H, Lq, Lk, hd, kpm, causal, scale, lse, probs);
+  return retr_check_launch("attention_probs");
+}
+
 template <typename T, int HDP>
 int fwd_t(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv, void* o,
           long ldo, int B, int H, int Lq, int Lk, int hd, const unsigned char* kpm, int causal,
@@ -527,12 +543,7 @@ int fwd_t(const void* q, long ldq, const void* k, long ldk, const void* v, long 
                      (const T*)k, ldk, (const T*)v, ldv, (T*)o, ldo, H, Lq, Lk, hd, kpm, causal,
                      scale, make_dp(p, seed), lse, kbr > 0 ? kbr : Lk);
   if (retr_check_launch("attention_fwd")) return 1;
-  if (probs) {
-    dim3 g2(cdiv((long)Lq * Lk, 256), B);
-    hipLaunchKernelGGL((attn_probs_kernel<T>), g2, dim3(256), 0, st, (const T*)q, ldq,
-                       (const T*)k, ldk, H, Lq, Lk, hd, kpm, causal, scale, lse, probs);
-    return retr_check_launch("attention_probs");
-  }
+  if (probs) return launch_probs<T>(q, ldq, k, ldk, B, H, Lq, Lk, hd, kpm, causal, lse, probs, st);
   return 0;
 }
 
@@ -575,6 +586,13 @@ int retr_attention_fwd(int dtype, const void* q, long ldq, const void* k, long l
   RETR_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0, "attention: row strides %%8");
   if (B == 0 || Lq == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16 && (hd == 32 || hd == 64) && ldo % 4 == 0) {
+    if (int e = retr_attention_fwd2(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, hd, kpm,
+                                    causal, drop_p, seed, lse, st))
+      return e;
+    return probs ? launch_probs<bf16>(q, ldq, k, ldk, B, H, Lq, Lk, hd, kpm, causal, lse, probs, st)
+                 : 0;
+  }
   if (dtype == RETR_BF16) {
     if (hd <= 32) return fwd_t<bf16, 32>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed, lse, probs, st);
     return fwd_t<bf16, 64>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed, lse, probs, st);

@@ -1,0 +1,272 @@
+// Fused multi-head attention forward for bf16 operands, head dim 32 or 64 (the RE⫶TR shapes:
+// d_model 256 / 512 with 8 heads), on v_mfma_f32_32x32x16_bf16.
+//
+// Replaces the need_weights=False core of F.multi_head_attention_forward
+// (torch/nn/functional.py:6576-6606, used at models/ConcatTransformer.py:160,204,210 via
+// transformer_modules.py:38,66): S = (q hd^-1/2) k^T + mask, P = softmax(S), O = dropout(P) v.
+//
+// Structure (one wave = 32 queries; NW waves per block share K/V tiles of 64 keys in LDS):
+//  * swapped product S^T = K Q^T: the accumulator has the QUERY on the lane and 16 of the 32
+//    keys in registers (the other 16 in lane ^ 32), so the online softmax needs no LDS round
+//    trip: the row max is 16 register maxes + one xor-32 shuffle, the row sum stays
+//    lane-partial until the end;
+//  * P never leaves registers: the S^T accumulator, converted pairwise to bf16, is directly the
+//    B operand of O^T = V^T P^T (the C layout of one 32x32x16 MFMA is the k-permuted B layout
+//    of the next); V^T fragments come from the row-major V tile with ds_read_b64_tr_b16;
+//  * Q (prescaled by hd^-1/2 * log2 e, so the softmax runs on exp2) stays in registers;
+//  * K/V tiles: register-staged double buffer, one barrier per 64-key tile;
+//  * key-padding mask: one byte per lane per tile -> a wave-uniform 64-bit ballot; fully valid
+//    tiles skip masking; causal masking only on tiles that cross the diagonal;
+//  * dropout: 16-bit keep decisions from one 32-bit integer hash per key pair
+//    (common.hpp attn_keep), regenerated identically by the backward kernels.
+// The log-sum-exp (natural log) of every row is saved for the backward pass.
+#include "common.hpp"
+#include "../../include/retr_hip.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+RETR_DEVICE f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+RETR_DEVICE s16x4 tr16(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+RETR_DEVICE bf16x8 join(const s16x4& lo, const s16x4& hi) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int HD>
+struct Tile {
+  static constexpr int KT = 64;              // keys per LDS stage
+  static constexpr int RB = HD * 2 + 16;     // row bytes (16-byte pad against bank conflicts)
+  static constexpr int BYTES = KT * RB;      // one K or V tile
+  static constexpr int STAGE = 2 * BYTES;    // K tile then V tile
+  static constexpr int CPR = HD / 8;         // 16-byte chunks per row
+};
+
+// Stage K and V rows [key0, key0+64) of one (b, h) through registers into an LDS stage.
+template <int HD, int NT>
+struct KVStager {
+  static constexpr int NCH = 2 * Tile<HD>::KT * Tile<HD>::CPR / NT;   // chunks per thread
+  u32x4 reg[NCH];
+  RETR_DEVICE void load(const bf16* kb, long ldk, const bf16* vb, long ldv, int key0, int Lk,
+                        int tid) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int idx = tid + c * NT;
+      const int which = idx / (Tile<HD>::KT * Tile<HD>::CPR);
+      const int rem = idx % (Tile<HD>::KT * Tile<HD>::CPR);
+      const int row = rem / Tile<HD>::CPR, ch = rem % Tile<HD>::CPR;
+      const int key = key0 + row;
+      u32x4 v = u32x4{0u, 0u, 0u, 0u};
+      if (key < Lk)
+        v = which ? *(const u32x4*)(vb + (long)key * ldv + ch * 8)
+                  : *(const u32x4*)(kb + (long)key * ldk + ch * 8);
+      reg[c] = v;
+    }
+  }
+  RETR_DEVICE void store(char* stage, int tid) const {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int idx = tid + c * NT;
+      const int which = idx / (Tile<HD>::KT * Tile<HD>::CPR);
+      const int rem = idx % (Tile<HD>::KT * Tile<HD>::CPR);
+      const int row = rem / Tile<HD>::CPR, ch = rem % Tile<HD>::CPR;
+      *(u32x4*)(stage + which * Tile<HD>::BYTES + row * Tile<HD>::RB + ch * 16) = reg[c];
+    }
+  }
+};
+
+template <int HD, int NW>
+__global__ void __launch_bounds__(NW * 64)
+attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
+                 bf16* o, long ldo, int H, int Lq, int Lk, int kbr, const unsigned char* kpm,
+                 int causal, float qscale, DropoutParams dp, float* lse) {
+  using TL = Tile<HD>;
+  constexpr int NT = NW * 64, KS = HD / 16, DT = HD / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int qblk = blockIdx.x * (32 * NW);
+  const int q0 = qblk + wave * 32;
+  const int qi = q0 + r;                          // this lane's query
+  const bf16* kb = k + (long)b * kbr * ldk + h * HD;
+  const bf16* vb = v + (long)b * kbr * ldv + h * HD;
+
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[qi][16s + 8hh + j], prescaled
+  bf16x8 qf[KS];
+  {
+    const bf16* qr = q + ((long)b * Lq + (qi < Lq ? qi : Lq - 1)) * ldq + h * HD;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 x = *(const bf16x8*)(qr + 16 * s + 8 * hh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * qscale);
+      qf[s] = x;
+    }
+  }
+
+  int kend = Lk;
+  if (causal) kend = min(Lk, qblk + 32 * NW);
+  const int ntiles = (kend + TL::KT - 1) / TL::KT;
+
+  const bool drop = dp.thresh != 0;
+  const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
+  const uint32_t rowkey = drop ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
+
+  f32x16 O[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) O[dt][e] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  KVStager<HD, NT> stg;
+  stg.load(kb, ldk, vb, ldv, 0, Lk, tid);
+  stg.store(smem, tid);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int key0 = t * TL::KT;
+    const char* Kl = smem + (t & 1) * TL::STAGE;
+    const char* Vl = Kl + TL::BYTES;
+    if (t + 1 < ntiles) stg.load(kb, ldk, vb, ldv, key0 + TL::KT, Lk, tid);
+    // padding mask of the tile's 64 keys, wave-uniform
+    bool pad = key0 + lane >= Lk;
+    if (kpm && !pad) pad = kpm[(long)b * Lk + key0 + lane] != 0;
+    const unsigned long long pmask = __ballot(pad);
+    const bool diag = causal && (key0 + TL::KT - 1 > q0);
+
+    // S^T (two 32-key sub-tiles): rows = keys, lane = query
+    f32x16 S[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) S[sub][e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8 a = *(const bf16x8*)(Kl + (sub * 32 + r) * TL::RB + (16 * s + 8 * hh) * 2);
+        S[sub] = mfma32(a, qf[s], S[sub]);
+      }
+    }
+    if (pmask || diag) {
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int kl = sub * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          if (((pmask >> kl) & 1ull) || (diag && key0 + kl > qi)) S[sub][e] = -INFINITY;
+        }
+    }
+    // online softmax (log2 domain)
+    float mt = -INFINITY;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) mt = fmaxf(mt, S[sub][e]);
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = (mn == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mn);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) O[dt][e] *= alpha;
+    bf16x8 pf[4];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int kk = key0 + sub * 32 + 8 * g + 4 * hh;   // 4 consecutive keys
+        uint32_t b01 = 0, b23 = 0;
+        if (drop) {
+          b01 = attn_pair_bits(rowkey, kk);
+          b23 = attn_pair_bits(rowkey, kk + 2);
+        }
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const int e = 4 * g + e4;
+          float p = (mn == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(S[sub][e] - mn);
+          l += p;
+          if (drop) {
+            const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
+            p = kp ? p * dp.scale : 0.f;
+          }
+          pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
+        }
+      }
+    }
+    // O^T += V^T P^T  (A = V^T via transposed LDS reads, B = P in registers)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      const int qrow = (lane & 15) >> 2;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const char* lo = Vl + (16 * s + 4 * hh + qrow) * TL::RB + c0 * 2;
+        const bf16x8 a = join(tr16(lo), tr16(lo + 8 * TL::RB));
+        O[dt] = mfma32(a, pf[s], O[dt]);
+      }
+    }
+    if (t + 1 < ntiles) stg.store(smem + ((t + 1) & 1) * TL::STAGE, tid);
+    __syncthreads();
+  }
+
+  l += __shfl_xor(l, 32, 64);
+  if (qi < Lq) {
+    const float inv = 1.f / l;      // fully masked row: 0 * inf = NaN (torch's all -inf softmax)
+    bf16* orow = o + ((long)b * Lq + qi) * ldo + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 w;
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) w[e4] = (bf16)(O[dt][4 * g + e4] * inv);
+        *(bf16x4*)(orow + dt * 32 + 8 * g + 4 * hh) = w;
+      }
+    if (hh == 0 && lse) lse[((long)b * H + h) * Lq + qi] = (m + __log2f(l)) * kLn2;
+  }
+}
+
+template <int HD, int NW>
+int launch_fwd2(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+                void* o, long ldo, int B, int H, int Lq, int Lk, int kbr,
+                const unsigned char* kpm, int causal, float p, unsigned long long seed,
+                float* lse, hipStream_t st) {
+  const float qscale = kLog2e / sqrtf((float)HD);
+  const size_t lds = 2 * Tile<HD>::STAGE;
+  dim3 grid((Lq + 32 * NW - 1) / (32 * NW), H, B);
+  hipLaunchKernelGGL((attn_fwd2_kernel<HD, NW>), grid, dim3(NW * 64), lds, st, (const bf16*)q,
+                     ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, H, Lq, Lk, kbr,
+                     kpm, causal, qscale, make_dp(p, seed), lse);
+  return retr_check_launch("attention_fwd2");
+}
+
+}  // namespace
+
+// Internal entry (called by retr_attention_fwd for bf16 with hd in {32, 64}).
+int retr_attention_fwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
+                        long ldv, void* o, long ldo, int B, int H, int Lq, int Lk, int hd,
+                        const unsigned char* kpm, int causal, float p, unsigned long long seed,
+                        float* lse, hipStream_t st) {
+  const bool big = (long)B * H * ((Lq + 63) / 64) >= 1024;
+  if (hd == 32) {
+    return big ? launch_fwd2<32, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st)
+               : launch_fwd2<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st);
+  }
+  return big ? launch_fwd2<64, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st)
+             : launch_fwd2<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st);
+}

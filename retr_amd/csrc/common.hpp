@@ -67,6 +67,28 @@ inline DropoutParams make_dp(float p, unsigned long long seed) {
   return dp;
 }
 
+// ---- cheap attention-dropout RNG (fused attention kernels) -------------------------------------
+// keep(row, key) from 16 bits of a 32-bit integer hash; one hash serves the key pair
+// (2j, 2j+1).  row_key = attn_row_key(seed, row) is computed once per query row.  The keep
+// probability is quantised to 1/65536 (p = 0.1 -> 0.100006); scale stays 1/(1-p).
+RETR_DEVICE uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+RETR_DEVICE uint32_t attn_row_key(uint64_t seed, uint32_t row) {
+  return mix32((uint32_t)seed ^ mix32(row * 0x9E3779B9u + (uint32_t)(seed >> 32)));
+}
+RETR_DEVICE uint32_t attn_pair_bits(uint32_t row_key, uint32_t key) {
+  return mix32(row_key + (key >> 1) * 0x85EBCA77u);
+}
+RETR_DEVICE bool attn_keep(uint32_t bits, uint32_t key, uint32_t thresh16) {
+  return ((key & 1) ? (bits >> 16) : (bits & 0xffffu)) >= thresh16;
+}
+
 // ---- wave reductions (wave64) ------------------------------------------------------------------
 RETR_DEVICE float wave_sum(float v) {
 #pragma unroll

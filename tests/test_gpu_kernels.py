@@ -1,5 +1,6 @@
 """Per-kernel numerics of libretr_hip.so against plain PyTorch fp32 references (GPU box)."""
 import math
+import numpy as np
 
 import pytest
 import torch
@@ -281,3 +282,91 @@ def test_cross_entropy_and_argmax(dtype, tol):
     assert rel_err(lt.grad.float(), x.grad) < 5 * tol
     am = ops.argmax_rows(buf[:, :V])
     assert torch.equal(am, buf[:, :V].float().argmax(-1))
+
+
+def _mix32(x):
+    x = x.astype(np.uint64) & 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
+def attn_keep_mask(seed, B, H, Lq, Lk, p):
+    """numpy restatement of the fused attention kernels' dropout keep mask (csrc/common.hpp
+    attn_row_key / attn_pair_bits / attn_keep): [B, H, Lq, Lk] bool."""
+    thresh = int(np.float32(min(np.float32(p) * np.float32(4294967296.0), 4294967295.0)))
+    th16 = (thresh + 0x8000) >> 16
+    rows = np.arange(B * H * Lq, dtype=np.uint64)
+    s_lo, s_hi = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    rk = _mix32(s_lo ^ _mix32((rows * 0x9E3779B9 + s_hi) & 0xFFFFFFFF))
+    keys = np.arange(Lk, dtype=np.uint64)
+    bits = _mix32((rk[:, None] + (keys[None, :] >> 1) * 0x85EBCA77) & 0xFFFFFFFF)
+    half = np.where(keys[None, :] & 1, bits >> 16, bits & 0xFFFF)
+    return torch.from_numpy((half >= th16).reshape(B, H, Lq, Lk))
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("B,H,Lq,Lk,hd,causal,masked", [
+    (2, 8, 400, 400, 32, False, True), (2, 8, 128, 128, 32, True, True),
+    (2, 8, 128, 196, 64, False, True), (1, 8, 130, 625, 64, False, True)])
+def test_attention_dropout_exact_mask(dtype, tol, B, H, Lq, Lk, hd, causal, masked):
+    """Forward and backward with dropout p=0.1 against torch on the kernels' own keep mask
+    (restated in numpy): the backward regenerates exactly the forward's mask."""
+    from retr_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(7 * Lq + Lk + hd)
+    C = H * hd
+    q = torch.randn(B, Lq, C, generator=g).to(DEV).to(dtype)
+    k = torch.randn(B, Lk, C, generator=g).to(DEV).to(dtype)
+    v = torch.randn(B, Lk, C, generator=g).to(DEV).to(dtype)
+    kpm = None
+    if masked:
+        kpm = torch.zeros(B, Lk, dtype=torch.uint8)
+        kpm[:, Lk - Lk // 5:] = 1
+        kpm = kpm.to(DEV)
+    seed, p = 0x1234567887654321, 0.1
+    base = int(ops.seed_base().item())                 # dropout seed = op seed + step seed
+    keep = attn_keep_mask((seed + base) & (2 ** 64 - 1), B, H, Lq, Lk, p).to(DEV)
+    o = torch.empty(B * Lq, C, dtype=dtype, device=DEV)
+    lse = torch.empty(B * H * Lq, device=DEV)
+    ops.k_attention_fwd(q.view(-1, C), k.view(-1, C), v.view(-1, C), o, B, H, Lq, Lk, hd, kpm,
+                        causal, p, seed, lse)
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    qh = qr.view(B, Lq, H, hd).transpose(1, 2) * (1.0 / math.sqrt(hd))
+    kh = kr.view(B, Lk, H, hd).transpose(1, 2)
+    vh = vr.view(B, Lk, H, hd).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2)
+    if kpm is not None:
+        s = s.masked_fill(kpm.bool()[:, None, None, :], float("-inf"))
+    if causal:
+        s = s.masked_fill(torch.ones(Lq, Lk, dtype=torch.bool, device=DEV).triu(1),
+                          float("-inf"))
+    pm = s.softmax(-1) * keep / (1 - p)
+    ref = (pm @ vh).transpose(1, 2).reshape(B, Lq, C)
+    assert rel_err(o.view(B, Lq, C), ref) < tol
+    do = torch.randn(B, Lq, C, generator=g).to(DEV).to(dtype)
+    ref.backward(do.float())
+    dq = torch.empty_like(o)
+    dk = torch.empty(B * Lk, C, dtype=dtype, device=DEV)
+    dv = torch.empty_like(dk)
+    ops.k_attention_bwd(q.view(-1, C), k.view(-1, C), v.view(-1, C), o, do.view(-1, C), lse, dq,
+                        dk, dv, B, H, Lq, Lk, hd, kpm, causal, p, seed)
+    assert rel_err(dq.view(B, Lq, C), qr.grad) < 3 * tol
+    assert rel_err(dk.view(B, Lk, C), kr.grad) < 3 * tol
+    assert rel_err(dv.view(B, Lk, C), vr.grad) < 3 * tol
+
+
+def test_attention_fully_masked_rows_nan():
+    """A query row whose keys are all padded is NaN (torch softmax of an all -inf row)."""
+    from retr_amd import ops
+    B, H, L, hd = 2, 8, 64, 32
+    C = H * hd
+    q = torch.randn(B * L, C, device=DEV).to(torch.bfloat16)
+    kpm = torch.zeros(B, L, dtype=torch.uint8, device=DEV)
+    kpm[1] = 1
+    o = torch.empty(B * L, C, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B * H * L, device=DEV)
+    ops.k_attention_fwd(q, q, q, o, B, H, L, L, hd, kpm, False, 0.0, 0, lse)
+    assert torch.isfinite(o[:L].float()).all() and torch.isnan(o[L:].float()).all()
