@@ -19,6 +19,12 @@ int retr_attention_fwd2(const void* q, long ldq, const void* k, long ldk, const 
                         long ldv, void* o, long ldo, int B, int H, int Lq, int Lk, int hd,
                         const unsigned char* kpm, int causal, float p, unsigned long long seed,
                         float* lse, hipStream_t st);
+int retr_attention_bwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
+                        long ldv, const void* o, long ldo, const void* dout, long lddo,
+                        const float* lse, void* dq, long lddq, void* dk, long lddk, void* dv,
+                        long lddv, int B, int H, int Lq, int Lk, int hd,
+                        const unsigned char* kpm, int causal, float p, unsigned long long seed,
+                        float* D, hipStream_t st);
 
 using namespace retr;
 
@@ -641,6 +647,11 @@ int retr_attention_bwd(int dtype, const void* q, long ldq, const void* k, long l
                "attention: row strides %%8");
   if (B == 0 || Lq == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == RETR_BF16 && (hd == 32 || hd == 64) && lddq % 4 == 0 && lddk % 4 == 0 &&
+      lddv % 4 == 0)
+    return retr_attention_bwd2(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk,
+                               lddk, dv, lddv, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed,
+                               workspace, st);
   if (dtype == RETR_BF16) {
     if (hd <= 32) return bwd_t<bf16, 32>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed, workspace, st);
     return bwd_t<bf16, 64>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed, workspace, st);

@@ -270,3 +270,338 @@ int retr_attention_fwd2(const void* q, long ldq, const void* k, long ldk, const 
   return big ? launch_fwd2<64, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st)
              : launch_fwd2<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st);
 }
+
+// =============================================================================================
+// Backward (bf16, head dim 32 / 64).  Two kernels, no atomics (deterministic):
+//  * dq2:   one wave = 32 queries (query on the lane, as the forward).  Per 64-key LDS tile:
+//           S^T = K Q^T and dP^T = V dO^T, P = exp2(S^T - lse), dS = P (drop(dP) - D),
+//           dQ^T += K^T dS^T (K^T by transposed LDS reads).  D = rowsum(dO * O) is formed in
+//           the prologue from the lane's own dO / O fragments and written out for dkdv2.
+//  * dkdv2: one wave = 32 keys (key on the lane).  Per 64-query LDS tile (Q, dO, lse, D):
+//           S = Q K^T, dP = dO V^T, the same P / dS, then dV^T += dO^T drop(P) and
+//           dK^T += Q^T dS (dO^T / Q^T by transposed LDS reads).
+// Dropout masks are regenerated from the forward's (seed, row, key) hash.
+// =============================================================================================
+
+// one 64-row tile of two [rows][HD] tensors plus per-row scalars, register-staged into LDS
+template <int HD, int NT>
+struct RowStager {
+  KVStager<HD, NT> kv;
+  float lse2, dd;
+  uint32_t rk;
+  RETR_DEVICE void load(const bf16* a, long lda, const bf16* b, long ldb, int row0, int rows,
+                        const float* lse, const float* D, long sbase, uint64_t seed, bool drop,
+                        uint32_t rowbase, int tid) {
+    kv.load(a, lda, b, ldb, row0, rows, tid);
+    if (tid < 64) {
+      const int rr = row0 + tid;
+      const int rc = rr < rows ? rr : rows - 1;
+      lse2 = lse[sbase + rc] * kLog2e;
+      dd = D[sbase + rc];
+      rk = drop ? attn_row_key(seed, rowbase + (uint32_t)rr) : 0u;
+    }
+  }
+  RETR_DEVICE void store(char* stage, int tid) const {
+    kv.store(stage, tid);
+    if (tid < 64) {
+      float* ex = (float*)(stage + Tile<HD>::STAGE);
+      ex[tid] = lse2;
+      ex[64 + tid] = dd;
+      ((uint32_t*)ex)[128 + tid] = rk;
+    }
+  }
+};
+
+template <int HD, int NW>
+__global__ void __launch_bounds__(NW * 64)
+attn_bwd_dq2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
+                    const bf16* o, long ldo, const bf16* dout, long lddo, const float* lse,
+                    float* Dout, bf16* dq, long lddq, int H, int Lq, int Lk,
+                    const unsigned char* kpm, int causal, float qscale, float scale,
+                    DropoutParams dp) {
+  using TL = Tile<HD>;
+  constexpr int NT = NW * 64, KS = HD / 16, DT = HD / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int qblk = blockIdx.x * (32 * NW);
+  const int q0 = qblk + wave * 32;
+  const int qi = q0 + r;
+  const int qc = qi < Lq ? qi : Lq - 1;
+  const bf16* kb = k + (long)b * Lk * ldk + h * HD;
+  const bf16* vb = v + (long)b * Lk * ldv + h * HD;
+  const long srow = ((long)b * H + h) * Lq + qc;
+
+  bf16x8 qf[KS], dof[KS];
+  float dpart = 0.f;
+  {
+    const bf16* qr = q + ((long)b * Lq + qc) * ldq + h * HD;
+    const bf16* dr = dout + ((long)b * Lq + qc) * lddo + h * HD;
+    const bf16* orr = o + ((long)b * Lq + qc) * ldo + h * HD;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 x = *(const bf16x8*)(qr + 16 * s + 8 * hh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * qscale);
+      qf[s] = x;
+      const bf16x8 d8 = *(const bf16x8*)(dr + 16 * s + 8 * hh);
+      const bf16x8 o8 = *(const bf16x8*)(orr + 16 * s + 8 * hh);
+      dof[s] = d8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dpart += (float)d8[j] * (float)o8[j];
+    }
+  }
+  const float Dq = dpart + __shfl_xor(dpart, 32, 64);
+  if (hh == 0 && qi < Lq) Dout[srow] = Dq;
+  const float lq2 = lse[srow] * kLog2e;
+
+  int kend = Lk;
+  if (causal) kend = min(Lk, qblk + 32 * NW);
+  const int ntiles = (kend + TL::KT - 1) / TL::KT;
+  const bool drop = dp.thresh != 0;
+  const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
+  const uint32_t rowkey = drop ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
+
+  f32x16 G[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) G[dt][e] = 0.f;
+
+  KVStager<HD, NT> stg;
+  stg.load(kb, ldk, vb, ldv, 0, Lk, tid);
+  stg.store(smem, tid);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int key0 = t * TL::KT;
+    const char* Kl = smem + (t & 1) * TL::STAGE;
+    const char* Vl = Kl + TL::BYTES;
+    if (t + 1 < ntiles) stg.load(kb, ldk, vb, ldv, key0 + TL::KT, Lk, tid);
+    bool pad = key0 + lane >= Lk;
+    if (kpm && !pad) pad = kpm[(long)b * Lk + key0 + lane] != 0;
+    const unsigned long long pmask = __ballot(pad);
+    const bool diag = causal && (key0 + TL::KT - 1 > q0);
+    bf16x8 sf[4];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x16 S, P;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) S[e] = 0.f, P[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int off = (sub * 32 + r) * TL::RB + (16 * s + 8 * hh) * 2;
+        S = mfma32(*(const bf16x8*)(Kl + off), qf[s], S);
+        P = mfma32(*(const bf16x8*)(Vl + off), dof[s], P);     // dP^T
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int kk = key0 + sub * 32 + 8 * g + 4 * hh;
+        uint32_t b01 = 0, b23 = 0;
+        if (drop) {
+          b01 = attn_pair_bits(rowkey, kk);
+          b23 = attn_pair_bits(rowkey, kk + 2);
+        }
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
+          const bool msk = ((pmask >> kl) & 1ull) || (diag && key0 + kl > qi);
+          const float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - lq2);
+          float dpv = P[e];
+          if (drop) dpv = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? dpv * dp.scale : 0.f;
+          sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - Dq));
+        }
+      }
+    }
+    // dQ^T += K^T dS^T
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      const int qrow = (lane & 15) >> 2;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const char* lo = Kl + (16 * s + 4 * hh + qrow) * TL::RB + c0 * 2;
+        G[dt] = mfma32(join(tr16(lo), tr16(lo + 8 * TL::RB)), sf[s], G[dt]);
+      }
+    }
+    if (t + 1 < ntiles) stg.store(smem + ((t + 1) & 1) * TL::STAGE, tid);
+    __syncthreads();
+  }
+  if (qi < Lq) {
+    bf16* row = dq + ((long)b * Lq + qi) * lddq + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 w;
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) w[e4] = (bf16)(G[dt][4 * g + e4] * scale);
+        *(bf16x4*)(row + dt * 32 + 8 * g + 4 * hh) = w;
+      }
+  }
+}
+
+template <int HD, int NW>
+__global__ void __launch_bounds__(NW * 64)
+attn_bwd_dkdv2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v,
+                      long ldv, const bf16* dout, long lddo, const float* lse, const float* D,
+                      bf16* dk, long lddk, bf16* dv, long lddv, int H, int Lq, int Lk,
+                      const unsigned char* kpm, int causal, float kscale, float scale,
+                      DropoutParams dp) {
+  using TL = Tile<HD>;
+  constexpr int NT = NW * 64, KS = HD / 16, DT = HD / 32;
+  constexpr int STAGE = TL::STAGE + 3 * 64 * 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int kblk = blockIdx.x * (32 * NW);
+  const int kj = kblk + wave * 32 + r;          // this lane's key
+  const int kc = kj < Lk ? kj : Lk - 1;
+  const bf16* qb = q + (long)b * Lq * ldq + h * HD;
+  const bf16* db = dout + (long)b * Lq * lddo + h * HD;
+  const long sbase = ((long)b * H + h) * Lq;
+
+  bf16x8 kf[KS], vf[KS];
+  {
+    const bf16* kr = k + ((long)b * Lk + kc) * ldk + h * HD;
+    const bf16* vr = v + ((long)b * Lk + kc) * ldv + h * HD;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 x = *(const bf16x8*)(kr + 16 * s + 8 * hh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * kscale);
+      kf[s] = x;
+      vf[s] = *(const bf16x8*)(vr + 16 * s + 8 * hh);
+    }
+  }
+  const bool kmask = kj >= Lk || (kpm && kpm[(long)b * Lk + kc]);
+  const bool drop = dp.thresh != 0;
+  const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
+  const uint64_t seed = drop ? dp_seed(dp) : 0ull;
+
+  f32x16 GK[DT], GV[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) GK[dt][e] = 0.f, GV[dt][e] = 0.f;
+
+  const int qstart = causal ? (kblk / TL::KT) * TL::KT : 0;
+  RowStager<HD, NT> stg;
+  stg.load(qb, ldq, db, lddo, qstart, Lq, lse, D, sbase, seed, drop,
+           (uint32_t)((b * H + h) * Lq), tid);
+  stg.store(smem, tid);
+  __syncthreads();
+  int it = 0;
+  for (int qt = qstart; qt < Lq; qt += TL::KT, ++it) {
+    const char* Ql = smem + (it & 1) * STAGE;
+    const char* Dl = Ql + TL::BYTES;
+    const float* ex = (const float*)(Ql + TL::STAGE);
+    if (qt + TL::KT < Lq)
+      stg.load(qb, ldq, db, lddo, qt + TL::KT, Lq, lse, D, sbase, seed, drop,
+               (uint32_t)((b * H + h) * Lq), tid);
+    bf16x8 pf[4], sf[4];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x16 S, P;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) S[e] = 0.f, P[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int off = (sub * 32 + r) * TL::RB + (16 * s + 8 * hh) * 2;
+        S = mfma32(*(const bf16x8*)(Ql + off), kf[s], S);       // S = Q K^T (key on lane)
+        P = mfma32(*(const bf16x8*)(Dl + off), vf[s], P);       // dP = dO V^T
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ql = sub * 32 + 8 * g + 4 * hh;               // 4 consecutive queries
+        const f32x4 l4 = *(const f32x4*)(ex + ql);
+        const f32x4 d4 = *(const f32x4*)(ex + 64 + ql);
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const int e = 4 * g + e4, qq = qt + ql + e4;
+          const bool msk = kmask || qq >= Lq || (causal && kj > qq);
+          float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - l4[e4]);
+          float dpv = P[e], pm = p;
+          if (drop) {
+            const uint32_t rk = ((const uint32_t*)ex)[128 + ql + e4];
+            const bool kp = attn_keep(attn_pair_bits(rk, (uint32_t)kj), (uint32_t)kj, th16);
+            dpv = kp ? dpv * dp.scale : 0.f;
+            pm = kp ? p * dp.scale : 0.f;
+          }
+          pf[2 * sub + (e >> 3)][e & 7] = (bf16)pm;
+          sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - d4[e4]));
+        }
+      }
+    }
+    // dV^T += dO^T drop(P);  dK^T += Q^T dS  (A operands by transposed reads of the tiles)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      const int qrow = (lane & 15) >> 2;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int roff = (16 * s + 4 * hh + qrow) * TL::RB + c0 * 2;
+        GV[dt] = mfma32(join(tr16(Dl + roff), tr16(Dl + roff + 8 * TL::RB)), pf[s], GV[dt]);
+        GK[dt] = mfma32(join(tr16(Ql + roff), tr16(Ql + roff + 8 * TL::RB)), sf[s], GK[dt]);
+      }
+    }
+    if (qt + TL::KT < Lq) stg.store(smem + ((it + 1) & 1) * STAGE, tid);
+    __syncthreads();
+  }
+  if (kj < Lk) {
+    bf16* krow = dk + ((long)b * Lk + kj) * lddk + h * HD;
+    bf16* vrow = dv + ((long)b * Lk + kj) * lddv + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 wk, wv;
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          wk[e4] = (bf16)(GK[dt][4 * g + e4] * scale);
+          wv[e4] = (bf16)GV[dt][4 * g + e4];
+        }
+        *(bf16x4*)(krow + dt * 32 + 8 * g + 4 * hh) = wk;
+        *(bf16x4*)(vrow + dt * 32 + 8 * g + 4 * hh) = wv;
+      }
+  }
+}
+
+template <int HD, int NW>
+int launch_bwd2(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+                const void* o, long ldo, const void* dout, long lddo, const float* lse,
+                void* dq, long lddq, void* dk, long lddk, void* dv, long lddv, int B, int H,
+                int Lq, int Lk, const unsigned char* kpm, int causal, float p,
+                unsigned long long seed, float* D, hipStream_t st) {
+  const float scale = 1.f / sqrtf((float)HD);
+  const float cs = kLog2e * scale;
+  const DropoutParams dp = make_dp(p, seed);
+  hipLaunchKernelGGL((attn_bwd_dq2_kernel<HD, NW>), dim3((Lq + 32 * NW - 1) / (32 * NW), H, B),
+                     dim3(NW * 64), 2 * Tile<HD>::STAGE, st, (const bf16*)q, ldq,
+                     (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
+                     (const bf16*)dout, lddo, lse, D, (bf16*)dq, lddq, H, Lq, Lk, kpm, causal,
+                     cs, scale, dp);
+  if (int e = retr_check_launch("attention_bwd_dq2")) return e;
+  hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<HD, NW>),
+                     dim3((Lk + 32 * NW - 1) / (32 * NW), H, B), dim3(NW * 64),
+                     2 * (Tile<HD>::STAGE + 3 * 64 * 4), st, (const bf16*)q, ldq,
+                     (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo, lse, D,
+                     (bf16*)dk, lddk, (bf16*)dv, lddv, H, Lq, Lk, kpm, causal, cs, scale, dp);
+  return retr_check_launch("attention_bwd_dkdv2");
+}
+
+int retr_attention_bwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
+                        long ldv, const void* o, long ldo, const void* dout, long lddo,
+                        const float* lse, void* dq, long lddq, void* dk, long lddk, void* dv,
+                        long lddv, int B, int H, int Lq, int Lk, int hd,
+                        const unsigned char* kpm, int causal, float p, unsigned long long seed,
+                        float* D, hipStream_t st) {
+  if (hd == 32)
+    return launch_bwd2<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk,
+                              lddk, dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, st);
+  return launch_bwd2<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk,
+                            dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, st);
+}

@@ -167,6 +167,126 @@ struct ConvWgradB {  // B(row = kh,kw,ci ; k = pixel n,oh,ow) = X[n, oh*s-p+kh d
   }
 };
 
+// ---- stride-2 data gradient by output phase ------------------------------------------------
+// For stride 2 (dilation 1) only taps kh == (ih + p) mod 2 reach an input row ih, so the
+// dgrad of each of the four (ih, iw) parity classes is a dense implicit GEMM over its own tap
+// subset: no MFMA work on the structurally zero (tap, pixel) pairs that the generic
+// ConvDgradA loader multiplies (3/4 of them for 1x1 and ~5/9 for 3x3 stride-2 convs).
+struct Phase {
+  int a, b;          // parity class of (ih + p, iw + p)
+  int ih0, iw0;      // first input row / column of the class
+  int Hp, Wp;        // rows / columns of the class
+  int nkh, nkw;      // taps of the class: kh = a + 2 ti, kw = b + 2 tj
+};
+
+template <typename T>
+struct ConvDgradPhaseA {  // A(m = n,i',j' ; k = ti,tj,co) = G[n, i' + ch(ti), j' + cw(tj), co]
+  static constexpr bool kContig = true;
+  const T* gr;
+  Geom g;
+  Phase ph;
+  int M, K;
+  struct Ctx { const T* img; int i, j; bool ok; };
+  struct KCur { int k, c, ti, tj; };
+  RETR_DEVICE Ctx row_ctx(int r) const {
+    Ctx c;
+    c.ok = r < M;
+    const int rr = c.ok ? r : 0;
+    const int hw = ph.Hp * ph.Wp;
+    const int n = rr / hw, rem = rr - n * hw;
+    c.i = rem / ph.Wp;
+    c.j = rem - c.i * ph.Wp;
+    c.img = gr + (long)n * g.OH * g.OW * g.Co;
+    return c;
+  }
+  RETR_DEVICE KCur kcur(int k) const {
+    KCur t;
+    t.k = k;
+    const int tap = k / g.Co;
+    t.c = k - tap * g.Co;
+    t.ti = tap / ph.nkw;
+    t.tj = tap - t.ti * ph.nkw;
+    return t;
+  }
+  RETR_DEVICE void advance(KCur& t, int d) const {
+    t.k += d;
+    t.c += d;
+    while (t.c >= g.Co) {
+      t.c -= g.Co;
+      if (++t.tj == ph.nkw) {
+        t.tj = 0;
+        ++t.ti;
+      }
+    }
+  }
+  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& t) const {
+    if (!c.ok || t.k >= K) return zero16();
+    // oh = (ih + p - kh) / 2 with ih = ih0 + 2 i, kh = a + 2 ti
+    const int oh = c.i + ((ph.ih0 + g.p - ph.a) >> 1) - t.ti;
+    const int ow = c.j + ((ph.iw0 + g.p - ph.b) >> 1) - t.tj;
+    if ((unsigned)oh >= (unsigned)g.OH || (unsigned)ow >= (unsigned)g.OW) return zero16();
+    return *(const u32x4*)(c.img + ((long)oh * g.OW + ow) * g.Co + t.c);
+  }
+};
+
+template <typename T>
+struct DgradPhaseW {  // B(row = ci ; k = ti,tj,co) = Wt[ci][a + 2ti][b + 2tj][co]
+  static constexpr bool kContig = true;
+  const T* wt;
+  Geom g;
+  Phase ph;
+  int rows, K;
+  struct Ctx { const T* row; bool ok; };
+  struct KCur { int k, c, ti, tj; };
+  RETR_DEVICE Ctx row_ctx(int r) const {
+    return Ctx{wt + (long)(r < rows ? r : 0) * g.KH * g.KW * g.Co, r < rows};
+  }
+  RETR_DEVICE KCur kcur(int k) const {
+    KCur t;
+    t.k = k;
+    const int tap = k / g.Co;
+    t.c = k - tap * g.Co;
+    t.ti = tap / ph.nkw;
+    t.tj = tap - t.ti * ph.nkw;
+    return t;
+  }
+  RETR_DEVICE void advance(KCur& t, int d) const {
+    t.k += d;
+    t.c += d;
+    while (t.c >= g.Co) {
+      t.c -= g.Co;
+      if (++t.tj == ph.nkw) {
+        t.tj = 0;
+        ++t.ti;
+      }
+    }
+  }
+  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& t) const {
+    if (!c.ok || t.k >= K) return zero16();
+    const int kh = ph.a + 2 * t.ti, kw = ph.b + 2 * t.tj;
+    return *(const u32x4*)(c.row + ((long)kh * g.KW + kw) * g.Co + t.c);
+  }
+};
+
+// epilogue adaptor: phase-local GEMM row -> NHWC pixel row of dx
+template <class EP>
+struct EpiPhaseRows {
+  EP ep;
+  int Hp, Wp, H, W, ih0, iw0;
+  static constexpr bool kRowSum = false;
+  float* rowsum = nullptr;
+  RETR_DEVICE int map(int m) const {
+    const int hw = Hp * Wp;
+    const int n = m / hw, rem = m - n * hw;
+    const int i = rem / Wp, j = rem - i * Wp;
+    return (n * H + ih0 + 2 * i) * W + iw0 + 2 * j;
+  }
+  RETR_DEVICE void apply(int m, int n, float v) const { ep.apply(map(m), n, v); }
+  RETR_DEVICE void apply8(int m, int n, float (&v)[8]) const { ep.apply8(map(m), n, v); }
+  RETR_DEVICE void empty_split(int, int) const {}
+  RETR_DEVICE bool lane_contiguous() const { return false; }
+};
+
 template <int FAM, typename T, class LA, class LB, class EP>
 int launch_auto(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits,
                 hipStream_t st, const char* what) {
@@ -199,6 +319,28 @@ int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* a
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseK<T> la{(const T*)dy, (long)g.Co, M, K};
     return launch_auto<kFamConvDgrad, T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad_1x1");
+  }
+  if (g.s == 2 && g.d == 1) {
+    for (int a = 0; a < 2; ++a)
+      for (int bb = 0; bb < 2; ++bb) {
+        Phase ph;
+        ph.a = a;
+        ph.b = bb;
+        ph.ih0 = ((a - g.p) % 2 + 2) % 2;
+        ph.iw0 = ((bb - g.p) % 2 + 2) % 2;
+        ph.Hp = g.H > ph.ih0 ? (g.H - ph.ih0 + 1) / 2 : 0;
+        ph.Wp = g.W > ph.iw0 ? (g.W - ph.iw0 + 1) / 2 : 0;
+        ph.nkh = g.KH > a ? (g.KH - a + 1) / 2 : 0;
+        ph.nkw = g.KW > bb ? (g.KW - bb + 1) / 2 : 0;
+        const int Mp = g.Nb * ph.Hp * ph.Wp, Kp = ph.nkh * ph.nkw * g.Co;
+        if (Mp == 0) continue;
+        ConvDgradPhaseA<T> pa{(const T*)dy, g, ph, Mp, Kp};
+        DgradPhaseW<T> pb{(const T*)wt, g, ph, N, Kp};
+        EpiPhaseRows<EpiDgrad<T, T, T>> pe{ep, ph.Hp, ph.Wp, g.H, g.W, ph.ih0, ph.iw0};
+        if (int e = launch_auto<kFamConvDgrad, T>(pa, pb, pe, Mp, N, Kp, 1, st, "conv_dgrad_s2"))
+          return e;
+      }
+    return 0;
   }
   ConvDgradA<T> la{(const T*)dy, g, M, K};
   return launch_auto<kFamConvDgrad, T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad");

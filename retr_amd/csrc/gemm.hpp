@@ -189,7 +189,7 @@ gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
   const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
   const int kb = blockIdx.y * kchunk;
   const int ke = min(K, kb + kchunk);
-  if (kb >= ke) {
+  if (kb >= ke && K > 0) {   // (K == 0: no reduction, the epilogue still runs on zeros)
     ep.empty_split(m0, n0);
     return;
   }
@@ -324,7 +324,8 @@ int launch_gemm(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, i
   int ksteps = cdiv(K, BK);
   if (splits > ksteps) splits = ksteps;
   int kchunk = cdiv(ksteps, splits) * BK;
-  splits = cdiv(K, kchunk);
+  splits = K > 0 ? cdiv(K, kchunk) : 1;
+  if (K == 0) kchunk = BK;
   dim3 grid(tm * tn, splits);
   constexpr size_t lds = gemm_lds_bytes<T, BM, BN>();
   if constexpr (lds > 65536) {
