@@ -38,6 +38,7 @@ RETR_DEVICE u32x4 zero16() { return u32x4{0u, 0u, 0u, 0u}; }
 // half of a transposed read land on distinct banks.
 template <int ROWS>
 RETR_DEVICE int kmaj_off(int k, int r) {  // r multiple of 4
+  static_assert(ROWS >= 64, "k-major image needs >= 64 rows (swizzle stays inside the row)");
   constexpr int RB = ROWS * 2;
   int f;
   if constexpr (ROWS >= 128) f = 4 * ((k & 3) | (((k >> 3) & 1) << 2));
@@ -339,6 +340,19 @@ int launch_gemm(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, i
   hipLaunchKernelGGL((gemm_kernel<FAM, T, BM, BN, LA, LB, EP>), grid, dim3(256), lds, st, la, lb, ep,
                      M, N, K, kchunk, tn);
   return retr_check_launch(what);
+}
+
+// Tile choice for a single-pass (no split-K) GEMM: the biggest tile that still puts about one
+// block on every CU.  The transformer's skinny GEMMs (M 2048-6400, N 256) otherwise run on
+// 32-100 blocks of 128x128 and leave most of the 256 CUs idle.
+template <int FAM, typename T, class LA, class LB, class EP>
+int launch_sized(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, hipStream_t st,
+                 const char* what) {
+  const long b128 = (long)cdiv(M, 128) * cdiv(N, 128);
+  const long b64 = (long)cdiv(M, 64) * cdiv(N, 64);
+  if (b128 >= 240) return launch_gemm<FAM, T, 128, 128>(la, lb, ep, M, N, K, 1, st, what);
+  if (b64 >= 192 || N < 64) return launch_gemm<FAM, T, 64, 64>(la, lb, ep, M, N, K, 1, st, what);
+  return launch_gemm<FAM, T, 32, 64>(la, lb, ep, M, N, K, 1, st, what);
 }
 
 // Split-K heuristic: aim for >= ~2 waves of blocks over 256 CUs when the reduction is long.

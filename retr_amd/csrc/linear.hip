@@ -20,9 +20,7 @@ int linear_fwd_t(const void* x, long ldx, const void* w, long ldw, const float* 
   DropoutParams dp = make_dp(p, seed);
   EpiFwd<TO, float> ep{(TO*)y, ldy, bias, res, ldr, relu, dp, (long)N};
   ep.set_vec();
-  if (M >= 2048 && N >= 128)
-    return launch_gemm<kFamLinearFwd, T, 128, 128>(la, lb, ep, M, N, K, 1, st, "linear_fwd");
-  return launch_gemm<kFamLinearFwd, T, 64, 64>(la, lb, ep, M, N, K, 1, st, "linear_fwd");
+  return launch_sized<kFamLinearFwd, T>(la, lb, ep, M, N, K, st, "linear_fwd");
 }
 
 template <typename T, typename TO, typename TA>
@@ -36,14 +34,10 @@ int linear_dgrad_t(const void* dy, long lddy, const void* w, long ldw, void* dx,
   ep.set_vec();
   if (w_trans) {
     DenseK<T> lb{(const T*)w, ldw, K, N};
-    if (M >= 2048 && K >= 128)
-      return launch_gemm<kFamLinearDgrad, T, 128, 128>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
-    return launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
+    return launch_sized<kFamLinearDgrad, T>(la, lb, ep, M, K, N, st, "linear_dgrad");
   }
   DenseT<T> lb{(const T*)w, ldw, K, N};
-  if (M >= 2048 && K >= 128)
-    return launch_gemm<kFamLinearDgrad, T, 128, 128>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
-  return launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, ep, M, K, N, 1, st, "linear_dgrad");
+  return launch_sized<kFamLinearDgrad, T>(la, lb, ep, M, K, N, st, "linear_dgrad");
 }
 
 // zero an fp32 [rows][cols] region with row stride ld (stream-ordered, graph-capturable)

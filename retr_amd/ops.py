@@ -57,6 +57,36 @@ def bump_seed(delta=0x9E3779B97F4A7C1):
     call("retr_seed_bump", ptr(seed_base()), delta, _st())
 
 
+_SIDE = {}
+
+
+class _Overlap:
+    """Weight-gradient GEMMs on a second stream, overlapping the data-gradient chain of the
+    same backward Function (both are short, latency-bound launches at the transformer's
+    shapes).  ``side()`` forks the side stream from everything issued so far on the current
+    stream; ``join()`` makes the current stream wait for the side work before the Function
+    returns its gradients, so autograd, the caching allocator and graph capture (the side
+    branch rejoins the capture stream) see ordinary single-stream semantics."""
+
+    def __init__(self):
+        self.main = torch.cuda.current_stream()
+        dev = self.main.device
+        st = _SIDE.get(dev)
+        if st is None:
+            st = _SIDE[dev] = torch.cuda.Stream(device=dev)
+        self.stream = st
+        self.used = False
+
+    def side(self):
+        self.stream.wait_stream(self.main)
+        self.used = True
+        return torch.cuda.stream(self.stream)
+
+    def join(self):
+        if self.used:
+            self.main.wait_stream(self.stream)
+
+
 def dcode(dtype):
     if dtype == torch.bfloat16:
         return BF16
@@ -317,19 +347,23 @@ class _SelfAttnBlock(torch.autograd.Function):
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
         (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
-        k_linear_wgrad(dbr, o, dw_out, db_out, accumulate=True)
+        ov = _Overlap()
+        with ov.side():
+            k_linear_wgrad(dbr, o, dw_out, db_out, accumulate=True)
         do = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
         dqk = torch.empty(M, 2 * C, dtype=cdtype, device=dev)
         dv = torch.empty(M, C, dtype=cdtype, device=dev)
         k_attention_bwd(qk[:, :C], qk[:, C:], v, o, do, lse, dqk[:, :C], dqk[:, C:], dv, B, H,
                         L, L, hd, kpm, causal, drop_attn, s_att)
-        k_linear_wgrad(dqk, npos, dw_in[: 2 * C], db_in[: 2 * C], accumulate=True)
-        k_linear_wgrad(dv, n, dw_in[2 * C:], db_in[2 * C:], accumulate=True)
+        with ov.side():
+            k_linear_wgrad(dqk, npos, dw_in[: 2 * C], db_in[: 2 * C], accumulate=True)
+            k_linear_wgrad(dv, n, dw_in[2 * C:], db_in[2 * C:], accumulate=True)
         dnpos = torch.empty(M, C, dtype=cdtype, device=dev)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dqk, wint[:, : 2 * C], dnpos)
         k_linear_dgrad(dv, wint[:, 2 * C:], dn)
+        ov.join()
         return (dnpos, dn, dout, dw_in, db_in, dw_out, db_out) + (None,) * 9
 
 
@@ -380,7 +414,9 @@ class _CrossAttnBlock(torch.autograd.Function):
         dbr = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
         (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
-        k_linear_wgrad(dbr, o, dw_out, db_out, accumulate=True)
+        ov = _Overlap()
+        with ov.side():
+            k_linear_wgrad(dbr, o, dw_out, db_out, accumulate=True)
         do = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
         dq = torch.empty(Mq, C, dtype=cdtype, device=dev)
@@ -388,15 +424,17 @@ class _CrossAttnBlock(torch.autograd.Function):
         dv = torch.empty(Mk, C, dtype=cdtype, device=dev)
         k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, False, drop_attn,
                         s_att)
-        k_linear_wgrad(dq, qpos, dw_in[:C], db_in[:C], accumulate=True)
-        k_linear_wgrad(dk, mem_pos, dw_in[C: 2 * C], db_in[C: 2 * C], accumulate=True)
-        k_linear_wgrad(dv, mem, dw_in[2 * C:], db_in[2 * C:], accumulate=True)
+        with ov.side():
+            k_linear_wgrad(dq, qpos, dw_in[:C], db_in[:C], accumulate=True)
+            k_linear_wgrad(dk, mem_pos, dw_in[C: 2 * C], db_in[C: 2 * C], accumulate=True)
+            k_linear_wgrad(dv, mem, dw_in[2 * C:], db_in[2 * C:], accumulate=True)
         dqpos = torch.empty(Mq, C, dtype=cdtype, device=dev)
         dmem_pos = torch.empty(Mk, C, dtype=cdtype, device=dev)
         dmem = torch.empty(Mk, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dq, wint[:, :C], dqpos)
         k_linear_dgrad(dk, wint[:, C: 2 * C], dmem_pos)
         k_linear_dgrad(dv, wint[:, 2 * C:], dmem)
+        ov.join()
         return (dqpos, dmem_pos, dmem, dout, dw_in, db_in, dw_out, db_out) + (None,) * 9
 
 
@@ -431,12 +469,16 @@ class _FFNBlock(torch.autograd.Function):
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, seed)
         (dw1, _), (db1, _), (dw2, _), (db2, _) = map(grad_buffer, ctx.gparams)
-        k_linear_wgrad(dbr, h, dw2, db2, accumulate=True)
+        ov = _Overlap()
+        with ov.side():
+            k_linear_wgrad(dbr, h, dw2, db2, accumulate=True)
         dh = torch.empty(M, F, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, w2t, dh, gate=h)
-        k_linear_wgrad(dh, n, dw1, db1, accumulate=True)
+        with ov.side():
+            k_linear_wgrad(dh, n, dw1, db1, accumulate=True)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dh, w1t, dn)
+        ov.join()
         return dn, dout, dw1, db1, dw2, db2, None, None
 
 
@@ -606,15 +648,20 @@ class _MLPHead(torch.autograd.Function):
         w3t = WEIGHTS.get_t(w3, cdtype, rows=Vp)
         (dw1, _), (db1, _), (dw2, _), (db2, _), (dw3, _), (db3, _) = map(grad_buffer,
                                                                          ctx.gparams)
-        k_linear_wgrad(dl, h2, dw3, db3, accumulate=True)     # N = V rows of the padded dl
+        ov = _Overlap()
+        with ov.side():
+            k_linear_wgrad(dl, h2, dw3, db3, accumulate=True)  # N = V rows of the padded dl
         dh2 = torch.empty_like(h2)
         k_linear_dgrad(dl, w3t, dh2, gate=h2)
-        k_linear_wgrad(dh2, h1, dw2, db2, accumulate=True)
+        with ov.side():
+            k_linear_wgrad(dh2, h1, dw2, db2, accumulate=True)
         dh1 = torch.empty_like(h1)
         k_linear_dgrad(dh2, w2t, dh1, gate=h1)
-        k_linear_wgrad(dh1, hs, dw1, db1, accumulate=True)
+        with ov.side():
+            k_linear_wgrad(dh1, hs, dw1, db1, accumulate=True)
         dhs = torch.empty_like(hs)
         k_linear_dgrad(dh1, w1t, dhs)
+        ov.join()
         return dhs, dw1, db1, dw2, db2, dw3, db3, None, None, None
 
 

@@ -186,27 +186,41 @@ class _Backbone(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        # The data-gradient chain runs on the current stream; every weight gradient only needs
+        # its conv's output gradient and input, so it runs on the side stream (ops._Overlap)
+        # concurrently with the rest of the chain.  Tensors the side work reads stay referenced
+        # in ``keep`` until the final join, so the caching allocator cannot hand their memory
+        # to the chain while the side stream still reads it.
+        from .ops import _Overlap
         runner = ctx.runner
         grads = {}
         g = g.contiguous()
         saved = ctx.saved_acts
+        ov = _Overlap()
+        keep = []
+
+        def wgrad(spec, G, x, shape):
+            keep.extend((G, x))
+            with ov.side():
+                grads[spec.conv.weight] = _conv_wgrad(spec, G, x, shape)
+
         for idx in range(len(saved) - 1, -1, -1):
             blk, (inp, ishape, h1, s1, h2, s2) = saved[idx]
             need_dx = idx > 0 and saved[idx - 1][0] is runner.blocks[runner.blocks.index(blk) - 1]
             G3 = g
             if blk.kind == "bottleneck":
                 c1, c2, c3 = blk.convs
-                grads[c3.conv.weight] = _conv_wgrad(c3, G3, h2, s2)
+                wgrad(c3, G3, h2, s2)
                 G2 = _conv_dgrad(c3, G3, s2, gate=h2)
-                grads[c2.conv.weight] = _conv_wgrad(c2, G2, h1, s1)
+                wgrad(c2, G2, h1, s1)
                 G1 = _conv_dgrad(c2, G2, s1, gate=h1)
             else:
                 c1, c2 = blk.convs
-                grads[c2.conv.weight] = _conv_wgrad(c2, G3, h1, s1)
+                wgrad(c2, G3, h1, s1)
                 G1 = _conv_dgrad(c2, G3, s1, gate=h1)
-            grads[c1.conv.weight] = _conv_wgrad(c1, G1, inp, ishape)
+            wgrad(c1, G1, inp, ishape)
             if blk.ds is not None:
-                grads[blk.ds.conv.weight] = _conv_wgrad(blk.ds, G3, inp, ishape)
+                wgrad(blk.ds, G3, inp, ishape)
             if need_dx:
                 if blk.ds is not None:
                     tmp = _conv_dgrad(c1, G1, ishape)
@@ -215,6 +229,8 @@ class _Backbone(torch.autograd.Function):
                     g = _conv_dgrad(c1, G1, ishape, addend=G3, gate=inp)
             else:
                 g = None
+        ov.join()
+        del keep
         out = [None, None]
         for w in runner.weights:
             gw = grads.get(w)
