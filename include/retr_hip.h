@@ -90,11 +90,13 @@ int retr_mask_nearest(const unsigned char* m, unsigned char* out, int N, int H, 
 int retr_layernorm_fwd(int dtype, const float* x, long ldx, const float* gamma,
                        const float* beta, float eps, int M, int C, void* y, long ldy, void* y2,
                        const float* pos, int period, float* mean, float* rstd, void* stream);
-/* dx = [addend +] LN'(dy [+ dy2]); dgamma/dbeta accumulate (fp32) */
+/* dx = [addend +] LN'(dy [+ dy2]); dgamma/dbeta accumulate (fp32) via per-block partials in
+ * `workspace` (retr_layernorm_bwd_workspace bytes) reduced in a fixed order (deterministic) */
 int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, const float* x,
                        long ldx, const float* gamma, const float* mean, const float* rstd, int M,
                        int C, float* dx, long lddx, const float* addend, float* dgamma,
-                       float* dbeta, void* stream);
+                       float* dbeta, float* workspace, void* stream);
+size_t retr_layernorm_bwd_workspace(int M, int C);
 
 /* ---- DecoderEmbeddings: word[caps] + pos[t] -> LayerNorm(eps) -> dropout
  * (models/transformer_modules.py:113-129) ------------------------------------------------- */

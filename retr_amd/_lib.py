@@ -43,7 +43,9 @@ _SIGS = {
     "retr_maxpool3x3s2": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "retr_mask_nearest": [_P, _P, _I, _I, _I, _I, _I, _P],
     "retr_layernorm_fwd": [_I, _P, _L, _P, _P, _F, _I, _I, _P, _L, _P, _P, _I, _P, _P, _P],
-    "retr_layernorm_bwd": [_I, _P, _P, _L, _P, _L, _P, _P, _P, _I, _I, _P, _L, _P, _P, _P, _P],
+    "retr_layernorm_bwd": [_I, _P, _P, _L, _P, _L, _P, _P, _P, _I, _I, _P, _L, _P, _P, _P, _P,
+                           _P],
+    "retr_layernorm_bwd_workspace": [_I, _I],
     "retr_embed_ln_fwd": [_P, _I, _I, _I, _P, _P, _P, _P, _F, _F, _U64, _P, _P, _P, _P],
     "retr_embed_ln_bwd": [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _U64, _P, _P, _P, _P, _I,
                           _P],
@@ -70,6 +72,7 @@ _SIGS = {
     "retr_adamw_update": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P],
 }
 _RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
+            "retr_layernorm_bwd_workspace": _SZ,
             "retr_set_seed_base": None}
 
 _lib = None

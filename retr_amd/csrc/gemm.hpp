@@ -322,11 +322,15 @@ int launch_gemm(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, i
   constexpr int BK = Elem<T>::BK;
   const int tm = cdiv(M, BM), tn = cdiv(N, BN);
   if (splits < 1) splits = 1;
-  int ksteps = cdiv(K, BK);
-  if (splits > ksteps) splits = ksteps;
-  int kchunk = cdiv(ksteps, splits) * BK;
-  splits = K > 0 ? cdiv(K, kchunk) : 1;
-  if (K == 0) kchunk = BK;
+  const int ksteps = cdiv(K, BK);
+  int kchunk = BK;                 // K == 0: one split, the epilogue runs on zeros
+  if (K > 0) {
+    if (splits > ksteps) splits = ksteps;
+    kchunk = cdiv(ksteps, splits) * BK;
+    splits = cdiv(K, kchunk);
+  } else {
+    splits = 1;
+  }
   dim3 grid(tm * tn, splits);
   constexpr size_t lds = gemm_lds_bytes<T, BM, BN>();
   if constexpr (lds > 65536) {

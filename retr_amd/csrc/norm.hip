@@ -48,7 +48,7 @@ template <typename T, int PER>
 __global__ void __launch_bounds__(256)
 ln_bwd_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, const float* gamma,
               const float* mean, const float* rstd, int M, int C, float* dx, long lddx,
-              const float* addend, float* dgamma, float* dbeta, int rows_per_block) {
+              const float* addend, float* part, int rows_per_block) {
   __shared__ float red[2][4][1024];
   int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float pg[PER], pb[PER];
@@ -82,18 +82,33 @@ ln_bwd_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, co
       dx[(long)row * lddx + c] = o;
     }
   }
-  if (!dgamma && !dbeta) return;
+  if (!part) return;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     red[0][wave][lane + 64 * i] = pg[i];
     red[1][wave][lane + 64 * i] = pb[i];
   }
   __syncthreads();
+  // per-block partial sums (fixed order), reduced by ln_param_reduce_kernel: deterministic,
+  // and no contention of every block adding into the same 2C words
+  float* pw = part + (long)blockIdx.x * 2 * C;
   for (int c = threadIdx.x; c < C; c += 256) {
-    float a = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
-    float b = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
-    if (dgamma) atomicAdd(dgamma + c, a);
-    if (dbeta) atomicAdd(dbeta + c, b);
+    pw[c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    pw[C + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  }
+}
+
+// dgamma[c] += sum_b part[b][0][c];  dbeta[c] += sum_b part[b][1][c]  (blocks in order)
+__global__ void ln_param_reduce_kernel(const float* part, int nblk, int C, float* dgamma,
+                                       float* dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * C) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += part[(long)b * 2 * C + c];
+  if (c < C) {
+    if (dgamma) dgamma[c] += s;
+  } else if (dbeta) {
+    dbeta[c - C] += s;
   }
 }
 
@@ -187,6 +202,7 @@ embed_ln_bwd_kernel(const long long* tok, int M, int T, int C, const float* word
   }
 }
 
+
 #define PER_SWITCH(C, MACRO)          \
   switch ((C) / 64) {                 \
     case 1: MACRO(1); break;          \
@@ -250,26 +266,36 @@ int retr_layernorm_fwd(int dtype, const float* x, long ldx, const float* gamma,
 int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, const float* x,
                        long ldx, const float* gamma, const float* mean, const float* rstd, int M,
                        int C, float* dx, long lddx, const float* addend, float* dgamma,
-                       float* dbeta, void* stream) {
+                       float* dbeta, float* workspace, void* stream) {
   if (M == 0) return 0;
   RETR_REQUIRE(C % 64 == 0, "layernorm: C=%d must be a multiple of 64", C);
   RETR_REQUIRE(dy || dy2, "layernorm_bwd: no incoming gradient");
   RETR_REQUIRE(mean && rstd && gamma && dx, "layernorm_bwd: missing saved statistics");
+  RETR_REQUIRE(!(dgamma || dbeta) || workspace, "layernorm_bwd: dgamma/dbeta need a workspace");
   hipStream_t st = (hipStream_t)stream;
-  int rpb = 16;  // 4 rows per wave: enough blocks to fill 256 CUs at M ~ 2k-6k rows
+  const int rpb = 16;  // 4 rows per wave: enough blocks to fill 256 CUs at M ~ 2k-6k rows
   dim3 grid(cdiv(M, rpb));
+  float* part = (dgamma || dbeta) ? workspace : nullptr;
 #define LNB(P)                                                                                     \
   if (dtype == RETR_BF16)                                                                          \
     hipLaunchKernelGGL((ln_bwd_kernel<bf16, P>), grid, dim3(256), 0, st, (const bf16*)dy,          \
                        (const bf16*)dy2, lddy, x, ldx, gamma, mean, rstd, M, C, dx, lddx, addend,  \
-                       dgamma, dbeta, rpb);                                                        \
+                       part, rpb);                                                                 \
   else                                                                                             \
     hipLaunchKernelGGL((ln_bwd_kernel<float, P>), grid, dim3(256), 0, st, (const float*)dy,        \
                        (const float*)dy2, lddy, x, ldx, gamma, mean, rstd, M, C, dx, lddx, addend, \
-                       dgamma, dbeta, rpb);
+                       part, rpb);
   PER_SWITCH(C, LNB)
 #undef LNB
-  return retr_check_launch("layernorm_bwd");
+  if (int e = retr_check_launch("layernorm_bwd")) return e;
+  if (!part) return 0;
+  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, st, part,
+                     (int)grid.x, C, dgamma, dbeta);
+  return retr_check_launch("layernorm_param_reduce");
+}
+
+size_t retr_layernorm_bwd_workspace(int M, int C) {
+  return sizeof(float) * 2 * (size_t)C * (size_t)cdiv(M, 16);
 }
 
 int retr_embed_ln_fwd(const long long* tokens, int B, int T, int C, const float* word,

@@ -104,16 +104,15 @@ class ConcatTransformer(nn.Module):
         atts = []
         for layer in self.encoder.layers:
             sa = layer.self_attn
-            n, npos = ops.ln_pos(x, sa.norm, cdtype, pos=pe, period=period)
-            r = ops.self_attn_block(sa, npos, n, x, B, S, kpm_src, False, self.training, cdtype,
-                                    want_probs=want_att)
+            r = ops.self_attn_block(sa, x, pe, period, B, S, kpm_src, False, self.training,
+                                    cdtype, want_probs=want_att)
             if want_att:
                 x, a = r
                 atts.append(a)
             else:
                 x = r
             ff = layer.ff
-            x = ops.ffn_block(ff, ops.ln_pos(x, ff.norm, cdtype), x, self.training, cdtype)
+            x = ops.ffn_block(ff, x, self.training, cdtype)
         if self.encoder.norm is None:
             # pre_norm=False: the reference builds no encoder norm (:23-24) and the decoder
             # reads the raw residual stream as memory
@@ -135,8 +134,7 @@ class ConcatTransformer(nn.Module):
         att_s, att_x = [], []
         for layer in self.decoder.layers:
             sa = layer.tgt_self_attn
-            n, npos = ops.ln_pos(y, sa.norm, cdtype, pos=qpos, period=T)
-            r = ops.self_attn_block(sa, npos, n, y, B, T, kpm_tgt, True, self.training, cdtype,
+            r = ops.self_attn_block(sa, y, qpos, T, B, T, kpm_tgt, True, self.training, cdtype,
                                     want_probs=want_att)
             if want_att:
                 y, a = r
@@ -144,16 +142,15 @@ class ConcatTransformer(nn.Module):
             else:
                 y = r
             ca = layer.tgt_src_cross_attn
-            qp = ops.ln_pos(y, ca.norm, cdtype, pos=qpos, period=T, mode="pos")
-            r = ops.cross_attn_block(ca, qp, mem_pos, mem, y, B, T, S, kpm_src, self.training,
-                                     cdtype, want_probs=want_att)
+            r = ops.cross_attn_block(ca, y, qpos, T, mem_pos, mem, B, T, S, kpm_src,
+                                     self.training, cdtype, want_probs=want_att)
             if want_att:
                 y, a = r
                 att_x.append(a)
             else:
                 y = r
             ff = layer.ff
-            y = ops.ffn_block(ff, ops.ln_pos(y, ff.norm, cdtype), y, self.training, cdtype)
+            y = ops.ffn_block(ff, y, self.training, cdtype)
         hs = ops.ln_pos(y, self.decoder.norm, cdtype)
         return hs, att_s, att_x
 

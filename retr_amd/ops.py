@@ -58,6 +58,10 @@ def bump_seed(delta=0x9E3779B97F4A7C1):
 
 
 _SIDE = {}
+# Side-stream overlap switches (A/B-tested by tools/ab_step.py, profiles/r2_ab_side_stream.txt:
+# with the whole step in one hipGraph the extra cross-stream edges cost more than the overlap
+# gains, so both are off by default): transformer blocks / backbone.
+OVERLAP = {"transformer": False, "backbone": False}
 
 
 class _Overlap:
@@ -68,8 +72,9 @@ class _Overlap:
     returns its gradients, so autograd, the caching allocator and graph capture (the side
     branch rejoins the capture stream) see ordinary single-stream semantics."""
 
-    def __init__(self):
+    def __init__(self, enabled=True):
         self.main = torch.cuda.current_stream()
+        self.enabled = enabled
         dev = self.main.device
         st = _SIDE.get(dev)
         if st is None:
@@ -78,6 +83,9 @@ class _Overlap:
         self.used = False
 
     def side(self):
+        if not self.enabled:
+            import contextlib
+            return contextlib.nullcontext()
         self.stream.wait_stream(self.main)
         self.used = True
         return torch.cuda.stream(self.stream)
@@ -225,6 +233,12 @@ def k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, caus
          drop_p, seed, ptr(ws), _st())
 
 
+def ln_workspace(M, C, dev):
+    """fp32 scratch for the LayerNorm backward's per-block dgamma/dbeta partials."""
+    n = (2 * C * ((M + 15) // 16))
+    return torch.empty(n, dtype=torch.float32, device=dev)
+
+
 def _rows(t):
     return t.reshape(-1, t.shape[-1]) if t.dim() != 2 else t
 
@@ -280,9 +294,10 @@ class _LnPos(torch.autograd.Function):
             if dy is not None and dy.dtype != dy2.dtype:
                 dy2 = dy2.to(dy.dtype)
         ref = dy if dy is not None else dy2
+        ws = ln_workspace(M, C, x.device)
         call("retr_layernorm_bwd", dcode(ref.dtype), ptr(dy), ptr(dy2), C, ptr(x), x.stride(0),
              ptr(gamma), ptr(mean), ptr(rstd), M, C, ptr(dx), dx.stride(0), None, ptr(dgamma),
-             ptr(dbeta), _st())
+             ptr(dbeta), ptr(ws), _st())
         dpos = None
         if ctx.pos_shape is not None and ctx.needs_input_grad[3] and dy2 is not None:
             dpos, _ = grad_buffer(pp)
@@ -299,16 +314,59 @@ def ln_pos(x, norm, cdtype, pos=None, period=None, mode=None, eps=None):
                         norm.eps if eps is None else eps, cdtype, mode)
 
 
+def _ln_fwd(x, gamma, beta, eps, cdtype, pos=None, period=1, plain=True, with_pos=False):
+    """LayerNorm kernel: (LN(x) | None, LN(x)+pos[row % period] | None, mean, rstd)."""
+    M, C = x.shape
+    dev = x.device
+    y = torch.empty(M, C, dtype=cdtype, device=dev) if plain else None
+    y2 = torch.empty(M, C, dtype=cdtype, device=dev) if with_pos else None
+    mean = torch.empty(M, dtype=torch.float32, device=dev)
+    rstd = torch.empty_like(mean)
+    posd = pos.detach().contiguous() if pos is not None else None
+    call("retr_layernorm_fwd", dcode(cdtype), ptr(x), x.stride(0), ptr(gamma), ptr(beta),
+         float(eps), M, C, ptr(y), C, ptr(y2), ptr(posd), int(period or 1), ptr(mean),
+         ptr(rstd), _st())
+    return y, y2, mean, rstd
+
+
+def _ln_bwd(x, gamma, beta, mean, rstd, dy, dy2, addend, pos=None, period=1, need_dpos=False):
+    """dx = addend + LN'(dy + dy2) (fp32), dgamma/dbeta into their gradient buffers, and the
+    position gradient (rows summed by row % period) when ``need_dpos``."""
+    M, C = x.shape
+    ref = dy if dy is not None else dy2
+    if dy is not None and dy2 is not None and dy.dtype != dy2.dtype:
+        dy2 = dy2.to(dy.dtype)
+    dx = torch.empty(M, C, dtype=torch.float32, device=x.device)
+    dgamma, _ = grad_buffer(gamma)
+    dbeta, _ = grad_buffer(beta)
+    ws = ln_workspace(M, C, x.device)
+    call("retr_layernorm_bwd", dcode(ref.dtype), ptr(dy), ptr(dy2), C, ptr(x), x.stride(0),
+         ptr(gamma), ptr(mean), ptr(rstd), M, C, ptr(dx), dx.stride(0), ptr(addend),
+         ptr(dgamma), ptr(dbeta), ptr(ws), _st())
+    dpos = None
+    if need_dpos and dy2 is not None:
+        dpos, _ = grad_buffer(pos)
+        call("retr_pos_grad", dcode(dy2.dtype), ptr(dy2), dy2.stride(0), M, C, int(period),
+             ptr(dpos), _st())
+    return dx, dgamma, dbeta, dpos
+
+
 # ---------------------------------------------------------------------------------------------
 # attention sub-layers
 # ---------------------------------------------------------------------------------------------
 
 class _SelfAttnBlock(torch.autograd.Function):
-    """x_new = res + drop(out_proj(MHA(q=k=npos, v=n)))  — SelfAttResidual."""
+    """x_new = x + drop(out_proj(MHA(q=k=LN(x)+pos, v=LN(x))))  — SelfAttResidual
+    (models/transformer_modules.py:22-46) with its pre-norm inside the Function: the
+    backward returns dx = dout + LN'(dnpos + dn) in one LayerNorm-backward pass (no separate
+    residual-gradient add)."""
 
     @staticmethod
-    def forward(ctx, npos, n, res, w_in, b_in, w_out, b_out, B, L, H, kpm, causal, drop_attn,
-                drop_res, cdtype, want_probs):
+    def forward(ctx, x, ln_w, ln_b, pos, period, eps, w_in, b_in, w_out, b_out, B, L, H, kpm,
+                causal, drop_attn, drop_res, cdtype, want_probs):
+        _lib.require_device(x)
+        n, npos, mean, rstd = _ln_fwd(x, ln_w, ln_b, eps, cdtype, pos, period, True, True)
+        res = x
         M, C = n.shape
         hd = C // H
         win = WEIGHTS.get(w_in, cdtype)
@@ -326,8 +384,9 @@ class _SelfAttnBlock(torch.autograd.Function):
                         s_att, lse, probs)
         out = torch.empty(M, C, dtype=torch.float32, device=dev)
         k_linear_fwd(o, wout, b_out.detach(), out, res=res, drop_p=drop_res, seed=s_res)
-        ctx.save_for_backward(npos, n, qk, v, o, lse, kpm, w_in, w_out)
+        ctx.save_for_backward(npos, n, qk, v, o, lse, kpm, w_in, w_out, x, ln_w, mean, rstd)
         ctx.gparams = (w_in, b_in, w_out, b_out)
+        ctx.ln = (ln_w, ln_b, pos, period)
         ctx.cfg = (B, L, H, causal, drop_attn, drop_res, s_att, s_res, cdtype)
         if want_probs:
             ctx.mark_non_differentiable(probs)
@@ -336,7 +395,7 @@ class _SelfAttnBlock(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, dprobs=None):
-        npos, n, qk, v, o, lse, kpm, w_in, w_out = ctx.saved_tensors
+        npos, n, qk, v, o, lse, kpm, w_in, w_out, x, ln_w, mean, rstd = ctx.saved_tensors
         B, L, H, causal, drop_attn, drop_res, s_att, s_res, cdtype = ctx.cfg
         M, C = n.shape
         hd = C // H
@@ -347,7 +406,7 @@ class _SelfAttnBlock(torch.autograd.Function):
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
         (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
-        ov = _Overlap()
+        ov = _Overlap(OVERLAP["transformer"])
         with ov.side():
             k_linear_wgrad(dbr, o, dw_out, db_out, accumulate=True)
         do = torch.empty(M, C, dtype=cdtype, device=dev)
@@ -363,16 +422,24 @@ class _SelfAttnBlock(torch.autograd.Function):
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dqk, wint[:, : 2 * C], dnpos)
         k_linear_dgrad(dv, wint[:, 2 * C:], dn)
+        _, ln_b, pos, period = ctx.ln
+        dx, dlw, dlb, dpos = _ln_bwd(x, ln_w, ln_b, mean, rstd, dn, dnpos, dout, pos, period,
+                                     ctx.needs_input_grad[3])
         ov.join()
-        return (dnpos, dn, dout, dw_in, db_in, dw_out, db_out) + (None,) * 9
+        return (dx, dlw, dlb, dpos, None, None, dw_in, db_in, dw_out, db_out) + (None,) * 9
 
 
 class _CrossAttnBlock(torch.autograd.Function):
-    """y_new = res + drop(out_proj(MHA(q=qpos, k=mem_pos, v=mem)))  — CrossAttResidual."""
+    """y_new = y + drop(out_proj(MHA(q=LN(y)+qpos, k=mem_pos, v=mem)))  — CrossAttResidual
+    (models/transformer_modules.py:49-74) with its pre-norm inside the Function (see
+    _SelfAttnBlock)."""
 
     @staticmethod
-    def forward(ctx, qpos, mem_pos, mem, res, w_in, b_in, w_out, b_out, B, Lq, Lk, H, kpm,
-                drop_attn, drop_res, cdtype, want_probs):
+    def forward(ctx, y, ln_w, ln_b, qp, period, eps, mem_pos, mem, w_in, b_in, w_out, b_out, B,
+                Lq, Lk, H, kpm, drop_attn, drop_res, cdtype, want_probs):
+        _lib.require_device(y)
+        _, qpos, mean, rstd = _ln_fwd(y, ln_w, ln_b, eps, cdtype, qp, period, False, True)
+        res = y
         Mq, C = qpos.shape
         Mk = mem.shape[0]
         hd = C // H
@@ -392,8 +459,10 @@ class _CrossAttnBlock(torch.autograd.Function):
         k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, False, drop_attn, s_att, lse, probs)
         out = torch.empty(Mq, C, dtype=torch.float32, device=dev)
         k_linear_fwd(o, wout, b_out.detach(), out, res=res, drop_p=drop_res, seed=s_res)
-        ctx.save_for_backward(qpos, mem_pos, mem, q, k, v, o, lse, kpm, w_in, w_out)
+        ctx.save_for_backward(qpos, mem_pos, mem, q, k, v, o, lse, kpm, w_in, w_out, y, ln_w,
+                              mean, rstd)
         ctx.gparams = (w_in, b_in, w_out, b_out)
+        ctx.ln = (ln_w, ln_b, qp, period)
         ctx.cfg = (B, Lq, Lk, H, drop_attn, drop_res, s_att, s_res, cdtype)
         if want_probs:
             ctx.mark_non_differentiable(probs)
@@ -402,7 +471,8 @@ class _CrossAttnBlock(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout, dprobs=None):
-        qpos, mem_pos, mem, q, k, v, o, lse, kpm, w_in, w_out = ctx.saved_tensors
+        qpos, mem_pos, mem, q, k, v, o, lse, kpm, w_in, w_out, y, ln_w, mean, rstd = \
+            ctx.saved_tensors
         B, Lq, Lk, H, drop_attn, drop_res, s_att, s_res, cdtype = ctx.cfg
         Mq, C = qpos.shape
         Mk = mem.shape[0]
@@ -414,7 +484,7 @@ class _CrossAttnBlock(torch.autograd.Function):
         dbr = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
         (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
-        ov = _Overlap()
+        ov = _Overlap(OVERLAP["transformer"])
         with ov.side():
             k_linear_wgrad(dbr, o, dw_out, db_out, accumulate=True)
         do = torch.empty(Mq, C, dtype=cdtype, device=dev)
@@ -434,15 +504,23 @@ class _CrossAttnBlock(torch.autograd.Function):
         k_linear_dgrad(dq, wint[:, :C], dqpos)
         k_linear_dgrad(dk, wint[:, C: 2 * C], dmem_pos)
         k_linear_dgrad(dv, wint[:, 2 * C:], dmem)
+        _, ln_b, qp, period = ctx.ln
+        dy, dlw, dlb, dqp = _ln_bwd(y, ln_w, ln_b, mean, rstd, None, dqpos, dout, qp, period,
+                                    ctx.needs_input_grad[3])
         ov.join()
-        return (dqpos, dmem_pos, dmem, dout, dw_in, db_in, dw_out, db_out) + (None,) * 9
+        return (dy, dlw, dlb, dqp, None, None, dmem_pos, dmem, dw_in, db_in, dw_out,
+                db_out) + (None,) * 9
 
 
 class _FFNBlock(torch.autograd.Function):
-    """x_new = res + drop(W2 relu(W1 n + b1) + b2)  — FFResidual(feed_forward)."""
+    """x_new = x + drop(W2 relu(W1 LN(x) + b1) + b2)  — FFResidual(feed_forward)
+    (models/transformer_modules.py:6-11, 77-97) with its pre-norm inside the Function."""
 
     @staticmethod
-    def forward(ctx, n, res, w1, b1, w2, b2, drop_res, cdtype):
+    def forward(ctx, x, ln_w, ln_b, eps, w1, b1, w2, b2, drop_res, cdtype):
+        _lib.require_device(x)
+        n, _, mean, rstd = _ln_fwd(x, ln_w, ln_b, eps, cdtype)
+        res = x
         M, C = n.shape
         F = w1.shape[0]
         dev = n.device
@@ -452,14 +530,15 @@ class _FFNBlock(torch.autograd.Function):
         out = torch.empty(M, C, dtype=torch.float32, device=dev)
         seed = next_seed()
         k_linear_fwd(h, w2c, b2.detach(), out, res=res, drop_p=drop_res, seed=seed)
-        ctx.save_for_backward(n, h, w1, w2)
+        ctx.save_for_backward(n, h, w1, w2, x, ln_w, mean, rstd)
         ctx.gparams = (w1, b1, w2, b2)
+        ctx.ln_b = ln_b
         ctx.cfg = (drop_res, seed, cdtype)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        n, h, w1, w2 = ctx.saved_tensors
+        n, h, w1, w2, x, ln_w, mean, rstd = ctx.saved_tensors
         drop_res, seed, cdtype = ctx.cfg
         M, C = n.shape
         F = h.shape[1]
@@ -469,7 +548,7 @@ class _FFNBlock(torch.autograd.Function):
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, seed)
         (dw1, _), (db1, _), (dw2, _), (db2, _) = map(grad_buffer, ctx.gparams)
-        ov = _Overlap()
+        ov = _Overlap(OVERLAP["transformer"])
         with ov.side():
             k_linear_wgrad(dbr, h, dw2, db2, accumulate=True)
         dh = torch.empty(M, F, dtype=cdtype, device=dev)
@@ -478,34 +557,39 @@ class _FFNBlock(torch.autograd.Function):
             k_linear_wgrad(dh, n, dw1, db1, accumulate=True)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dh, w1t, dn)
+        dx, dlw, dlb, _ = _ln_bwd(x, ln_w, ctx.ln_b, mean, rstd, dn, None, dout)
         ov.join()
-        return dn, dout, dw1, db1, dw2, db2, None, None
+        return dx, dlw, dlb, None, dw1, db1, dw2, db2, None, None
 
 
-def self_attn_block(res_mod, npos, n, res, B, L, kpm, causal, training, cdtype,
+def self_attn_block(res_mod, x, pos, period, B, L, kpm, causal, training, cdtype,
                     want_probs=False):
-    """res_mod: SelfAttResidual container (.sublayer = nn.MultiheadAttention, .dropout)."""
+    """res_mod: SelfAttResidual container (.norm, .sublayer = nn.MultiheadAttention,
+    .dropout); x: fp32 residual rows [B*L, C]; pos: position rows (table[row % period])."""
     sub = res_mod.sublayer
-    return _SelfAttnBlock.apply(npos, n, res, sub.in_proj_weight, sub.in_proj_bias,
+    return _SelfAttnBlock.apply(x, res_mod.norm.weight, res_mod.norm.bias, pos, period,
+                                res_mod.norm.eps, sub.in_proj_weight, sub.in_proj_bias,
                                 sub.out_proj.weight, sub.out_proj.bias, B, L, sub.num_heads, kpm,
                                 causal, _drop_p(training, sub.dropout),
                                 _drop_p(training, res_mod.dropout.p), cdtype, want_probs)
 
 
-def cross_attn_block(res_mod, qpos, mem_pos, mem, res, B, Lq, Lk, kpm, training, cdtype,
+def cross_attn_block(res_mod, y, qpos, period, mem_pos, mem, B, Lq, Lk, kpm, training, cdtype,
                      want_probs=False):
-    """res_mod: CrossAttResidual container."""
+    """res_mod: CrossAttResidual container; y: fp32 residual rows of the queries."""
     sub = res_mod.sublayer
-    return _CrossAttnBlock.apply(qpos, mem_pos, mem, res, sub.in_proj_weight, sub.in_proj_bias,
-                                 sub.out_proj.weight, sub.out_proj.bias, B, Lq, Lk,
-                                 sub.num_heads, kpm, _drop_p(training, sub.dropout),
+    return _CrossAttnBlock.apply(y, res_mod.norm.weight, res_mod.norm.bias, qpos, period,
+                                 res_mod.norm.eps, mem_pos, mem, sub.in_proj_weight,
+                                 sub.in_proj_bias, sub.out_proj.weight, sub.out_proj.bias, B,
+                                 Lq, Lk, sub.num_heads, kpm, _drop_p(training, sub.dropout),
                                  _drop_p(training, res_mod.dropout.p), cdtype, want_probs)
 
 
-def ffn_block(res_mod, n, res, training, cdtype):
-    """res_mod: FFResidual container (.sublayer = Sequential(Linear, ReLU, Linear))."""
+def ffn_block(res_mod, x, training, cdtype):
+    """res_mod: FFResidual container (.norm, .sublayer = Sequential(Linear, ReLU, Linear))."""
     seq = res_mod.sublayer
-    return _FFNBlock.apply(n, res, seq[0].weight, seq[0].bias, seq[2].weight, seq[2].bias,
+    return _FFNBlock.apply(x, res_mod.norm.weight, res_mod.norm.bias, res_mod.norm.eps,
+                           seq[0].weight, seq[0].bias, seq[2].weight, seq[2].bias,
                            _drop_p(training, res_mod.dropout.p), cdtype)
 
 
@@ -648,7 +732,7 @@ class _MLPHead(torch.autograd.Function):
         w3t = WEIGHTS.get_t(w3, cdtype, rows=Vp)
         (dw1, _), (db1, _), (dw2, _), (db2, _), (dw3, _), (db3, _) = map(grad_buffer,
                                                                          ctx.gparams)
-        ov = _Overlap()
+        ov = _Overlap(OVERLAP["transformer"])
         with ov.side():
             k_linear_wgrad(dl, h2, dw3, db3, accumulate=True)  # N = V rows of the padded dl
         dh2 = torch.empty_like(h2)
@@ -818,7 +902,7 @@ class _LearnedPos(torch.autograd.Function):
         # no gradient, as from nn.Embedding with ids arange(S)
         call("retr_layernorm_bwd", F32, ptr(dtab), None, C, ptr(wd), wd.stride(0), ptr(gamma),
              ptr(mean), ptr(rstd), S, C, ptr(dw), dw.stride(0), None, ptr(dgamma), ptr(dbeta),
-             _st())
+             ptr(ln_workspace(S, C, dev)), _st())
         return dw, dgamma, dbeta, None, None, None, None
 
 

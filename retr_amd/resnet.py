@@ -191,12 +191,12 @@ class _Backbone(torch.autograd.Function):
         # concurrently with the rest of the chain.  Tensors the side work reads stay referenced
         # in ``keep`` until the final join, so the caching allocator cannot hand their memory
         # to the chain while the side stream still reads it.
-        from .ops import _Overlap
+        from .ops import OVERLAP, _Overlap
         runner = ctx.runner
         grads = {}
         g = g.contiguous()
         saved = ctx.saved_acts
-        ov = _Overlap()
+        ov = _Overlap(OVERLAP["backbone"])
         keep = []
 
         def wgrad(spec, G, x, shape):

@@ -1,0 +1,75 @@
+"""A/B timing of the graphed cfg2 training step under code-path variants, in ONE process with
+interleaved rounds (cdna_hip_programming.md §5.4 rule 24).  Each variant is a dict of switches
+applied before its own capture; prints per-variant median / min ms per step.
+
+    python tools/ab_step.py --variants base,side_all --rounds 5 --steps 10
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from retr_amd import ops  # noqa: E402
+from retr_amd.engine import GraphedTrainStep  # noqa: E402
+from retr_amd.models.utils import NestedTensor  # noqa: E402
+from retr_amd.synthetic import synthetic_captions, synthetic_images  # noqa: E402
+
+VARIANTS = {
+    "base": {},
+    "side_bb": {("OVERLAP", "backbone"): True},
+    "side_tr": {("OVERLAP", "transformer"): True},
+    "side_all": {("OVERLAP", "backbone"): True, ("OVERLAP", "transformer"): True},
+}
+
+
+def apply(v):
+    ops.OVERLAP.update({"backbone": False, "transformer": False})
+    for (table, key), val in VARIANTS[v].items():
+        getattr(ops, table)[key] = val
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="base,side_all")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    cfg = bench.cfg2()
+    names = args.variants.split(",")
+    runs = {}
+    img, mask = synthetic_images(16, 640, seed=1000)
+    caps, cm = synthetic_captions(16, 128, cfg.vocab_size, seed=2000)
+    samples = (NestedTensor(img.to(dev), mask.to(dev)),)
+    caps, cm = caps.to(dev), cm.to(dev)
+    for v in names:
+        apply(v)
+        model, crit = bench.build(cfg, dev)
+        model.train()
+        opt = bench.make_optimizer(model, cfg, fused=True)
+        g = GraphedTrainStep(model, crit, opt, cfg.clip_max_norm)
+        g(samples, caps, cm)
+        torch.cuda.synchronize()
+        runs[v] = g
+    res = {v: [] for v in names}
+    for _ in range(args.rounds):
+        for v in names:
+            g = runs[v]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                g(samples, caps, cm)
+            torch.cuda.synchronize()
+            res[v].append((time.perf_counter() - t0) / args.steps * 1e3)
+    for v in names:
+        print(f"{v:14s} median {statistics.median(res[v]):7.3f} ms  min {min(res[v]):7.3f} ms  "
+              f"rounds {[round(x, 3) for x in res[v]]}")
+
+
+if __name__ == "__main__":
+    main()
