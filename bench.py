@@ -77,14 +77,18 @@ def train_bench(args, rank, world, device):
     from retr_amd.engine import GraphedTrainStep, train_step
     cfg = cfg2()
     model, crit = build(cfg, device)
-    graphed = world == 1 and not args.eager
-    opt = make_optimizer(model, cfg, capturable=graphed, fused=not args.torch_adamw)
+    graphed = not args.eager
     sync = None
     if world > 1:
-        from retr_amd.ddp import GradSync, broadcast_parameters
+        from retr_amd.ddp import broadcast_parameters
         broadcast_parameters(model)
+    opt = make_optimizer(model, cfg, capturable=graphed, fused=not args.torch_adamw)
+    if world > 1:
+        # zero-copy buckets on FusedAdamW's gradient arena; a graphed step runs them between
+        # its forward/backward graph and its optimizer graph
+        from retr_amd.ddp import GradSync
         sync = GradSync([p for p in model.parameters() if p.requires_grad],
-                        bucket_mb=cfg.grad_bucket_mb)
+                        bucket_mb=cfg.grad_bucket_mb, optimizer=opt)
     B, H = args.batch, args.size
     img, mask = synthetic_images(B, H, seed=1000 + rank)
     caps, cap_mask = synthetic_captions(B, cfg.max_position_embeddings, cfg.vocab_size,
@@ -334,7 +338,9 @@ def main():
                           "global_batch": world * args.batch, "seq_len": 128,
                           "parallelism": f"dp{world}"},
                "loss": round(loss, 4), "roofline": roof, "cpu_baseline": cpu,
-               "launch": "eager" if (args.eager or world > 1) else "hipGraph (whole step)",
+               "launch": ("eager" if args.eager else
+                          "hipGraph (whole step)" if world == 1 else
+                          "hipGraph (fwd+bwd) + RCCL all-reduce + hipGraph (clip+AdamW)"),
                "optimizer": "torch.optim.AdamW" if args.torch_adamw else "FusedAdamW",
                "decode": decode, "kernel_families": families}
         print(json.dumps(out), flush=True)

@@ -29,6 +29,14 @@ int retr_abi_version(void);
  * training loop advances once per step (retr_seed_bump), so a captured hipGraph replays with
  * fresh masks.  NULL (default) -> the per-op seed alone. */
 void retr_set_seed_base(const unsigned long long* device_ptr);
+/* Deterministic mode (config.deterministic): 1 = every reduction runs in a fixed order, so two
+ * runs on the same inputs are bitwise equal — linear weight-gradient GEMMs are not split over K
+ * (no fp32 atomics) and bias gradients use an ordered column sum instead of the fused row sums.
+ * 0 (default) = split-K with fp32 atomics for the linear weight gradients.  (Convolution weight
+ * gradients, LayerNorm / embedding parameter gradients, attention backward, the loss and the
+ * optimizer reductions are fixed-order in both modes.) */
+void retr_set_deterministic(int on);
+int retr_get_deterministic(void);
 int retr_seed_bump(unsigned long long* device_ptr, unsigned long long delta, void* stream);
 /* Measurement only (bench.py kernel probe; no reference counterpart): one wave busy-waits
  * `us` microseconds on the device clock, so a following event pair times device execution
@@ -68,12 +76,16 @@ int retr_conv2d_fwd(int dtype, const void* x, int Nb, int H, int W, int C, const
 int retr_conv2d_dgrad(int dtype, const void* dy, int Nb, int H, int W, int C, const void* wt,
                       void* dx, int Co, int KH, int KW, int stride, int pad, int dil,
                       const void* addend, const void* gate, void* stream);
-/* ws[Co][KH*KW*C] = dWeff (fp32, overwritten; NHWC tap order) */
+/* ws[splits][Co][KH*KW*C] = partial dWeff per slice of the pixel reduction (fp32, plain
+ * stores, overwritten; NHWC tap order; no atomics).  splits = retr_conv2d_wgrad_splits(...) */
 int retr_conv2d_wgrad(int dtype, const void* dy, const void* x, int Nb, int H, int W, int C,
                       float* ws, int Co, int KH, int KW, int stride, int pad, int dil,
                       void* stream);
+int retr_conv2d_wgrad_splits(int dtype, int Nb, int H, int W, int C, int Co, int KH, int KW,
+                             int stride, int pad, int dil);
+/* grad[Co][Ci][KH][KW] (=|+=) scale[co] * sum_s ws[s] (slices added in order: deterministic) */
 int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,
-                           int Cp, int KH, int KW, int accumulate, void* stream);
+                           int Cp, int KH, int KW, int accumulate, int splits, void* stream);
 /* NCHW fp32 image -> NHWC (channels zero-padded to Cp) */
 int retr_nchw_to_nhwc(int dtype, const float* x, void* y, int N, int C, int H, int W, int Cp,
                       void* stream);
@@ -104,10 +116,15 @@ int retr_embed_ln_fwd(const long long* tokens, int B, int T, int C, const float*
                       const float* posw, const float* gamma, const float* beta, float eps,
                       float drop_p, unsigned long long seed, float* y, float* mean, float* rstd,
                       void* stream);
+/* deterministic (no atomics): dword rows are summed in token-position order by one writer,
+ * dposw over the batch in order, dgamma/dbeta from per-block partials in block order.
+ * workspace: retr_embed_ln_bwd_workspace(B, T, C) bytes. */
 int retr_embed_ln_bwd(const long long* tokens, int B, int T, int C, const float* word,
                       const float* posw, const float* gamma, const float* mean, const float* rstd,
                       const float* dy, float drop_p, unsigned long long seed, float* dword,
-                      float* dposw, float* dgamma, float* dbeta, int padding_idx, void* stream);
+                      float* dposw, float* dgamma, float* dbeta, int padding_idx,
+                      void* workspace, void* stream);
+size_t retr_embed_ln_bwd_workspace(int B, int T, int C);
 
 /* ---- multi-head attention core: softmax(q k^T * hd^-1/2 + mask) -> dropout -> @ v
  * (torch/nn/functional.py:6576-6606 need_weights path used by models/ConcatTransformer.py:160,

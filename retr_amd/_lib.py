@@ -38,7 +38,8 @@ _SIGS = {
     "retr_conv2d_fwd": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "retr_conv2d_dgrad": [_I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "retr_conv2d_wgrad": [_I, _P, _P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P],
-    "retr_conv_wgrad_unpack": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "retr_conv_wgrad_unpack": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "retr_conv2d_wgrad_splits": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
     "retr_nchw_to_nhwc": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "retr_maxpool3x3s2": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "retr_mask_nearest": [_P, _P, _I, _I, _I, _I, _I, _P],
@@ -48,7 +49,10 @@ _SIGS = {
     "retr_layernorm_bwd_workspace": [_I, _I],
     "retr_embed_ln_fwd": [_P, _I, _I, _I, _P, _P, _P, _P, _F, _F, _U64, _P, _P, _P, _P],
     "retr_embed_ln_bwd": [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _U64, _P, _P, _P, _P, _I,
-                          _P],
+                          _P, _P],
+    "retr_embed_ln_bwd_workspace": [_I, _I, _I],
+    "retr_set_deterministic": [_I],
+    "retr_get_deterministic": [],
     "retr_attention_fwd": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _P, _I, _F,
                            _U64, _P, _P, _P],
     "retr_attention_bwd": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _P, _L, _P, _L, _P,
@@ -72,7 +76,8 @@ _SIGS = {
     "retr_adamw_update": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P],
 }
 _RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
-            "retr_layernorm_bwd_workspace": _SZ,
+            "retr_layernorm_bwd_workspace": _SZ, "retr_embed_ln_bwd_workspace": _SZ,
+            "retr_set_deterministic": None,
             "retr_set_seed_base": None}
 
 _lib = None

@@ -4,6 +4,8 @@
 * ``dtype``: 'bf16' (default; bf16 operands, fp32 accumulation/master weights) or 'fp32'
   (exact-f32 MFMA, the parity mode used against the reference CPU path).
 * ``grad_bucket_mb``: data-parallel gradient bucket size.
+* ``deterministic``: fixed-order reductions everywhere (no split-K fp32 atomics), so two runs
+  on the same inputs give bitwise-equal gradients and weights (``retr_set_deterministic``).
 """
 from os.path import join
 
@@ -51,6 +53,7 @@ class Config(object):
         # MI355X build knobs (absent from reference configs -> defaults below)
         self.dtype = "bf16"
         self.grad_bucket_mb = 64
+        self.deterministic = False
 
 
 def compute_dtype(config):

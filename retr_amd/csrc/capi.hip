@@ -31,6 +31,11 @@ static const unsigned long long* g_seed_base = nullptr;
 const unsigned long long* retr_seed_base() { return g_seed_base; }
 extern "C" void retr_set_seed_base(const unsigned long long* p) { g_seed_base = p; }
 
+static int g_deterministic = 0;
+int retr_deterministic() { return g_deterministic; }
+extern "C" void retr_set_deterministic(int on) { g_deterministic = on ? 1 : 0; }
+extern "C" int retr_get_deterministic(void) { return g_deterministic; }
+
 __global__ void seed_bump_kernel(unsigned long long* p, unsigned long long d) { *p += d; }
 extern "C" int retr_seed_bump(unsigned long long* p, unsigned long long delta, void* stream) {
   hipLaunchKernelGGL(seed_bump_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, p, delta);

@@ -6,7 +6,7 @@
 //             with ih = oh*s - p + kh*d  (stride handled by a divisibility test)
 //   wgrad   : dWeff[co, (kh,kw,ci)] = sum_pixels G[pix,co] X[pix @ (kh,kw), ci]   (split-K)
 //             then dW = dWeff * bn_scale, scattered to the OIHW parameter layout.
-#include "gemm.hpp"
+#include "gemm2.hpp"
 #include "epilogues.hpp"
 #include "../../include/retr_hip.h"
 
@@ -71,11 +71,11 @@ struct ConvFwdA {  // A(m = n,oh,ow ; k = kh,kw,ci)
   }
   RETR_DEVICE KCur kcur(int k) const { return tap_cur(k, g.C, g.KW, g.d); }
   RETR_DEVICE void advance(KCur& t, int d) const { tap_advance(t, d, g.C, g.KW, g.d); }
-  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& t) const {
-    if (!c.ok || t.k >= K) return zero16();
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& t) const {
+    if (!c.ok || t.k >= K) return nullptr;
     int ih = c.ihb + t.khd, iw = c.iwb + t.kwd;
-    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return zero16();
-    return *(const u32x4*)(c.img + ((long)ih * g.W + iw) * g.C + t.c);
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return nullptr;
+    return c.img + ((long)ih * g.W + iw) * g.C + t.c;
   }
 };
 
@@ -101,18 +101,18 @@ struct ConvDgradA {  // A(m = n,ih,iw ; k = kh,kw,co) = G[n, (ih+p-kh d)/s, (iw+
   }
   RETR_DEVICE KCur kcur(int k) const { return tap_cur(k, g.Co, g.KW, g.d); }
   RETR_DEVICE void advance(KCur& t, int d) const { tap_advance(t, d, g.Co, g.KW, g.d); }
-  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& t) const {
-    if (!c.ok || t.k >= K) return zero16();
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& t) const {
+    if (!c.ok || t.k >= K) return nullptr;
     int th = c.ihp - t.khd, tw = c.iwp - t.kwd;
-    if (th < 0 || tw < 0) return zero16();
+    if (th < 0 || tw < 0) return nullptr;
     int oh = th, ow = tw;
     if (g.s != 1) {
       oh = th / g.s;
       ow = tw / g.s;
-      if (oh * g.s != th || ow * g.s != tw) return zero16();
+      if (oh * g.s != th || ow * g.s != tw) return nullptr;
     }
-    if (oh >= g.OH || ow >= g.OW) return zero16();
-    return *(const u32x4*)(c.img + ((long)oh * g.OW + ow) * g.Co + t.c);
+    if (oh >= g.OH || ow >= g.OW) return nullptr;
+    return c.img + ((long)oh * g.OW + ow) * g.Co + t.c;
   }
 };
 
@@ -159,11 +159,11 @@ struct ConvWgradB {  // B(row = kh,kw,ci ; k = pixel n,oh,ow) = X[n, oh*s-p+kh d
       }
     }
   }
-  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& k) const {
-    if (!c.ok || k.m >= M) return zero16();
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& k) const {
+    if (!c.ok || k.m >= M) return nullptr;
     int ih = k.oh * g.s + c.khd, iw = k.ow * g.s + c.kwd;
-    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return zero16();
-    return *(const u32x4*)(x + (((long)k.n * g.H + ih) * g.W + iw) * g.C + c.ci);
+    if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return nullptr;
+    return x + (((long)k.n * g.H + ih) * g.W + iw) * g.C + c.ci;
   }
 };
 
@@ -219,13 +219,13 @@ struct ConvDgradPhaseA {  // A(m = n,i',j' ; k = ti,tj,co) = G[n, i' + ch(ti), j
       }
     }
   }
-  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& t) const {
-    if (!c.ok || t.k >= K) return zero16();
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& t) const {
+    if (!c.ok || t.k >= K) return nullptr;
     // oh = (ih + p - kh) / 2 with ih = ih0 + 2 i, kh = a + 2 ti
     const int oh = c.i + ((ph.ih0 + g.p - ph.a) >> 1) - t.ti;
     const int ow = c.j + ((ph.iw0 + g.p - ph.b) >> 1) - t.tj;
-    if ((unsigned)oh >= (unsigned)g.OH || (unsigned)ow >= (unsigned)g.OW) return zero16();
-    return *(const u32x4*)(c.img + ((long)oh * g.OW + ow) * g.Co + t.c);
+    if ((unsigned)oh >= (unsigned)g.OH || (unsigned)ow >= (unsigned)g.OW) return nullptr;
+    return c.img + ((long)oh * g.OW + ow) * g.Co + t.c;
   }
 };
 
@@ -261,10 +261,10 @@ struct DgradPhaseW {  // B(row = ci ; k = ti,tj,co) = Wt[ci][a + 2ti][b + 2tj][c
       }
     }
   }
-  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& t) const {
-    if (!c.ok || t.k >= K) return zero16();
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& t) const {
+    if (!c.ok || t.k >= K) return nullptr;
     const int kh = ph.a + 2 * t.ti, kw = ph.b + 2 * t.tj;
-    return *(const u32x4*)(c.row + ((long)kh * g.KW + kw) * g.Co + t.c);
+    return c.row + ((long)kh * g.KW + kw) * g.Co + t.c;
   }
 };
 
@@ -290,8 +290,59 @@ struct EpiPhaseRows {
 template <int FAM, typename T, class LA, class LB, class EP>
 int launch_auto(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits,
                 hipStream_t st, const char* what) {
-  if (N >= 128 && M >= 4096) return launch_gemm<FAM, T, 128, 128>(la, lb, ep, M, N, K, splits, st, what);
-  return launch_gemm<FAM, T, 64, 64>(la, lb, ep, M, N, K, splits, st, what);
+  if constexpr (sizeof(T) == 2) {
+    return launch_big<FAM>(la, lb, ep, M, N, K, splits, st, what);
+  } else {
+    if (N >= 128 && M >= 4096) return launch_gemm<FAM, T, 128, 128>(la, lb, ep, M, N, K, splits, st, what);
+    return launch_gemm<FAM, T, 64, 64>(la, lb, ep, M, N, K, splits, st, what);
+  }
+}
+
+// Weight-gradient GEMM (fp32 target, split over the pixel reduction).  Split-K slices write
+// partial slabs ws[s] with plain stores (no fp32 atomics: atomics run at ~1.3 TB/s chip-wide
+// and made split-K the cost of these GEMMs); retr_conv_wgrad_unpack adds the slabs in order
+// while it re-lays the gradient out to OIHW, so the result is deterministic.
+struct WgradPlan {
+  int tile;     // 128: gemm2 128x128 (LDS-DMA), 129: reg-staged 128x128, 64: 64x64
+  int splits;
+};
+
+template <typename T>
+WgradPlan wgrad_plan(int R, int Ncols, int Mp) {
+  constexpr int BK = Elem<T>::BK;
+  WgradPlan p{64, 1};
+  if (R >= 128 && Ncols >= 128) p.tile = sizeof(T) == 2 ? 128 : 129;
+  const int bm = p.tile == 64 ? 64 : 128;
+  const int bn = bm;
+  const long tiles = (long)cdiv(R, bm) * cdiv(Ncols, bn);
+  const int ksteps = cdiv(Mp, BK);
+  // about two blocks per CU (the 128x128 kernel runs 2 per CU), >= 8 K-steps per slice,
+  // <= 128 slabs (tools/gemm_tune: 8-32 slices within 10 % of the best on 16-36 tiles; the
+  // 1-2 tile GEMMs of 1x1 convs over 160x160 maps need more)
+  long s = (512 + tiles - 1) / tiles;
+  if (s > ksteps / 8) s = ksteps / 8;
+  if (s > 128) s = 128;
+  if (s < 1) s = 1;
+  // the launcher rounds the slice length up to whole K-steps: report the slices it will use
+  const int kchunk = cdiv(ksteps, (int)s) * BK;
+  p.splits = cdiv(Mp, kchunk);
+  return p;
+}
+
+template <int FAM, typename T, class LA, class LB>
+int launch_wgrad(const LA& la, const LB& lb, float* ws, long ldws, int R, int Ncols, int Mp,
+                 hipStream_t st, const char* what) {
+  const WgradPlan p = wgrad_plan<T>(R, Ncols, Mp);
+  const int s = p.splits;
+  EpiAccF32 ep{ws, ldws, 0, 0, 1, nullptr};
+  ep.split_stride = s > 1 ? (long)R * ldws : 0;
+  ep.set_vec();
+  if constexpr (sizeof(T) == 2) {
+    if (p.tile == 128) return launch_gemm2<FAM, 128, 128, 2, 2, 2>(la, lb, ep, R, Ncols, Mp, s, st, what);
+  } else {
+    if (p.tile == 129) return launch_gemm<FAM, T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, what);
+  }
+  return launch_gemm<FAM, T, 64, 64>(la, lb, ep, R, Ncols, Mp, s, st, what);
 }
 
 template <typename T>
@@ -351,25 +402,12 @@ int conv_wgrad_t(const void* dy, const void* x, Geom g, float* ws, hipStream_t s
   int Mp = g.Nb * g.OH * g.OW;          // reduction length (pixels)
   int R = g.Co, Ncols = g.KH * g.KW * g.C;
   DenseT<T> la{(const T*)dy, (long)g.Co, R, Mp};
-  constexpr int BK = Elem<T>::BK;
-  bool big = R >= 128 && Ncols >= 128;
-  int s = big ? pick_splits(R, Ncols, Mp, 128, 128, BK) : pick_splits(R, Ncols, Mp, 64, 64, BK);
-  if (s > 1) {  // ws is an output (overwritten): zero it only when split-K adds atomically
-    if (hipMemsetAsync(ws, 0, sizeof(float) * (size_t)R * Ncols, st) != hipSuccess) {
-      retr_set_error("conv_wgrad: memset failed");
-      return 1;
-    }
-  }
-  EpiAccF32 ep{ws, (long)Ncols, s > 1, 0, s == 1, nullptr};
-  ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseT<T> lb{(const T*)x, (long)g.C, Ncols, Mp};
-    return big ? launch_gemm<kFamConvWgrad, T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad_1x1")
-               : launch_gemm<kFamConvWgrad, T, 64, 64>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad_1x1");
+    return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st, "conv_wgrad_1x1");
   }
   ConvWgradB<T> lb{(const T*)x, g, Ncols, Mp};
-  return big ? launch_gemm<kFamConvWgrad, T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad")
-             : launch_gemm<kFamConvWgrad, T, 64, 64>(la, lb, ep, R, Ncols, Mp, s, st, "conv_wgrad");
+  return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st, "conv_wgrad");
 }
 
 // ---- weight packing: fp32 OIHW (+ FrozenBN buffers) -> folded [Co][KH][KW][Cp] and the
@@ -404,8 +442,9 @@ __global__ void conv_pack_kernel(const float* w, const float* bnw, const float* 
 }
 
 __global__ void wgrad_unpack_kernel(const float* ws, const float* scale, float* grad, int Co,
-                                    int Ci, int Cp, int KH, int KW, int accumulate) {
-  long total = (long)Co * Ci * KH * KW;
+                                    int Ci, int Cp, int KH, int KW, int accumulate, int splits) {
+  const long total = (long)Co * Ci * KH * KW;
+  const long slab = (long)Co * KH * KW * Cp;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
     int kw = i % KW;
@@ -414,7 +453,9 @@ __global__ void wgrad_unpack_kernel(const float* ws, const float* scale, float* 
     t /= KH;
     int ci = t % Ci;
     int co = (int)(t / Ci);
-    float v = ws[((long)co * KH * KW + kh * KW + kw) * Cp + ci];
+    const long src = ((long)co * KH * KW + kh * KW + kw) * Cp + ci;
+    float v = ws[src];
+    for (int s = 1; s < splits; ++s) v += ws[src + s * slab];
     if (scale) v *= scale[co];
     grad[i] = accumulate ? grad[i] + v : v;
   }
@@ -478,12 +519,21 @@ int retr_conv_pack(int dtype, const float* w, const float* bn_w, const float* bn
   return retr_check_launch("conv_pack");
 }
 
+int retr_conv2d_wgrad_splits(int dtype, int Nb, int H, int W, int C, int Co, int KH, int KW,
+                             int stride, int pad, int dil) {
+  Geom g = make_geom(Nb, H, W, C, Co, KH, KW, stride, pad, dil);
+  const int Mp = g.Nb * g.OH * g.OW, Ncols = g.KH * g.KW * g.C;
+  return dtype == RETR_BF16 ? wgrad_plan<bf16>(g.Co, Ncols, Mp).splits
+                            : wgrad_plan<float>(g.Co, Ncols, Mp).splits;
+}
+
 int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,
-                           int Cp, int KH, int KW, int accumulate, void* stream) {
+                           int Cp, int KH, int KW, int accumulate, int splits, void* stream) {
+  RETR_REQUIRE(splits >= 1, "conv_wgrad_unpack: splits=%d", splits);
   long total = (long)Co * Ci * KH * KW;
   int grid = (int)(total / 256 + 1 < 4096 ? total / 256 + 1 : 4096);
   hipLaunchKernelGGL(wgrad_unpack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, scale,
-                     grad, Co, Ci, Cp, KH, KW, accumulate);
+                     grad, Co, Ci, Cp, KH, KW, accumulate, splits);
   return retr_check_launch("conv_wgrad_unpack");
 }
 

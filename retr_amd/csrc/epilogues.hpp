@@ -152,15 +152,17 @@ struct EpiAccF32 {
   int vec;
   int overwrite;
   float* rowsum;
+  long split_stride = 0;   // > 0: split-K slice blockIdx.y writes its own slab out + y*stride
   static constexpr bool kRowSum = true;
+  RETR_DEVICE float* base() const { return out + (long)blockIdx.y * split_stride; }
   RETR_DEVICE void apply(int m, int n, float v) const {
-    float* p = out + (long)m * ldo + n;
+    float* p = base() + (long)m * ldo + n;
     if (atomic) atomicAdd(p, v);
     else if (overwrite) *p = v;
     else *p += v;
   }
   RETR_DEVICE void apply8(int m, int n, float (&v)[8]) const {
-    float* p = out + (long)m * ldo + n;
+    float* p = base() + (long)m * ldo + n;
     if (atomic || !vec) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) apply(m, n + e, v[e]);

@@ -32,6 +32,11 @@ RETR_DEVICE int lds_off(int r, int c) { return r * kBKBytes + ((c ^ ((r >> 1) & 
 
 RETR_DEVICE u32x4 zero16() { return u32x4{0u, 0u, 0u, 0u}; }
 
+// Loaders return the address of a 16-byte operand chunk, or nullptr for a chunk outside the
+// operand (padding, ragged edges): register staging reads it as zeros, LDS-DMA staging
+// (gemm2.hpp) points the lane at a zero page instead.
+RETR_DEVICE u32x4 ld16(const void* p) { return p ? *(const u32x4*)p : zero16(); }
+
 // k-major LDS image [BK][ROWS] (bf16) of an operand whose global chunks run along rows: written
 // with 16-byte stores, read as MFMA fragments with ds_read_b64_tr_b16 (gfx950 transposing LDS
 // read).  The 8-byte column unit is XOR-swizzled by k so the 8 k-rows touched by one 32-lane
@@ -99,12 +104,12 @@ struct Stager {
   RETR_DEVICE void fetch(const L& l) {
     if constexpr (L::kContig) {
 #pragma unroll
-      for (int i = 0; i < NCH; ++i) reg[i] = l.load(ctx[i], kc[0]);
+      for (int i = 0; i < NCH; ++i) reg[i] = ld16(l.addr(ctx[i], kc[0]));
       l.advance(kc[0], BK);
     } else {
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
-        reg[i] = l.load(ctx[0], kc[i]);
+        reg[i] = ld16(l.addr(ctx[0], kc[i]));
         l.advance(kc[i], BK);
       }
     }
@@ -388,9 +393,9 @@ struct DenseK {
   RETR_DEVICE Ctx row_ctx(int r) const { return Ctx{p + (long)r * ld, r < rows}; }
   RETR_DEVICE KCur kcur(int k) const { return KCur{k}; }
   RETR_DEVICE void advance(KCur& c, int d) const { c.k += d; }
-  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& k) const {
-    if (!c.ok || k.k >= K) return zero16();
-    return *(const u32x4*)(c.row + k.k);
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& k) const {
+    if (!c.ok || k.k >= K) return nullptr;
+    return c.row + k.k;
   }
 };
 
@@ -408,9 +413,9 @@ struct DenseT {
   RETR_DEVICE Ctx row_ctx(int r) const { return Ctx{p + r, r < rows}; }
   RETR_DEVICE KCur kcur(int k) const { return KCur{k, (long)k * ld}; }
   RETR_DEVICE void advance(KCur& c, int d) const { c.k += d; c.off += (long)d * ld; }
-  RETR_DEVICE u32x4 load(const Ctx& c, const KCur& k) const {
-    if (!c.ok || k.k >= K) return zero16();
-    return *(const u32x4*)(c.col + k.off);
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& k) const {
+    if (!c.ok || k.k >= K) return nullptr;
+    return c.col + k.off;
   }
 };
 

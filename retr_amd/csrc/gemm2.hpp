@@ -1,0 +1,285 @@
+// Large-tile bf16 MFMA GEMM for gfx950 with LDS-DMA (global_load_lds_dwordx4) staging.
+//
+//   C[m][n] = sum_k A(m,k) * B(n,k), same loader / epilogue contracts as gemm.hpp.
+//
+//  * Operand tiles go straight from global memory into LDS (no VGPR round trip, no ds_write
+//    pass): a wave-instruction writes 1 KiB, lane-linear, at a wave-uniform LDS base.  The
+//    LDS images are the ones gemm.hpp's fragment reads expect (XOR-swizzled [rows][8 chunks]
+//    for k-contiguous operands, the k-major [BK][rows] image read with ds_read_b64_tr_b16 for
+//    row-contiguous ones); the swizzle is applied on the SOURCE side: each lane loads the
+//    logical chunk that belongs at its linear slot.  For every tile shape used here that
+//    logical chunk column is a per-thread constant, so the loaders keep their k cursors.
+//  * Chunks outside the operand (conv padding, ragged M/N/K edges) are read from a zero page.
+//  * S-stage LDS ring, one raw s_barrier per K-step: tile t+S-1 is issued right after the
+//    barrier that retires tile t, so S-2 tiles stay in flight across it (counted vmcnt, never
+//    a vmcnt(0) in the steady state: __syncthreads() would drain the DMA queue).
+//  * BM x BN block tile over (BM/WM) x (BN/WN) waves, 16x16x32 bf16 MFMA, fp32 accumulation;
+//    epilogue through LDS (8 consecutive columns per thread, 16-byte global accesses).
+//  * XCD-aware block order and split-K over blockIdx.y as in gemm.hpp.
+#pragma once
+#include "gemm.hpp"
+
+namespace retr {
+
+static __device__ __attribute__((aligned(64))) unsigned int g_zero_page[64];  // 256 B of zeros
+
+RETR_DEVICE void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16,
+                                   0, 0);
+}
+
+template <int N>
+RETR_DEVICE void wait_vmcnt_lgkm0() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(N) : "memory");
+}
+
+RETR_DEVICE void raw_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS-DMA stager of one ROWS x BK operand tile (bf16) for an NT-thread block.
+template <int ROWS, int NT, class L>
+struct GStager {
+  static constexpr int EPC = 8, BK = 64;
+  static constexpr int CPR = ROWS / 8;          // 16-byte slots per k-row of the k-major image
+  static constexpr int NCH = ROWS * 8 / NT;     // chunks per thread per tile
+  static_assert(NCH >= 1 && (ROWS * 8) % NT == 0, "tile too small for the block");
+  static_assert(L::kContig || ((8 * NT / ROWS) % 16 == 0 && NT % CPR == 0),
+                "k-major image: thread's k rows must share one swizzle phase");
+  typename L::Ctx ctx[L::kContig ? NCH : 1];
+  typename L::KCur kc[L::kContig ? 1 : NCH];
+
+  RETR_DEVICE void init(const L& l, int row0, int tid, int kb) {
+    if constexpr (L::kContig) {
+      // linear slot (row r = tid/8 + (NT/8) i, slot tid%8) holds chunk slot ^ ((r>>1)&7)
+      const int c = (tid & 7) ^ ((tid >> 4) & 7);
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) ctx[i] = l.row_ctx(row0 + (tid >> 3) + (NT / 8) * i);
+      kc[0] = l.kcur(kb + c * EPC);
+    } else {
+      // linear slot (k = tid/CPR + (NT/CPR) i, slot tid%CPR) holds row-chunk slot ^ (f(k)/2)
+      const int k0 = tid / CPR, slot = tid % CPR;
+      int f;
+      if constexpr (ROWS >= 128) f = 4 * ((k0 & 3) | (((k0 >> 3) & 1) << 2));
+      else f = 4 * (((k0 >> 1) & 1) | (((k0 >> 3) & 1) << 1));
+      const int c = slot ^ (f >> 1);
+      ctx[0] = l.row_ctx(row0 + c * EPC);
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) kc[i] = l.kcur(kb + k0 + (NT / CPR) * i);
+    }
+  }
+  // issue the tile at the cursors into the image at `lds`, then advance the cursors
+  RETR_DEVICE void issue(const L& l, char* lds, int wave) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const void* p = L::kContig ? l.addr(ctx[i], kc[0]) : l.addr(ctx[0], kc[i]);
+      glds16(p ? p : (const void*)g_zero_page, lds + (NT * i + wave * 64) * 16);
+      if constexpr (!L::kContig) l.advance(kc[i], BK);
+    }
+    if constexpr (L::kContig) l.advance(kc[0], BK);
+  }
+};
+
+template <int BM, int BN, int EPB>
+constexpr int epi_bands() {
+  return EPB > 0 ? EPB : ((size_t)BM * (BN + 4) * 4 > 160 * 1024 ? 2 : 1);
+}
+
+// EPB: epilogue row bands (0 = as few as fit in LDS); S = 1: single-buffered (small-K GEMMs,
+// where the LDS footprint, not the pipeline depth, limits the blocks per CU)
+template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB, class LA, class LB, class EP>
+__global__ void __launch_bounds__(WM * WN * 64)
+gemm2_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
+  using T = bf16;
+  constexpr int NT = WM * WN * 64;
+  constexpr int BK = 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int kStage = (BM + BN) * kBKBytes;
+  using SA = GStager<BM, NT, LA>;
+  using SB = GStager<BN, NT, LB>;
+  constexpr int LPT = SA::NCH + SB::NCH;        // DMA instructions per wave per tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nblk = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  const int kb = blockIdx.y * kchunk;
+  const int ke = min(K, kb + kchunk);
+  if (kb >= ke && K > 0) {
+    ep.empty_split(m0, n0);
+    return;
+  }
+  const int nk = K > 0 ? (ke - kb + BK - 1) / BK : 0;
+
+  SA sa;
+  SB sb;
+  sa.init(la, m0, tid, kb);
+  sb.init(lb, n0, tid, kb);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) {
+    if (s < nk) {
+      sa.issue(la, smem + s * kStage, wave);
+      sb.issue(lb, smem + s * kStage + BM * kBKBytes, wave);
+    }
+  }
+
+  for (int t = 0; t < nk; ++t) {
+    if constexpr (S == 1) {
+      if (t > 0) raw_barrier();          // every wave is done reading the previous tile
+      sa.issue(la, smem, wave);
+      sb.issue(lb, smem + BM * kBKBytes, wave);
+      wait_vmcnt_lgkm0<0>();
+    } else if constexpr (S > 2) {
+      if (t + S - 2 < nk) wait_vmcnt_lgkm0<LPT * (S - 2)>();
+      else wait_vmcnt_lgkm0<0>();
+    } else {
+      wait_vmcnt_lgkm0<0>();
+    }
+    raw_barrier();
+    if (S > 1 && t + S - 1 < nk) {
+      char* st = smem + ((t + S - 1) % S) * kStage;
+      sa.issue(la, st, wave);
+      sb.issue(lb, st + BM * kBKBytes, wave);
+    }
+    const char* A = smem + (t % S) * kStage;
+    const char* B = A + BM * kBKBytes;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      u32x4 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = Stager<T, BM, LA>::frag(A, wm * WTM + 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = Stager<T, BN, LB>::frag(B, wn * WTN + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mfma_step<T>(acc[i][j], af[i], bfr[j]);
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue through LDS (see gemm.hpp), in EP_PASSES row bands when the fp32 tile does
+  // not fit in LDS (wave rows wm belong to band wm / (WM / EP_PASSES))
+  constexpr int CS = BN + 4;
+  constexpr int EP_PASSES = epi_bands<BM, BN, EPB>();
+  constexpr int BAND = BM / EP_PASSES;
+  float* ct = (float*)smem;
+#pragma unroll
+  for (int pass = 0; pass < EP_PASSES; ++pass) {
+    if (pass > 0) __syncthreads();
+    if (wm / (WM / EP_PASSES) == pass) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            ct[(wm * WTM - pass * BAND + 16 * i + 4 * (lane >> 4) + e) * CS + wn * WTN + 16 * j +
+               (lane & 15)] = acc[i][j][e];
+    }
+    __syncthreads();
+    const int mb = m0 + pass * BAND;
+    if (ep.lane_contiguous()) {
+      for (int q = tid; q < BAND * BN; q += NT) {
+        const int r = q / BN, c = q % BN;
+        const int m = mb + r, n = n0 + c;
+        if (m < M && n < N) ep.apply(m, n, ct[r * CS + c]);
+      }
+      continue;
+    }
+    constexpr int CH = BN / 8;
+#pragma unroll 2
+    for (int q = tid; q < BAND * CH; q += NT) {
+      const int r = q / CH, c = (q % CH) * 8;
+      const int m = mb + r, n = n0 + c;
+      if (m >= M || n >= N) continue;
+      const f32x4 lo = *(const f32x4*)(ct + r * CS + c);
+      const f32x4 hi = *(const f32x4*)(ct + r * CS + c + 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (n + 8 <= N) {
+        ep.apply8(m, n, v);
+      } else {
+        for (int e = 0; e < 8 && n + e < N; ++e) ep.apply(m, n + e, v[e]);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int S, int EPB>
+constexpr size_t gemm2_lds_bytes() {
+  constexpr size_t stage = (size_t)S * (BM + BN) * kBKBytes;
+  constexpr size_t epi = (size_t)BM * (BN + 4) * 4 / epi_bands<BM, BN, EPB>();
+  return stage > epi ? stage : epi;
+}
+
+template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB = 0, class LA, class LB,
+          class EP>
+int launch_gemm2(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits,
+                 hipStream_t st, const char* what) {
+  constexpr int BK = 64;
+  const int tm = cdiv(M, BM), tn = cdiv(N, BN);
+  if (splits < 1) splits = 1;
+  const int ksteps = cdiv(K, BK);
+  int kchunk = BK;
+  if (K > 0) {
+    if (splits > ksteps) splits = ksteps;
+    kchunk = cdiv(ksteps, splits) * BK;
+    splits = cdiv(K, kchunk);
+  } else {
+    splits = 1;
+  }
+  dim3 grid(tm * tn, splits);
+  constexpr size_t lds = gemm2_lds_bytes<BM, BN, S, EPB>();
+  auto kern = gemm2_kernel<FAM, BM, BN, WM, WN, S, EPB, LA, LB, EP>;
+  if constexpr (lds > 65536) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(WM * WN * 64), lds, st, la, lb, ep, M, N, K, kchunk, tn);
+  return retr_check_launch(what);
+}
+
+// Tile choice for the large bf16 GEMMs (convolutions, big linears), from the tools/gemm_tune
+// sweep on MI355X (profiles/r2_gemm_tune.txt): the 4-wave 128x128 LDS-DMA tile with a 2-stage
+// ring (2 blocks per CU) is the fastest on every conv-shaped GEMM; 128x64 (3 stages) for N=64;
+// the 8-wave 256x256 tile only for very wide outputs (the 30522-word head); small grids fall
+// back to the register-staged 64x64 kernel of gemm.hpp.  ``splits`` > 1 only for
+// weight-gradient GEMMs (split over the pixel / token reduction).
+template <int FAM, class LA, class LB, class EP>
+int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits,
+               hipStream_t st, const char* what) {
+  const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * splits;
+  const long t128 = (long)cdiv(M, 128) * cdiv(N, 128) * splits;
+  const long t12864 = (long)cdiv(M, 128) * cdiv(N, 64) * splits;
+  if (K <= 128 && splits == 1 && N > 64 && t128 >= 160)   // small K: 4 blocks per CU
+    return launch_gemm2<FAM, 128, 128, 2, 2, 1, 2>(la, lb, ep, M, N, K, splits, st, what);
+  if (N >= 4096 && t256 >= 256)
+    return launch_gemm2<FAM, 256, 256, 2, 4, 2>(la, lb, ep, M, N, K, splits, st, what);
+  if (N > 64 && t128 >= 160)
+    return launch_gemm2<FAM, 128, 128, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
+  if (N <= 64 && t12864 >= 160)
+    return launch_gemm2<FAM, 128, 64, 2, 2, 3>(la, lb, ep, M, N, K, splits, st, what);
+  return launch_gemm<FAM, bf16, 64, 64>(la, lb, ep, M, N, K, splits, st, what);
+}
+
+}  // namespace retr

@@ -3,13 +3,26 @@
 //   dgrad   : dX = gate(dY W [+ addend])   dY [M][N]
 //   wgrad   : dW += dY^T X                 (fp32, split-K + atomics)
 //   bias    : db += colsum(dY)
-#include "gemm.hpp"
+#include "gemm2.hpp"
 #include "epilogues.hpp"
 #include "../../include/retr_hip.h"
 
 using namespace retr;
 
 namespace {
+
+// bf16 forward / data-gradient GEMMs with enough 128x128 tiles to fill the GPU (MLP head, FFN
+// expansions) go to the LDS-DMA kernels of gemm2.hpp; the rest keep the occupancy-sized
+// register-staged kernel.
+template <int FAM, typename T, class LA, class LB, class EP>
+int launch_linear(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, hipStream_t st,
+                  const char* what) {
+  if constexpr (sizeof(T) == 2) {
+    if ((long)cdiv(M, 128) * cdiv(N, 128) >= 160 && K >= 128)
+      return launch_big<FAM>(la, lb, ep, M, N, K, 1, st, what);
+  }
+  return launch_sized<FAM, T>(la, lb, ep, M, N, K, st, what);
+}
 
 template <typename T, typename TO>
 int linear_fwd_t(const void* x, long ldx, const void* w, long ldw, const float* bias, void* y,
@@ -20,7 +33,7 @@ int linear_fwd_t(const void* x, long ldx, const void* w, long ldw, const float* 
   DropoutParams dp = make_dp(p, seed);
   EpiFwd<TO, float> ep{(TO*)y, ldy, bias, res, ldr, relu, dp, (long)N};
   ep.set_vec();
-  return launch_sized<kFamLinearFwd, T>(la, lb, ep, M, N, K, st, "linear_fwd");
+  return launch_linear<kFamLinearFwd, T>(la, lb, ep, M, N, K, st, "linear_fwd");
 }
 
 template <typename T, typename TO, typename TA>
@@ -34,10 +47,10 @@ int linear_dgrad_t(const void* dy, long lddy, const void* w, long ldw, void* dx,
   ep.set_vec();
   if (w_trans) {
     DenseK<T> lb{(const T*)w, ldw, K, N};
-    return launch_sized<kFamLinearDgrad, T>(la, lb, ep, M, K, N, st, "linear_dgrad");
+    return launch_linear<kFamLinearDgrad, T>(la, lb, ep, M, K, N, st, "linear_dgrad");
   }
   DenseT<T> lb{(const T*)w, ldw, K, N};
-  return launch_sized<kFamLinearDgrad, T>(la, lb, ep, M, K, N, st, "linear_dgrad");
+  return launch_linear<kFamLinearDgrad, T>(la, lb, ep, M, K, N, st, "linear_dgrad");
 }
 
 // zero an fp32 [rows][cols] region with row stride ld (stream-ordered, graph-capturable)
@@ -52,6 +65,36 @@ int zero_f32(float* p, long ld, int rows, int cols, hipStream_t st) {
   return 0;
 }
 
+// Deterministic column sums db[n] (=|+=) sum_m dY[m][n]: one 1024-thread block per 64 columns,
+// wave w sums rows w, w+16, ... in order, the 16 wave partials are added in wave order.
+template <typename T>
+__global__ void __launch_bounds__(1024)
+colsum_det_kernel(const T* dy, long ld, int M, int N, float* db, int accumulate) {
+  __shared__ float part[16][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (n < N) {
+#pragma unroll 8
+    for (int m = wave; m < M; m += 16) s += to_f(dy[(long)m * ld + n]);
+  }
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += part[w][lane];
+    db[n] = accumulate ? db[n] + t : t;
+  }
+}
+
+template <typename T>
+int colsum_det(const void* dy, long ld, int M, int N, float* db, int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_det_kernel<T>, dim3(cdiv(N, 64)), dim3(1024), 0, st, (const T*)dy, ld,
+                     M, N, db, accumulate);
+  return retr_check_launch("bias_grad_det");
+}
+
 template <typename T>
 int linear_wgrad_t(const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw,
                    int M, int N, int K, float* db, int accumulate, hipStream_t st) {
@@ -61,6 +104,12 @@ int linear_wgrad_t(const void* dy, long lddy, const void* x, long ldx, float* dw
   constexpr int BK = Elem<T>::BK;
   const bool big = N >= 512 && K >= 128;
   int s = big ? pick_splits(N, K, M, 128, 128, BK) : pick_splits(N, K, M, 64, 64, BK);
+  if (retr_deterministic()) {
+    // no split-K atomics, no fused (LDS-atomic) row sums: ordered column sums instead
+    s = 1;
+    if (db && colsum_det<T>(dy, lddy, M, N, db, accumulate, st)) return 1;
+    db = nullptr;
+  }
   if (!accumulate) {
     if (s > 1 && zero_f32(dw, lddw, N, K, st)) return 1;
     if (db && zero_f32(db, N, 1, N, st)) return 1;
@@ -143,6 +192,10 @@ int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long 
 int retr_bias_grad(int dtype, const void* dy, long lddy, int M, int N, float* db, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) return 0;
+  if (retr_deterministic()) {
+    return dtype == RETR_BF16 ? colsum_det<bf16>(dy, lddy, M, N, db, 1, st)
+                              : colsum_det<float>(dy, lddy, M, N, db, 1, st);
+  }
   int rows = 64;
   dim3 grid(cdiv(N, 256), cdiv(M, rows));
   if (dtype == RETR_BF16)

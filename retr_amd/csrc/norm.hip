@@ -149,12 +149,18 @@ embed_ln_fwd_kernel(const long long* tok, int M, int T, int C, const float* word
   }
 }
 
+// DecoderEmbeddings backward, deterministic (no atomics).  Kernel 1: per row the gradient of
+// LN(word[t] + pos[p]) w.r.t. its input, o[row] -> workspace `dsum`, and per-block partial sums
+// of the LayerNorm parameter gradients -> `part` (reduced in block order by
+// ln_param_reduce_kernel).  Kernel 2 scatters o into the word-embedding rows: the block of the
+// first occurrence of a token sums every row holding that token in row order (single writer
+// per embedding row).  Kernel 3 sums o over the batch per position (learned position table).
 template <int PER>
 __global__ void __launch_bounds__(256)
 embed_ln_bwd_kernel(const long long* tok, int M, int T, int C, const float* word,
                     const float* posw, const float* gamma, const float* mean, const float* rstd,
-                    const float* dy, DropoutParams dp, float* dword, float* dposw, float* dgamma,
-                    float* dbeta, int padding_idx, int rows_per_block) {
+                    const float* dy, DropoutParams dp, float* dsum, float* part,
+                    int rows_per_block) {
   __shared__ float red[2][4][1024];
   int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float pg[PER], pb[PER];
@@ -183,9 +189,7 @@ embed_ln_bwd_kernel(const long long* tok, int M, int T, int C, const float* word
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int c = lane + 64 * i;
-      float o = rs * (g[i] - s1 - xh[i] * s2);
-      if (dword && t != padding_idx) atomicAdd(dword + t * C + c, o);
-      if (dposw) atomicAdd(dposw + (long)p * C + c, o);
+      dsum[(long)row * C + c] = rs * (g[i] - s1 - xh[i] * s2);
     }
   }
 #pragma unroll
@@ -194,12 +198,62 @@ embed_ln_bwd_kernel(const long long* tok, int M, int T, int C, const float* word
     red[1][wave][lane + 64 * i] = pb[i];
   }
   __syncthreads();
+  float* pw = part + (long)blockIdx.x * 2 * C;
   for (int c = threadIdx.x; c < C; c += 256) {
-    float a = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
-    float b = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
-    if (dgamma) atomicAdd(dgamma + c, a);
-    if (dbeta) atomicAdd(dbeta + c, b);
+    pw[c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    pw[C + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
   }
+}
+
+// one block per row i; only the block of the first occurrence of tok[i] writes dword[tok[i]]
+__global__ void __launch_bounds__(256)
+embed_word_scatter_kernel(const long long* tok, int M, int C, const float* dsum, float* dword,
+                          int padding_idx) {
+  __shared__ int list[256];
+  __shared__ int cnt[4];
+  __shared__ int earlier;
+  const int i = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const long long t = tok[i];
+  if (t == padding_idx) return;
+  if (tid == 0) earlier = 0;
+  __syncthreads();
+  int e = 0;
+  for (int j = tid; j < i; j += 256) e |= (tok[j] == t);
+  if (e) earlier = 1;
+  __syncthreads();
+  if (earlier) return;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};   // columns tid + 256 q (C <= 1024)
+  for (int j0 = i; j0 < M; j0 += 256) {
+    const int j = j0 + tid;
+    const bool hit = j < M && tok[j] == t;
+    const unsigned long long bal = __ballot(hit);
+    if (lane == 0) cnt[wave] = __popcll(bal);
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wave; ++w) base += cnt[w];
+    const int n = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+    if (hit) list[base + __popcll(bal & ((1ull << lane) - 1ull))] = j;
+    __syncthreads();
+    for (int k = 0; k < n; ++k) {            // matching rows in increasing row order
+      const float* src = dsum + (long)list[k] * C;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (tid + 256 * q < C) acc[q] += src[tid + 256 * q];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (tid + 256 * q < C) dword[t * C + tid + 256 * q] += acc[q];
+}
+
+// dposw[p][c] += sum_b dsum[b*T + p][c]  (batch order)
+__global__ void embed_pos_reduce_kernel(const float* dsum, int B, int T, int C, float* dposw) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= (long)T * C) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += dsum[(long)b * T * C + i];
+  dposw[i] += s;
 }
 
 
@@ -315,22 +369,48 @@ int retr_embed_ln_fwd(const long long* tokens, int B, int T, int C, const float*
   return retr_check_launch("embed_ln_fwd");
 }
 
+size_t retr_embed_ln_bwd_workspace(int B, int T, int C) {
+  const long M = (long)B * T;
+  return sizeof(float) * ((size_t)M * C + 2 * (size_t)C * (size_t)cdiv(M, 32));
+}
+
 int retr_embed_ln_bwd(const long long* tokens, int B, int T, int C, const float* word,
                       const float* posw, const float* gamma, const float* mean, const float* rstd,
                       const float* dy, float drop_p, unsigned long long seed, float* dword,
-                      float* dposw, float* dgamma, float* dbeta, int padding_idx, void* stream) {
+                      float* dposw, float* dgamma, float* dbeta, int padding_idx,
+                      void* workspace, void* stream) {
   int M = B * T;
   if (M == 0) return 0;
+  RETR_REQUIRE(workspace != nullptr, "embed_ln_bwd: workspace required");
+  RETR_REQUIRE(C <= 1024, "embed_ln_bwd: C=%d > 1024", C);
   hipStream_t st = (hipStream_t)stream;
   DropoutParams dp = make_dp(drop_p, seed);
-  int rpb = 32;
-  dim3 grid(cdiv(M, rpb));
+  const int rpb = 32;
+  const int nblk = cdiv(M, rpb);
+  float* dsum = (float*)workspace;
+  float* part = dsum + (size_t)M * C;
 #define EB(P)                                                                                   \
-  hipLaunchKernelGGL((embed_ln_bwd_kernel<P>), grid, dim3(256), 0, st, tokens, M, T, C, word, posw, \
-                     gamma, mean, rstd, dy, dp, dword, dposw, dgamma, dbeta, padding_idx, rpb);
+  hipLaunchKernelGGL((embed_ln_bwd_kernel<P>), dim3(nblk), dim3(256), 0, st, tokens, M, T, C,   \
+                     word, posw, gamma, mean, rstd, dy, dp, dsum, part, rpb);
   PER_SWITCH(C, EB)
 #undef EB
-  return retr_check_launch("embed_ln_bwd");
+  if (int e = retr_check_launch("embed_ln_bwd")) return e;
+  if (dword) {
+    hipLaunchKernelGGL(embed_word_scatter_kernel, dim3(M), dim3(256), 0, st, tokens, M, C, dsum,
+                       dword, padding_idx);
+    if (int e = retr_check_launch("embed_word_scatter")) return e;
+  }
+  if (dposw) {
+    hipLaunchKernelGGL(embed_pos_reduce_kernel, dim3(cdiv((long)T * C, 256)), dim3(256), 0, st,
+                       dsum, B, T, C, dposw);
+    if (int e = retr_check_launch("embed_pos_reduce")) return e;
+  }
+  if (dgamma || dbeta) {
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, st, part,
+                       nblk, C, dgamma, dbeta);
+    if (int e = retr_check_launch("embed_param_reduce")) return e;
+  }
+  return 0;
 }
 
 }  // extern "C"

@@ -46,14 +46,20 @@ def clip_and_step(model, optimizer, max_norm):
     optimizer.step()
 
 
-def train_step(model, criterion, samples, caps, cap_masks, optimizer, max_norm, grad_sync=None):
-    """One reference training step (engine.py:70-83) — returns the loss tensor (no host sync)."""
+def forward_backward(model, criterion, samples, caps, cap_masks, optimizer):
+    """engine.py:70-79: forward, CE loss, zero_grad, backward (no host sync)."""
     from . import ops
     ops.bump_seed()
     outputs = model(*samples, caps[:, :-1], cap_masks[:, :-1])
     loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
     optimizer.zero_grad()
     loss.backward()
+    return loss
+
+
+def train_step(model, criterion, samples, caps, cap_masks, optimizer, max_norm, grad_sync=None):
+    """One reference training step (engine.py:70-83) — returns the loss tensor (no host sync)."""
+    loss = forward_backward(model, criterion, samples, caps, cap_masks, optimizer)
     if grad_sync is not None:
         grad_sync.synchronize()
     clip_and_step(model, optimizer, max_norm)
@@ -78,6 +84,11 @@ class GraphedTrainStep:
     convolution weights, captured decode graphs) never serve values from before the replay,
     and FusedAdamW's host step counters advance with the device counter.
 
+    Data parallel (``grad_sync``): the step is captured as two graphs -- forward + backward,
+    then clip + optimizer -- and every replay runs the bucketed RCCL all-reduces of
+    ``grad_sync`` (deferred mode: in place on FusedAdamW's gradient arena) between them, so no
+    collective is captured inside a graph.
+
     Requirements: ``optimizer`` built with ``capturable=True`` (or a retr_amd FusedAdamW, whose
     step counter and lr live on the device); fixed batch shapes.
     """
@@ -86,6 +97,7 @@ class GraphedTrainStep:
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
         self.max_norm, self.grad_sync, self.warmup = max_norm, grad_sync, warmup
         self.graph = None
+        self.graph_opt = None
         self.static = None
         self.loss = None
         self._active = None
@@ -94,6 +106,30 @@ class GraphedTrainStep:
         s_img, s_mask, s_caps, s_cm = self.static
         return train_step(self.model, self.criterion, (NestedTensor(s_img, s_mask),), s_caps,
                           s_cm, self.optimizer, self.max_norm, self.grad_sync)
+
+    def _fb(self):
+        s_img, s_mask, s_caps, s_cm = self.static
+        return forward_backward(self.model, self.criterion, (NestedTensor(s_img, s_mask),),
+                                s_caps, s_cm, self.optimizer)
+
+    def _capture(self):
+        self.graph = torch.cuda.CUDAGraph()
+        if self.grad_sync is None:
+            with torch.cuda.graph(self.graph):
+                self.loss = self._step().detach()
+            return
+        gs = self.grad_sync
+        defer = gs.defer
+        gs.defer = True                      # hooks only route gradients while capturing
+        try:
+            with torch.cuda.graph(self.graph):
+                self.loss = self._fb().detach()
+            gs.synchronize()                 # eager: p.grad -> bucket views for the 2nd graph
+            self.graph_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_opt, pool=self.graph.pool()):
+                clip_and_step(self.model, self.optimizer, self.max_norm)
+        finally:
+            gs.defer = defer
 
     def _params(self):
         return [p for g in self.optimizer.param_groups for p in g["params"]]
@@ -160,14 +196,15 @@ class GraphedTrainStep:
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
             self.optimizer.zero_grad(set_to_none=True)
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
-                self.loss = self._step().detach()
+            self._capture()
             self._active = list(getattr(self.optimizer, "_last_active", []))
             self._restore(snap)
         if hasattr(self.optimizer, "sync_hyper"):
             self.optimizer.sync_hyper()      # lr schedule changes reach the captured kernels
         self.graph.replay()
+        if self.graph_opt is not None:
+            self.grad_sync.synchronize()     # RCCL all-reduce of every bucket, then the update
+            self.graph_opt.replay()
         if hasattr(self.optimizer, "_advance_host"):
             self.optimizer._advance_host(self._active)
         self._bump()

@@ -230,6 +230,9 @@ def build_model(config):
         raise NotImplementedError()
     model = Model(backbone, transformer, None, config.hidden_dim, config.vocab_size)
     model.set_compute_dtype(compute_dtype(config))
+    if getattr(config, "deterministic", False):
+        from .. import ops
+        ops.set_deterministic(True)
     print(f"Built {model.__class__.__name__} model with {transformer.__class__.__name__}")
     criterion = CrossEntropyLoss()
     return model, criterion

@@ -95,6 +95,17 @@ class _Overlap:
             self.main.wait_stream(self.stream)
 
 
+def set_deterministic(on=True):
+    """Fixed-order reductions in every kernel (config.deterministic): weight-gradient GEMMs
+    without split-K atomics, ordered bias-gradient column sums.  Process-wide."""
+    call("retr_set_deterministic", 1 if on else 0)
+
+
+def is_deterministic():
+    from ._lib import load
+    return bool(load().retr_get_deterministic())
+
+
 def dcode(dtype):
     if dtype == torch.bfloat16:
         return BF16
@@ -627,9 +638,11 @@ class _EmbedLN(torch.autograd.Function):
         dev = word.device
         dy = dy.contiguous()
         (dword, _), (dposw, _), (dgamma, _), (dbeta, _) = map(grad_buffer, ctx.gparams)
+        M = B * T    # workspace: retr_embed_ln_bwd_workspace(B, T, C) bytes
+        ws = torch.empty(M * C + 2 * C * ((M + 31) // 32), dtype=torch.float32, device=dev)
         call("retr_embed_ln_bwd", ptr(caps), B, T, C, ptr(word), ptr(posw), ptr(gamma),
              ptr(mean), ptr(rstd), ptr(dy), drop_p, seed, ptr(dword), ptr(dposw), ptr(dgamma),
-             ptr(dbeta), -1 if padding_idx is None else int(padding_idx), _st())
+             ptr(dbeta), -1 if padding_idx is None else int(padding_idx), ptr(ws), _st())
         return None, dword, dposw, dgamma, dbeta, None, None, None
 
 

@@ -130,15 +130,23 @@ def _conv_dgrad(spec, g, in_shape, addend=None, gate=None):
     return dx
 
 
+def wgrad_splits(dtype, n, h, w, c, spec):
+    """Number of pixel-reduction slices (partial slabs) retr_conv2d_wgrad writes."""
+    return int(_lib.load().retr_conv2d_wgrad_splits(dcode(dtype), n, h, w, c, spec.cout, spec.k,
+                                                     spec.k, spec.s, spec.p, spec.d))
+
+
 def _conv_wgrad(spec, g, x, in_shape):
     n, h, w, c = in_shape
     _, _, _, scale = PACKS.get(spec, g.dtype)
-    ws = torch.empty(spec.cout, spec.k * spec.k * c, dtype=torch.float32, device=g.device)
+    splits = wgrad_splits(g.dtype, n, h, w, c, spec)
+    ws = torch.empty(splits, spec.cout, spec.k * spec.k * c, dtype=torch.float32,
+                     device=g.device)
     call("retr_conv2d_wgrad", dcode(g.dtype), ptr(g), ptr(x), n, h, w, c, ptr(ws), spec.cout,
          spec.k, spec.k, spec.s, spec.p, spec.d, _st())
     grad, _ = grad_buffer(spec.conv.weight)     # sole writer: overwrite mode below
     call("retr_conv_wgrad_unpack", ptr(ws), ptr(scale), ptr(grad), spec.cout, spec.cin, c, spec.k,
-         spec.k, 0, _st())
+         spec.k, 0, splits, _st())
     return grad
 
 

@@ -99,3 +99,23 @@ def synthetic_captions(batch, max_len, vocab_size, seed=0, bos=101, eos=102, pad
         caps[b, 1 + n] = eos
     caps = torch.from_numpy(caps)
     return caps, caps == pad
+
+
+class SyntheticRefDataset(torch.utils.data.Dataset):
+    """RefCocoCaption-shaped dataset (the output tuple of data_utils/refcoco.py:105-188:
+    ann_id, image [3, H, H], mask [H, H], caps [T+1], cap_mask [T+1]) on synthetic data, for
+    the data-parallel launcher and its tests (RefCOCO itself is not fetched here)."""
+    return_global_context = False
+    return_location_features = False
+
+    def __init__(self, config, n, size, seed=0):
+        self.img, self.mask = synthetic_images(n, size, seed=31 + seed, pad_band=True)
+        self.caps, self.cap_mask = synthetic_captions(n, config.max_position_embeddings,
+                                                      config.vocab_size, seed=32 + seed)
+        self.annot = [(i, "img", f"caption {i}", [0, 0, 1, 1]) for i in range(n)]
+
+    def __len__(self):
+        return len(self.caps)
+
+    def __getitem__(self, i):
+        return i, self.img[i], self.mask[i], self.caps[i], self.cap_mask[i]

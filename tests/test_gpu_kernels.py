@@ -6,7 +6,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from retr_amd import ops, resnet
+from retr_amd import _lib, ops, resnet
 from retr_amd._lib import call, ptr
 
 pytestmark = pytest.mark.gpu
@@ -20,7 +20,8 @@ def rel_err(a, b):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("M,N,K", [(64, 64, 64), (200, 96, 136), (2048, 256, 256),
-                                   (4100, 520, 72), (37, 30522, 64)])
+                                   (4100, 520, 72), (37, 30522, 64),
+                                   (6400, 2048, 256), (5000, 1800, 264), (5000, 264, 1800)])
 def test_linear_fwd_dgrad_wgrad(dtype, tol, M, N, K):
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     x = torch.randn(M, K, generator=g).to(DEV)
@@ -95,9 +96,30 @@ def _pack(w, cdtype):
     return wp, wt, bias, scale, cp, (bw, bb, rm, rv)
 
 
+# Shapes large enough for the LDS-DMA tiles of gemm2.hpp (256x128, 256x64, 128x128 blocks,
+# split-K weight gradients, stride-2 phase dgrad, dilation, ragged M).
+BIG_CONVS = [
+    (16, 64, 63, 256, 3, 1, 1, 1),
+    (16, 64, 64, 64, 3, 1, 1, 1),
+    (4, 128, 60, 256, 1, 1, 0, 1),
+    (8, 128, 81, 128, 3, 2, 1, 1),
+    (8, 256, 30, 256, 3, 1, 2, 2),
+    (16, 256, 41, 512, 1, 2, 0, 1),
+]
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 5e-6), (torch.bfloat16, 2e-2)])
 @pytest.mark.parametrize("cfg", CONVS)
 def test_conv_fwd_dgrad_wgrad(dtype, tol, cfg):
+    _check_conv(dtype, tol, cfg)
+
+
+@pytest.mark.parametrize("cfg", BIG_CONVS)
+def test_conv_big_bf16(cfg):
+    _check_conv(torch.bfloat16, 2e-2, cfg)
+
+
+def _check_conv(dtype, tol, cfg):
     N, Ci, H, Co, k, s, p, d = cfg
     g = torch.Generator(device="cpu").manual_seed(sum(cfg))
     x = torch.randn(N, Ci, H, H, generator=g)
@@ -128,11 +150,15 @@ def test_conv_fwd_dgrad_wgrad(dtype, tol, cfg):
         call("retr_conv2d_dgrad", ops.dcode(dtype), ptr(gn), N, H, H, cp, ptr(wt), ptr(dx), Co,
              k, k, s, p, d, None, None, ops._st())
         assert rel_err(dx.permute(0, 3, 1, 2), xreq.grad) < tol
-    ws = torch.zeros(Co, k * k * cp, device=DEV)
+    splits = _lib.load().retr_conv2d_wgrad_splits(ops.dcode(dtype), N, H, H, cp, Co, k, k, s,
+                                                  p, d)
+    assert splits >= 1
+    ws = torch.full((splits, Co, k * k * cp), float("nan"), device=DEV)   # overwritten
     call("retr_conv2d_wgrad", ops.dcode(dtype), ptr(gn), ptr(xn), N, H, H, cp, ptr(ws), Co, k, k,
          s, p, d, ops._st())
     grad = torch.empty(Co, Ci, k, k, device=DEV)
-    call("retr_conv_wgrad_unpack", ptr(ws), None, ptr(grad), Co, Ci, cp, k, k, 0, ops._st())
+    call("retr_conv_wgrad_unpack", ptr(ws), None, ptr(grad), Co, Ci, cp, k, k, 0, splits,
+         ops._st())
     assert rel_err(grad, wreq.grad) < tol
 
 

@@ -99,10 +99,23 @@ def _groups(model, cfg):
                         if "backbone" in n and p.requires_grad], "lr": cfg.lr_backbone}]
 
 
-def test_train_steps_fused_vs_torch_optimizer():
+@pytest.fixture
+def deterministic_mode(request):
+    from retr_amd import ops
+    ops.set_deterministic(request.param)
+    yield request.param
+    ops.set_deterministic(False)
+
+
+@pytest.mark.parametrize("deterministic_mode", [False, True], indirect=True)
+def test_train_steps_fused_vs_torch_optimizer(deterministic_mode):
     """Three engine.train_step's with FusedAdamW (gradients written straight into the arena)
-    against the same model with torch.optim.AdamW + clip_grad_norm_."""
+    against the same model with torch.optim.AdamW + clip_grad_norm_.  In deterministic mode
+    both models' gradients come from identical fixed-order kernels, so only the optimizer
+    arithmetic differs (2e-6 per step in test_fused_adamw_matches_torch, compounded over the
+    three steps); otherwise split-K fp32 atomics add in a run-dependent order."""
     from retr_amd.engine import train_step
+    tol_loss, tol_p = (1e-6, 1e-5) if deterministic_mode else (1e-5, 5e-5)
     cfg, m1, crit = _micro_model()
     _, m2, _ = _micro_model()
     o1 = FusedAdamW(_groups(m1, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay)
@@ -114,7 +127,7 @@ def test_train_steps_fused_vs_torch_optimizer():
     for _ in range(3):
         l1 = train_step(m1, crit, samples, caps, cm, o1, 0.1)
         l2 = train_step(m2, crit, samples, caps, cm, o2, 0.1)
-        assert abs(l1.item() - l2.item()) <= 1e-5 * abs(l2.item())
+        assert abs(l1.item() - l2.item()) <= tol_loss * abs(l2.item())
     # gradients are written straight into the arena; only parameters with several
     # contributors (the learned query positions, shared by the decoder layers) are summed by
     # autograd outside it and copied in
@@ -122,11 +135,14 @@ def test_train_steps_fused_vs_torch_optimizer():
     in_arena = sum(p.grad.data_ptr() == p._retr_grad_view.data_ptr() for p in ps)
     assert in_arena >= len(ps) - 2, (in_arena, len(ps))
     for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
-        assert _rel(a.detach(), b.detach()) < 5e-5, n
+        assert _rel(a.detach(), b.detach()) < tol_p, n
 
 
-def test_gradient_accumulation_with_arena():
-    """Two backward passes without zero_grad accumulate exactly like autograd's default."""
+@pytest.mark.parametrize("deterministic_mode", [False, True], indirect=True)
+def test_gradient_accumulation_with_arena(deterministic_mode):
+    """Two backward passes without zero_grad accumulate exactly like autograd's default
+    (bitwise 2 g and g in deterministic mode)."""
+    tol = 1e-7 if deterministic_mode else 1e-5     # fp32 atomics: order may differ
     cfg, model, crit = _micro_model()
     opt = FusedAdamW(_groups(model, cfg), lr=cfg.lr)
     samples, caps, cm = _batch(cfg)
@@ -141,12 +157,14 @@ def test_gradient_accumulation_with_arena():
     loss().backward()
     for n, p in model.named_parameters():
         if n in g1:
-            assert _rel(p.grad, 2 * g1[n]) < 1e-5, n     # fp32 atomics: order may differ
+            assert _rel(p.grad, 2 * g1[n]) < tol, n
     opt.zero_grad()
     loss().backward()
     for n, p in model.named_parameters():
         if n in g1:
-            assert _rel(p.grad, g1[n]) < 1e-5, n
+            assert _rel(p.grad, g1[n]) < tol, n
+            if deterministic_mode:
+                assert torch.equal(p.grad, g1[n]), n
 
 
 def test_graphed_step_with_fused_adamw_matches_eager():

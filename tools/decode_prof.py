@@ -1,0 +1,49 @@
+"""Decode-only driver for profiling (rocprofv3 --kernel-trace --stats -- python tools/decode_prof.py):
+cfg5 (ResNet-50 dilation 224x224, 6/6 d256, bf16), batch 64, greedy (and beam with --beam K),
+captured step graphs; prints ms per batch and per step."""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bench import build, cfg5  # noqa: E402
+from retr_amd.eval_utils.decode import IncrementalBeam, greedy  # noqa: E402
+from retr_amd.models.utils import NestedTensor  # noqa: E402
+from retr_amd.synthetic import synthetic_images  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--beam", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+    model, _ = build(cfg5(), "cuda")
+    model.eval()
+    img, mask = synthetic_images(a.batch, 224, seed=3000)
+    samples = [NestedTensor(img.cuda(), mask.cuda())]
+    T = 128
+    if a.beam > 1:
+        bm = IncrementalBeam(model, a.beam)
+        fn = lambda: bm(samples, T, 101, 102)  # noqa: E731
+    else:
+        fn = lambda: greedy(samples, model, max_len=T, bos_token=101, eos_token=102)  # noqa: E731
+    ids = fn()
+    torch.cuda.synchronize()
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        ids = fn()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        steps = int((ids != 0).sum(1).max().item())
+        print(f"beam {a.beam}: {dt * 1e3:.2f} ms/batch, {a.batch / dt:.1f} refs/s, "
+              f"{dt * 1e3 / max(1, steps - 1):.3f} ms/step over {steps} tokens", flush=True)
+
+
+if __name__ == "__main__":
+    main()
