@@ -211,6 +211,31 @@ int retr_adamw_update(float* param, float* grad, float* exp_avg, float* exp_avg_
                       const float* step, float step_offset, const float* partials, int nparts,
                       float max_norm, void* stream);
 
+/* ---- fused incremental-decode step (csrc/decode.hip; eval_utils/decode.py:53-81 in KV-cache
+ * form, decoder layer models/ConcatTransformer.py:187-214 + transformer_modules.py:22-97).
+ * bf16 weights [N][K] row-major, fp32 residual rows [R][C], bf16 activations.
+ * dec_gemm: out = A W^T + b (opt. ReLU) over N columns; column n goes to segment s = n / segw:
+ * row r -> d_s + r * rs_s + (n - s*segw) (bf16); pos_s selects A = a_pos, else a_plain. */
+int retr_dec_gemm(const void* a_plain, const void* a_pos, int R, int C, const void* w,
+                  const float* bias, int N, void* d0, long rs0, int pos0, void* d1, long rs1,
+                  int pos1, void* d2, long rs2, int pos2, int segw, int relu, void* stream);
+/* x = xin (+ b2 + sum_j slabs[j], in slab order); xout = x (optional); n = LN(x) (bf16),
+ * npos = LN(x) + pos (bf16, optional) */
+int retr_dec_rows(const float* xin, const float* slabs, int nslab, const float* b2, int R, int C,
+                  float* xout, const float* gamma, const float* beta, float eps, const float* pos,
+                  void* n, void* npos, void* stream);
+/* per query row: multi-head attention over Lk cache/memory rows ((anc ? anc[r][j] : r/kv_group)
+ * * Lmax + j; kpm [R/kv_group][Lk]), xo = x + o Wo^T + bo, then LN(xo) (+pos) -> q2 = (.) Wq^T
+ * + bq, or q2 = LN(xo) when wq is NULL */
+int retr_dec_attn_row(const void* q, const void* k, const void* v, int R, int C, int H, int Lk,
+                      int Lmax, int kv_group, const int* anc, const unsigned char* kpm,
+                      const float* x, const void* wo, const float* bo, float* xo,
+                      const float* gamma, const float* beta, float eps, const float* pos,
+                      const void* wq, const float* bq, void* q2, void* stream);
+/* FFN over hidden units [32 j, 32 j + 32): slabs[j] = relu(n3 W1_j^T + b1_j) W2[:, j]^T (fp32) */
+int retr_dec_ffn(const void* n3, int R, int C, const void* w1, const float* b1, const void* w2,
+                 int F, float* slabs, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

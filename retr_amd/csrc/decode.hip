@@ -1,0 +1,537 @@
+// Fused kernels of one incremental decode step (greedy / beam; eval_utils/decode.py:53-81 run as
+// the KV-cache form).  A decode step has R = B*K query rows (one per caption /
+// beam) of width C; each decoder layer (models/ConcatTransformer.py:187-214,
+// models/transformer_modules.py:22-97, pre-norm) runs as five launches instead of thirteen:
+//
+//   dec_gemm         [q | k | v] = (LN1(x) (+pos)) W_in^T + b_in, k/v appended to the cache
+//                    (also the head's first MLP layer)
+//   dec_attn_row     per row: self-attention over the cache (beam ancestry), out-proj, residual,
+//                    LN2 (+pos), cross-attention query projection
+//   dec_attn_row     per row: cross-attention over the image memory, out-proj, residual, LN3
+//   dec_ffn          FFN1 + ReLU + FFN2 split over the hidden units: partial slabs
+//   dec_rows         x = x + b2 + sum of the slabs (fixed order), then the next LN1 (+pos)
+//                    (the final decoder LN before the head)
+//
+// bf16 operands, fp32 accumulation and residual stream, exactly the roundings of the unfused
+// path (bf16 GEMM inputs, bf16 q/k/v/attention output, fp32 residual).  Every kernel is
+// latency-bound at R = 64: the point is fewer dependent launches per step.
+#include "common.hpp"
+#include "../../include/retr_hip.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+RETR_DEVICE f4 mfma16(const u32x4& a, const u32x4& b, f4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+}
+
+// ---- LayerNorm of one row by one wave: the arithmetic of ln_fwd_kernel (norm.hip) ----------
+template <int PER>
+RETR_DEVICE void ln_row_wave(const float (&v)[PER], const float* gamma, const float* beta,
+                             float eps, int C, int lane, float (&o)[PER]) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) s += v[i];
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    o[i] = (v[i] - mean) * rstd * gamma[c] + beta[c];
+  }
+}
+
+// ---- dec_gemm ---------------------------------------------------------------------------------
+// y = A W^T + b (opt. ReLU) over R rows, A bf16 [R][C] in global memory: segment s (output columns
+// [s*segw, (s+1)*segw)) reads A = a_pos if seg_pos[s] else a_plain, and writes its rows to
+// seg_base[s] + r * seg_rs[s] + (n - s*segw) (bf16).  Every operand fragment is loaded before the
+// first MFMA (the kernel is latency-bound at R = 64).
+struct Segs {
+  bf16* base[3];
+  long rs[3];
+  int pos[3];
+};
+
+template <int PER>
+__global__ void __launch_bounds__(256)
+dec_gemm_kernel(const bf16* a_plain, const bf16* a_pos, int R, const bf16* w, const float* bias,
+                int N, Segs segs, int segw, int relu) {
+  constexpr int C = PER * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 32, r0 = blockIdx.y * 64;
+  const int seg = n0 / segw;
+  const bf16* A = segs.pos[seg] ? a_pos : a_plain;
+  u32x4 bw[2][C / 32], af[C / 32];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + 16 * j + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < C / 32; ++ks)
+      bw[j][ks] = n < N ? *(const u32x4*)(w + (long)n * C + 32 * ks + 8 * (lane >> 4))
+                        : u32x4{0u, 0u, 0u, 0u};
+  }
+  const int ar = r0 + 16 * wave + (lane & 15);
+#pragma unroll
+  for (int ks = 0; ks < C / 32; ++ks)
+    af[ks] = ar < R ? *(const u32x4*)(A + (long)ar * C + 32 * ks + 8 * (lane >> 4))
+                    : u32x4{0u, 0u, 0u, 0u};
+  f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int ks = 0; ks < C / 32; ++ks) {
+    acc[0] = mfma16(af[ks], bw[0][ks], acc[0]);
+    acc[1] = mfma16(af[ks], bw[1][ks], acc[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + 16 * j + (lane & 15);
+    if (n >= N) continue;
+    const float b = bias ? bias[n] : 0.f;
+    bf16* dst = segs.base[seg] + (n - seg * segw);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = r0 + 16 * wave + 4 * (lane >> 4) + e;
+      if (r >= R) continue;
+      float v = acc[j][e] + b;
+      if (relu) v = fmaxf(v, 0.f);
+      dst[(long)r * segs.rs[seg]] = (bf16)v;
+    }
+  }
+}
+
+// ---- dec_rows: residual update + LayerNorm, one wave per row ----------------------------------
+// x = xin (+ b2 + sum_j slabs[j], slabs in order); xout = x (if given); n = LN(x) (bf16),
+// npos = LN(x) + pos (bf16, if given).  The LN arithmetic of ln_fwd_kernel (norm.hip).
+template <int PER>
+__global__ void __launch_bounds__(256)
+dec_rows_kernel(const float* xin, const float* slabs, int nslab, const float* b2, int R,
+                float* xout, const float* gamma, const float* beta, float eps, const float* pos,
+                bf16* n, bf16* npos) {
+  constexpr int C = PER * 64;
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const long RC = (long)R * C;
+  float v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) v[i] = xin[(long)r * C + lane + 64 * i];
+  if (slabs) {
+    float s[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) s[i] = 0.f;
+    constexpr int CHUNK = 16;                      // CHUNK x PER loads in flight
+    for (int j0 = 0; j0 < nslab; j0 += CHUNK) {
+      float t[CHUNK][PER];
+#pragma unroll
+      for (int u = 0; u < CHUNK; ++u)
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+          t[u][i] = j0 + u < nslab ? slabs[(long)(j0 + u) * RC + (long)r * C + lane + 64 * i] : 0.f;
+#pragma unroll
+      for (int u = 0; u < CHUNK; ++u)
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+          if (j0 + u < nslab) s[i] += t[u][i];
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) v[i] = v[i] + (s[i] + b2[lane + 64 * i]);
+  }
+  if (xout) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) xout[(long)r * C + lane + 64 * i] = v[i];
+  }
+  float o[PER];
+  ln_row_wave<PER>(v, gamma, beta, eps, C, lane, o);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    n[(long)r * C + c] = (bf16)o[i];
+    if (npos) npos[(long)r * C + c] = (bf16)(o[i] + pos[c]);
+  }
+}
+
+// ---- dec_attn_row ----------------------------------------------------------------------------
+// One block per query row r.  Multi-head attention of q[r] over Lk keys (self: cache rows
+// (anc ? anc[r][j] : r) * Lmax + j; cross: rows (r / kv_group) * Lmax + j, masked by kpm),
+// then xo = x + o W_o^T + b_o (fp32 row), then LN(xo) (+pos) -> either W_q2 (.) + b_q2 -> q2
+// (bf16) or, without W_q2, the LN output itself -> q2 (bf16).
+struct AttnRowArgs {
+  const bf16* q;            // [R][C]
+  const bf16* k;            // cache / memory rows [.][C]
+  const bf16* v;
+  int Lk, Lmax, kv_group;
+  const int* anc;           // [R][Lmax] beam ancestry or null
+  const unsigned char* kpm; // [R / kv_group][Lk] or null
+  const float* x;           // residual in [R][C]
+  const bf16* wo;           // [C][C]
+  const float* bo;
+  float* xo;                // residual out [R][C]
+  const float* gamma;
+  const float* beta;
+  float eps;
+  const float* pos;         // [C] or null
+  const bf16* wq;           // [C][C] or null
+  const float* bq;
+  bf16* q2;                 // [R][C]
+};
+
+// out[n] = sum_k W[n][k] a[k] for n in [0, C): each half-wave dots one weight row per step
+// (16-byte loads); U rows per half-wave are loaded before any is reduced (latency-bound at R=64)
+template <int C, int NT>
+RETR_DEVICE void gemv_rows(const bf16* W, const float* a, float* out, int tid) {
+  constexpr int HW = NT / 32;                    // half-waves
+  constexpr int CH = C / 8 / 32;                 // 16-byte chunks per lane per row
+  constexpr int RPH = C / HW;                    // rows per half-wave
+  constexpr int U = RPH < 8 ? RPH : 8;
+  const int hw = tid >> 5, hl = tid & 31;
+#pragma unroll
+  for (int r0 = 0; r0 < RPH; r0 += U) {
+    bf16x8 wv[U][CH];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int n = hw + HW * (r0 + u);
+#pragma unroll
+      for (int c = 0; c < CH; ++c) wv[u][c] = *(const bf16x8*)(W + (long)n * C + 8 * (hl + 32 * c));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int k0 = 8 * (hl + 32 * c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (float)wv[u][c][e] * a[k0 + e];
+      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (hl == 0) out[hw + HW * (r0 + u)] = s;
+    }
+  }
+}
+
+// gemv split in two: load the half-wave's rows (C = 256: all 16 rows of a 512-thread block at
+// once), then dot them
+template <int C, int NT>
+struct GemvFrag {
+  static constexpr int HW = NT / 32, CH = C / 8 / 32, RPH = C / HW;
+  bf16x8 wv[RPH][CH];
+  RETR_DEVICE void load(const bf16* W, int tid) {
+    const int hw = tid >> 5, hl = tid & 31;
+#pragma unroll
+    for (int u = 0; u < RPH; ++u)
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+        wv[u][c] = *(const bf16x8*)(W + (long)(hw + HW * u) * C + 8 * (hl + 32 * c));
+  }
+  RETR_DEVICE void dot(const float* a, float* out, int tid) const {
+    const int hw = tid >> 5, hl = tid & 31;
+#pragma unroll
+    for (int u = 0; u < RPH; ++u) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int k0 = 8 * (hl + 32 * c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (float)wv[u][c][e] * a[k0 + e];
+      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (hl == 0) out[hw + HW * u] = s;
+    }
+  }
+};
+
+template <int PER, int HD, int MK>
+__global__ void __launch_bounds__(512)
+dec_attn_row_kernel(AttnRowArgs a, float scale) {
+  constexpr int C = PER * 64, H = C / HD, NT = 512, NW = NT / 64;
+  constexpr int HPW = (H + NW - 1) / NW;         // heads per wave
+  __shared__ float qs[C];                        // scaled, rounded query
+  __shared__ float ob[C];                        // attention output (bf16-rounded) / LN output
+  __shared__ float yb[C];                        // GEMV result
+  __shared__ float pb[NW][64 * MK];              // probabilities of the wave's current head
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = blockIdx.x;
+  constexpr bool kPre = C == 256;                // out-proj rows prefetched during attention
+  GemvFrag<C, NT> wo;
+  if constexpr (kPre) wo.load(a.wo, tid);
+  for (int c = tid; c < C; c += NT) qs[c] = (float)(bf16)((float)a.q[(long)r * C + c] * scale);
+  const int kvb = r / a.kv_group;
+  const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
+  const unsigned char* km = a.kpm ? a.kpm + (long)kvb * a.Lk : nullptr;
+  const int Lk = a.Lk;
+  long krow[MK];                                 // cache / memory row of key lane + 64 m
+  bool kok[MK];
+#pragma unroll
+  for (int m = 0; m < MK; ++m) {
+    const int j = lane + 64 * m;
+    kok[m] = j < Lk && !(km && km[j]);
+    krow[m] = j < Lk ? (ar ? (long)ar[j] : (long)kvb) * a.Lmax + j : 0;
+  }
+  __syncthreads();
+  float* p = pb[wave];
+#pragma unroll
+  for (int hh = 0; hh < HPW; ++hh) {
+    const int h = wave * HPW + hh;
+    if (h >= H) break;
+    bf16x8 kv[MK][HD / 8];
+#pragma unroll
+    for (int m = 0; m < MK; ++m)
+#pragma unroll
+      for (int d0 = 0; d0 < HD / 8; ++d0)
+        kv[m][d0] = kok[m] ? *(const bf16x8*)(a.k + krow[m] * C + h * HD + 8 * d0) : bf16x8{};
+    // first 8 value rows of this lane's PV share, loaded before the scores are reduced
+    constexpr int NG = HD / 8, NPART = 64 / NG;
+    const int g = lane % NG, part = lane / NG;
+    bf16x8 vpre[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = part + NPART * u;
+      const long row = j < Lk ? (ar ? (long)ar[j] : (long)kvb) * a.Lmax + j : 0;
+      vpre[u] = j < Lk ? *(const bf16x8*)(a.v + row * C + h * HD + 8 * g) : bf16x8{};
+    }
+    float sc[MK];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int m = 0; m < MK; ++m) {
+      float s = -INFINITY;
+      if (kok[m]) {
+        s = 0.f;
+#pragma unroll
+        for (int d0 = 0; d0 < HD / 8; ++d0)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s += qs[h * HD + 8 * d0 + e] * (float)kv[m][d0][e];
+      }
+      sc[m] = s;
+      mx = fmaxf(mx, s);
+    }
+    mx = wave_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int m = 0; m < MK; ++m) {
+      const float e = (mx == -INFINITY || sc[m] == -INFINITY) ? 0.f : __expf(sc[m] - mx);
+      p[lane + 64 * m] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    const float inv = 1.f / sum;
+    // P V: lane = (dim group g of 8 dims, key part): keys j = part, part + NPART, ...
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j0 = part; j0 < Lk; j0 += NPART * 8) {
+      bf16x8 vv[8];
+      float pj[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + NPART * u;
+        const bool ok = j < Lk;
+        if (j0 == part) {
+          vv[u] = vpre[u];
+        } else {
+          const long row = ok ? (ar ? (long)ar[j] : (long)kvb) * a.Lmax + j : 0;
+          vv[u] = ok ? *(const bf16x8*)(a.v + row * C + h * HD + 8 * g) : bf16x8{};
+        }
+        pj[u] = ok ? p[j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += pj[u] * (float)vv[u][e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = NG; o < 64; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
+    if (part == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ob[h * HD + 8 * g + e] = (float)(bf16)(acc[e] * inv);
+    }
+  }
+  __syncthreads();
+  if constexpr (kPre) wo.dot(ob, yb, tid);
+  else gemv_rows<C, NT>(a.wo, ob, yb, tid);
+  GemvFrag<C, NT> wq;
+  if (kPre && a.wq) wq.load(a.wq, tid);           // in flight across the residual + LN
+  __syncthreads();
+  // residual (fp32) and the next LayerNorm, one wave (the ln_fwd_kernel arithmetic)
+  if (wave == 0) {
+    float v[PER], o[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = a.x[(long)r * C + c] + (yb[c] + a.bo[c]);
+      a.xo[(long)r * C + c] = v[i];
+    }
+    ln_row_wave<PER>(v, a.gamma, a.beta, a.eps, C, lane, o);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      const float t = (float)(bf16)(a.pos ? o[i] + a.pos[c] : o[i]);
+      if (a.wq) ob[c] = t;
+      else a.q2[(long)r * C + c] = (bf16)t;
+    }
+  }
+  if (!a.wq) return;
+  __syncthreads();
+  if constexpr (kPre) wq.dot(ob, yb, tid);
+  else gemv_rows<C, NT>(a.wq, ob, yb, tid);
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) a.q2[(long)r * C + c] = (bf16)(yb[c] + a.bq[c]);
+}
+
+// ---- dec_ffn: FFN1 + ReLU + FFN2 over hidden units [32 j, 32 j + 32) -> slab j -----------------
+template <int PER>
+__global__ void __launch_bounds__(256)
+dec_ffn_kernel(const bf16* n3, int R, const bf16* w1, const float* b1, const bf16* w2, int F,
+               float* slabs) {
+  constexpr int C = PER * 64;
+  constexpr int HS = 32 + 8;
+  __shared__ __attribute__((aligned(16))) bf16 Hs[64 * HS];     // relu(h) [64 rows][32 units]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j0 = blockIdx.x * 32, r0 = blockIdx.y * 64;
+  constexpr int NT = C / 16;                     // output column tiles of FFN2
+  // every fragment of both weight slices and of the wave's 16 input rows, before any MFMA
+  u32x4 w1f[2][C / 32], af[C / 32], w2f[NT];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ks = 0; ks < C / 32; ++ks)
+      w1f[t][ks] = *(const u32x4*)(w1 + (long)(j0 + 16 * t + (lane & 15)) * C + 32 * ks +
+                                   8 * (lane >> 4));
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    w2f[t] = *(const u32x4*)(w2 + (long)(16 * t + (lane & 15)) * F + j0 + 8 * (lane >> 4));
+  const int ar = r0 + 16 * wave + (lane & 15);
+#pragma unroll
+  for (int ks = 0; ks < C / 32; ++ks)
+    af[ks] = ar < R ? *(const u32x4*)(n3 + (long)ar * C + 32 * ks + 8 * (lane >> 4))
+                    : u32x4{0u, 0u, 0u, 0u};
+  f4 h[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int ks = 0; ks < C / 32; ++ks) {
+    h[0] = mfma16(af[ks], w1f[0][ks], h[0]);
+    h[1] = mfma16(af[ks], w1f[1][ks], h[1]);
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int jj = 16 * t + (lane & 15);
+    const float b = b1[j0 + jj];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      Hs[(16 * wave + 4 * (lane >> 4) + e) * HS + jj] = (bf16)fmaxf(h[t][e] + b, 0.f);
+  }
+  __syncthreads();
+  // partial[r][n] = sum_{jj < 32} H[r][jj] W2[n][j0 + jj]; wave = 16 rows x all C columns
+  const u32x4 a0 = *(const u32x4*)(Hs + (16 * wave + (lane & 15)) * HS + 8 * (lane >> 4));
+  float* slab = slabs + (long)blockIdx.x * R * C;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int n = 16 * t + (lane & 15);
+    const f4 acc = mfma16(a0, w2f[t], f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = r0 + 16 * wave + 4 * (lane >> 4) + e;
+      if (r < R) slab[(long)r * C + n] = acc[e];
+    }
+  }
+}
+
+template <typename K>
+void set_lds(K kern, size_t bytes) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+    done = true;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int retr_dec_gemm(const void* a_plain, const void* a_pos, int R, int C, const void* w,
+                  const float* bias, int N, void* d0, long rs0, int pos0, void* d1, long rs1,
+                  int pos1, void* d2, long rs2, int pos2, int segw, int relu, void* stream) {
+  RETR_REQUIRE(C == 256 || C == 512, "dec_gemm: C=%d (256 | 512)", C);
+  RETR_REQUIRE(segw % 32 == 0 && N <= 3 * segw && N % 32 == 0, "dec_gemm: N=%d segw=%d", N,
+               segw);
+  if (R == 0) return 0;
+  Segs s{{(bf16*)d0, (bf16*)d1, (bf16*)d2}, {rs0, rs1, rs2}, {pos0, pos1, pos2}};
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(N / 32, cdiv(R, 64));
+  if (C == 256)
+    hipLaunchKernelGGL(dec_gemm_kernel<4>, grid, dim3(256), 0, st, (const bf16*)a_plain,
+                       (const bf16*)a_pos, R, (const bf16*)w, bias, N, s, segw, relu);
+  else
+    hipLaunchKernelGGL(dec_gemm_kernel<8>, grid, dim3(256), 0, st, (const bf16*)a_plain,
+                       (const bf16*)a_pos, R, (const bf16*)w, bias, N, s, segw, relu);
+  return retr_check_launch("dec_gemm");
+}
+
+int retr_dec_rows(const float* xin, const float* slabs, int nslab, const float* b2, int R, int C,
+                  float* xout, const float* gamma, const float* beta, float eps, const float* pos,
+                  void* n, void* npos, void* stream) {
+  RETR_REQUIRE(C == 256 || C == 512, "dec_rows: C=%d (256 | 512)", C);
+  if (R == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (C == 256)
+    hipLaunchKernelGGL(dec_rows_kernel<4>, dim3(cdiv(R, 4)), dim3(256), 0, st, xin, slabs, nslab,
+                       b2, R, xout, gamma, beta, eps, pos, (bf16*)n, (bf16*)npos);
+  else
+    hipLaunchKernelGGL(dec_rows_kernel<8>, dim3(cdiv(R, 4)), dim3(256), 0, st, xin, slabs, nslab,
+                       b2, R, xout, gamma, beta, eps, pos, (bf16*)n, (bf16*)npos);
+  return retr_check_launch("dec_rows");
+}
+
+int retr_dec_attn_row(const void* q, const void* k, const void* v, int R, int C, int H, int Lk,
+                      int Lmax, int kv_group, const int* anc, const unsigned char* kpm,
+                      const float* x, const void* wo, const float* bo, float* xo,
+                      const float* gamma, const float* beta, float eps, const float* pos,
+                      const void* wq, const float* bq, void* q2, void* stream) {
+  const int hd = C / H;
+  RETR_REQUIRE((C == 256 || C == 512) && (hd == 32 || hd == 64) && H % 4 == 0,
+               "dec_attn_row: C=%d H=%d unsupported", C, H);
+  RETR_REQUIRE(Lk > 0 && Lk <= 512, "dec_attn_row: Lk=%d (1..512)", Lk);
+  if (R == 0) return 0;
+  AttnRowArgs a{(const bf16*)q, (const bf16*)k, (const bf16*)v, Lk, Lmax, kv_group, anc, kpm, x,
+                (const bf16*)wo, bo, xo, gamma, beta, eps, pos, (const bf16*)wq, bq, (bf16*)q2};
+  const float scale = 1.0f / sqrtf((float)hd);
+  hipStream_t st = (hipStream_t)stream;
+#define ATT(P, HDV, MKV) \
+  hipLaunchKernelGGL((dec_attn_row_kernel<P, HDV, MKV>), dim3(R), dim3(512), 0, st, a, scale)
+#define ATT_MK(P, HDV)                 \
+  if (Lk <= 128) ATT(P, HDV, 2);       \
+  else if (Lk <= 256) ATT(P, HDV, 4);  \
+  else ATT(P, HDV, 8);
+  if (C == 256 && hd == 32) { ATT_MK(4, 32) }
+  else if (C == 256) { ATT_MK(4, 64) }
+  else if (hd == 32) { ATT_MK(8, 32) }
+  else { ATT_MK(8, 64) }
+#undef ATT_MK
+#undef ATT
+  return retr_check_launch("dec_attn_row");
+}
+
+int retr_dec_ffn(const void* n3, int R, int C, const void* w1, const float* b1, const void* w2,
+                 int F, float* slabs, void* stream) {
+  RETR_REQUIRE((C == 256 || C == 512) && F % 32 == 0, "dec_ffn: C=%d F=%d", C, F);
+  if (R == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(F / 32, cdiv(R, 64));
+  if (C == 256)
+    hipLaunchKernelGGL(dec_ffn_kernel<4>, grid, dim3(256), 0, st, (const bf16*)n3, R,
+                       (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
+  else
+    hipLaunchKernelGGL(dec_ffn_kernel<8>, grid, dim3(256), 0, st, (const bf16*)n3, R,
+                       (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
+  return retr_check_launch("dec_ffn");
+}
+
+}  // extern "C"

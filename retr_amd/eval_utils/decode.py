@@ -69,6 +69,8 @@ class _DecodeState:
         self.mean = torch.empty(R, dtype=f32, device=dev)
         self.rstd = torch.empty_like(self.mean)
         self.ffh = torch.empty(R, F, dtype=cd, device=dev)
+        self.q2 = torch.empty_like(self.n)
+        self.slabs = torch.empty(F // 32, R, C, dtype=f32, device=dev)   # fused FFN partials
         self.h1 = torch.empty(R, 512, dtype=cd, device=dev)
         self.h2 = torch.empty(R, 512, dtype=cd, device=dev)
         self.Vp = (V + 63) // 64 * 64
@@ -98,11 +100,12 @@ class IncrementalGreedy:
     beam = False
     K = 1
 
-    def __init__(self, model, use_graphs=True):
+    def __init__(self, model, use_graphs=True, fused=True):
         self.model = model
         self.tr = model.transformer
         self.cdtype = model.cdtype
         self.use_graphs = use_graphs
+        self.fused = fused
         if not hasattr(model, "_retr_decode_states"):
             model._retr_decode_states = {}
         self.states = model._retr_decode_states
@@ -116,8 +119,19 @@ class IncrementalGreedy:
     def _signature(self):
         return tuple((p._version, p.data_ptr()) for p in self.model.parameters())
 
+    def _fusable(self, st):
+        layers = list(self.tr.decoder.layers)
+        C = st.n.shape[1]
+        H = layers[0].tgt_self_attn.sublayer.num_heads
+        F = layers[0].ff.sublayer[0].weight.shape[0]
+        return (self.fused and self.cdtype == torch.bfloat16 and C in (256, 512)
+                and C // H in (32, 64) and H % 4 == 0 and F % 32 == 0 and st.S <= 512
+                and st.T <= 512 and self.model.mlp.layers[0].weight.shape[0] % 32 == 0)
+
     def _step(self, st, i, eos_token):
         """Kernels of decode step i (reads token i, writes caption column i+1)."""
+        if self._fusable(st):
+            return self._step_fused(st, i, eos_token)
         model, tr, cd = self.model, self.tr, self.cdtype
         B, S, T, R = st.B, st.S, st.T, st.R
         C = st.n.shape[1]
@@ -172,6 +186,68 @@ class IncrementalGreedy:
                      st.head_bias, st.logits)
         self._select(st, i, V, eos_token, s)
 
+    def _step_fused(self, st, i, eos_token):
+        """Decode step i as five fused launches per decoder layer (csrc/decode.hip):
+        [q|k|v] GEMM (+cache append); self-attention + out-proj + residual + LN2 + cross query;
+        cross-attention + out-proj + residual + LN3; FFN split over hidden units; ordered slab
+        reduce + residual + the next LayerNorm."""
+        model, tr, cd = self.model, self.tr, self.cdtype
+        S, T, R = st.S, st.T, st.R
+        C = st.n.shape[1]
+        layers = list(tr.decoder.layers)
+        H = layers[0].tgt_self_attn.sublayer.num_heads
+        F = layers[0].ff.sublayer[0].weight.shape[0]
+        W = lambda p: ops.WEIGHTS.get(p, cd)        # noqa: E731
+        emb = tr.embeddings
+        qp = emb.position_embeddings.weight.detach()[i]
+        s = _st()
+        x, xa = st.y, st.y2
+        call("retr_embed_ln_fwd", ptr(st.tok), R, 1, C, ptr(emb.word_embeddings.weight), ptr(qp),
+             ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias), float(emb.LayerNorm.eps), 0.0, 0,
+             ptr(x), ptr(st.mean), ptr(st.rstd), s)
+        n0 = layers[0].tgt_self_attn.norm
+        call("retr_dec_rows", ptr(x), None, 0, None, R, C, None, ptr(n0.weight), ptr(n0.bias),
+             float(n0.eps), ptr(qp), ptr(st.n), ptr(st.npos), s)
+        anc = ptr(st.anc) if self.beam else None
+        nslab = F // 32
+        for li, layer in enumerate(layers):
+            sa, ca, ff = layer.tgt_self_attn, layer.tgt_src_cross_attn, layer.ff
+            sub, csub = sa.sublayer, ca.sublayer
+            kc, vc = st.kc[li], st.vc[li]
+            call("retr_dec_gemm", ptr(st.n), ptr(st.npos), R, C, ptr(W(sub.in_proj_weight)),
+                 ptr(sub.in_proj_bias), 3 * C, ptr(st.q), C, 1, ptr(kc) + 2 * i * C, T * C, 1,
+                 ptr(vc) + 2 * i * C, T * C, 0, C, 0, s)
+            call("retr_dec_attn_row", ptr(st.q), ptr(kc), ptr(vc), R, C, H, i + 1, T, 1, anc,
+                 None, ptr(x), ptr(W(sub.out_proj.weight)), ptr(sub.out_proj.bias), ptr(xa),
+                 ptr(ca.norm.weight), ptr(ca.norm.bias), float(ca.norm.eps), ptr(qp),
+                 ptr(W(csub.in_proj_weight)), ptr(csub.in_proj_bias), ptr(st.q2), s)
+            x, xa = xa, x
+            call("retr_dec_attn_row", ptr(st.q2), ptr(st.kx[li]), ptr(st.vx[li]), R, C, H, S, S,
+                 st.K, None, ptr(st.kpm), ptr(x), ptr(W(csub.out_proj.weight)),
+                 ptr(csub.out_proj.bias), ptr(xa), ptr(ff.norm.weight), ptr(ff.norm.bias),
+                 float(ff.norm.eps), None, None, None, ptr(st.o), s)
+            x, xa = xa, x
+            f0, f2 = ff.sublayer[0], ff.sublayer[2]
+            call("retr_dec_ffn", ptr(st.o), R, C, ptr(W(f0.weight)), ptr(f0.bias),
+                 ptr(W(f2.weight)), F, ptr(st.slabs), s)
+            # residual + FFN partials, then the next layer's LN1 (+pos) or the final LN
+            if li + 1 < len(layers):
+                nx, npos = layers[li + 1].tgt_self_attn.norm, ptr(st.npos)
+            else:
+                nx, npos = tr.decoder.norm, None
+            call("retr_dec_rows", ptr(x), ptr(st.slabs), nslab, ptr(f2.bias), R, C, ptr(xa),
+                 ptr(nx.weight), ptr(nx.bias), float(nx.eps), ptr(qp) if npos else None,
+                 ptr(st.n), npos, s)
+            x, xa = xa, x
+        l1, l2, l3 = model.mlp.layers
+        V = l3.weight.shape[0]
+        H1 = l1.weight.shape[0]
+        call("retr_dec_gemm", ptr(st.n), None, R, C, ptr(W(l1.weight)), ptr(l1.bias), H1,
+             ptr(st.h1), H1, 0, None, 0, 0, None, 0, 0, H1, 1, s)
+        k_linear_fwd(st.h1, W(l2.weight), l2.bias.detach(), st.h2, relu=1)
+        k_linear_fwd(st.h2, ops.WEIGHTS.get(l3.weight, cd, rows=st.Vp), st.head_bias, st.logits)
+        self._select(st, i, V, eos_token, s)
+
     def _select(self, st, i, V, eos_token, s):
         """Greedy: first-index argmax + the reference's finished/early-exit bookkeeping."""
         cd = self.cdtype
@@ -210,7 +286,7 @@ class IncrementalGreedy:
                                f"({qpos_w.shape[0]}) at non-singleton dimension 0")
         C = mem.shape[1]
         layers = list(tr.decoder.layers)
-        key = (type(self).__name__, self.K, B, S, T, cd, int(eos_token))
+        key = (type(self).__name__, self.K, B, S, T, cd, int(eos_token), bool(self.fused))
         st = self.states.get(key)
         if st is None:
             st = self._new_state(B, S, T, C, layers[0].ff.sublayer[0].weight.shape[0],
