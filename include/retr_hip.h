@@ -56,6 +56,13 @@ int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long 
                       long lddx, int dx_f32, int M, int N, int K, const void* addend,
                       int addend_f32, long lda, const void* gate, long ldg, int w_trans,
                       void* stream);
+/* dx = gate( dy W ) with the N-long reduction split into `splits` slices that write fp32 slabs
+ * ws[splits][M][K] (plain stores), added in slice order by a second kernel (deterministic): the
+ * MLP head's data gradient (N = 30528 vocabulary rows, M*K small) */
+int retr_linear_dgrad_splitk(int dtype, const void* dy, long lddy, const void* w, long ldw,
+                             void* dx, long lddx, int dx_f32, int M, int N, int K,
+                             const void* gate, long ldg, int w_trans, float* ws, int splits,
+                             void* stream);
 /* dw[N][K] (=|+=) dy^T x (fp32); db[N] (=|+=) column sums of dy (fused; db may be NULL).
  * accumulate = 0: dw/db are overwritten (no pre-zeroing needed); 1: added to.
  * N may be ragged when lddy covers N rounded up to the 16-byte vector (padded dy rows). */

@@ -455,7 +455,15 @@ __global__ void wgrad_unpack_kernel(const float* ws, const float* scale, float* 
     int co = (int)(t / Ci);
     const long src = ((long)co * KH * KW + kh * KW + kw) * Cp + ci;
     float v = ws[src];
-    for (int s = 1; s < splits; ++s) v += ws[src + s * slab];
+    int s = 1;
+    for (; s + 7 < splits; s += 8) {           // eight slab loads in flight, added in order
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = ws[src + (s + u) * slab];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += t[u];
+    }
+    for (; s < splits; ++s) v += ws[src + s * slab];
     if (scale) v *= scale[co];
     grad[i] = accumulate ? grad[i] + v : v;
   }

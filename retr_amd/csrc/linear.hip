@@ -53,6 +53,58 @@ int linear_dgrad_t(const void* dy, long lddy, const void* w, long ldw, void* dx,
   return launch_linear<kFamLinearDgrad, T>(la, lb, ep, M, K, N, st, "linear_dgrad");
 }
 
+// dx = gate(sum_s ws[s]) for a data-gradient GEMM split over its (long) reduction: slices wrote
+// fp32 slabs ws[s][M][K] with plain stores; added in slice order (deterministic)
+template <typename TO, typename TG>
+__global__ void dgrad_slab_reduce_kernel(const float* ws, int splits, int M, int K, const TG* gate,
+                                         long ldg, TO* dx, long lddx) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long MK = (long)M * K;
+  if (i >= MK) return;
+  const int m = (int)(i / K), k = (int)(i % K);
+  float t[16];
+  float v = 0.f;
+  for (int s0 = 0; s0 < splits; s0 += 16) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) t[u] = s0 + u < splits ? ws[(long)(s0 + u) * MK + i] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (s0 + u < splits) v += t[u];
+  }
+  if (gate && !(to_f(gate[(long)m * ldg + k]) > 0.f)) v = 0.f;
+  dx[(long)m * lddx + k] = from_f<TO>(v);
+}
+
+template <typename T, typename TO>
+int linear_dgrad_splitk_t(const void* dy, long lddy, const void* w, long ldw, void* dx, long lddx,
+                          int M, int N, int K, const void* gate, long ldg, int w_trans, float* ws,
+                          int splits, hipStream_t st) {
+  DenseK<T> la{(const T*)dy, lddy, M, N};
+  EpiAccF32 ep{ws, (long)K, 0, 0, 1, nullptr};
+  ep.split_stride = (long)M * K;
+  ep.set_vec();
+  // the launcher may round the slice count down to whole K-steps: slabs it does not write
+  // must not be read
+  constexpr int BK = Elem<T>::BK;
+  const int ksteps = cdiv(N, BK);
+  if (splits > ksteps) splits = ksteps;
+  splits = cdiv(N, cdiv(ksteps, splits) * BK);
+  int e;
+  if (w_trans) {
+    DenseK<T> lb{(const T*)w, ldw, K, N};
+    if constexpr (sizeof(T) == 2) e = launch_big<kFamLinearDgrad>(la, lb, ep, M, K, N, splits, st, "linear_dgrad_splitk");
+    else e = launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, ep, M, K, N, splits, st, "linear_dgrad_splitk");
+  } else {
+    DenseT<T> lb{(const T*)w, ldw, K, N};
+    if constexpr (sizeof(T) == 2) e = launch_big<kFamLinearDgrad>(la, lb, ep, M, K, N, splits, st, "linear_dgrad_splitk");
+    else e = launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, ep, M, K, N, splits, st, "linear_dgrad_splitk");
+  }
+  if (e) return e;
+  hipLaunchKernelGGL((dgrad_slab_reduce_kernel<TO, T>), dim3(cdiv((long)M * K, 256)), dim3(256), 0,
+                     st, ws, splits, M, K, (const T*)gate, ldg, (TO*)dx, lddx);
+  return retr_check_launch("linear_dgrad_splitk reduce");
+}
+
 // zero an fp32 [rows][cols] region with row stride ld (stream-ordered, graph-capturable)
 int zero_f32(float* p, long ld, int rows, int cols, hipStream_t st) {
   hipError_t e = (ld == cols) ? hipMemsetAsync(p, 0, sizeof(float) * (size_t)rows * cols, st)
@@ -172,6 +224,25 @@ int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long 
                "linear_dgrad: N/K/ld must be %%4");
   return linear_dgrad_t<float, float, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda,
                                              gate, ldg, w_trans, st);
+}
+
+int retr_linear_dgrad_splitk(int dtype, const void* dy, long lddy, const void* w, long ldw,
+                             void* dx, long lddx, int dx_f32, int M, int N, int K,
+                             const void* gate, long ldg, int w_trans, float* ws, int splits,
+                             void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (M == 0) return 0;
+  RETR_REQUIRE(splits >= 1 && ws != nullptr, "linear_dgrad_splitk: splits=%d", splits);
+  if (dtype == RETR_BF16) {
+    RETR_REQUIRE(N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0 && ldw % 8 == 0,
+                 "linear_dgrad_splitk: N/K/ld must be %%8");
+    return dx_f32 ? linear_dgrad_splitk_t<bf16, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, gate, ldg, w_trans, ws, splits, st)
+                  : linear_dgrad_splitk_t<bf16, bf16>(dy, lddy, w, ldw, dx, lddx, M, N, K, gate, ldg, w_trans, ws, splits, st);
+  }
+  RETR_REQUIRE(N % 4 == 0 && K % 4 == 0 && lddy % 4 == 0 && ldw % 4 == 0,
+               "linear_dgrad_splitk: N/K/ld must be %%4");
+  return linear_dgrad_splitk_t<float, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, gate, ldg,
+                                             w_trans, ws, splits, st);
 }
 
 int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long ldx, float* dw,

@@ -56,30 +56,59 @@ ln_bwd_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, co
   for (int i = 0; i < PER; ++i) pg[i] = pb[i] = 0.f;
   int r0 = blockIdx.x * rows_per_block;
   int r1 = min(M, r0 + rows_per_block);
-  for (int row = r0 + wave; row < r1; row += 4) {
-    float mu = mean[row], rs = rstd[row];
-    float g[PER], xh[PER];
-    float s1 = 0.f, s2 = 0.f;
+  // the wave's rows in batches of RB: every load of a batch is issued before the first
+  // reduction, and the batch's independent shuffle chains interleave (latency-bound otherwise)
+  constexpr int RB = 4;
+  for (int rb = r0 + wave; rb < r1; rb += 4 * RB) {
+    float d[RB][PER], xv[RB][PER], ad[RB][PER], mu[RB], rs[RB];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      int c = lane + 64 * i;
-      float d = dy ? to_f(dy[(long)row * lddy + c]) : 0.f;
-      if (dy2) d += to_f(dy2[(long)row * lddy + c]);
-      xh[i] = (x[(long)row * ldx + c] - mu) * rs;
-      pg[i] += d * xh[i];
-      pb[i] += d;
-      g[i] = d * gamma[c];
-      s1 += g[i];
-      s2 += g[i] * xh[i];
+    for (int u = 0; u < RB; ++u) {
+      const int row = rb + 4 * u;
+      const bool ok = row < r1;
+      mu[u] = ok ? mean[row] : 0.f;
+      rs[u] = ok ? rstd[row] : 0.f;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int c = lane + 64 * i;
+        float t = (ok && dy) ? to_f(dy[(long)row * lddy + c]) : 0.f;
+        if (ok && dy2) t += to_f(dy2[(long)row * lddy + c]);
+        d[u][i] = t;
+        xv[u][i] = ok ? x[(long)row * ldx + c] : 0.f;
+        ad[u][i] = (ok && addend) ? addend[(long)row * ldx + c] : 0.f;
+      }
     }
-    s1 = wave_sum(s1) / C;
-    s2 = wave_sum(s2) / C;
+    float s1[RB], s2[RB], g[RB][PER], xh[RB][PER];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      int c = lane + 64 * i;
-      float o = rs * (g[i] - s1 - xh[i] * s2);
-      if (addend) o += addend[(long)row * ldx + c];
-      dx[(long)row * lddx + c] = o;
+    for (int u = 0; u < RB; ++u) {
+      s1[u] = 0.f;
+      s2[u] = 0.f;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int c = lane + 64 * i;
+        xh[u][i] = (xv[u][i] - mu[u]) * rs[u];
+        pg[i] += d[u][i] * xh[u][i];
+        pb[i] += d[u][i];
+        g[u][i] = d[u][i] * gamma[c];
+        s1[u] += g[u][i];
+        s2[u] += g[u][i] * xh[u][i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      s1[u] = wave_sum(s1[u]) / C;
+      s2[u] = wave_sum(s2[u]) / C;
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int row = rb + 4 * u;
+      if (row >= r1) continue;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int c = lane + 64 * i;
+        float o = rs[u] * (g[u][i] - s1[u] - xh[u][i] * s2[u]);
+        if (addend) o += ad[u][i];
+        dx[(long)row * lddx + c] = o;
+      }
     }
   }
   if (!part) return;
@@ -98,17 +127,37 @@ ln_bwd_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, co
   }
 }
 
-// dgamma[c] += sum_b part[b][0][c];  dbeta[c] += sum_b part[b][1][c]  (blocks in order)
-__global__ void ln_param_reduce_kernel(const float* part, int nblk, int C, float* dgamma,
-                                       float* dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * C) return;
+// dgamma[c] += sum_b part[b][0][c];  dbeta[c] += sum_b part[b][1][c].  Fixed-order two-level sum
+// (deterministic): one 1024-thread block per 64 of the 2C columns; wave w adds partial rows
+// b = w, w + 16, ... (eight loads in flight per lane), then the 16 wave sums are added in wave
+// order.  (A single thread per column walking all M/16 partials was latency-bound: ~55 us.)
+__global__ void __launch_bounds__(1024)
+ln_param_reduce_kernel(const float* part, int nblk, int C, float* dgamma, float* dbeta) {
+  __shared__ float red[16][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(long)b * 2 * C + c];
+  if (c < 2 * C) {
+    int b = wave;
+    for (; b + 16 * 7 < nblk; b += 16 * 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(long)(b + 16 * u) * 2 * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < nblk; b += 16) s += part[(long)b * 2 * C + c];
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave != 0 || c >= 2 * C) return;
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) t += red[w][lane];
   if (c < C) {
-    if (dgamma) dgamma[c] += s;
+    if (dgamma) dgamma[c] += t;
   } else if (dbeta) {
-    dbeta[c - C] += s;
+    dbeta[c - C] += t;
   }
 }
 
@@ -343,7 +392,7 @@ int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, co
 #undef LNB
   if (int e = retr_check_launch("layernorm_bwd")) return e;
   if (!part) return 0;
-  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, st, part,
+  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(2 * C, 64)), dim3(1024), 0, st, part,
                      (int)grid.x, C, dgamma, dbeta);
   return retr_check_launch("layernorm_param_reduce");
 }
@@ -406,7 +455,7 @@ int retr_embed_ln_bwd(const long long* tokens, int B, int T, int C, const float*
     if (int e = retr_check_launch("embed_pos_reduce")) return e;
   }
   if (dgamma || dbeta) {
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(2 * C, 256)), dim3(256), 0, st, part,
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(2 * C, 64)), dim3(1024), 0, st, part,
                        nblk, C, dgamma, dbeta);
     if (int e = retr_check_launch("embed_param_reduce")) return e;
   }

@@ -16,6 +16,8 @@ reference computes as separate PyTorch ops:
 Tensors of the residual stream are fp32; GEMM operands are the compute dtype (bf16 or fp32).
 All ops raise on non-HIP tensors (no CPU fallback).
 """
+import os
+
 import torch
 
 from . import _lib
@@ -145,7 +147,11 @@ class _WeightCache:
 
     def get_t(self, p, dtype, rows=None):
         """W^T [K][rows] (compute dtype) of a [N][K...] parameter, rows >= N zero-padded: the
-        K-contiguous B operand of the data-gradient GEMM dX = dY W."""
+        B operand of the data-gradient GEMM dX = dY W.  By default a view of the row-major
+        copy (``get``) that the GEMM reads transposed through LDS (no per-step transpose
+        kernels); with DGRAD_TRANSPOSED_COPIES a materialised K-contiguous transpose."""
+        if not DGRAD_TRANSPOSED_COPIES:
+            return _TView(self.get(p, dtype, rows).reshape(rows or p.shape[0], -1))
         n = p.shape[0]
         rows = rows or n
         key = ("T", dtype, rows)
@@ -165,6 +171,28 @@ class _WeightCache:
 
 
 WEIGHTS = _WeightCache()
+
+# dgrad B operand: False (default) = the row-major weight copy read transposed in LDS
+# (ds_read_b64_tr_b16), True = a K-contiguous transposed copy per weight version (one
+# transpose_cast launch per weight and step); env RETR_DGRAD_TRANSPOSED=1 for A/B runs
+DGRAD_TRANSPOSED_COPIES = os.environ.get("RETR_DGRAD_TRANSPOSED", "0") == "1"
+
+
+class _TView:
+    """W^T of a row-major [N][K] weight copy without materialising it: ``shape`` is (K, N) and
+    ``[:, a:b]`` selects rows a:b of W (the in-projection's q/k/v blocks)."""
+
+    def __init__(self, w):
+        self.w = w
+
+    @property
+    def shape(self):
+        return (self.w.shape[1], self.w.shape[0])
+
+    def __getitem__(self, idx):
+        rows, cols = idx
+        assert rows == slice(None)
+        return _TView(self.w[cols])
 
 
 def _pad_vec(v, n):
@@ -194,14 +222,29 @@ def k_linear_fwd(x, w, bias, y, relu=0, res=None, drop_p=0.0, seed=0):
 
 
 def k_linear_dgrad(dy, wt, dx, addend=None, gate=None):
-    """dx = gate(dy W [+ addend]) with ``wt`` = W^T [K][N] (see _WeightCache.get_t)."""
+    """dx = gate(dy W [+ addend]) with ``wt`` = W^T [K][N] (see _WeightCache.get_t): a
+    materialised transpose, or a _TView of the row-major W [N][K]."""
     M = dy.shape[0]
     K, N = wt.shape
-    call("retr_linear_dgrad", dcode(dy.dtype), ptr(dy), dy.stride(0), ptr(wt), wt.stride(0),
+    if isinstance(wt, _TView):
+        w, w_trans = wt.w, 0
+    else:
+        w, w_trans = wt, 1
+    if addend is None and N >= 8192 and M * K <= (1 << 21):
+        # long reduction, few output tiles (the MLP head's vocabulary): split it 8 ways into
+        # fp32 slabs added in order by a second kernel
+        splits = 8
+        ws = torch.empty(splits, M, K, dtype=torch.float32, device=dy.device)
+        call("retr_linear_dgrad_splitk", dcode(dy.dtype), ptr(dy), dy.stride(0), ptr(w),
+             w.stride(0), ptr(dx), dx.stride(0), int(dx.dtype == torch.float32), M, N, K,
+             ptr(gate), gate.stride(0) if gate is not None else 0, w_trans, ptr(ws), splits,
+             _st())
+        return
+    call("retr_linear_dgrad", dcode(dy.dtype), ptr(dy), dy.stride(0), ptr(w), w.stride(0),
          ptr(dx), dx.stride(0), int(dx.dtype == torch.float32), M, N, K, ptr(addend),
          int(addend is not None and addend.dtype == torch.float32),
          addend.stride(0) if addend is not None else 0, ptr(gate),
-         gate.stride(0) if gate is not None else 0, 1, _st())
+         gate.stride(0) if gate is not None else 0, w_trans, _st())
 
 
 def k_linear_wgrad(dy, x, dw, db=None, accumulate=False):

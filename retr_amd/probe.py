@@ -42,7 +42,7 @@ def flops_of(name, a):
     if name in ("retr_linear_fwd",):
         m, n, k = a[9], a[10], a[11]
         return "linear_fwd", 2.0 * m * n * k
-    if name == "retr_linear_dgrad":
+    if name in ("retr_linear_dgrad", "retr_linear_dgrad_splitk"):
         m, n, k = a[8], a[9], a[10]
         return "linear_dgrad", 2.0 * m * n * k
     if name == "retr_linear_wgrad":
@@ -69,6 +69,8 @@ def shape_of(name, a):
         return f"M{a[9]} N{a[10]} K{a[11]} relu{a[12]} res{int(bool(a[13]))}"
     if name == "retr_linear_dgrad":
         return f"M{a[8]} N{a[9]} K{a[10]} add{int(bool(a[11]))} gate{int(bool(a[14]))}"
+    if name == "retr_linear_dgrad_splitk":
+        return f"M{a[8]} N{a[9]} K{a[10]} gate{int(bool(a[11]))} split{a[15]}"
     if name == "retr_linear_wgrad":
         return f"M{a[7]} N{a[8]} K{a[9]} db{int(bool(a[10]))} acc{a[11]}"
     if name == "retr_attention_fwd":
@@ -79,13 +81,14 @@ def shape_of(name, a):
 
 
 TRACKED = ("retr_conv2d_fwd", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
-           "retr_linear_dgrad", "retr_linear_wgrad", "retr_attention_fwd", "retr_attention_bwd")
+           "retr_linear_dgrad", "retr_linear_dgrad_splitk", "retr_linear_wgrad",
+           "retr_attention_fwd", "retr_attention_bwd")
 
 
-FAMILY_SYMBOL = {"linear_fwd": "gemm_kernel<0,", "linear_dgrad": "gemm_kernel<1,",
-                 "linear_wgrad": "gemm_kernel<2,", "conv_fwd": "gemm_kernel<3,",
-                 "conv_dgrad": "gemm_kernel<4,", "conv_wgrad": "gemm_kernel<5,",
-                 "attention_fwd": "attn_fwd_kernel",
+FAMILY_SYMBOL = {"linear_fwd": "gemm{,2}_kernel<0,", "linear_dgrad": "gemm{,2}_kernel<1,",
+                 "linear_wgrad": "gemm{,2}_kernel<2,", "conv_fwd": "gemm{,2}_kernel<3,",
+                 "conv_dgrad": "gemm{,2}_kernel<4,", "conv_wgrad": "gemm{,2}_kernel<5,",
+                 "attention_fwd": "attn_fwd{,2}_kernel",
                  "attention_bwd": "attn_bwd_"}
 
 
@@ -93,11 +96,11 @@ def family_of_symbol(name):
     """Family key of a rocprof kernel name (mangled ``_ZN4retr11gemm_kernelILi3E...`` or
     demangled ``retr::gemm_kernel<3, ...>``), or None."""
     import re
-    m = re.search(r"gemm_kernelILi(\d+)E", name) or re.search(r"gemm_kernel<(\d+),", name)
+    m = re.search(r"gemm2?_kernelILi(\d+)E", name) or re.search(r"gemm2?_kernel<(\d+),", name)
     if m:
         return ("linear_fwd", "linear_dgrad", "linear_wgrad", "conv_fwd", "conv_dgrad",
                 "conv_wgrad")[int(m.group(1))]
-    if "attn_fwd_kernel" in name:
+    if re.search(r"attn_fwd\d*_kernel", name):
         return "attention_fwd"
     if "attn_bwd_" in name:
         return "attention_bwd"

@@ -396,3 +396,23 @@ def test_attention_fully_masked_rows_nan():
     lse = torch.empty(B * H * L, device=DEV)
     ops.k_attention_fwd(q, q, q, o, B, H, L, L, hd, kpm, False, 0.0, 0, lse)
     assert torch.isfinite(o[:L].float()).all() and torch.isnan(o[L:].float()).all()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("view", [True, False])
+def test_linear_dgrad_split_reduction(dtype, tol, view):
+    """dx = gate(dy W) with the vocabulary-long reduction split into ordered fp32 slabs (the MLP
+    head's data gradient), W given row-major (read transposed) or as a materialised W^T."""
+    M, N, K = 300, 30528, 512
+    g = torch.Generator(device="cpu").manual_seed(9)
+    dy = torch.randn(M, N, generator=g).to(DEV).to(dtype)
+    w = (torch.randn(N, K, generator=g) / 100).to(DEV).to(dtype)
+    gate = torch.randn(M, K, generator=g).to(DEV).to(dtype)
+    dx = torch.empty(M, K, dtype=dtype, device=DEV)
+    wt = ops._TView(w) if view else w.t().contiguous()
+    ops.k_linear_dgrad(dy, wt, dx, gate=gate)
+    ref = (dy.float() @ w.float()) * (gate.float() > 0)
+    assert rel_err(dx.float(), ref) < tol
+    dx2 = torch.empty_like(dx)
+    ops.k_linear_dgrad(dy, wt, dx2, gate=gate)
+    assert torch.equal(dx, dx2)                      # slabs added in order: deterministic
