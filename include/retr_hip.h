@@ -213,10 +213,11 @@ int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, f
  *   n % 4 == 0, all arrays 16-byte aligned. */
 int retr_adamw_sumsq(const float* grad, long n, float* partials, int nparts, float* step,
                      void* stream);
+/* param_bf16 (optional): bf16 copy of the updated parameters (the GEMM weight shadow) */
 int retr_adamw_update(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n,
                       const float* hyper, double beta1, double beta2, float eps,
                       const float* step, float step_offset, const float* partials, int nparts,
-                      float max_norm, void* stream);
+                      float max_norm, void* param_bf16, void* stream);
 
 /* ---- fused incremental-decode step (csrc/decode.hip; eval_utils/decode.py:53-81 in KV-cache
  * form, decoder layer models/ConcatTransformer.py:187-214 + transformer_modules.py:22-97).

@@ -113,20 +113,24 @@ class GraphedTrainStep:
                                 s_caps, s_cm, self.optimizer)
 
     def _capture(self):
+        # thread-local capture: other threads' HIP calls stay legal meanwhile (the RCCL
+        # process-group watchdog polls its work events from its own thread)
+        mode = "thread_local"
         self.graph = torch.cuda.CUDAGraph()
         if self.grad_sync is None:
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=mode):
                 self.loss = self._step().detach()
             return
         gs = self.grad_sync
         defer = gs.defer
         gs.defer = True                      # hooks only route gradients while capturing
         try:
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, capture_error_mode=mode):
                 self.loss = self._fb().detach()
             gs.synchronize()                 # eager: p.grad -> bucket views for the 2nd graph
             self.graph_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_opt, pool=self.graph.pool()):
+            with torch.cuda.graph(self.graph_opt, pool=self.graph.pool(),
+                                  capture_error_mode=mode):
                 clip_and_step(self.model, self.optimizer, self.max_norm)
         finally:
             gs.defer = defer
@@ -178,6 +182,9 @@ class GraphedTrainStep:
         for p in self._params():
             if p.requires_grad:
                 inc(p)
+        if hasattr(self.optimizer, "mark_shadow_fresh") and self._active:
+            # the captured update rewrote the bf16 shadow of every parameter it stepped
+            self.optimizer.mark_shadow_fresh(self._active)
 
     def __call__(self, samples, caps, cap_masks):
         nt = samples[0]

@@ -130,6 +130,16 @@ class _WeightCache:
         rows = rows or p.shape[0]
         if dtype == torch.float32 and rows == p.shape[0] and p.is_contiguous():
             return p.detach()
+        sh = getattr(p, "_retr_shadow", None)
+        if sh is not None and dtype == torch.bfloat16 and rows == p.shape[0]:
+            # FusedAdamW's bf16 parameter shadow (written by its update kernel): cast into it
+            # only when the parameter changed some other way
+            ver = (p._version, p.data_ptr())
+            if getattr(p, "_retr_shadow_ver", None) != ver:
+                src = p.detach().contiguous()
+                call("retr_cast", dcode(dtype), ptr(src), ptr(sh), src.numel(), _st())
+                p._retr_shadow_ver = ver
+            return sh
         key = (dtype, rows)
         ent = getattr(p, self.ATTR, None)   # cache lives on the parameter object itself
         ver = (p._version, p.data_ptr())

@@ -79,13 +79,14 @@ def grad_buffer(p, shape=None):
 
 class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
-                 amsgrad=False, maximize=False, **unused):
+                 amsgrad=False, maximize=False, bf16_shadow=True, **unused):
         if amsgrad or maximize:
             raise NotImplementedError("FusedAdamW: amsgrad / maximize are not supported")
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False,
                         maximize=False, foreach=None, capturable=True, differentiable=False,
                         fused=None)
         super().__init__(params, defaults)
+        self._shadow = bool(bf16_shadow)
         self._build()
 
     # -- arena construction ----------------------------------------------------------------
@@ -113,6 +114,9 @@ class FusedAdamW(torch.optim.Optimizer):
         self.G = torch.zeros_like(self.P)
         self.M = torch.zeros_like(self.P)
         self.V = torch.zeros_like(self.P)
+        # bf16 shadow of P, rewritten by every update: the compute-dtype weight copies the GEMMs
+        # read (ops._WeightCache hands out p._retr_shadow while it is current)
+        self.P16 = torch.empty(total, dtype=torch.bfloat16, device=dev) if self._shadow else None
         self.arena = _GradArena(self.G)
         self._step_t = torch.zeros(1, dtype=torch.float32, device=dev)   # device step count
         self._global = 0                                  # host mirror of _step_t
@@ -129,9 +133,27 @@ class FusedAdamW(torch.optim.Optimizer):
                 p.data = view
                 p._retr_grad_view = self.G[o:o + n].view_as(p)
                 p._retr_arena = self.arena
+                if self.P16 is not None:
+                    p._retr_shadow = self.P16[o:o + n].view_as(p)
                 self.state[p] = {"exp_avg": self.M[o:o + n].view_as(p),
                                  "exp_avg_sq": self.V[o:o + n].view_as(p)}
         self.sync_hyper()
+        self.sync_shadow()
+
+    def sync_shadow(self):
+        """Re-cast the whole bf16 shadow from P (after P was written outside step())."""
+        if self.P16 is None:
+            return
+        call("retr_cast", 1, ptr(self.P), ptr(self.P16), self.P.numel(), stream())
+        self.mark_shadow_fresh([p for g in self.param_groups for p in g["params"]])
+
+    def mark_shadow_fresh(self, params):
+        """Record that the shadow of ``params`` holds their current values (their autograd
+        version as of now): ops._WeightCache then serves it without a cast."""
+        if self.P16 is None:
+            return
+        for p in params:
+            p._retr_shadow_ver = (p._version, p.data_ptr())
 
     def sync_hyper(self):
         """Copy (lr, weight_decay) of every group to the device if they changed."""
@@ -229,13 +251,15 @@ class FusedAdamW(torch.optim.Optimizer):
             call("retr_adamw_update", ptr(self.P) + 4 * lo, ptr(self.G) + 4 * lo,
                  ptr(self.M) + 4 * lo, ptr(self.V) + 4 * lo, hi - lo, ptr(self._hyper) + 8 * gi,
                  float(b1), float(b2), float(eps), ptr(self._step_t), float(off),
-                 ptr(self._partials), nparts, float(max_norm) if clip else 0.0, st)
+                 ptr(self._partials), nparts, float(max_norm) if clip else 0.0,
+                 ptr(self.P16) + 2 * lo if self.P16 is not None else None, st)
         self._advance_host(active)
         self._last_active = active
         for p in foreign:          # clipped values back into gradients living elsewhere
             if clip:
                 p.grad.copy_(p._retr_grad_view)
         _bump_versions(self.param_groups)
+        self.mark_shadow_fresh(active)     # the update wrote their shadow too
         return loss
 
     def _advance_host(self, active):
@@ -260,6 +284,7 @@ class FusedAdamW(torch.optim.Optimizer):
             self._step_t.copy_(t)
         self._global = g
         self._counts = dict(counts)
+        self.sync_shadow()
 
     def state_dict(self):
         """torch.optim.AdamW layout: per-parameter 'step' (CPU float tensor) + moments."""
