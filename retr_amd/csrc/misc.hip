@@ -21,6 +21,57 @@ __global__ void nchw_to_nhwc_kernel(const float* x, T* y, int N, int C, int H, i
   }
 }
 
+// bf16, Cp == 8: one thread per pixel reads its C (<= 8) channel planes (coalesced along w) and
+// writes the pixel's 16-byte chunk
+__global__ void nchw_to_nhwc8_kernel(const float* x, bf16* y, int N, int C, int H, int W) {
+  const long HW = (long)H * W, total = (long)N * HW;
+  for (long pix = blockIdx.x * (long)blockDim.x + threadIdx.x; pix < total;
+       pix += (long)gridDim.x * blockDim.x) {
+    const long n = pix / HW, hw = pix - n * HW;
+    bf16x8 o;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o[c] = (bf16)(c < C ? x[(n * C + c) * HW + hw] : 0.f);
+    *(bf16x8*)(y + pix * 8) = o;
+  }
+}
+
+// bf16 MaxPool2d(3, 2, 1) NHWC, C % 8 == 0: one thread per (output pixel, 8 channels), 16-byte
+// loads of the 3x3 window and one 16-byte store
+__global__ void maxpool8_kernel(const bf16* x, bf16* y, int N, int H, int W, int C, int OH,
+                                int OW) {
+  const int C8 = C / 8;
+  const long total = (long)N * OH * OW * C8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    const long pix = i / C8;
+    const int ow = (int)(pix % OW);
+    const long t = pix / OW;
+    const int oh = (int)(t % OH);
+    const int n = (int)(t / OH);
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = oh * 2 - 1 + kh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = ow * 2 - 1 + kw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const bf16x8 v = *(const bf16x8*)(x + (((long)n * H + ih) * W + iw) * C + 8 * c8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)v[e]);
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)m[e];
+    *(bf16x8*)(y + pix * C + 8 * c8) = o;
+  }
+}
+
 // MaxPool2d(kernel 3, stride 2, padding 1) NHWC; padding acts as -inf.
 template <typename T>
 __global__ void maxpool_kernel(const T* x, T* y, int N, int H, int W, int C, int OH, int OW) {
@@ -108,7 +159,12 @@ int retr_nchw_to_nhwc(int dtype, const float* x, void* y, int N, int C, int H, i
   if (total == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == RETR_BF16)
-    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, x, (bf16*)y, N, C, H, W, Cp);
+    if (Cp == 8) {
+      const long pixels = (long)N * H * W;
+      hipLaunchKernelGGL(nchw_to_nhwc8_kernel, dim3(grid_for(pixels)), dim3(256), 0, st, x, (bf16*)y, N, C, H, W);
+    } else {
+      hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, x, (bf16*)y, N, C, H, W, Cp);
+    }
   else
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x, (float*)y, N, C, H, W, Cp);
   return retr_check_launch("nchw_to_nhwc");
@@ -120,7 +176,10 @@ int retr_maxpool3x3s2(int dtype, const void* x, void* y, int N, int H, int W, in
   if (total == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == RETR_BF16)
-    hipLaunchKernelGGL(maxpool_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, N, H, W, C, OH, OW);
+    if (C % 8 == 0)
+      hipLaunchKernelGGL(maxpool8_kernel, dim3(grid_for(total / 8)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, N, H, W, C, OH, OW);
+    else
+      hipLaunchKernelGGL(maxpool_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, N, H, W, C, OH, OW);
   else
     hipLaunchKernelGGL(maxpool_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)x, (float*)y, N, H, W, C, OH, OW);
   return retr_check_launch("maxpool3x3s2");

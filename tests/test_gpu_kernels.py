@@ -416,3 +416,24 @@ def test_linear_dgrad_split_reduction(dtype, tol, view):
     dx2 = torch.empty_like(dx)
     ops.k_linear_dgrad(dy, wt, dx2, gate=gate)
     assert torch.equal(dx, dx2)                      # slabs added in order: deterministic
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_stem_layout_and_maxpool(dtype):
+    """NCHW fp32 image -> NHWC (channels zero-padded to 8) and MaxPool2d(3, 2, 1) on NHWC
+    (torchvision's stem, models/backbone.py:65-69) against torch."""
+    g = torch.Generator(device="cpu").manual_seed(4)
+    N, C, H, W = 3, 3, 37, 42
+    x = torch.randn(N, C, H, W, generator=g).to(DEV)
+    y = torch.empty(N, H, W, 8, dtype=dtype, device=DEV)
+    call("retr_nchw_to_nhwc", ops.dcode(dtype), ptr(x), ptr(y), N, C, H, W, 8, ops._st())
+    ref = torch.zeros(N, H, W, 8, device=DEV)
+    ref[..., :C] = x.permute(0, 2, 3, 1)
+    assert torch.equal(y.float(), ref.to(dtype).float())
+    Cm, Hm, Wm = 64, 33, 40
+    xm = torch.randn(N, Hm, Wm, Cm, generator=g).to(DEV).to(dtype)
+    OH, OW = (Hm - 1) // 2 + 1, (Wm - 1) // 2 + 1
+    ym = torch.empty(N, OH, OW, Cm, dtype=dtype, device=DEV)
+    call("retr_maxpool3x3s2", ops.dcode(dtype), ptr(xm), ptr(ym), N, Hm, Wm, Cm, OH, OW, ops._st())
+    refm = F.max_pool2d(xm.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.equal(ym.float(), refm)
