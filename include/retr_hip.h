@@ -71,6 +71,60 @@ int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long 
 /* db[N] += column sums of dy[M][N] */
 int retr_bias_grad(int dtype, const void* dy, long lddy, int M, int N, float* db, void* stream);
 
+/* Launch-configuration overrides for on-GPU tuning sweeps (tools/group_micro.py); value 0 =
+ * the built-in choice.  Returns the previous value (-1: unknown knob). */
+enum {
+  RETR_TUNE_GROUP_TILE = 0,     /* grouped fwd/dgrad GEMM tile: 64 or 128 */
+  RETR_TUNE_GROUP_STAGES = 1,   /* its LDS ring depth: 64-tile 2|4, 128-tile 1|2|3 */
+  RETR_TUNE_WGRAD_TILE = 2,     /* grouped weight-gradient tile: 64 or 128 */
+  RETR_TUNE_WGRAD_STAGES = 3,   /* its ring depth: 2|4 (64), 2|3 (128) */
+  RETR_TUNE_WGRAD_KC = 4,       /* weight-gradient K-slice length in tokens (multiple of 64) */
+  RETR_TUNE_COUNT = 8
+};
+int retr_tune(int knob, int value);
+
+/* ---- grouped projections (csrc/linear_group.hip): up to 16 independent GEMMs of one block in
+ * one launch -- the q|k and v in-projections of SelfAttResidual, q / k / v of CrossAttResidual
+ * (models/transformer_modules.py:38,66 -> torch/nn/functional.py:5785-5850), their data
+ * gradients, and the weight gradients of a whole block.  fp32 (dtype 0) runs the problems one
+ * by one through the single-GEMM entry points. */
+typedef struct {
+  const void* x; long ldx;          /* [M][K] */
+  const void* w; long ldw;          /* [N][K] */
+  const float* bias;                /* [N] or NULL */
+  void* y; long ldy;                /* [M][N] (dtype, or fp32 when y_f32) */
+  const float* residual; long ldr;  /* [M][N] fp32 or NULL */
+  float drop_p; unsigned long long seed;
+  int M, N, K, relu;
+} retr_linear_fwd_desc;
+int retr_linear_fwd_group(int dtype, int y_f32, int n, const retr_linear_fwd_desc* d,
+                          void* stream);
+
+typedef struct {
+  const void* dy; long lddy;        /* [M][N] */
+  const void* w; long ldw;          /* W [N][K] (w_trans 0) or W^T [K][N] (w_trans 1) */
+  void* dx; long lddx;              /* [M][K] */
+  const void* addend; long lda;     /* or NULL */
+  const void* gate; long ldg;       /* or NULL */
+  int M, N, K, pad;
+} retr_linear_dgrad_desc;
+int retr_linear_dgrad_group(int dtype, int dx_f32, int addend_f32, int w_trans, int n,
+                            const retr_linear_dgrad_desc* d, void* stream);
+
+/* dw[N][K] (=|+=) dy^T x, db[N] (=|+=) colsum dy for up to 8 problems: token-split fp32 slabs
+ * (plain stores) summed in slice order by a second launch -- deterministic, no atomics.
+ * workspace: retr_linear_wgrad_group_workspace(n, d) bytes of device memory. */
+typedef struct {
+  const void* dy; long lddy;        /* [M][N] */
+  const void* x; long ldx;          /* [M][K] */
+  float* dw; long lddw;             /* [N][K] */
+  float* db;                        /* [N] or NULL */
+  int M, N, K, accumulate;
+} retr_linear_wgrad_desc;
+size_t retr_linear_wgrad_group_workspace(int n, const retr_linear_wgrad_desc* d);
+int retr_linear_wgrad_group(int dtype, int n, const retr_linear_wgrad_desc* d, void* workspace,
+                            void* stream);
+
 /* ---- ResNet convolutions (torchvision conv stack via models/backbone.py:65-69, FrozenBN
  * models/backbone.py:41-51 folded into the weights) --------------------------------------- */
 int retr_conv_pack(int dtype, const float* w, const float* bn_w, const float* bn_b,

@@ -21,6 +21,32 @@ _D = ctypes.c_double
 _U64 = ctypes.c_ulonglong
 _SZ = ctypes.c_size_t
 
+
+
+class LinearFwdDesc(ctypes.Structure):
+    """retr_linear_fwd_desc (include/retr_hip.h)"""
+    _fields_ = [("x", _P), ("ldx", _L), ("w", _P), ("ldw", _L), ("bias", _P), ("y", _P),
+                ("ldy", _L), ("residual", _P), ("ldr", _L), ("drop_p", _F), ("seed", _U64),
+                ("M", _I), ("N", _I), ("K", _I), ("relu", _I)]
+
+
+class LinearDgradDesc(ctypes.Structure):
+    """retr_linear_dgrad_desc"""
+    _fields_ = [("dy", _P), ("lddy", _L), ("w", _P), ("ldw", _L), ("dx", _P), ("lddx", _L),
+                ("addend", _P), ("lda", _L), ("gate", _P), ("ldg", _L), ("M", _I), ("N", _I),
+                ("K", _I), ("pad", _I)]
+
+
+class LinearWgradDesc(ctypes.Structure):
+    """retr_linear_wgrad_desc"""
+    _fields_ = [("dy", _P), ("lddy", _L), ("x", _P), ("ldx", _L), ("dw", _P), ("lddw", _L),
+                ("db", _P), ("M", _I), ("N", _I), ("K", _I), ("accumulate", _I)]
+
+
+_PFD = ctypes.POINTER(LinearFwdDesc)
+_PDD = ctypes.POINTER(LinearDgradDesc)
+_PWD = ctypes.POINTER(LinearWgradDesc)
+
 # name -> argtypes (all functions return int unless listed in _RESTYPE)
 _SIGS = {
     "retr_abi_version": [],
@@ -36,6 +62,10 @@ _SIGS = {
                                  _P],
     "retr_linear_wgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _I, _P],
     "retr_bias_grad": [_I, _P, _L, _I, _I, _P, _P],
+    "retr_linear_fwd_group": [_I, _I, _I, _PFD, _P],
+    "retr_linear_dgrad_group": [_I, _I, _I, _I, _I, _PDD, _P],
+    "retr_linear_wgrad_group_workspace": [_I, _PWD],
+    "retr_linear_wgrad_group": [_I, _I, _PWD, _P, _P],
     "retr_conv_pack": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "retr_conv2d_fwd": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "retr_conv2d_dgrad": [_I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P],
@@ -55,6 +85,7 @@ _SIGS = {
     "retr_embed_ln_bwd_workspace": [_I, _I, _I],
     "retr_set_deterministic": [_I],
     "retr_get_deterministic": [],
+    "retr_tune": [_I, _I],
     "retr_attention_fwd": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _P, _I, _F,
                            _U64, _P, _P, _P],
     "retr_attention_bwd": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _P, _L, _P, _L, _P,
@@ -84,6 +115,7 @@ _SIGS = {
 }
 _RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
             "retr_layernorm_bwd_workspace": _SZ, "retr_embed_ln_bwd_workspace": _SZ,
+            "retr_linear_wgrad_group_workspace": _SZ,
             "retr_set_deterministic": None,
             "retr_set_seed_base": None}
 

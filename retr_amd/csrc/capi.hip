@@ -36,6 +36,15 @@ int retr_deterministic() { return g_deterministic; }
 extern "C" void retr_set_deterministic(int on) { g_deterministic = on ? 1 : 0; }
 extern "C" int retr_get_deterministic(void) { return g_deterministic; }
 
+static int g_tune[RETR_TUNE_COUNT] = {0};
+int retr_tune_get(int knob) { return knob >= 0 && knob < RETR_TUNE_COUNT ? g_tune[knob] : 0; }
+extern "C" int retr_tune(int knob, int value) {
+  if (knob < 0 || knob >= RETR_TUNE_COUNT) return -1;
+  const int old = g_tune[knob];
+  g_tune[knob] = value;
+  return old;
+}
+
 __global__ void seed_bump_kernel(unsigned long long* p, unsigned long long d) { *p += d; }
 extern "C" int retr_seed_bump(unsigned long long* p, unsigned long long delta, void* stream) {
   hipLaunchKernelGGL(seed_bump_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, p, delta);

@@ -57,6 +57,7 @@ RETR_DEVICE uint64_t dp_seed(const DropoutParams& dp) {
   return dp.base ? dp.seed + *dp.base : dp.seed;
 }
 const unsigned long long* retr_seed_base();
+int retr_tune_get(int knob);  // retr_tune (capi.hip): launch-configuration overrides, 0 = auto
 int retr_deterministic();   // retr_set_deterministic (capi.hip): fixed-order reductions only
 inline DropoutParams make_dp(float p, unsigned long long seed) {
   DropoutParams dp{seed, 0u, 1.f, nullptr};

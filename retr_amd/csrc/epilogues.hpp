@@ -152,9 +152,12 @@ struct EpiAccF32 {
   int vec;
   int overwrite;
   float* rowsum;
-  long split_stride = 0;   // > 0: split-K slice blockIdx.y writes its own slab out + y*stride
+  long split_stride = 0;   // > 0: split-K slice s writes its own slab out + s * stride
+  int split = -1;          // the slice index (grouped launches); -1: blockIdx.y
   static constexpr bool kRowSum = true;
-  RETR_DEVICE float* base() const { return out + (long)blockIdx.y * split_stride; }
+  RETR_DEVICE float* base() const {
+    return out + (long)(split >= 0 ? split : (int)blockIdx.y) * split_stride;
+  }
   RETR_DEVICE void apply(int m, int n, float v) const {
     float* p = base() + (long)m * ldo + n;
     if (atomic) atomicAdd(p, v);

@@ -17,6 +17,9 @@
 //    epilogue through LDS (8 consecutive columns per thread, 16-byte global accesses).
 //  * XCD-aware block order and split-K over blockIdx.y as in gemm.hpp.
 #pragma once
+#include <type_traits>
+#include <utility>
+
 #include "gemm.hpp"
 
 namespace retr {
@@ -87,11 +90,29 @@ constexpr int epi_bands() {
   return EPB > 0 ? EPB : ((size_t)BM * (BN + 4) * 4 > 160 * 1024 ? 2 : 1);
 }
 
+template <int BM, int BN, int S, int EPB>
+constexpr size_t gemm2_lds_bytes() {
+  constexpr size_t stage = (size_t)S * (BM + BN) * kBKBytes;
+  constexpr size_t epi = (size_t)BM * (BN + 4) * 4 / epi_bands<BM, BN, EPB>();
+  return stage > epi ? stage : epi;
+}
+
 // EPB: epilogue row bands (0 = as few as fit in LDS); S = 1: single-buffered (small-K GEMMs,
 // where the LDS footprint, not the pipeline depth, limits the blocks per CU)
+// XCD-aware block order: hardware dispatches block b to XCD b % 8; consecutive logical
+// blocks (neighbouring tiles sharing operand rows) land on one XCD and share its L2
+RETR_DEVICE int xcd_remap(int bid, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// One BM x BN output tile (index `tile` in row-major tile order), K range
+// [split * kchunk, (split + 1) * kchunk).
 template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB, class LA, class LB, class EP>
-__global__ void __launch_bounds__(WM * WN * 64)
-gemm2_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
+RETR_DEVICE __attribute__((always_inline)) void gemm2_tile(const LA& la, const LB& lb,
+                                                           const EP& ep, int M, int N, int K,
+                                                           int kchunk, int tiles_n, int tile,
+                                                           int split) {
   using T = bf16;
   constexpr int NT = WM * WN * 64;
   constexpr int BK = 64;
@@ -105,14 +126,8 @@ gemm2_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int nblk = gridDim.x;
-  int bid = blockIdx.x;
-  {
-    const int q = nblk / 8, r = nblk % 8, x = bid % 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-  }
-  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
-  const int kb = blockIdx.y * kchunk;
+  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  const int kb = split * kchunk;
   const int ke = min(K, kb + kchunk);
   if (kb >= ke && K > 0) {
     ep.empty_split(m0, n0);
@@ -221,12 +236,111 @@ gemm2_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) 
   }
 }
 
-template <int BM, int BN, int S, int EPB>
-constexpr size_t gemm2_lds_bytes() {
-  constexpr size_t stage = (size_t)S * (BM + BN) * kBKBytes;
-  constexpr size_t epi = (size_t)BM * (BN + 4) * 4 / epi_bands<BM, BN, EPB>();
-  return stage > epi ? stage : epi;
+template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB, class LA, class LB, class EP>
+__global__ void __launch_bounds__(WM * WN * 64)
+gemm2_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
+  gemm2_tile<FAM, BM, BN, WM, WN, S, EPB>(la, lb, ep, M, N, K, kchunk, tiles_n,
+                                          xcd_remap(blockIdx.x, gridDim.x), blockIdx.y);
 }
+
+// ---- grouped launch: up to G independent GEMMs with the same operand/epilogue types (the
+// projections of one attention block, the weight gradients of one layer, ...) in one grid.
+// Problem i owns blocks [blk0, blk0 + tiles * splits) of the (XCD-remapped) block order,
+// split-major so the blocks of one K-slice of one problem are neighbours.
+template <class LA, class LB, class EP>
+struct GProb {
+  LA la;
+  LB lb;
+  EP ep;
+  int M, N, K, kchunk, tiles_n, tiles, blk0, nblk;
+};
+
+template <class LA, class LB, class EP, int G>
+struct GGroup {
+  GProb<LA, LB, EP> p[G];
+  int n;
+};
+
+template <class E, class = void>
+struct has_split_slot : std::false_type {};
+template <class E>
+struct has_split_slot<E, std::void_t<decltype(std::declval<E&>().split)>> : std::true_type {};
+
+template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB, class LA, class LB, class EP,
+          int G>
+__global__ void __launch_bounds__(WM * WN * 64)
+gemm2_group_kernel(GGroup<LA, LB, EP, G> g) {
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < G; ++i)
+    if (i < g.n && bid >= g.p[i].blk0) p = i;
+  const GProb<LA, LB, EP>& d = g.p[p];
+  const int local = bid - d.blk0;
+  if (local >= d.nblk) return;
+  const int split = local / d.tiles, tile = local - split * d.tiles;
+  if constexpr (has_split_slot<EP>::value) {
+    EP ep = d.ep;
+    ep.split = split;
+    gemm2_tile<FAM, BM, BN, WM, WN, S, EPB>(d.la, d.lb, ep, d.M, d.N, d.K, d.kchunk, d.tiles_n,
+                                            tile, split);
+  } else {
+    gemm2_tile<FAM, BM, BN, WM, WN, S, EPB>(d.la, d.lb, d.ep, d.M, d.N, d.K, d.kchunk,
+                                            d.tiles_n, tile, split);
+  }
+}
+
+// Host side of a grouped launch: fill problems with add(), then launch().
+template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB, class LA, class LB, class EP,
+          int G>
+struct Group2 {
+  GGroup<LA, LB, EP, G> g{};
+  int blocks = 0;
+  int add(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits) {
+    if (g.n >= G) return 1;
+    constexpr int BK = 64;
+    GProb<LA, LB, EP>& d = g.p[g.n];
+    d.la = la;
+    d.lb = lb;
+    d.ep = ep;
+    d.M = M;
+    d.N = N;
+    d.K = K;
+    d.tiles_n = cdiv(N, BN);
+    d.tiles = cdiv(M, BM) * d.tiles_n;
+    if (splits < 1) splits = 1;
+    const int ksteps = cdiv(K, BK);
+    d.kchunk = BK;
+    if (K > 0) {
+      if (splits > ksteps) splits = ksteps;
+      d.kchunk = cdiv(ksteps, splits) * BK;
+      splits = cdiv(K, d.kchunk);
+    } else {
+      splits = 1;
+    }
+    d.blk0 = blocks;
+    d.nblk = d.tiles * splits;
+    blocks += d.nblk;
+    ++g.n;
+    return 0;
+  }
+  int launch(hipStream_t st, const char* what) {
+    if (blocks == 0) return 0;
+    constexpr size_t lds = gemm2_lds_bytes<BM, BN, S, EPB>();
+    auto kern = gemm2_group_kernel<FAM, BM, BN, WM, WN, S, EPB, LA, LB, EP, G>;
+    if constexpr (lds > 65536) {
+      static bool attr_set = false;
+      if (!attr_set) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        attr_set = true;
+      }
+    }
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(WM * WN * 64), lds, st, g);
+    return retr_check_launch(what);
+  }
+};
+
 
 template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB = 0, class LA, class LB,
           class EP>

@@ -1,0 +1,382 @@
+// Grouped linear GEMMs: the independent projections of one transformer block in ONE launch.
+//
+// At d_model 256 a single projection (e.g. M 2048-6400 tokens x N 256 x K 256) is a few
+// hundred MFMA tiles of work: alone it cannot fill 256 CUs and its runtime is pipeline fill and
+// drain.  The attention block's q|k and v projections (models/transformer_modules.py:38,66 ->
+// torch/nn/functional.py:5785-5850), the cross-attention's q, k and v, the data gradients of
+// the same, and the weight gradients of every projection of a block are independent GEMMs:
+// gemm2.hpp's grouped kernel runs up to kMaxGroup of them in one grid (per-problem operands,
+// shapes and epilogues; blocks partitioned by a prefix over the problems).
+//
+// Weight gradients (dW += dY^T X, db += colsum dY) are split over the token dimension into
+// fp32 slabs written with plain stores; the bias gradient is one more GEMM problem against a
+// ones vector (dY^T 1); a second launch adds every problem's slabs in slice order into dW / db.
+// Deterministic by construction, no float atomics.
+#include "gemm2.hpp"
+#include "epilogues.hpp"
+#include "../../include/retr_hip.h"
+
+using namespace retr;
+
+namespace {
+
+constexpr int kMaxGroup = 16;
+constexpr int kMaxWgrad = 8;   // weight-gradient problems per group (x2 with the bias rows)
+
+static __device__ __attribute__((aligned(16))) unsigned short g_ones_bf16[8] = {
+    0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+
+const bf16* ones_ptr() {
+  static const bf16* p = nullptr;
+  if (!p) {
+    void* a = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_ones_bf16)) == hipSuccess) p = (const bf16*)a;
+  }
+  return p;
+}
+
+// the K-slice count the launcher will actually use for `splits` requested slices (whole K-steps)
+int norm_splits(int K, int splits) {
+  constexpr int BK = 64;
+  if (K <= 0) return 1;
+  const int ksteps = cdiv(K, BK);
+  if (splits < 1) splits = 1;
+  if (splits > ksteps) splits = ksteps;
+  return cdiv(K, cdiv(ksteps, splits) * BK);
+}
+
+// ---- forward / data-gradient groups: tile by the group's total tile count
+template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB, class LA, class LB, class EP>
+int run_group(int n, const LA* la, const LB* lb, const EP* ep, const int* M, const int* N,
+              const int* K, hipStream_t st, const char* what) {
+  Group2<FAM, BM, BN, WM, WN, S, EPB, LA, LB, EP, kMaxGroup> g;
+  for (int i = 0; i < n; ++i)
+    if (M[i] > 0 && g.add(la[i], lb[i], ep[i], M[i], N[i], K[i], 1)) return 1;
+  return g.launch(st, what);
+}
+
+template <int FAM, class LA, class LB, class EP>
+int launch_group(int n, const LA* la, const LB* lb, const EP* ep, const int* M, const int* N,
+                 const int* K, hipStream_t st, const char* what) {
+  long t128 = 0;
+  int kmax = 0;
+  for (int i = 0; i < n; ++i) {
+    t128 += (long)cdiv(M[i], 128) * cdiv(N[i], 128);
+    kmax = K[i] > kmax ? K[i] : kmax;
+  }
+  int tile = retr_tune_get(RETR_TUNE_GROUP_TILE);
+  int stages = retr_tune_get(RETR_TUNE_GROUP_STAGES);
+  // tools/group_micro.py (profiles/r2_group_micro.txt): the 64x64 two-stage tile wins on every
+  // block-sized group at d_model 256 (more blocks in flight beat the larger tile's reuse)
+  if (tile != 64 && tile != 128) tile = t128 >= 400 ? 128 : 64;
+  if (tile == 128) {
+    if (stages == 0) stages = kmax <= 128 ? 1 : 2;
+    if (stages == 1)
+      return run_group<FAM, 128, 128, 2, 2, 1, 2>(n, la, lb, ep, M, N, K, st, what);
+    if (stages == 3)
+      return run_group<FAM, 128, 128, 2, 2, 3, 0>(n, la, lb, ep, M, N, K, st, what);
+    return run_group<FAM, 128, 128, 2, 2, 2, 0>(n, la, lb, ep, M, N, K, st, what);
+  }
+  if (stages == 4) return run_group<FAM, 64, 64, 2, 2, 4, 0>(n, la, lb, ep, M, N, K, st, what);
+  return run_group<FAM, 64, 64, 2, 2, 2, 0>(n, la, lb, ep, M, N, K, st, what);
+}
+
+template <typename TO>
+int fwd_group_t(int n, const retr_linear_fwd_desc* d, hipStream_t st) {
+  DenseK<bf16> la[kMaxGroup], lb[kMaxGroup];
+  EpiFwd<TO, float> ep[kMaxGroup];
+  int M[kMaxGroup], N[kMaxGroup], K[kMaxGroup];
+  for (int i = 0; i < n; ++i) {
+    const retr_linear_fwd_desc& q = d[i];
+    la[i] = DenseK<bf16>{(const bf16*)q.x, q.ldx, q.M, q.K};
+    lb[i] = DenseK<bf16>{(const bf16*)q.w, q.ldw, q.N, q.K};
+    ep[i] = EpiFwd<TO, float>{(TO*)q.y, q.ldy, q.bias, q.residual, q.ldr, q.relu,
+                              make_dp(q.drop_p, q.seed), (long)q.N};
+    ep[i].set_vec();
+    M[i] = q.M;
+    N[i] = q.N;
+    K[i] = q.K;
+  }
+  return launch_group<kFamLinearFwd>(n, la, lb, ep, M, N, K, st, "linear_fwd_group");
+}
+
+template <typename TO, typename TA, class LB>
+int dgrad_group_t(int n, const retr_linear_dgrad_desc* d, hipStream_t st) {
+  DenseK<bf16> la[kMaxGroup];
+  LB lb[kMaxGroup];
+  EpiDgrad<TO, TA, bf16> ep[kMaxGroup];
+  int M[kMaxGroup], N[kMaxGroup], K[kMaxGroup];
+  for (int i = 0; i < n; ++i) {
+    const retr_linear_dgrad_desc& q = d[i];
+    // dX[m][k] = sum_n dY[m][n] W[n][k]: A = dY (reduction over N), B(k, n) = W[n][k]
+    la[i] = DenseK<bf16>{(const bf16*)q.dy, q.lddy, q.M, q.N};
+    lb[i] = LB{(const bf16*)q.w, q.ldw, q.K, q.N};
+    ep[i] = EpiDgrad<TO, TA, bf16>{(TO*)q.dx, q.lddx, (const TA*)q.addend, q.lda,
+                                   (const bf16*)q.gate, q.ldg};
+    ep[i].set_vec();
+    M[i] = q.M;
+    N[i] = q.K;
+    K[i] = q.N;
+  }
+  return launch_group<kFamLinearDgrad>(n, la, lb, ep, M, N, K, st, "linear_dgrad_group");
+}
+
+// ---- weight-gradient groups
+struct WPlan {
+  int tile;                   // 128 or 64
+  int stages;                 // LDS ring depth
+  int n;                      // GEMM problems (dW problems + bias problems)
+  int src[2 * kMaxWgrad];     // descriptor index of each problem
+  int bias[2 * kMaxWgrad];    // 1: the problem is the bias-gradient column of src
+  int splits[2 * kMaxWgrad];
+  long ws_off[2 * kMaxWgrad]; // float offset of the problem's slabs
+  long ws_floats;
+};
+
+WPlan wgrad_plan(int n, const retr_linear_wgrad_desc* d) {
+  WPlan p{};
+  long t128 = 0;
+  for (int i = 0; i < n; ++i)
+    if (d[i].M > 0) t128 += (long)cdiv(d[i].N, 128) * cdiv(d[i].K, 128);
+  // 128x128 tiles only for token-heavy groups (the encoder FFN: 64 tiles x 6400 tokens);
+  // 64x64 with 512-1024-token slices elsewhere (tools/group_micro.py sweep)
+  long tok128 = 0;
+  for (int i = 0; i < n; ++i)
+    if (d[i].M > 0) tok128 += (long)cdiv(d[i].N, 128) * cdiv(d[i].K, 128) * d[i].M;
+  p.tile = tok128 >= 400000 ? 128 : 64;
+  (void)t128;
+  const int tt = retr_tune_get(RETR_TUNE_WGRAD_TILE);
+  if (tt == 64 || tt == 128) p.tile = tt;
+  p.stages = retr_tune_get(RETR_TUNE_WGRAD_STAGES);
+  if (p.stages == 0) p.stages = 2;
+  // one K-slice length (in tokens) for the whole group: about two blocks per CU over the
+  // group's tiles, at least 4 K-steps per slice
+  long tok_tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    if (d[i].M <= 0) continue;
+    long tiles = (long)cdiv(d[i].N, p.tile) * cdiv(d[i].K, p.tile);
+    if (d[i].db) tiles += cdiv(d[i].N, p.tile);
+    tok_tiles += tiles * d[i].M;
+  }
+  const long target = 512;   // blocks
+  long kc = (tok_tiles + target - 1) / target;
+  kc = (kc + 63) / 64 * 64;
+  if (kc < (p.tile == 128 ? 256 : 512)) kc = p.tile == 128 ? 256 : 512;
+  if (retr_tune_get(RETR_TUNE_WGRAD_KC) > 0) kc = retr_tune_get(RETR_TUNE_WGRAD_KC);
+  for (int i = 0; i < n; ++i) {
+    if (d[i].M <= 0) continue;
+    const int s = norm_splits(d[i].M, cdiv(d[i].M, (int)kc));
+    for (int b = 0; b < (d[i].db ? 2 : 1); ++b) {
+      const int j = p.n++;
+      p.src[j] = i;
+      p.bias[j] = b;
+      p.splits[j] = s;
+      p.ws_off[j] = p.ws_floats;
+      p.ws_floats += (long)s * d[i].N * (b ? 1 : d[i].K);
+      p.ws_floats = (p.ws_floats + 3) / 4 * 4;   // 16-byte aligned slabs
+    }
+  }
+  return p;
+}
+
+struct SlabSum {
+  const float* ws;
+  float* dst;
+  long ld;        // dst row stride
+  long slab;      // floats per slab (rows * cols)
+  int rows, cols, splits, accumulate, blk0, nblk, vec;
+};
+
+struct SlabGroup {
+  SlabSum p[2 * kMaxWgrad];
+  int n;
+};
+
+constexpr int kSlabPerThread = 4;
+
+// dst (=|+=) sum_s ws[s] in slice order; 4 consecutive elements per thread
+__global__ void __launch_bounds__(256) slab_sum_group_kernel(SlabGroup g) {
+  const int bid = blockIdx.x;
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < 2 * kMaxWgrad; ++i)
+    if (i < g.n && bid >= g.p[i].blk0) p = i;
+  const SlabSum& d = g.p[p];
+  const long e0 = ((long)(bid - d.blk0) * 256 + threadIdx.x) * kSlabPerThread;
+  if (e0 >= d.slab) return;
+  float v[kSlabPerThread] = {0.f, 0.f, 0.f, 0.f};
+  if (d.vec) {
+    int s = 0;
+    for (; s + 3 < d.splits; s += 4) {
+      f32x4 t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = *(const f32x4*)(d.ws + (long)(s + u) * d.slab + e0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += t[u][e];
+    }
+    for (; s < d.splits; ++s) {
+      const f32x4 t = *(const f32x4*)(d.ws + (long)s * d.slab + e0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += t[e];
+    }
+    const long r = e0 / d.cols, c = e0 - r * d.cols;
+    float* o = d.dst + r * d.ld + c;
+    if (d.accumulate) {
+      const f32x4 a = *(const f32x4*)o;
+      *(f32x4*)o = f32x4{a[0] + v[0], a[1] + v[1], a[2] + v[2], a[3] + v[3]};
+    } else {
+      *(f32x4*)o = f32x4{v[0], v[1], v[2], v[3]};
+    }
+    return;
+  }
+  for (int e = 0; e < kSlabPerThread; ++e) {
+    const long i = e0 + e;
+    if (i >= d.slab) break;
+    float t = 0.f;
+    for (int s = 0; s < d.splits; ++s) t += d.ws[(long)s * d.slab + i];
+    const long r = i / d.cols, c = i - r * d.cols;
+    float* o = d.dst + r * d.ld + c;
+    *o = d.accumulate ? *o + t : t;
+  }
+}
+
+template <int BM, int S>
+int wgrad_group_gemm(const WPlan& p, const retr_linear_wgrad_desc* d, float* ws, hipStream_t st) {
+  using L = DenseT<bf16>;
+  Group2<kFamLinearWgrad, BM, BM, 2, 2, S, 0, L, L, EpiAccF32, 2 * kMaxWgrad> g;
+  const bf16* ones = ones_ptr();
+  if (!ones) {
+    retr_set_error("linear_wgrad_group: ones vector unavailable");
+    return 1;
+  }
+  for (int j = 0; j < p.n; ++j) {
+    const retr_linear_wgrad_desc& q = d[p.src[j]];
+    // dW[n][k] = sum_m dY[m][n] X[m][k]: A(n, m) = dY[m][n], B(k, m) = X[m][k]
+    L la{(const bf16*)q.dy, q.lddy, q.N, q.M};
+    const int cols = p.bias[j] ? 1 : q.K;
+    // the bias column: B(0, m) = 1 (a 16-byte ones chunk re-read for every token, ld 0)
+    L lb = p.bias[j] ? L{ones, 0, 1, q.M} : L{(const bf16*)q.x, q.ldx, q.K, q.M};
+    EpiAccF32 ep{ws + p.ws_off[j], (long)cols, 0, 0, 1, nullptr};
+    ep.split_stride = (long)q.N * cols;
+    ep.set_vec();
+    if (g.add(la, lb, ep, q.N, cols, q.M, p.splits[j])) return 1;
+  }
+  return g.launch(st, "linear_wgrad_group");
+}
+
+}  // namespace
+
+extern "C" {
+
+int retr_linear_fwd_group(int dtype, int y_f32, int n, const retr_linear_fwd_desc* d,
+                          void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RETR_REQUIRE(n >= 0 && n <= kMaxGroup, "linear_fwd_group: n=%d (max %d)", n, kMaxGroup);
+  if (dtype != RETR_BF16) {
+    for (int i = 0; i < n; ++i) {
+      const retr_linear_fwd_desc& q = d[i];
+      int e = retr_linear_fwd(dtype, q.x, q.ldx, q.w, q.ldw, q.bias, q.y, q.ldy, y_f32, q.M, q.N,
+                              q.K, q.relu, q.residual, q.ldr, q.drop_p, q.seed, stream);
+      if (e) return e;
+    }
+    return 0;
+  }
+  for (int i = 0; i < n; ++i)
+    RETR_REQUIRE(d[i].M >= 0 && d[i].N > 0 && d[i].K > 0 && d[i].K % 8 == 0 &&
+                     d[i].ldx % 8 == 0 && d[i].ldw % 8 == 0,
+                 "linear_fwd_group[%d]: bad shape M=%d N=%d K=%d", i, d[i].M, d[i].N, d[i].K);
+  return y_f32 ? fwd_group_t<float>(n, d, st) : fwd_group_t<bf16>(n, d, st);
+}
+
+int retr_linear_dgrad_group(int dtype, int dx_f32, int addend_f32, int w_trans, int n,
+                            const retr_linear_dgrad_desc* d, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RETR_REQUIRE(n >= 0 && n <= kMaxGroup, "linear_dgrad_group: n=%d (max %d)", n, kMaxGroup);
+  if (dtype != RETR_BF16) {
+    for (int i = 0; i < n; ++i) {
+      const retr_linear_dgrad_desc& q = d[i];
+      int e = retr_linear_dgrad(dtype, q.dy, q.lddy, q.w, q.ldw, q.dx, q.lddx, dx_f32, q.M, q.N,
+                                q.K, q.addend, addend_f32, q.lda, q.gate, q.ldg, w_trans, stream);
+      if (e) return e;
+    }
+    return 0;
+  }
+  for (int i = 0; i < n; ++i)
+    RETR_REQUIRE(d[i].M >= 0 && d[i].N > 0 && d[i].K > 0 && d[i].N % 8 == 0 &&
+                     d[i].lddy % 8 == 0 && d[i].ldw % 8 == 0,
+                 "linear_dgrad_group[%d]: bad shape M=%d N=%d K=%d", i, d[i].M, d[i].N, d[i].K);
+  if (w_trans) {
+    if (dx_f32) return addend_f32 ? dgrad_group_t<float, float, DenseK<bf16>>(n, d, st)
+                                  : dgrad_group_t<float, bf16, DenseK<bf16>>(n, d, st);
+    return addend_f32 ? dgrad_group_t<bf16, float, DenseK<bf16>>(n, d, st)
+                      : dgrad_group_t<bf16, bf16, DenseK<bf16>>(n, d, st);
+  }
+  if (dx_f32) return addend_f32 ? dgrad_group_t<float, float, DenseT<bf16>>(n, d, st)
+                                : dgrad_group_t<float, bf16, DenseT<bf16>>(n, d, st);
+  return addend_f32 ? dgrad_group_t<bf16, float, DenseT<bf16>>(n, d, st)
+                    : dgrad_group_t<bf16, bf16, DenseT<bf16>>(n, d, st);
+}
+
+size_t retr_linear_wgrad_group_workspace(int n, const retr_linear_wgrad_desc* d) {
+  if (n <= 0 || n > kMaxWgrad) return 0;
+  return (size_t)wgrad_plan(n, d).ws_floats * sizeof(float);
+}
+
+int retr_linear_wgrad_group(int dtype, int n, const retr_linear_wgrad_desc* d, void* workspace,
+                            void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RETR_REQUIRE(n >= 0 && n <= kMaxWgrad, "linear_wgrad_group: n=%d (max %d)", n, kMaxWgrad);
+  if (dtype != RETR_BF16) {
+    for (int i = 0; i < n; ++i) {
+      const retr_linear_wgrad_desc& q = d[i];
+      int e = retr_linear_wgrad(dtype, q.dy, q.lddy, q.x, q.ldx, q.dw, q.lddw, q.M, q.N, q.K,
+                                q.db, q.accumulate, stream);
+      if (e) return e;
+    }
+    return 0;
+  }
+  for (int i = 0; i < n; ++i)
+    RETR_REQUIRE(d[i].M >= 0 && d[i].N > 0 && d[i].K > 0 && d[i].K % 8 == 0 &&
+                     d[i].lddy % 8 == 0 && d[i].ldx % 8 == 0 && d[i].lddy >= (d[i].N + 7) / 8 * 8,
+                 "linear_wgrad_group[%d]: bad shape M=%d N=%d K=%d", i, d[i].M, d[i].N, d[i].K);
+  const WPlan p = wgrad_plan(n, d);
+  if (p.n == 0) return 0;
+  RETR_REQUIRE(workspace != nullptr, "linear_wgrad_group: workspace required");
+  float* ws = (float*)workspace;
+  int e;
+  if (p.tile == 128) e = p.stages == 3 ? wgrad_group_gemm<128, 3>(p, d, ws, st)
+                                       : wgrad_group_gemm<128, 2>(p, d, ws, st);
+  else e = p.stages == 4 ? wgrad_group_gemm<64, 4>(p, d, ws, st)
+                         : wgrad_group_gemm<64, 2>(p, d, ws, st);
+  if (e) return e;
+  SlabGroup sg{};
+  int blocks = 0;
+  for (int j = 0; j < p.n; ++j) {
+    const retr_linear_wgrad_desc& q = d[p.src[j]];
+    SlabSum& s = sg.p[sg.n++];
+    s.ws = ws + p.ws_off[j];
+    s.rows = q.N;
+    s.cols = p.bias[j] ? 1 : q.K;
+    s.dst = p.bias[j] ? q.db : q.dw;
+    s.ld = p.bias[j] ? 1 : q.lddw;
+    s.slab = (long)s.rows * s.cols;
+    s.splits = p.splits[j];
+    s.accumulate = q.accumulate;
+    s.vec = (s.cols % 4 == 0 && s.ld % 4 == 0 && ((uintptr_t)s.dst & 15) == 0) ||
+            (s.cols == 1 && s.rows % 4 == 0 && ((uintptr_t)s.dst & 15) == 0);
+    if (s.cols == 1) {   // a bias vector: one row of N elements
+      s.cols = s.rows;
+      s.rows = 1;
+      s.ld = s.cols;
+    }
+    s.blk0 = blocks;
+    s.nblk = (int)cdiv(s.slab, 256L * kSlabPerThread);
+    blocks += s.nblk;
+  }
+  hipLaunchKernelGGL(slab_sum_group_kernel, dim3(blocks), dim3(256), 0, st, sg);
+  return retr_check_launch("linear_wgrad_group sum");
+}
+
+}  // extern "C"

@@ -266,6 +266,68 @@ def k_linear_wgrad(dy, x, dw, db=None, accumulate=False):
          ptr(dw), dw.stride(0), M, N, K, ptr(db), int(accumulate), _st())
 
 
+def k_linear_fwd_group(items):
+    """One launch for independent projections: items of (x, w, bias, y[, relu, res, drop_p,
+    seed]); every y has the same dtype (csrc/linear_group.hip)."""
+    n = len(items)
+    arr = (_lib.LinearFwdDesc * n)()
+    for i, it in enumerate(items):
+        x, w, bias, y = it[:4]
+        relu, res, drop_p, seed = (tuple(it[4:]) + (0, None, 0.0, 0)[len(it) - 4:])
+        d = arr[i]
+        d.x, d.ldx, d.w, d.ldw = ptr(x), x.stride(0), ptr(w), w.stride(0)
+        d.bias, d.y, d.ldy = ptr(bias), ptr(y), y.stride(0)
+        d.residual, d.ldr = ptr(res), res.stride(0) if res is not None else 0
+        d.drop_p, d.seed = drop_p, seed
+        d.M, d.N, d.K, d.relu = x.shape[0], w.shape[0], x.shape[1], relu
+    y0 = items[0][3]
+    call("retr_linear_fwd_group", dcode(items[0][0].dtype), int(y0.dtype == torch.float32), n,
+         arr, _st())
+
+
+def k_linear_dgrad_group(items):
+    """One launch for independent data gradients: items of (dy, wt, dx[, addend, gate]) with
+    wt as in k_linear_dgrad (all _TView or all materialised)."""
+    n = len(items)
+    arr = (_lib.LinearDgradDesc * n)()
+    w_trans = None
+    for i, it in enumerate(items):
+        dy, wt, dx = it[:3]
+        addend = it[3] if len(it) > 3 else None
+        gate = it[4] if len(it) > 4 else None
+        K, N = wt.shape
+        if isinstance(wt, _TView):
+            w, wtr = wt.w, 0
+        else:
+            w, wtr = wt, 1
+        assert w_trans is None or w_trans == wtr, "dgrad group: mixed weight layouts"
+        w_trans = wtr
+        d = arr[i]
+        d.dy, d.lddy, d.w, d.ldw = ptr(dy), dy.stride(0), ptr(w), w.stride(0)
+        d.dx, d.lddx = ptr(dx), dx.stride(0)
+        d.addend, d.lda = ptr(addend), addend.stride(0) if addend is not None else 0
+        d.gate, d.ldg = ptr(gate), gate.stride(0) if gate is not None else 0
+        d.M, d.N, d.K = dy.shape[0], N, K
+    dx0, a0 = items[0][2], items[0][3] if len(items[0]) > 3 else None
+    call("retr_linear_dgrad_group", dcode(items[0][0].dtype), int(dx0.dtype == torch.float32),
+         int(a0 is not None and a0.dtype == torch.float32), w_trans, n, arr, _st())
+
+
+def k_linear_wgrad_group(items):
+    """One GEMM launch + one ordered slab-sum launch for the weight (and bias) gradients of
+    several projections: items of (dy, x, dw, db, accumulate)."""
+    n = len(items)
+    arr = (_lib.LinearWgradDesc * n)()
+    for i, (dy, x, dw, db, acc) in enumerate(items):
+        d = arr[i]
+        d.dy, d.lddy, d.x, d.ldx = ptr(dy), dy.stride(0), ptr(x), x.stride(0)
+        d.dw, d.lddw, d.db = ptr(dw), dw.stride(0), ptr(db)
+        d.M, d.N, d.K, d.accumulate = dy.shape[0], dw.shape[0], x.shape[1], int(acc)
+    nbytes = _lib.load().retr_linear_wgrad_group_workspace(n, arr)
+    ws = torch.empty(max(1, nbytes // 4), dtype=torch.float32, device=items[0][0].device)
+    call("retr_linear_wgrad_group", dcode(items[0][0].dtype), n, arr, ptr(ws), _st())
+
+
 def _empty(*shape, dev):
     return torch.empty(shape, dtype=torch.float32, device=dev)
 
@@ -438,8 +500,8 @@ class _SelfAttnBlock(torch.autograd.Function):
         dev = n.device
         qk = torch.empty(M, 2 * C, dtype=cdtype, device=dev)
         v = torch.empty(M, C, dtype=cdtype, device=dev)
-        k_linear_fwd(npos, win[: 2 * C], b_in[: 2 * C].detach(), qk)
-        k_linear_fwd(n, win[2 * C:], b_in[2 * C:].detach(), v)
+        k_linear_fwd_group([(npos, win[: 2 * C], b_in[: 2 * C].detach(), qk),
+                            (n, win[2 * C:], b_in[2 * C:].detach(), v)])
         o = torch.empty(M, C, dtype=cdtype, device=dev)
         lse = torch.empty(B * H * L, dtype=torch.float32, device=dev)
         s_att, s_res = next_seed(), next_seed()
@@ -470,26 +532,22 @@ class _SelfAttnBlock(torch.autograd.Function):
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
         (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
-        ov = _Overlap(OVERLAP["transformer"])
-        with ov.side():
-            k_linear_wgrad(dbr, o, dw_out, db_out, accumulate=True)
         do = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
         dqk = torch.empty(M, 2 * C, dtype=cdtype, device=dev)
         dv = torch.empty(M, C, dtype=cdtype, device=dev)
         k_attention_bwd(qk[:, :C], qk[:, C:], v, o, do, lse, dqk[:, :C], dqk[:, C:], dv, B, H,
                         L, L, hd, kpm, causal, drop_attn, s_att)
-        with ov.side():
-            k_linear_wgrad(dqk, npos, dw_in[: 2 * C], db_in[: 2 * C], accumulate=True)
-            k_linear_wgrad(dv, n, dw_in[2 * C:], db_in[2 * C:], accumulate=True)
         dnpos = torch.empty(M, C, dtype=cdtype, device=dev)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
-        k_linear_dgrad(dqk, wint[:, : 2 * C], dnpos)
-        k_linear_dgrad(dv, wint[:, 2 * C:], dn)
+        k_linear_dgrad_group([(dqk, wint[:, : 2 * C], dnpos), (dv, wint[:, 2 * C:], dn)])
+        # the block's three weight gradients (+ biases): one grouped GEMM + one slab sum
+        k_linear_wgrad_group([(dbr, o, dw_out, db_out, True),
+                              (dqk, npos, dw_in[: 2 * C], db_in[: 2 * C], True),
+                              (dv, n, dw_in[2 * C:], db_in[2 * C:], True)])
         _, ln_b, pos, period = ctx.ln
         dx, dlw, dlb, dpos = _ln_bwd(x, ln_w, ln_b, mean, rstd, dn, dnpos, dout, pos, period,
                                      ctx.needs_input_grad[3])
-        ov.join()
         return (dx, dlw, dlb, dpos, None, None, dw_in, db_in, dw_out, db_out) + (None,) * 9
 
 
@@ -513,9 +571,9 @@ class _CrossAttnBlock(torch.autograd.Function):
         q = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k = torch.empty(Mk, C, dtype=cdtype, device=dev)
         v = torch.empty(Mk, C, dtype=cdtype, device=dev)
-        k_linear_fwd(qpos, win[:C], b_in[:C].detach(), q)
-        k_linear_fwd(mem_pos, win[C: 2 * C], b_in[C: 2 * C].detach(), k)
-        k_linear_fwd(mem, win[2 * C:], b_in[2 * C:].detach(), v)
+        k_linear_fwd_group([(qpos, win[:C], b_in[:C].detach(), q),
+                            (mem_pos, win[C: 2 * C], b_in[C: 2 * C].detach(), k),
+                            (mem, win[2 * C:], b_in[2 * C:].detach(), v)])
         o = torch.empty(Mq, C, dtype=cdtype, device=dev)
         lse = torch.empty(B * H * Lq, dtype=torch.float32, device=dev)
         s_att, s_res = next_seed(), next_seed()
@@ -548,9 +606,6 @@ class _CrossAttnBlock(torch.autograd.Function):
         dbr = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, s_res)
         (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
-        ov = _Overlap(OVERLAP["transformer"])
-        with ov.side():
-            k_linear_wgrad(dbr, o, dw_out, db_out, accumulate=True)
         do = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
         dq = torch.empty(Mq, C, dtype=cdtype, device=dev)
@@ -558,20 +613,18 @@ class _CrossAttnBlock(torch.autograd.Function):
         dv = torch.empty(Mk, C, dtype=cdtype, device=dev)
         k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, False, drop_attn,
                         s_att)
-        with ov.side():
-            k_linear_wgrad(dq, qpos, dw_in[:C], db_in[:C], accumulate=True)
-            k_linear_wgrad(dk, mem_pos, dw_in[C: 2 * C], db_in[C: 2 * C], accumulate=True)
-            k_linear_wgrad(dv, mem, dw_in[2 * C:], db_in[2 * C:], accumulate=True)
         dqpos = torch.empty(Mq, C, dtype=cdtype, device=dev)
         dmem_pos = torch.empty(Mk, C, dtype=cdtype, device=dev)
         dmem = torch.empty(Mk, C, dtype=cdtype, device=dev)
-        k_linear_dgrad(dq, wint[:, :C], dqpos)
-        k_linear_dgrad(dk, wint[:, C: 2 * C], dmem_pos)
-        k_linear_dgrad(dv, wint[:, 2 * C:], dmem)
+        k_linear_dgrad_group([(dq, wint[:, :C], dqpos), (dk, wint[:, C: 2 * C], dmem_pos),
+                              (dv, wint[:, 2 * C:], dmem)])
+        k_linear_wgrad_group([(dbr, o, dw_out, db_out, True),
+                              (dq, qpos, dw_in[:C], db_in[:C], True),
+                              (dk, mem_pos, dw_in[C: 2 * C], db_in[C: 2 * C], True),
+                              (dv, mem, dw_in[2 * C:], db_in[2 * C:], True)])
         _, ln_b, qp, period = ctx.ln
         dy, dlw, dlb, dqp = _ln_bwd(y, ln_w, ln_b, mean, rstd, None, dqpos, dout, qp, period,
                                     ctx.needs_input_grad[3])
-        ov.join()
         return (dy, dlw, dlb, dqp, None, None, dmem_pos, dmem, dw_in, db_in, dw_out,
                 db_out) + (None,) * 9
 
@@ -612,17 +665,12 @@ class _FFNBlock(torch.autograd.Function):
         dbr = torch.empty(M, C, dtype=cdtype, device=dev)
         k_dropout_apply(dout, dbr, drop_res, seed)
         (dw1, _), (db1, _), (dw2, _), (db2, _) = map(grad_buffer, ctx.gparams)
-        ov = _Overlap(OVERLAP["transformer"])
-        with ov.side():
-            k_linear_wgrad(dbr, h, dw2, db2, accumulate=True)
         dh = torch.empty(M, F, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, w2t, dh, gate=h)
-        with ov.side():
-            k_linear_wgrad(dh, n, dw1, db1, accumulate=True)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dh, w1t, dn)
+        k_linear_wgrad_group([(dbr, h, dw2, db2, True), (dh, n, dw1, db1, True)])
         dx, dlw, dlb, _ = _ln_bwd(x, ln_w, ctx.ln_b, mean, rstd, dn, None, dout)
-        ov.join()
         return dx, dlw, dlb, None, dw1, db1, dw2, db2, None, None
 
 

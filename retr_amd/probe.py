@@ -48,6 +48,10 @@ def flops_of(name, a):
     if name == "retr_linear_wgrad":
         m, n, k = a[7], a[8], a[9]
         return "linear_wgrad", 2.0 * m * n * k
+    if name in _GROUPS:
+        fam, ia = _GROUPS[name]
+        n, arr = a[ia - 1], a[ia]
+        return fam, sum(2.0 * arr[i].M * arr[i].N * arr[i].K for i in range(n))
     if name == "retr_attention_fwd":
         b, h, lq, lk, hd, causal = a[9], a[10], a[11], a[12], a[13], a[15]
         return "attention_fwd", 4.0 * b * h * lq * lk * hd * (0.5 if causal else 1.0)
@@ -57,8 +61,16 @@ def flops_of(name, a):
     return name, 0.0
 
 
+# grouped launches: name -> (family, index of the descriptor array in the call's arguments)
+_GROUPS = {"retr_linear_fwd_group": ("linear_fwd", 3), "retr_linear_dgrad_group": ("linear_dgrad", 5),
+           "retr_linear_wgrad_group": ("linear_wgrad", 2)}
+
+
 def shape_of(name, a):
     """Short shape tag of a call (for the per-shape breakdown)."""
+    if name in _GROUPS:
+        n, arr = a[_GROUPS[name][1] - 1], a[_GROUPS[name][1]]
+        return "group " + " + ".join(f"M{arr[i].M} N{arr[i].N} K{arr[i].K}" for i in range(n))
     if name == "retr_conv2d_fwd":
         return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} ->{a[10]} k{a[11]} s{a[13]} d{a[15]}"
     if name == "retr_conv2d_dgrad":
@@ -82,11 +94,13 @@ def shape_of(name, a):
 
 TRACKED = ("retr_conv2d_fwd", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
            "retr_linear_dgrad", "retr_linear_dgrad_splitk", "retr_linear_wgrad",
+           "retr_linear_fwd_group", "retr_linear_dgrad_group", "retr_linear_wgrad_group",
            "retr_attention_fwd", "retr_attention_bwd")
 
 
-FAMILY_SYMBOL = {"linear_fwd": "gemm{,2}_kernel<0,", "linear_dgrad": "gemm{,2}_kernel<1,",
-                 "linear_wgrad": "gemm{,2}_kernel<2,", "conv_fwd": "gemm{,2}_kernel<3,",
+FAMILY_SYMBOL = {"linear_fwd": "gemm{,2,2_group}_kernel<0,",
+                 "linear_dgrad": "gemm{,2,2_group}_kernel<1,",
+                 "linear_wgrad": "gemm{,2,2_group}_kernel<2,", "conv_fwd": "gemm{,2}_kernel<3,",
                  "conv_dgrad": "gemm{,2}_kernel<4,", "conv_wgrad": "gemm{,2}_kernel<5,",
                  "attention_fwd": "attn_fwd{,2}_kernel",
                  "attention_bwd": "attn_bwd_"}
@@ -96,7 +110,8 @@ def family_of_symbol(name):
     """Family key of a rocprof kernel name (mangled ``_ZN4retr11gemm_kernelILi3E...`` or
     demangled ``retr::gemm_kernel<3, ...>``), or None."""
     import re
-    m = re.search(r"gemm2?_kernelILi(\d+)E", name) or re.search(r"gemm2?_kernel<(\d+),", name)
+    m = re.search(r"gemm2?(?:_group)?_kernelILi(\d+)E", name) or \
+        re.search(r"gemm2?(?:_group)?_kernel<(\d+),", name)
     if m:
         return ("linear_fwd", "linear_dgrad", "linear_wgrad", "conv_fwd", "conv_dgrad",
                 "conv_wgrad")[int(m.group(1))]

@@ -59,7 +59,33 @@ def test_beam_matches_oracle_restatement(K):
             ref = orc.beam_search(
                 lambda c, m: orc.caption_forward(sd, cfg, img_r, mask_r, c, m), B, T, K, 101,
                 eos)
-        assert torch.equal(ids.cpu(), ref), (K, eos, ids.cpu(), ref)
+        got = ids.cpu()
+        for b in range(B):
+            if torch.equal(got[b], ref[b]):
+                continue
+            # a near-tie between candidate scores resolved differently by the GPU's and the
+            # CPU's fp32 rounding: accept only if the GPU's best caption scores (oracle log-prob,
+            # teacher-forced) at least as well as the oracle's best, within 1e-4 per step
+            sg = _seq_score(sd, cfg, images[b:b + 1], mask[b:b + 1], got[b], eos)
+            sr = _seq_score(sd, cfg, images[b:b + 1], mask[b:b + 1], ref[b], eos)
+            assert sg >= sr - 1e-4 * T, (K, eos, b, sg, sr, got[b], ref[b])
+
+
+def _seq_score(sd, cfg, img, mask, seq, eos):
+    """Sum of the oracle's log-probabilities of ``seq``'s tokens after BOS up to its first EOS
+    (or the last column): the beam score of that caption."""
+    T = seq.shape[0]
+    cap = seq.clone().unsqueeze(0)
+    with torch.no_grad():
+        logits = orc.caption_forward(sd, cfg, img, mask, cap, torch.zeros(1, T, dtype=torch.bool))
+    lp = torch.log_softmax(logits[0].double(), -1)
+    total = 0.0
+    for i in range(T - 1):
+        t = int(seq[i + 1])
+        total += float(lp[i, t])
+        if t == eos:
+            break
+    return total
 
 
 def test_beam_cfg5_shape_bf16():

@@ -70,6 +70,80 @@ def test_linear_fwd_dgrad_wgrad(dtype, tol, M, N, K):
     assert rel_err(dw4, ref[:N]) < tol and rel_err(db4, dyc.float().sum(0)[:N]) < tol
 
 
+# grouped launches (csrc/linear_group.hip): shapes of one attention / FFN block, ragged edges
+GROUPS = {
+    "enc_attn": [(6400, 512, 256), (6400, 256, 256), (6400, 256, 256)],
+    "dec_cross": [(2048, 256, 256), (6400, 256, 256), (6400, 256, 256), (2048, 256, 256)],
+    "ffn": [(6400, 2048, 256), (6400, 256, 2048)],
+    "small_ragged": [(100, 64, 64), (37, 136, 72), (513, 264, 128)],
+}
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("name", list(GROUPS))
+def test_linear_groups(dtype, tol, name):
+    shapes = GROUPS[name]
+    g = torch.Generator(device="cpu").manual_seed(len(name))
+    rnd = lambda *s, sc=1.0: (torch.randn(*s, generator=g) * sc).to(DEV)  # noqa: E731
+    # forward: y = relu?(x W^T + b) (+ res), alternating variants, all bf16 / fp32 outputs
+    for y_f32 in (False, True):
+        items, refs = [], []
+        for i, (M, N, K) in enumerate(shapes):
+            x, w, b = rnd(M, K).to(dtype), rnd(N, K, sc=K ** -0.5).to(dtype), rnd(N)
+            relu, res = i % 2, (rnd(M, N) if (y_f32 and i % 2 == 0) else None)
+            y = torch.empty(M, N, device=DEV, dtype=torch.float32 if y_f32 else dtype)
+            items.append((x, w, b, y, relu, res))
+            r = x.float() @ w.float().t() + b
+            r = torch.relu(r) if relu else r
+            refs.append(r + res if res is not None else r)
+        ops.k_linear_fwd_group(items)
+        for it, r in zip(items, refs):
+            assert rel_err(it[3].float(), r) < tol
+    # data gradients: dx = gate(dy W [+ addend]), W read transposed (_TView) or W^T copies
+    for view in (True, False):
+        items, refs = [], []
+        for i, (M, N, K) in enumerate(shapes):
+            dy, w = rnd(M, N).to(dtype), rnd(N, K, sc=N ** -0.5).to(dtype)
+            gate = rnd(M, K).to(dtype) if i % 2 else None
+            add = rnd(M, K) if i == 0 else None
+            dx = torch.empty(M, K, device=DEV)
+            wt = ops._TView(w) if view else w.t().contiguous()
+            items.append((dy, wt, dx, add, gate) if add is not None or gate is not None
+                         else (dy, wt, dx))
+            r = dy.float() @ w.float()
+            r = r + add if add is not None else r
+            refs.append(r * (gate.float() > 0) if gate is not None else r)
+        # addend must be uniformly fp32 or absent within a group: split the first one off
+        ops.k_linear_dgrad_group(items[:1])
+        ops.k_linear_dgrad_group([(it[0], it[1], it[2], None, it[4]) if len(it) > 3 else it
+                                  for it in items[1:]])
+        for it, r in zip(items, refs):
+            assert rel_err(it[2], r) < tol
+    # weight + bias gradients, accumulate and overwrite, twice: bit-identical (ordered sums)
+    for acc in (True, False):
+        items, refs = [], []
+        for i, (M, N, K) in enumerate(shapes):
+            dy, x = rnd(M, N).to(dtype), rnd(M, K).to(dtype)
+            dw = torch.ones(N, K, device=DEV) if acc else torch.full((N, K), float("nan"),
+                                                                     device=DEV)
+            db = (torch.ones(N, device=DEV) if acc else torch.full((N,), float("nan"),
+                                                                   device=DEV)) \
+                if i != 1 else None
+            items.append((dy, x, dw, db, acc))
+            refs.append((dy.float().t() @ x.float() + acc, dy.float().sum(0) + acc))
+        ops.k_linear_wgrad_group(items)
+        first = [(it[2].clone(), None if it[3] is None else it[3].clone()) for it in items]
+        for it, (rw, rb) in zip(items, refs):
+            assert rel_err(it[2], rw) < tol
+            if it[3] is not None:
+                assert rel_err(it[3], rb) < tol
+        if not acc and dtype == torch.bfloat16:   # (fp32 runs the single-GEMM kernels)
+            ops.k_linear_wgrad_group(items)
+            for it, (fw, fb) in zip(items, first):
+                assert torch.equal(it[2], fw)
+                assert fb is None or torch.equal(it[3], fb)
+
+
 CONVS = [  # (N, Cin, H, Cout, k, stride, pad, dil)
     (2, 64, 16, 64, 1, 1, 0, 1),
     (2, 64, 15, 128, 1, 2, 0, 1),
