@@ -79,6 +79,11 @@ enum {
   RETR_TUNE_WGRAD_TILE = 2,     /* grouped weight-gradient tile: 64 or 128 */
   RETR_TUNE_WGRAD_STAGES = 3,   /* its ring depth: 2|4 (64), 2|3 (128) */
   RETR_TUNE_WGRAD_KC = 4,       /* weight-gradient K-slice length in tokens (multiple of 64) */
+  RETR_TUNE_ATTN_MODE = 5,      /* bf16 attention: 1 streaming K/V tiles, 2 LDS-resident */
+  RETR_TUNE_BIG_TILE = 6,       /* large bf16 GEMMs (convs): 1 128x128 S1, 2 128x128 S2,
+                                   3 256x256, 4 128x64 S3, 5 reg-staged 64x64, 6 64x64 S2,
+                                   7 128x128 S1 one epilogue band */
+  RETR_TUNE_NT_STORE = 7,       /* 1: non-temporal GEMM output stores */
   RETR_TUNE_COUNT = 8
 };
 int retr_tune(int knob, int value);

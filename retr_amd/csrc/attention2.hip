@@ -255,6 +255,572 @@ int launch_fwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
   return retr_check_launch("attention_fwd2");
 }
 
+// =============================================================================================
+// Sequence-resident variants (fwd3 / dq3 / dkdv3).  At the RE⫶TR sizes (S = 400 image tokens,
+// T = 128 caption tokens, hd 32) a block's whole K/V (or Q/dO) slice is 28-64 KB: it is pulled
+// into LDS once with LDS-DMA (global_load_lds_dwordx4, every tile in flight together, one
+// vmcnt(0) + barrier), and the tile loop then runs from LDS with no per-tile load latency,
+// register staging or barriers.  Rows are unpadded and XOR-swizzled by 16-byte chunk
+// (chunk' = chunk ^ (row / rows-per-256-byte-sweep)), applied on the source side of the DMA,
+// so both the row-fragment reads and the ds_read_b64_tr_b16 transposed reads are
+// bank-conflict-free.  The math per tile is the streaming kernels' (same fragments, same
+// order), so results are bit-identical to them.
+// =============================================================================================
+
+static __device__ __attribute__((aligned(64))) unsigned int g_attn_zero[64];
+
+template <int HD>
+struct RL {
+  static constexpr int RB = HD * 2;           // row bytes
+  static constexpr int CPR = HD / 8;          // 16-byte chunks per row
+  static constexpr int RPW = 256 / RB;        // rows per 256-byte bank sweep
+  static constexpr int TILE = 64 * RB;        // one 64-row tile
+  RETR_DEVICE static int swz(int r) { return (r / RPW) & (CPR - 1); }
+  // byte offset of logical 16-byte chunk lc of row r
+  RETR_DEVICE static int off(int r, int lc) { return r * RB + ((lc ^ swz(r)) << 4); }
+  // byte offset of element column `col` (8-byte aligned group) of row r
+  RETR_DEVICE static int offc(int r, int col) {
+    return r * RB + ((((col >> 3) ^ swz(r))) << 4) + (col & 7) * 2;
+  }
+};
+
+// DMA rows [0, ntiles*64) of a [rows][ld] bf16 slice (rows >= valid read zeros) into the
+// swizzled image at `lds`; wave w issues instructions w, w + NW, ...
+template <int HD, int NW>
+RETR_DEVICE void dma_rows(char* lds, const bf16* base, long ld, int ntiles, int valid, int wave,
+                          int lane) {
+  using L = RL<HD>;
+  const int ninstr = ntiles * 64 * L::CPR / 64;
+  for (int i = wave; i < ninstr; i += NW) {
+    const int j = i * 64 + lane;
+    const int row = j / L::CPR, pc = j % L::CPR;
+    const int lc = pc ^ L::swz(row);
+    const void* src = row < valid ? (const void*)(base + (long)row * ld + lc * 8)
+                                  : (const void*)g_attn_zero;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(lds + i * 1024),
+                                     16, 0, 0);
+  }
+}
+
+RETR_DEVICE void dma_drain_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
+template <int HD>
+size_t res_lds_fwd(int ntiles) { return (size_t)2 * ntiles * RL<HD>::TILE + 8 * ntiles; }
+template <int HD>
+size_t res_lds_dkdv(int ntiles) { return (size_t)2 * ntiles * RL<HD>::TILE + 12 * 64 * ntiles; }
+
+template <int HD, int NW>
+__global__ void __launch_bounds__(NW * 64)
+attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
+                 bf16* o, long ldo, int H, int Lq, int Lk, int kbr, const unsigned char* kpm,
+                 int causal, float qscale, DropoutParams dp, float* lse, int ntiles_max) {
+  using L = RL<HD>;
+  constexpr int KS = HD / 16, DT = HD / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int qblk = blockIdx.x * (32 * NW);
+  const int q0 = qblk + wave * 32;
+  const int qi = q0 + r;
+  const bf16* kb = k + (long)b * kbr * ldk + h * HD;
+  const bf16* vb = v + (long)b * kbr * ldv + h * HD;
+
+  int kend = Lk;
+  if (causal) kend = min(Lk, qblk + 32 * NW);
+  const int ntiles = (kend + 63) / 64;
+  char* Ks = smem;
+  char* Vs = smem + (size_t)ntiles_max * L::TILE;
+  unsigned long long* pm = (unsigned long long*)(smem + (size_t)2 * ntiles_max * L::TILE);
+  dma_rows<HD, NW>(Ks, kb, ldk, ntiles, kend, wave, lane);
+  dma_rows<HD, NW>(Vs, vb, ldv, ntiles, kend, wave, lane);
+  for (int t = wave; t < ntiles; t += NW) {
+    const int key = t * 64 + lane;
+    bool pad = key >= Lk;
+    if (kpm && !pad) pad = kpm[(long)b * Lk + key] != 0;
+    const unsigned long long bm = __ballot(pad);
+    if (lane == 0) pm[t] = bm;
+  }
+
+  bf16x8 qf[KS];
+  {
+    const bf16* qr = q + ((long)b * Lq + (qi < Lq ? qi : Lq - 1)) * ldq + h * HD;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 x = *(const bf16x8*)(qr + 16 * s + 8 * hh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * qscale);
+      qf[s] = x;
+    }
+  }
+  const bool drop = dp.thresh != 0;
+  const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
+  const uint32_t rowkey = drop ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
+
+  f32x16 O[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) O[dt][e] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  dma_drain_barrier();
+
+  // a wave's own causal range can end before the block's
+  const int wtiles = causal ? min(ntiles, (q0 + 32 + 63) / 64) : ntiles;
+  for (int t = 0; t < wtiles; ++t) {
+    const int key0 = t * 64;
+    const char* Kl = Ks + t * L::TILE;
+    const char* Vl = Vs + t * L::TILE;
+    const unsigned long long pmask = pm[t];
+    const bool diag = causal && (key0 + 63 > q0);
+    f32x16 S[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) S[sub][e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8 a = *(const bf16x8*)(Kl + L::off(sub * 32 + r, 2 * s + hh));
+        S[sub] = mfma32(a, qf[s], S[sub]);
+      }
+    }
+    if (pmask || diag) {
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int kl = sub * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+          if (((pmask >> kl) & 1ull) || (diag && key0 + kl > qi)) S[sub][e] = -INFINITY;
+        }
+    }
+    float mt = -INFINITY;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) mt = fmaxf(mt, S[sub][e]);
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float mn = fmaxf(m, mt);
+    const float alpha = (mn == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mn);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) O[dt][e] *= alpha;
+    bf16x8 pf[4];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int kk = key0 + sub * 32 + 8 * g + 4 * hh;
+        uint32_t b01 = 0, b23 = 0;
+        if (drop) {
+          b01 = attn_pair_bits(rowkey, kk);
+          b23 = attn_pair_bits(rowkey, kk + 2);
+        }
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const int e = 4 * g + e4;
+          float p = (mn == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(S[sub][e] - mn);
+          l += p;
+          if (drop) {
+            const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
+            p = kp ? p * dp.scale : 0.f;
+          }
+          pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
+        }
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      const int qrow = (lane & 15) >> 2;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int row = 16 * s + 4 * hh + qrow;
+        const bf16x8 a = join(tr16(Vl + L::offc(row, c0)), tr16(Vl + L::offc(row + 8, c0)));
+        O[dt] = mfma32(a, pf[s], O[dt]);
+      }
+    }
+  }
+
+  l += __shfl_xor(l, 32, 64);
+  if (qi < Lq) {
+    const float inv = 1.f / l;
+    bf16* orow = o + ((long)b * Lq + qi) * ldo + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 w;
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) w[e4] = (bf16)(O[dt][4 * g + e4] * inv);
+        *(bf16x4*)(orow + dt * 32 + 8 * g + 4 * hh) = w;
+      }
+    if (hh == 0 && lse) lse[((long)b * H + h) * Lq + qi] = (m + __log2f(l)) * kLn2;
+  }
+}
+
+template <int HD, int NW>
+__global__ void __launch_bounds__(NW * 64)
+attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
+                    const bf16* o, long ldo, const bf16* dout, long lddo, const float* lse,
+                    float* Dout, bf16* dq, long lddq, int H, int Lq, int Lk,
+                    const unsigned char* kpm, int causal, float qscale, float scale,
+                    DropoutParams dp, int ntiles_max) {
+  using L = RL<HD>;
+  constexpr int KS = HD / 16, DT = HD / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int qblk = blockIdx.x * (32 * NW);
+  const int q0 = qblk + wave * 32;
+  const int qi = q0 + r;
+  const int qc = qi < Lq ? qi : Lq - 1;
+  const bf16* kb = k + (long)b * Lk * ldk + h * HD;
+  const bf16* vb = v + (long)b * Lk * ldv + h * HD;
+  const long srow = ((long)b * H + h) * Lq + qc;
+
+  int kend = Lk;
+  if (causal) kend = min(Lk, qblk + 32 * NW);
+  const int ntiles = (kend + 63) / 64;
+  char* Ks = smem;
+  char* Vs = smem + (size_t)ntiles_max * L::TILE;
+  unsigned long long* pm = (unsigned long long*)(smem + (size_t)2 * ntiles_max * L::TILE);
+  dma_rows<HD, NW>(Ks, kb, ldk, ntiles, kend, wave, lane);
+  dma_rows<HD, NW>(Vs, vb, ldv, ntiles, kend, wave, lane);
+  for (int t = wave; t < ntiles; t += NW) {
+    const int key = t * 64 + lane;
+    bool pad = key >= Lk;
+    if (kpm && !pad) pad = kpm[(long)b * Lk + key] != 0;
+    const unsigned long long bm = __ballot(pad);
+    if (lane == 0) pm[t] = bm;
+  }
+
+  bf16x8 qf[KS], dof[KS];
+  float dpart = 0.f;
+  {
+    const bf16* qr = q + ((long)b * Lq + qc) * ldq + h * HD;
+    const bf16* dr = dout + ((long)b * Lq + qc) * lddo + h * HD;
+    const bf16* orr = o + ((long)b * Lq + qc) * ldo + h * HD;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 x = *(const bf16x8*)(qr + 16 * s + 8 * hh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * qscale);
+      qf[s] = x;
+      const bf16x8 d8 = *(const bf16x8*)(dr + 16 * s + 8 * hh);
+      const bf16x8 o8 = *(const bf16x8*)(orr + 16 * s + 8 * hh);
+      dof[s] = d8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dpart += (float)d8[j] * (float)o8[j];
+    }
+  }
+  const float Dq = dpart + __shfl_xor(dpart, 32, 64);
+  if (hh == 0 && qi < Lq) Dout[srow] = Dq;
+  const float lq2 = lse[srow] * kLog2e;
+  const bool drop = dp.thresh != 0;
+  const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
+  const uint32_t rowkey = drop ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
+
+  f32x16 G[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) G[dt][e] = 0.f;
+  dma_drain_barrier();
+
+  const int wtiles = causal ? min(ntiles, (q0 + 32 + 63) / 64) : ntiles;
+  for (int t = 0; t < wtiles; ++t) {
+    const int key0 = t * 64;
+    const char* Kl = Ks + t * L::TILE;
+    const char* Vl = Vs + t * L::TILE;
+    const unsigned long long pmask = pm[t];
+    const bool diag = causal && (key0 + 63 > q0);
+    bf16x8 sf[4];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x16 S, P;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) S[e] = 0.f, P[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int off = L::off(sub * 32 + r, 2 * s + hh);
+        S = mfma32(*(const bf16x8*)(Kl + off), qf[s], S);
+        P = mfma32(*(const bf16x8*)(Vl + off), dof[s], P);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int kk = key0 + sub * 32 + 8 * g + 4 * hh;
+        uint32_t b01 = 0, b23 = 0;
+        if (drop) {
+          b01 = attn_pair_bits(rowkey, kk);
+          b23 = attn_pair_bits(rowkey, kk + 2);
+        }
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
+          const bool msk = ((pmask >> kl) & 1ull) || (diag && key0 + kl > qi);
+          const float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - lq2);
+          float dpv = P[e];
+          if (drop) dpv = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? dpv * dp.scale : 0.f;
+          sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - Dq));
+        }
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      const int qrow = (lane & 15) >> 2;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int row = 16 * s + 4 * hh + qrow;
+        G[dt] = mfma32(join(tr16(Kl + L::offc(row, c0)), tr16(Kl + L::offc(row + 8, c0))),
+                       sf[s], G[dt]);
+      }
+    }
+  }
+  if (qi < Lq) {
+    bf16* row = dq + ((long)b * Lq + qi) * lddq + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 w;
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) w[e4] = (bf16)(G[dt][4 * g + e4] * scale);
+        *(bf16x4*)(row + dt * 32 + 8 * g + 4 * hh) = w;
+      }
+  }
+}
+
+template <int HD, int NW>
+__global__ void __launch_bounds__(NW * 64)
+attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v,
+                      long ldv, const bf16* dout, long lddo, const float* lse, const float* D,
+                      bf16* dk, long lddk, bf16* dv, long lddv, int H, int Lq, int Lk,
+                      const unsigned char* kpm, int causal, float kscale, float scale,
+                      DropoutParams dp, int ntiles_max) {
+  using L = RL<HD>;
+  constexpr int KS = HD / 16, DT = HD / 32, NT = NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int kblk = blockIdx.x * (32 * NW);
+  const int kj = kblk + wave * 32 + r;
+  const int kc = kj < Lk ? kj : Lk - 1;
+  const bf16* qb = q + (long)b * Lq * ldq + h * HD;
+  const bf16* db = dout + (long)b * Lq * lddo + h * HD;
+  const long sbase = ((long)b * H + h) * Lq;
+  const bool drop = dp.thresh != 0;
+  const uint64_t seed = drop ? dp_seed(dp) : 0ull;
+
+  // queries [qstart, Lq) resident: tiles are numbered from qstart (causal skips the rows no key
+  // of this block sees)
+  const int qstart = causal ? (kblk / 64) * 64 : 0;
+  const int ntiles = (Lq - qstart + 63) / 64;
+  char* Qs = smem;
+  char* Ds = smem + (size_t)ntiles_max * L::TILE;
+  float* exl = (float*)(smem + (size_t)2 * ntiles_max * L::TILE);   // lse * log2e
+  float* exd = exl + 64 * ntiles_max;                                 // D
+  uint32_t* exk = (uint32_t*)(exd + 64 * ntiles_max);                 // dropout row keys
+  dma_rows<HD, NW>(Qs, qb + (long)qstart * ldq, ldq, ntiles, Lq - qstart, wave, lane);
+  dma_rows<HD, NW>(Ds, db + (long)qstart * lddo, lddo, ntiles, Lq - qstart, wave, lane);
+  for (int i = tid; i < ntiles * 64; i += NT) {
+    const int qq = qstart + i;
+    const int qcl = qq < Lq ? qq : Lq - 1;
+    exl[i] = lse[sbase + qcl] * kLog2e;
+    exd[i] = D[sbase + qcl];
+    exk[i] = drop ? attn_row_key(seed, (uint32_t)((b * H + h) * Lq) + (uint32_t)qq) : 0u;
+  }
+
+  bf16x8 kf[KS], vf[KS];
+  {
+    const bf16* kr = k + ((long)b * Lk + kc) * ldk + h * HD;
+    const bf16* vr = v + ((long)b * Lk + kc) * ldv + h * HD;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 x = *(const bf16x8*)(kr + 16 * s + 8 * hh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * kscale);
+      kf[s] = x;
+      vf[s] = *(const bf16x8*)(vr + 16 * s + 8 * hh);
+    }
+  }
+  const bool kmask = kj >= Lk || (kpm && kpm[(long)b * Lk + kc]);
+  const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
+
+  f32x16 GK[DT], GV[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) GK[dt][e] = 0.f, GV[dt][e] = 0.f;
+  dma_drain_barrier();
+
+  // a wave's keys see no query below its first key (causal): skip those tiles
+  const int wt0 = causal ? max(0, (kblk + wave * 32 - qstart) / 64) : 0;
+  for (int it = wt0; it < ntiles; ++it) {
+    const int qt = qstart + it * 64;
+    const char* Ql = Qs + it * L::TILE;
+    const char* Dl = Ds + it * L::TILE;
+    const float* el = exl + it * 64;
+    const float* ed = exd + it * 64;
+    const uint32_t* ek = exk + it * 64;
+    bf16x8 pf[4], sf[4];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x16 S, P;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) S[e] = 0.f, P[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int off = L::off(sub * 32 + r, 2 * s + hh);
+        S = mfma32(*(const bf16x8*)(Ql + off), kf[s], S);
+        P = mfma32(*(const bf16x8*)(Dl + off), vf[s], P);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ql = sub * 32 + 8 * g + 4 * hh;
+        const f32x4 l4 = *(const f32x4*)(el + ql);
+        const f32x4 d4 = *(const f32x4*)(ed + ql);
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const int e = 4 * g + e4, qq = qt + ql + e4;
+          const bool msk = kmask || qq >= Lq || (causal && kj > qq);
+          float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - l4[e4]);
+          float dpv = P[e], pmv = p;
+          if (drop) {
+            const bool kp = attn_keep(attn_pair_bits(ek[ql + e4], (uint32_t)kj), (uint32_t)kj,
+                                      th16);
+            dpv = kp ? dpv * dp.scale : 0.f;
+            pmv = kp ? p * dp.scale : 0.f;
+          }
+          pf[2 * sub + (e >> 3)][e & 7] = (bf16)pmv;
+          sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - d4[e4]));
+        }
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+      const int qrow = (lane & 15) >> 2;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int row = 16 * s + 4 * hh + qrow;
+        GV[dt] = mfma32(join(tr16(Dl + L::offc(row, c0)), tr16(Dl + L::offc(row + 8, c0))),
+                        pf[s], GV[dt]);
+        GK[dt] = mfma32(join(tr16(Ql + L::offc(row, c0)), tr16(Ql + L::offc(row + 8, c0))),
+                        sf[s], GK[dt]);
+      }
+    }
+  }
+  if (kj < Lk) {
+    bf16* krow = dk + ((long)b * Lk + kj) * lddk + h * HD;
+    bf16* vrow = dv + ((long)b * Lk + kj) * lddv + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 wk, wv;
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          wk[e4] = (bf16)(GK[dt][4 * g + e4] * scale);
+          wv[e4] = (bf16)GV[dt][4 * g + e4];
+        }
+        *(bf16x4*)(krow + dt * 32 + 8 * g + 4 * hh) = wk;
+        *(bf16x4*)(vrow + dt * 32 + 8 * g + 4 * hh) = wv;
+      }
+  }
+}
+
+constexpr size_t kResLdsMax = 80 * 1024;   // two blocks per CU
+
+template <class K>
+void allow_lds(K kern, size_t lds) {
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+}
+
+// resident mode: 0 auto, 1 streaming kernels only, 2 resident whenever it fits
+int attn_res_mode() { return retr_tune_get(RETR_TUNE_ATTN_MODE); }
+
+template <int HD, int NW>
+int launch_fwd3(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+                void* o, long ldo, int B, int H, int Lq, int Lk, const unsigned char* kpm,
+                int causal, float p, unsigned long long seed, float* lse, hipStream_t st) {
+  const float qscale = kLog2e / sqrtf((float)HD);
+  const int nt = (Lk + 63) / 64;
+  const size_t lds = res_lds_fwd<HD>(nt);
+  auto kern = attn_fwd3_kernel<HD, NW>;
+  allow_lds(kern, lds);
+  dim3 grid((Lq + 32 * NW - 1) / (32 * NW), H, B);
+  hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, st, (const bf16*)q, ldq, (const bf16*)k,
+                     ldk, (const bf16*)v, ldv, (bf16*)o, ldo, H, Lq, Lk, Lk, kpm, causal, qscale,
+                     make_dp(p, seed), lse, nt);
+  return retr_check_launch("attention_fwd3");
+}
+
+template <int HD, int NW>
+int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+                const void* o, long ldo, const void* dout, long lddo, const float* lse,
+                void* dq, long lddq, void* dk, long lddk, void* dv, long lddv, int B, int H,
+                int Lq, int Lk, const unsigned char* kpm, int causal, float p,
+                unsigned long long seed, float* D, int nwq, int nwk, hipStream_t st) {
+  const float scale = 1.f / sqrtf((float)HD);
+  const float cs = kLog2e * scale;
+  const DropoutParams dp = make_dp(p, seed);
+  const int ntk = (Lk + 63) / 64, ntq = (Lq + 63) / 64;
+  {
+    const size_t lds = res_lds_fwd<HD>(ntk);
+    if (nwq == 4) {
+      auto kern = attn_bwd_dq3_kernel<HD, 4>;
+      allow_lds(kern, lds);
+      hipLaunchKernelGGL(kern, dim3((Lq + 127) / 128, H, B), dim3(256), lds, st, (const bf16*)q,
+                         ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
+                         (const bf16*)dout, lddo, lse, D, (bf16*)dq, lddq, H, Lq, Lk, kpm, causal,
+                         cs, scale, dp, ntk);
+    } else {
+      auto kern = attn_bwd_dq3_kernel<HD, 2>;
+      allow_lds(kern, lds);
+      hipLaunchKernelGGL(kern, dim3((Lq + 63) / 64, H, B), dim3(128), lds, st, (const bf16*)q,
+                         ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
+                         (const bf16*)dout, lddo, lse, D, (bf16*)dq, lddq, H, Lq, Lk, kpm, causal,
+                         cs, scale, dp, ntk);
+    }
+    if (int e = retr_check_launch("attention_bwd_dq3")) return e;
+  }
+  const size_t lds = res_lds_dkdv<HD>(ntq);
+  if (nwk == 4) {
+    auto kern = attn_bwd_dkdv3_kernel<HD, 4>;
+    allow_lds(kern, lds);
+    hipLaunchKernelGGL(kern, dim3((Lk + 127) / 128, H, B), dim3(256), lds, st, (const bf16*)q,
+                       ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo, lse,
+                       D, (bf16*)dk, lddk, (bf16*)dv, lddv, H, Lq, Lk, kpm, causal, cs, scale, dp,
+                       ntq);
+  } else {
+    auto kern = attn_bwd_dkdv3_kernel<HD, 2>;
+    allow_lds(kern, lds);
+    hipLaunchKernelGGL(kern, dim3((Lk + 63) / 64, H, B), dim3(128), lds, st, (const bf16*)q,
+                       ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo, lse,
+                       D, (bf16*)dk, lddk, (bf16*)dv, lddv, H, Lq, Lk, kpm, causal, cs, scale, dp,
+                       ntq);
+  }
+  return retr_check_launch("attention_bwd_dkdv3");
+}
+
+// 4 waves per block when that still gives >= 384 blocks, else 2
+inline int pick_nw(int B, int H, int L) { return (long)B * H * ((L + 127) / 128) >= 384 ? 4 : 2; }
+
 }  // namespace
 
 // Internal entry (called by retr_attention_fwd for bf16 with hd in {32, 64}).
@@ -262,6 +828,17 @@ int retr_attention_fwd2(const void* q, long ldq, const void* k, long ldk, const 
                         long ldv, void* o, long ldo, int B, int H, int Lq, int Lk, int hd,
                         const unsigned char* kpm, int causal, float p, unsigned long long seed,
                         float* lse, hipStream_t st) {
+  const int mode = attn_res_mode();
+  const int ntk = (Lk + 63) / 64;
+  const bool fits = hd == 32 ? res_lds_fwd<32>(ntk) <= kResLdsMax : res_lds_fwd<64>(ntk) <= kResLdsMax;
+  if (mode != 1 && fits) {
+    const int nw = pick_nw(B, H, Lq);
+    if (hd == 32)
+      return nw == 4 ? launch_fwd3<32, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, st)
+                     : launch_fwd3<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, st);
+    return nw == 4 ? launch_fwd3<64, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, st)
+                   : launch_fwd3<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, st);
+  }
   const bool big = (long)B * H * ((Lq + 63) / 64) >= 1024;
   if (hd == 32) {
     return big ? launch_fwd2<32, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st)
@@ -599,6 +1176,19 @@ int retr_attention_bwd2(const void* q, long ldq, const void* k, long ldk, const 
                         long lddv, int B, int H, int Lq, int Lk, int hd,
                         const unsigned char* kpm, int causal, float p, unsigned long long seed,
                         float* D, hipStream_t st) {
+  const int mode = attn_res_mode();
+  const int ntk = (Lk + 63) / 64, ntq = (Lq + 63) / 64;
+  const bool fits = hd == 32 ? (res_lds_fwd<32>(ntk) <= kResLdsMax && res_lds_dkdv<32>(ntq) <= kResLdsMax)
+                             : (res_lds_fwd<64>(ntk) <= kResLdsMax && res_lds_dkdv<64>(ntq) <= kResLdsMax);
+  if (mode != 1 && fits) {
+    const int nwq = pick_nw(B, H, Lq), nwk = pick_nw(B, H, Lk);
+    if (hd == 32)
+      return launch_bwd3<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk,
+                                lddk, dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, nwq, nwk,
+                                st);
+    return launch_bwd3<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk,
+                              lddk, dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, nwq, nwk, st);
+  }
   if (hd == 32)
     return launch_bwd2<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk,
                               lddk, dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, st);

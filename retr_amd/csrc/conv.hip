@@ -283,6 +283,11 @@ struct EpiPhaseRows {
   }
   RETR_DEVICE void apply(int m, int n, float v) const { ep.apply(map(m), n, v); }
   RETR_DEVICE void apply8(int m, int n, float (&v)[8]) const { ep.apply8(map(m), n, v); }
+  using Pre = typename EP::Pre;
+  RETR_DEVICE void fetch8(int m, int n, Pre& p) const { ep.fetch8(map(m), n, p); }
+  RETR_DEVICE void apply8p(int m, int n, float (&v)[8], const Pre& p) const {
+    ep.apply8p(map(m), n, v, p);
+  }
   RETR_DEVICE void empty_split(int, int) const {}
   RETR_DEVICE bool lane_contiguous() const { return false; }
 };
@@ -360,6 +365,34 @@ int conv_fwd_t(const void* x, Geom g, const void* w, const float* bias, const vo
   return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd");
 }
 
+// dx = gate(addend) (or 0) at the pixels of the tap-less stride-2 phases in `zmask`
+// (bit (ih % 2) * 2 + iw % 2); 8 channels per thread
+__global__ void dgrad_phase_fill_kernel(bf16* dx, const bf16* addend, const bf16* gate, int H,
+                                        int W, int C, long chunks, int zmask) {
+  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (i >= chunks) return;
+  const int cpp = C / 8;
+  const long p = i / cpp;
+  const int c = (int)(i - p * cpp) * 8;
+  const int iw = (int)(p % W), ih = (int)((p / W) % H);
+  if (!((zmask >> ((ih & 1) * 2 + (iw & 1))) & 1)) return;
+  const long off = p * C + c;
+  bf16x8 v;
+  if (addend) {
+    v = *(const bf16x8*)(addend + off);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (bf16)0.f;
+  }
+  if (gate) {
+    const bf16x8 gg = *(const bf16x8*)(gate + off);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (!((float)gg[e] > 0.f)) v[e] = (bf16)0.f;
+  }
+  *(bf16x8*)(dx + off) = v;
+}
+
 template <typename T>
 int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* addend,
                  const void* gate, hipStream_t st) {
@@ -372,6 +405,27 @@ int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* a
     return launch_auto<kFamConvDgrad, T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad_1x1");
   }
   if (g.s == 2 && g.d == 1) {
+    // phases with no taps (a 1x1 stride-2 kernel reaches one pixel in four): dx = gate(addend)
+    // there, written by one elementwise pass instead of K = 0 GEMM launches
+    int zmask = 0;
+    for (int a = 0; a < 2; ++a)
+      for (int bb = 0; bb < 2; ++bb) {
+        const int nkh = g.KH > a ? (g.KH - a + 1) / 2 : 0;
+        const int nkw = g.KW > bb ? (g.KW - bb + 1) / 2 : 0;
+        if (nkh * nkw == 0) {
+          const int ih0 = ((a - g.p) % 2 + 2) % 2, iw0 = ((bb - g.p) % 2 + 2) % 2;
+          zmask |= 1 << (ih0 * 2 + iw0);
+        }
+      }
+    if (zmask && sizeof(T) == 2 && N % 8 == 0) {
+      const long chunks = (long)M * (N / 8);
+      hipLaunchKernelGGL(dgrad_phase_fill_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0,
+                         st, (bf16*)dx, (const bf16*)addend, (const bf16*)gate, g.H, g.W, N,
+                         chunks, zmask);
+      if (int e = retr_check_launch("conv_dgrad_phase_fill")) return e;
+    } else {
+      zmask = 0;
+    }
     for (int a = 0; a < 2; ++a)
       for (int bb = 0; bb < 2; ++bb) {
         Phase ph;
@@ -385,6 +439,7 @@ int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* a
         ph.nkw = g.KW > bb ? (g.KW - bb + 1) / 2 : 0;
         const int Mp = g.Nb * ph.Hp * ph.Wp, Kp = ph.nkh * ph.nkw * g.Co;
         if (Mp == 0) continue;
+        if (Kp == 0 && (zmask >> (ph.ih0 * 2 + ph.iw0) & 1)) continue;
         ConvDgradPhaseA<T> pa{(const T*)dy, g, ph, Mp, Kp};
         DgradPhaseW<T> pb{(const T*)wt, g, ph, N, Kp};
         EpiPhaseRows<EpiDgrad<T, T, T>> pe{ep, ph.Hp, ph.Wp, g.H, g.W, ph.ih0, ph.iw0};

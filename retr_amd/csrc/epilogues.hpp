@@ -3,6 +3,7 @@
 // vector accesses are 16-byte (bf16 x 8) or 2 x 16-byte (f32 x 8); an epilogue falls back to
 // scalar accesses when one of its row strides / base pointers is not 8-element aligned.
 #pragma once
+#include "../../include/retr_hip.h"
 #include "common.hpp"
 
 namespace retr {
@@ -28,6 +29,31 @@ template <> RETR_DEVICE void store8<bf16>(bf16* p, const float (&v)[8]) {
 template <> RETR_DEVICE void store8<float>(float* p, const float (&v)[8]) {
   *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
   *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+// 8 raw elements as loaded (bf16: one 16-byte register quad), widened at use
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16> {
+  bf16x8 x;
+  RETR_DEVICE void load(const bf16* p) { x = *(const bf16x8*)p; }
+  RETR_DEVICE float operator[](int e) const { return (float)x[e]; }
+};
+template <> struct Raw8<float> {
+  f32x4 a, b;
+  RETR_DEVICE void load(const float* p) { a = *(const f32x4*)p; b = *(const f32x4*)(p + 4); }
+  RETR_DEVICE float operator[](int e) const { return e < 4 ? a[e] : b[e - 4]; }
+};
+
+// streaming (non-temporal) variant: outputs read back only by a later kernel
+template <typename T> RETR_DEVICE void store8_nt(T* p, const float (&v)[8]);
+template <> RETR_DEVICE void store8_nt<bf16>(bf16* p, const float (&v)[8]) {
+  bf16x8 x;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = (bf16)v[e];
+  __builtin_nontemporal_store(__builtin_bit_cast(u32x4, x), (u32x4*)p);
+}
+template <> RETR_DEVICE void store8_nt<float>(float* p, const float (&v)[8]) {
+  __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, (f32x4*)p);
+  __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, (f32x4*)(p + 4));
 }
 
 // host helper: can rows of `ld` elements starting at `p` be accessed 8-wide?
@@ -88,14 +114,51 @@ struct EpiFwd {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
-    store8<TO>(out + (long)m * ldo + n, v);
+    if (nt) store8_nt<TO>(out + (long)m * ldo + n, v);
+    else store8<TO>(out + (long)m * ldo + n, v);
+  }
+  // operand prefetch: the GEMM issues every residual load of an epilogue band before it
+  // stages the accumulators, so the band's loads are in flight together
+  struct Pre {
+    Raw8<TR> r;
+  };
+  RETR_DEVICE void fetch8(int m, int n, Pre& p) const {
+    if (vec && res) p.r.load(res + (long)m * ldr + n);
+  }
+  RETR_DEVICE void apply8p(int m, int n, float (&v)[8], const Pre& p) const {
+    if (!vec || !res) return apply8(m, n, v);
+    if (bias) {
+      float b[8];
+      load8<float>(bias + n, b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += b[e];
+    }
+    if (relu == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (dp.thresh) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = retr_keep(dp_seed(dp), (uint64_t)m * drop_ld + n + e, dp.thresh) ? v[e] * dp.scale : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += p.r[e];
+    if (relu == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (nt) store8_nt<TO>(out + (long)m * ldo + n, v);
+    else store8<TO>(out + (long)m * ldo + n, v);
   }
   RETR_DEVICE void empty_split(int, int) const {}
   RETR_DEVICE bool lane_contiguous() const { return false; }
   static constexpr bool kRowSum = false;
   float* rowsum = nullptr;
+  int nt = 0;          // non-temporal output stores
   void set_vec() {
     vec = vec8_ok<TO>(out, ldo) && vec8_ok<TR>(res, ldr) && vec8_ok<float>(bias, 8);
+    nt = retr_tune_get(RETR_TUNE_NT_STORE) == 1;
   }
 };
 
@@ -132,13 +195,40 @@ struct EpiDgrad {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = g[e] > 0.f ? v[e] : 0.f;
     }
-    store8<TO>(out + (long)m * ldo + n, v);
+    if (nt) store8_nt<TO>(out + (long)m * ldo + n, v);
+    else store8<TO>(out + (long)m * ldo + n, v);
+  }
+  struct Pre {
+    Raw8<TA> a;
+    Raw8<TG> g;
+  };
+  RETR_DEVICE void fetch8(int m, int n, Pre& p) const {
+    if (!vec) return;
+    if (addend) p.a.load(addend + (long)m * lda + n);
+    if (gate) p.g.load(gate + (long)m * ldg + n);
+  }
+  RETR_DEVICE void apply8p(int m, int n, float (&v)[8], const Pre& p) const {
+    if (!vec) return apply8(m, n, v);
+    if (addend) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += p.a[e];
+    }
+    if (gate) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = p.g[e] > 0.f ? v[e] : 0.f;
+    }
+    if (nt) store8_nt<TO>(out + (long)m * ldo + n, v);
+    else store8<TO>(out + (long)m * ldo + n, v);
   }
   RETR_DEVICE void empty_split(int, int) const {}
   RETR_DEVICE bool lane_contiguous() const { return false; }
   static constexpr bool kRowSum = false;
   float* rowsum = nullptr;
-  void set_vec() { vec = vec8_ok<TO>(out, ldo) && vec8_ok<TA>(addend, lda) && vec8_ok<TG>(gate, ldg); }
+  int nt = 0;          // non-temporal output stores
+  void set_vec() {
+    vec = vec8_ok<TO>(out, ldo) && vec8_ok<TA>(addend, lda) && vec8_ok<TG>(gate, ldg);
+    nt = retr_tune_get(RETR_TUNE_NT_STORE) == 1;
+  }
 };
 
 // fp32 weight-gradient target: atomic when the GEMM is split over K (target pre-zeroed or

@@ -21,6 +21,7 @@
 #include <utility>
 
 #include "gemm.hpp"
+#include "../../include/retr_hip.h"
 
 namespace retr {
 
@@ -99,6 +100,19 @@ constexpr size_t gemm2_lds_bytes() {
 
 // EPB: epilogue row bands (0 = as few as fit in LDS); S = 1: single-buffered (small-K GEMMs,
 // where the LDS footprint, not the pipeline depth, limits the blocks per CU)
+template <class E, class = void>
+struct has_prefetch : std::false_type {};
+template <class E>
+struct has_prefetch<E, std::void_t<typename E::Pre>> : std::true_type {};
+template <class E, class = void>
+struct PreOf {
+  struct type {};
+};
+template <class E>
+struct PreOf<E, std::void_t<typename E::Pre>> {
+  using type = typename E::Pre;
+};
+
 // XCD-aware block order: hardware dispatches block b to XCD b % 8; consecutive logical
 // blocks (neighbouring tiles sharing operand rows) land on one XCD and share its L2
 RETR_DEVICE int xcd_remap(int bid, int nblk) {
@@ -194,10 +208,53 @@ RETR_DEVICE __attribute__((always_inline)) void gemm2_tile(const LA& la, const L
   constexpr int CS = BN + 4;
   constexpr int EP_PASSES = epi_bands<BM, BN, EPB>();
   constexpr int BAND = BM / EP_PASSES;
+  constexpr int CH = BN / 8;
+  constexpr int IT = BAND * CH / NT;            // 8-column chunks per thread per band
+  constexpr bool kPre = has_prefetch<EP>::value && (BAND * CH) % NT == 0 && IT <= 4;
   float* ct = (float*)smem;
 #pragma unroll
   for (int pass = 0; pass < EP_PASSES; ++pass) {
     if (pass > 0) __syncthreads();
+    if constexpr (kPre) {
+      // the band's epilogue operands (residual / addend / gate): all loads in flight while the
+      // accumulators go through LDS
+      typename PreOf<EP>::type pre[IT];
+      const int mb = m0 + pass * BAND;
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int q = tid + it * NT;
+        const int r = q / CH, c = (q % CH) * 8;
+        const int m = mb + r, n = n0 + c;
+        if (m < M && n + 8 <= N) ep.fetch8(m, n, pre[it]);
+      }
+      if (wm / (WM / EP_PASSES) == pass) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              ct[(wm * WTM - pass * BAND + 16 * i + 4 * (lane >> 4) + e) * CS + wn * WTN +
+                 16 * j + (lane & 15)] = acc[i][j][e];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int q = tid + it * NT;
+        const int r = q / CH, c = (q % CH) * 8;
+        const int m = mb + r, n = n0 + c;
+        if (m >= M || n >= N) continue;
+        const f32x4 lo = *(const f32x4*)(ct + r * CS + c);
+        const f32x4 hi = *(const f32x4*)(ct + r * CS + c + 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (n + 8 <= N) {
+          ep.apply8p(m, n, v, pre[it]);
+        } else {
+          for (int e = 0; e < 8 && n + e < N; ++e) ep.apply(m, n + e, v[e]);
+        }
+      }
+      continue;
+    }
     if (wm / (WM / EP_PASSES) == pass) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -218,7 +275,6 @@ RETR_DEVICE __attribute__((always_inline)) void gemm2_tile(const LA& la, const L
       }
       continue;
     }
-    constexpr int CH = BN / 8;
 #pragma unroll 2
     for (int q = tid; q < BAND * CH; q += NT) {
       const int r = q / CH, c = (q % CH) * 8;
@@ -385,6 +441,16 @@ int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, in
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * splits;
   const long t128 = (long)cdiv(M, 128) * cdiv(N, 128) * splits;
   const long t12864 = (long)cdiv(M, 128) * cdiv(N, 64) * splits;
+  switch (retr_tune_get(RETR_TUNE_BIG_TILE)) {   // sweep override (tools/conv_micro.py)
+    case 1: return launch_gemm2<FAM, 128, 128, 2, 2, 1, 2>(la, lb, ep, M, N, K, splits, st, what);
+    case 2: return launch_gemm2<FAM, 128, 128, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
+    case 3: return launch_gemm2<FAM, 256, 256, 2, 4, 2>(la, lb, ep, M, N, K, splits, st, what);
+    case 4: return launch_gemm2<FAM, 128, 64, 2, 2, 3>(la, lb, ep, M, N, K, splits, st, what);
+    case 5: return launch_gemm<FAM, bf16, 64, 64>(la, lb, ep, M, N, K, splits, st, what);
+    case 6: return launch_gemm2<FAM, 64, 64, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
+    case 7: return launch_gemm2<FAM, 128, 128, 2, 2, 1, 1>(la, lb, ep, M, N, K, splits, st, what);
+    default: break;
+  }
   if (K <= 128 && splits == 1 && N > 64 && t128 >= 160)   // small K: 4 blocks per CU
     return launch_gemm2<FAM, 128, 128, 2, 2, 1, 2>(la, lb, ep, M, N, K, splits, st, what);
   if (N >= 4096 && t256 >= 256)

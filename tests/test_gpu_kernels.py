@@ -511,3 +511,63 @@ def test_stem_layout_and_maxpool(dtype):
     call("retr_maxpool3x3s2", ops.dcode(dtype), ptr(xm), ptr(ym), N, Hm, Wm, Cm, OH, OW, ops._st())
     refm = F.max_pool2d(xm.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
     assert torch.equal(ym.float(), refm)
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,hd,causal,masked,p", [
+    (16, 8, 400, 400, 32, False, True, 0.1), (16, 8, 128, 400, 32, False, True, 0.1),
+    (16, 8, 128, 128, 32, True, False, 0.1), (3, 8, 100, 77, 32, False, True, 0.0),
+    (2, 8, 130, 200, 64, False, True, 0.1), (2, 8, 200, 200, 64, True, True, 0.0)])
+def test_attention_resident_equals_streaming(B, H, Lq, Lk, hd, causal, masked, p):
+    """The LDS-resident bf16 kernels (attention2.hip fwd3/dq3/dkdv3) compute the streaming
+    kernels' fragments in the same order: outputs, lse and all three gradients bit-identical."""
+    g = torch.Generator(device="cpu").manual_seed(Lq * 7 + Lk)
+    C = H * hd
+    bf = torch.bfloat16
+    q, k, v, do = (torch.randn(B * L, C, generator=g).to(DEV).to(bf) for L in (Lq, Lk, Lk, Lq))
+    kpm = None
+    if masked:
+        kpm = torch.zeros(B, Lk, dtype=torch.uint8)
+        kpm[:, Lk - Lk // 5:] = 1
+        kpm = kpm.to(DEV)
+    outs = []
+    for mode in (1, 2):
+        _lib.load().retr_tune(5, mode)
+        try:
+            o = torch.empty(B * Lq, C, dtype=bf, device=DEV)
+            lse = torch.empty(B * H * Lq, device=DEV)
+            ops.k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, causal, p, 1234, lse)
+            dq, dk, dv = (torch.empty_like(t) for t in (q, k, v))
+            ops.k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, causal, p,
+                                1234)
+            torch.cuda.synchronize()
+            outs.append((o, lse, dq, dk, dv))
+        finally:
+            _lib.load().retr_tune(5, 0)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("H,Ci,Co,k,p", [(16, 64, 128, 1, 0), (15, 64, 128, 1, 0),
+                                          (16, 32, 64, 3, 1)])
+def test_conv_dgrad_stride2_addend_gate(H, Ci, Co, k, p):
+    """Stride-2 data gradient with the residual addend and the ReLU gate (the downsample branch
+    of a bottleneck): tap-less phases of a 1x1 kernel are filled elementwise."""
+    N, s = 2, 2
+    g = torch.Generator(device="cpu").manual_seed(H + Ci + k)
+    bf = torch.bfloat16
+    w = torch.randn(Co, Ci, k, k, generator=g) / math.sqrt(Ci * k * k)
+    wp, wt, bias, scale, cp, _ = _pack(w.to(DEV), bf)
+    weff = (wp.float()[..., :Ci].permute(0, 3, 1, 2)).cpu()
+    OH = (H + 2 * p - (k - 1) - 1) // s + 1
+    gy = torch.randn(N, Co, OH, OH, generator=g).to(bf).float()
+    add = torch.randn(N, H, H, Ci, generator=g).to(bf)
+    gate = torch.randn(N, H, H, Ci, generator=g).to(bf)
+    xreq = torch.zeros(N, Ci, H, H, requires_grad=True)
+    F.conv2d(xreq, weff, stride=s, padding=p).backward(gy)
+    ref = (xreq.grad.permute(0, 2, 3, 1) + add.float()) * (gate.float() > 0)
+    gn = gy.permute(0, 2, 3, 1).contiguous().to(DEV).to(bf)
+    dx = torch.full((N, H, H, cp), float("nan"), dtype=bf, device=DEV)
+    add_d, gate_d = add.to(DEV), gate.to(DEV)     # kept alive across the launch
+    call("retr_conv2d_dgrad", ops.dcode(bf), ptr(gn), N, H, H, cp, ptr(wt), ptr(dx), Co, k, k, s,
+         p, 1, ptr(add_d), ptr(gate_d), ops._st())
+    assert rel_err(dx.float().cpu(), ref) < 1e-2

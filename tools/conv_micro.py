@@ -1,0 +1,89 @@
+"""Device-time sweep of the large-GEMM tile choice (retr_tune RETR_TUNE_BIG_TILE) on the
+memory-heavy ResNet-50 convolutions of cfg2 (batch 16, 640x640 input): 1x1 convolutions over
+the 160x160 / 80x80 / 40x40 maps with residual or addend, the stem and strided data gradients.
+20 calls captured in a hipGraph, best of 5 replays; achieved HBM GB/s from the operand and
+output bytes (algorithmic traffic).
+
+    python tools/conv_micro.py
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from retr_amd._lib import call, load, ptr, stream  # noqa: E402
+
+DEV = "cuda"
+BF = 1
+# (kind, N, H, W, C, Co, k, s, p, with residual/addend)
+SHAPES = [("fwd", 16, 160, 160, 64, 256, 1, 1, 0, 1), ("fwd", 16, 160, 160, 64, 256, 1, 1, 0, 0),
+          ("fwd", 16, 80, 80, 128, 512, 1, 1, 0, 1), ("fwd", 16, 40, 40, 256, 1024, 1, 1, 0, 1),
+          ("fwd", 16, 160, 160, 256, 64, 1, 1, 0, 0), ("fwd", 16, 160, 160, 64, 64, 3, 1, 1, 0),
+          ("fwd", 16, 640, 640, 8, 64, 7, 2, 3, 0),
+          ("dgrad", 16, 40, 40, 1024, 256, 1, 1, 0, 1), ("dgrad", 16, 80, 80, 512, 128, 1, 1, 0, 1),
+          ("dgrad", 16, 80, 80, 512, 1024, 1, 2, 0, 1), ("dgrad", 16, 40, 40, 1024, 2048, 1, 2, 0, 1)]
+
+
+VARIANTS = [(0, 0), (0, 1), (1, 0), (1, 1), (5, 0), (6, 0), (6, 1)]
+
+
+def timeit(fn, n=20):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(n):
+            fn()
+    best = float("inf")
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        graph.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e3 / n)
+    return best
+
+
+def main():
+    bf = torch.bfloat16
+    for kind, N, H, W, C, Co, k, s, p, extra in SHAPES:
+        OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        x = torch.randn(N * H * W * C, device=DEV).to(bf)
+        w = (torch.randn(Co * k * k * C, device=DEV) * 0.05).to(bf)
+        b = torch.randn(Co, device=DEV)
+        y = torch.empty(N * OH * OW * Co, dtype=bf, device=DEV)
+        if kind == "fwd":
+            res = torch.randn(N * OH * OW * Co, device=DEV).to(bf) if extra else None
+            fn = lambda: call("retr_conv2d_fwd", BF, ptr(x), N, H, W, C, ptr(w), ptr(b),  # noqa: E731
+                              ptr(res), ptr(y), Co, k, k, s, p, 1, 1, stream())
+            nbytes = 2 * (x.numel() + y.numel() * (2 if extra else 1) + w.numel())
+        else:
+            dy = torch.randn(N * OH * OW * Co, device=DEV).to(bf)
+            add = torch.randn(N * H * W * C, device=DEV).to(bf) if extra else None
+            dx = torch.empty(N * H * W * C, dtype=bf, device=DEV)
+            fn = lambda: call("retr_conv2d_dgrad", BF, ptr(dy), N, H, W, C, ptr(w), ptr(dx), Co,  # noqa: E731
+                              k, k, s, p, 1, ptr(add), None, stream())
+            nbytes = 2 * (dy.numel() + dx.numel() * (2 if extra else 1) + w.numel())
+        fl = 2.0 * N * OH * OW * Co * k * k * C
+        out = []
+        for tile, nt in VARIANTS:
+            load().retr_tune(6, tile)
+            load().retr_tune(7, nt)
+            try:
+                t = timeit(fn)
+            except RuntimeError as e:   # a tile the shape cannot use
+                out.append(f"t{tile}{'nt' if nt else ''}: -- ({str(e)[:30]})")
+                continue
+            out.append(f"t{tile}{'nt' if nt else ''}:{t:7.1f}us {nbytes / t / 1e3:5.0f}GB/s "
+                       f"{fl / t / 1e6:4.0f}TF")
+        load().retr_tune(6, 0)
+        load().retr_tune(7, 0)
+        print(f"{kind:5s} N{N} {H}x{W}x{C}->{Co} k{k}s{s} x{extra} | " + " | ".join(out),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
