@@ -56,13 +56,20 @@ int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long 
                       long lddx, int dx_f32, int M, int N, int K, const void* addend,
                       int addend_f32, long lda, const void* gate, long ldg, int w_trans,
                       void* stream);
-/* dx = gate( dy W ) with the N-long reduction split into `splits` slices that write fp32 slabs
- * ws[splits][M][K] (plain stores), added in slice order by a second kernel (deterministic): the
- * MLP head's data gradient (N = 30528 vocabulary rows, M*K small) */
+/* Split-K variants for GEMMs with few output tiles and a long reduction (FFN down-projections,
+ * FFN up-projection data gradients, the vocabulary head's data gradient): `splits` slices
+ * write fp32 slabs ws[splits][M][N_out] with plain stores, a second kernel adds them in slice
+ * order (deterministic) and applies the same epilogue as retr_linear_fwd / _dgrad.
+ * retr_linear_splits(dtype, M, N_out, K_reduction): the slice count to use (1 = don't split). */
+int retr_linear_splits(int dtype, int M, int N, int K);
+int retr_linear_fwd_splitk(int dtype, const void* x, long ldx, const void* w, long ldw,
+                           const float* bias, void* y, long ldy, int y_f32, int M, int N, int K,
+                           int relu, const float* residual, long ldr, float drop_p,
+                           unsigned long long seed, float* ws, int splits, void* stream);
 int retr_linear_dgrad_splitk(int dtype, const void* dy, long lddy, const void* w, long ldw,
                              void* dx, long lddx, int dx_f32, int M, int N, int K,
-                             const void* gate, long ldg, int w_trans, float* ws, int splits,
-                             void* stream);
+                             const void* addend, int addend_f32, long lda, const void* gate,
+                             long ldg, int w_trans, float* ws, int splits, void* stream);
 /* dw[N][K] (=|+=) dy^T x (fp32); db[N] (=|+=) column sums of dy (fused; db may be NULL).
  * accumulate = 0: dw/db are overwritten (no pre-zeroing needed); 1: added to.
  * N may be ragged when lddy covers N rounded up to the 16-byte vector (padded dy rows). */

@@ -58,8 +58,11 @@ _SIGS = {
     "retr_linear_dgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _L, _P, _L, _I,
                           _P],
     "retr_transpose_cast": [_I, _P, _P, _I, _I, _I, _P],
-    "retr_linear_dgrad_splitk": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _L, _I, _P, _I,
-                                 _P],
+    "retr_linear_splits": [_I, _I, _I, _I],
+    "retr_linear_fwd_splitk": [_I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _I, _P, _L, _F,
+                               _U64, _P, _I, _P],
+    "retr_linear_dgrad_splitk": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _L, _P, _L,
+                                 _I, _P, _I, _P],
     "retr_linear_wgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _I, _P],
     "retr_bias_grad": [_I, _P, _L, _I, _I, _P, _P],
     "retr_linear_fwd_group": [_I, _I, _I, _PFD, _P],

@@ -53,56 +53,105 @@ int linear_dgrad_t(const void* dy, long lddy, const void* w, long ldw, void* dx,
   return launch_linear<kFamLinearDgrad, T>(la, lb, ep, M, K, N, st, "linear_dgrad");
 }
 
-// dx = gate(sum_s ws[s]) for a data-gradient GEMM split over its (long) reduction: slices wrote
-// fp32 slabs ws[s][M][K] with plain stores; added in slice order (deterministic)
-template <typename TO, typename TG>
-__global__ void dgrad_slab_reduce_kernel(const float* ws, int splits, int M, int K, const TG* gate,
-                                         long ldg, TO* dx, long lddx) {
+// Split-K linears (few output tiles, long reduction: the FFN down-projections at d_model 256,
+// the FFN up-projections' data gradients, the vocabulary head's data gradient): the slices
+// write fp32 slabs ws[s][M][N] with plain stores; slab_epilogue_kernel adds them in slice order
+// (deterministic) and runs the GEMM's own epilogue (bias / ReLU / dropout / residual, or addend
+// / ReLU gate) on the sum.
+template <class EP>
+__global__ void slab_epilogue_kernel(const float* ws, int splits, int M, int N, EP ep) {
+  const int CH = (N + 7) / 8;
   const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const long MK = (long)M * K;
-  if (i >= MK) return;
-  const int m = (int)(i / K), k = (int)(i % K);
-  float t[16];
-  float v = 0.f;
-  for (int s0 = 0; s0 < splits; s0 += 16) {
+  if (i >= (long)M * CH) return;
+  const int m = (int)(i / CH), n = (int)(i % CH) * 8;
+  const long MN = (long)M * N;
+  const float* p = ws + (long)m * N + n;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (n + 8 <= N && N % 4 == 0) {
+    int s = 0;
+    for (; s + 3 < splits; s += 4) {
+      f32x4 a[4], b[4];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) t[u] = s0 + u < splits ? ws[(long)(s0 + u) * MK + i] : 0.f;
+      for (int u = 0; u < 4; ++u) {
+        a[u] = *(const f32x4*)(p + (s + u) * MN);
+        b[u] = *(const f32x4*)(p + (s + u) * MN + 4);
+      }
 #pragma unroll
-    for (int u = 0; u < 16; ++u)
-      if (s0 + u < splits) v += t[u];
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += a[u][e], v[e + 4] += b[u][e];
+    }
+    for (; s < splits; ++s) {
+      const f32x4 a = *(const f32x4*)(p + s * MN), b = *(const f32x4*)(p + s * MN + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += a[e], v[e + 4] += b[e];
+    }
+    ep.apply8(m, n, v);
+    return;
   }
-  if (gate && !(to_f(gate[(long)m * ldg + k]) > 0.f)) v = 0.f;
-  dx[(long)m * lddx + k] = from_f<TO>(v);
+  for (int e = 0; e < 8 && n + e < N; ++e) {
+    float t = 0.f;
+    for (int s = 0; s < splits; ++s) t += p[s * MN + e];
+    ep.apply(m, n + e, t);
+  }
+}
+
+// the K-slice count launch_big / launch_gemm will actually use for `splits` requested
+int norm_splits_k(int K, int BK, int splits) {
+  const int ksteps = cdiv(K, BK);
+  if (splits > ksteps) splits = ksteps;
+  if (splits < 1) splits = 1;
+  return cdiv(K, cdiv(ksteps, splits) * BK);
+}
+
+template <typename T, class LA, class LB, class EP>
+int splitk_run(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, float* ws,
+               int splits, int fam_dgrad, hipStream_t st, const char* what) {
+  constexpr int BK = Elem<T>::BK;
+  splits = norm_splits_k(K, BK, splits);
+  EpiAccF32 acc{ws, (long)N, 0, 0, 1, nullptr};
+  acc.split_stride = (long)M * N;
+  acc.set_vec();
+  int e;
+  if constexpr (sizeof(T) == 2) {
+    e = fam_dgrad ? launch_big<kFamLinearDgrad>(la, lb, acc, M, N, K, splits, st, what)
+                  : launch_big<kFamLinearFwd>(la, lb, acc, M, N, K, splits, st, what);
+  } else {
+    e = fam_dgrad ? launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, acc, M, N, K, splits, st, what)
+                  : launch_gemm<kFamLinearFwd, T, 64, 64>(la, lb, acc, M, N, K, splits, st, what);
+  }
+  if (e) return e;
+  const long chunks = (long)M * ((N + 7) / 8);
+  hipLaunchKernelGGL((slab_epilogue_kernel<EP>), dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0,
+                     st, ws, splits, M, N, ep);
+  return retr_check_launch(what);
 }
 
 template <typename T, typename TO>
-int linear_dgrad_splitk_t(const void* dy, long lddy, const void* w, long ldw, void* dx, long lddx,
-                          int M, int N, int K, const void* gate, long ldg, int w_trans, float* ws,
-                          int splits, hipStream_t st) {
-  DenseK<T> la{(const T*)dy, lddy, M, N};
-  EpiAccF32 ep{ws, (long)K, 0, 0, 1, nullptr};
-  ep.split_stride = (long)M * K;
+int linear_fwd_splitk_t(const void* x, long ldx, const void* w, long ldw, const float* bias,
+                        void* y, long ldy, int M, int N, int K, int relu, const float* res,
+                        long ldr, float p, unsigned long long seed, float* ws, int splits,
+                        hipStream_t st) {
+  DenseK<T> la{(const T*)x, ldx, M, K};
+  DenseK<T> lb{(const T*)w, ldw, N, K};
+  EpiFwd<TO, float> ep{(TO*)y, ldy, bias, res, ldr, relu, make_dp(p, seed), (long)N};
   ep.set_vec();
-  // the launcher may round the slice count down to whole K-steps: slabs it does not write
-  // must not be read
-  constexpr int BK = Elem<T>::BK;
-  const int ksteps = cdiv(N, BK);
-  if (splits > ksteps) splits = ksteps;
-  splits = cdiv(N, cdiv(ksteps, splits) * BK);
-  int e;
+  return splitk_run<T>(la, lb, ep, M, N, K, ws, splits, 0, st, "linear_fwd_splitk");
+}
+
+template <typename T, typename TO, typename TA>
+int linear_dgrad_splitk_t(const void* dy, long lddy, const void* w, long ldw, void* dx, long lddx,
+                          int M, int N, int K, const void* addend, long lda, const void* gate,
+                          long ldg, int w_trans, float* ws, int splits, hipStream_t st) {
+  DenseK<T> la{(const T*)dy, lddy, M, N};
+  EpiDgrad<TO, TA, T> ep{(TO*)dx, lddx, (const TA*)addend, lda, (const T*)gate, ldg};
+  ep.set_vec();
   if (w_trans) {
     DenseK<T> lb{(const T*)w, ldw, K, N};
-    if constexpr (sizeof(T) == 2) e = launch_big<kFamLinearDgrad>(la, lb, ep, M, K, N, splits, st, "linear_dgrad_splitk");
-    else e = launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, ep, M, K, N, splits, st, "linear_dgrad_splitk");
-  } else {
-    DenseT<T> lb{(const T*)w, ldw, K, N};
-    if constexpr (sizeof(T) == 2) e = launch_big<kFamLinearDgrad>(la, lb, ep, M, K, N, splits, st, "linear_dgrad_splitk");
-    else e = launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, ep, M, K, N, splits, st, "linear_dgrad_splitk");
+    return splitk_run<T>(la, lb, ep, M, K, N, ws, splits, 1, st, "linear_dgrad_splitk");
   }
-  if (e) return e;
-  hipLaunchKernelGGL((dgrad_slab_reduce_kernel<TO, T>), dim3(cdiv((long)M * K, 256)), dim3(256), 0,
-                     st, ws, splits, M, K, (const T*)gate, ldg, (TO*)dx, lddx);
-  return retr_check_launch("linear_dgrad_splitk reduce");
+  DenseT<T> lb{(const T*)w, ldw, K, N};
+  return splitk_run<T>(la, lb, ep, M, K, N, ws, splits, 1, st, "linear_dgrad_splitk");
 }
 
 // zero an fp32 [rows][cols] region with row stride ld (stream-ordered, graph-capturable)
@@ -226,23 +275,58 @@ int retr_linear_dgrad(int dtype, const void* dy, long lddy, const void* w, long 
                                              gate, ldg, w_trans, st);
 }
 
+int retr_linear_splits(int dtype, int M, int N, int K) {
+  // few 128x128 output tiles and a long reduction: split toward two blocks per CU, >= 8
+  // K-steps per slice, at most 8 slices (bf16; fp32 keeps single-pass GEMMs).
+  // tools/splitk_micro.py (profiles/r2_splitk_micro.txt): the vocabulary head's dgrad 276 us
+  // single-pass -> 84 us at 8 slices; the FFN shapes gain little beyond 4
+  if (dtype != RETR_BF16 || M <= 0) return 1;
+  const long tiles = (long)cdiv(M, 128) * cdiv(N, 128);
+  const int ksteps = cdiv(K, 64);
+  if (tiles >= 160 || ksteps < 16) return 1;
+  long s = (512 + tiles - 1) / tiles;
+  if (s > ksteps / 8) s = ksteps / 8;
+  if (s > 8) s = 8;
+  return s < 2 ? 1 : norm_splits_k(K, 64, (int)s);
+}
+
+int retr_linear_fwd_splitk(int dtype, const void* x, long ldx, const void* w, long ldw,
+                           const float* bias, void* y, long ldy, int y_f32, int M, int N, int K,
+                           int relu, const float* residual, long ldr, float drop_p,
+                           unsigned long long seed, float* ws, int splits, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (M == 0) return 0;
+  RETR_REQUIRE(splits >= 1 && ws != nullptr, "linear_fwd_splitk: splits=%d", splits);
+  if (dtype == RETR_BF16) {
+    RETR_REQUIRE(K % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0, "linear_fwd_splitk: K/ld must be %%8");
+    return y_f32 ? linear_fwd_splitk_t<bf16, float>(x, ldx, w, ldw, bias, y, ldy, M, N, K, relu, residual, ldr, drop_p, seed, ws, splits, st)
+                 : linear_fwd_splitk_t<bf16, bf16>(x, ldx, w, ldw, bias, y, ldy, M, N, K, relu, residual, ldr, drop_p, seed, ws, splits, st);
+  }
+  RETR_REQUIRE(K % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0, "linear_fwd_splitk: K/ld must be %%4");
+  return linear_fwd_splitk_t<float, float>(x, ldx, w, ldw, bias, y, ldy, M, N, K, relu, residual,
+                                           ldr, drop_p, seed, ws, splits, st);
+}
+
 int retr_linear_dgrad_splitk(int dtype, const void* dy, long lddy, const void* w, long ldw,
                              void* dx, long lddx, int dx_f32, int M, int N, int K,
-                             const void* gate, long ldg, int w_trans, float* ws, int splits,
-                             void* stream) {
+                             const void* addend, int addend_f32, long lda, const void* gate,
+                             long ldg, int w_trans, float* ws, int splits, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) return 0;
   RETR_REQUIRE(splits >= 1 && ws != nullptr, "linear_dgrad_splitk: splits=%d", splits);
   if (dtype == RETR_BF16) {
     RETR_REQUIRE(N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0 && ldw % 8 == 0,
                  "linear_dgrad_splitk: N/K/ld must be %%8");
-    return dx_f32 ? linear_dgrad_splitk_t<bf16, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, gate, ldg, w_trans, ws, splits, st)
-                  : linear_dgrad_splitk_t<bf16, bf16>(dy, lddy, w, ldw, dx, lddx, M, N, K, gate, ldg, w_trans, ws, splits, st);
+    if (dx_f32)
+      return addend_f32 ? linear_dgrad_splitk_t<bf16, float, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, w_trans, ws, splits, st)
+                        : linear_dgrad_splitk_t<bf16, float, bf16>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, w_trans, ws, splits, st);
+    return addend_f32 ? linear_dgrad_splitk_t<bf16, bf16, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, w_trans, ws, splits, st)
+                      : linear_dgrad_splitk_t<bf16, bf16, bf16>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend, lda, gate, ldg, w_trans, ws, splits, st);
   }
   RETR_REQUIRE(N % 4 == 0 && K % 4 == 0 && lddy % 4 == 0 && ldw % 4 == 0,
                "linear_dgrad_splitk: N/K/ld must be %%4");
-  return linear_dgrad_splitk_t<float, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, gate, ldg,
-                                             w_trans, ws, splits, st);
+  return linear_dgrad_splitk_t<float, float, float>(dy, lddy, w, ldw, dx, lddx, M, N, K, addend,
+                                                    lda, gate, ldg, w_trans, ws, splits, st);
 }
 
 int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long ldx, float* dw,

@@ -223,9 +223,32 @@ def _drop_p(module_training, p):
 # low-level launch wrappers (no autograd)
 # ---------------------------------------------------------------------------------------------
 
+def _splits(dtype, M, N, K):
+    """Split-K slice count for an M x N output over a K-long reduction (retr_linear_splits)."""
+    if dtype != torch.bfloat16:
+        return 1
+    key = (M, N, K)
+    s = _SPLITS.get(key)
+    if s is None:
+        s = _SPLITS[key] = int(_lib.load().retr_linear_splits(dcode(dtype), M, N, K))
+    return s
+
+
+_SPLITS = {}
+
+
 def k_linear_fwd(x, w, bias, y, relu=0, res=None, drop_p=0.0, seed=0):
     M, K = x.shape
     N = w.shape[0]
+    splits = _splits(x.dtype, M, N, K)
+    if splits > 1:
+        # few output tiles, long reduction (FFN down-projection): ordered fp32 slabs + epilogue
+        ws = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+        call("retr_linear_fwd_splitk", dcode(x.dtype), ptr(x), x.stride(0), ptr(w), w.stride(0),
+             ptr(bias), ptr(y), y.stride(0), int(y.dtype == torch.float32), M, N, K, relu,
+             ptr(res), res.stride(0) if res is not None else 0, drop_p, seed, ptr(ws), splits,
+             _st())
+        return
     call("retr_linear_fwd", dcode(x.dtype), ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(bias),
          ptr(y), y.stride(0), int(y.dtype == torch.float32), M, N, K, relu, ptr(res),
          res.stride(0) if res is not None else 0, drop_p, seed, _st())
@@ -240,15 +263,16 @@ def k_linear_dgrad(dy, wt, dx, addend=None, gate=None):
         w, w_trans = wt.w, 0
     else:
         w, w_trans = wt, 1
-    if addend is None and N >= 8192 and M * K <= (1 << 21):
-        # long reduction, few output tiles (the MLP head's vocabulary): split it 8 ways into
-        # fp32 slabs added in order by a second kernel
-        splits = 8
+    splits = _splits(dy.dtype, M, K, N)
+    if splits > 1:
+        # long reduction, few output tiles (FFN up-projection, the MLP head's vocabulary):
+        # fp32 slabs added in order by the epilogue kernel
         ws = torch.empty(splits, M, K, dtype=torch.float32, device=dy.device)
         call("retr_linear_dgrad_splitk", dcode(dy.dtype), ptr(dy), dy.stride(0), ptr(w),
              w.stride(0), ptr(dx), dx.stride(0), int(dx.dtype == torch.float32), M, N, K,
-             ptr(gate), gate.stride(0) if gate is not None else 0, w_trans, ptr(ws), splits,
-             _st())
+             ptr(addend), int(addend is not None and addend.dtype == torch.float32),
+             addend.stride(0) if addend is not None else 0, ptr(gate),
+             gate.stride(0) if gate is not None else 0, w_trans, ptr(ws), splits, _st())
         return
     call("retr_linear_dgrad", dcode(dy.dtype), ptr(dy), dy.stride(0), ptr(w), w.stride(0),
          ptr(dx), dx.stride(0), int(dx.dtype == torch.float32), M, N, K, ptr(addend),

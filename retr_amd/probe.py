@@ -39,7 +39,7 @@ def flops_of(name, a):
         _, _, _, n, h, w, c, _, co, kh, kw, s, p, d = a[:14]
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
         return "conv_wgrad", 2.0 * n * oh * ow * co * kh * kw * c
-    if name in ("retr_linear_fwd",):
+    if name in ("retr_linear_fwd", "retr_linear_fwd_splitk"):
         m, n, k = a[9], a[10], a[11]
         return "linear_fwd", 2.0 * m * n * k
     if name in ("retr_linear_dgrad", "retr_linear_dgrad_splitk"):
@@ -82,7 +82,9 @@ def shape_of(name, a):
     if name == "retr_linear_dgrad":
         return f"M{a[8]} N{a[9]} K{a[10]} add{int(bool(a[11]))} gate{int(bool(a[14]))}"
     if name == "retr_linear_dgrad_splitk":
-        return f"M{a[8]} N{a[9]} K{a[10]} gate{int(bool(a[11]))} split{a[15]}"
+        return f"M{a[8]} N{a[9]} K{a[10]} add{int(bool(a[11]))} gate{int(bool(a[14]))} split{a[18]}"
+    if name == "retr_linear_fwd_splitk":
+        return f"M{a[9]} N{a[10]} K{a[11]} relu{a[12]} res{int(bool(a[13]))} split{a[18]}"
     if name == "retr_linear_wgrad":
         return f"M{a[7]} N{a[8]} K{a[9]} db{int(bool(a[10]))} acc{a[11]}"
     if name == "retr_attention_fwd":
@@ -93,6 +95,7 @@ def shape_of(name, a):
 
 
 TRACKED = ("retr_conv2d_fwd", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
+           "retr_linear_fwd_splitk",
            "retr_linear_dgrad", "retr_linear_dgrad_splitk", "retr_linear_wgrad",
            "retr_linear_fwd_group", "retr_linear_dgrad_group", "retr_linear_wgrad_group",
            "retr_attention_fwd", "retr_attention_bwd")
