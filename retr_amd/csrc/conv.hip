@@ -122,48 +122,59 @@ struct ConvWgradB {  // B(row = kh,kw,ci ; k = pixel n,oh,ow) = X[n, oh*s-p+kh d
   const T* x;
   Geom g;
   int rows, M;
-  struct Ctx { int khd, kwd, ci; bool ok; };
-  struct KCur { int m, n, oh, ow; };
+  int adv_q, adv_r;   // one K-step (Elem<T>::BK pixels) = adv_q output rows + adv_r columns
+  struct Ctx { int khd, kwd; long off; bool ok; };
+  // the cursor keeps the output pixel (n, oh, ow) and the element offset of the input pixel
+  // (n, oh*s, ow*s): advancing one K-step is adds and at most a wrap or two, no divisions
+  struct KCur { int m, oh, ow; long base; };
   RETR_DEVICE Ctx row_ctx(int r) const {
     Ctx c;
     c.ok = r < rows;
     int rr = c.ok ? r : 0;
     int khw = rr / g.C;
-    c.ci = rr - khw * g.C;
+    const int ci = rr - khw * g.C;
     int kh = khw / g.KW, kw = khw - kh * g.KW;
     c.khd = kh * g.d - g.p;
     c.kwd = kw * g.d - g.p;
+    c.off = ((long)c.khd * g.W + c.kwd) * g.C + ci;
     return c;
   }
   RETR_DEVICE KCur kcur(int m) const {
     KCur k;
     k.m = m;
     int hw = g.OH * g.OW;
-    k.n = m / hw;
-    int rem = m - k.n * hw;
+    const int n = m / hw;
+    int rem = m - n * hw;
     k.oh = rem / g.OW;
     k.ow = rem - k.oh * g.OW;
+    k.base = (((long)n * g.H + k.oh * g.s) * g.W + k.ow * g.s) * g.C;
     return k;
   }
   RETR_DEVICE void advance(KCur& k, int d) const {
     k.m += d;
-    k.ow += d;
+    if (d != Elem<T>::BK) {   // generic step (not used by the GEMM cores)
+      k = kcur(k.m);
+      return;
+    }
+    const long rowC = (long)g.s * g.W * g.C;          // one output row down
+    k.ow += adv_r;
+    k.oh += adv_q;
+    k.base += (long)adv_q * rowC + (long)adv_r * g.s * g.C;
     if (k.ow >= g.OW) {
-      int q = k.ow / g.OW;
-      k.ow -= q * g.OW;
-      k.oh += q;
-      if (k.oh >= g.OH) {
-        int q2 = k.oh / g.OH;
-        k.oh -= q2 * g.OH;
-        k.n += q2;
-      }
+      k.ow -= g.OW;
+      k.oh += 1;
+      k.base += rowC - (long)g.OW * g.s * g.C;
+    }
+    while (k.oh >= g.OH) {                            // next image
+      k.oh -= g.OH;
+      k.base += ((long)g.H - (long)g.OH * g.s) * g.W * g.C;
     }
   }
   RETR_DEVICE const void* addr(const Ctx& c, const KCur& k) const {
     if (!c.ok || k.m >= M) return nullptr;
     int ih = k.oh * g.s + c.khd, iw = k.ow * g.s + c.kwd;
     if ((unsigned)ih >= (unsigned)g.H || (unsigned)iw >= (unsigned)g.W) return nullptr;
-    return x + (((long)k.n * g.H + ih) * g.W + iw) * g.C + c.ci;
+    return x + k.base + c.off;
   }
 };
 
@@ -461,7 +472,7 @@ int conv_wgrad_t(const void* dy, const void* x, Geom g, float* ws, hipStream_t s
     DenseT<T> lb{(const T*)x, (long)g.C, Ncols, Mp};
     return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st, "conv_wgrad_1x1");
   }
-  ConvWgradB<T> lb{(const T*)x, g, Ncols, Mp};
+  ConvWgradB<T> lb{(const T*)x, g, Ncols, Mp, Elem<T>::BK / g.OW, Elem<T>::BK % g.OW};
   return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st, "conv_wgrad");
 }
 
@@ -492,6 +503,40 @@ __global__ void conv_pack_kernel(const float* w, const float* bnw, const float* 
       else b = conv_bias ? conv_bias[co] : 0.f;
       if (bias_out) bias_out[co] = b;
       if (scale_out) scale_out[co] = scale;
+    }
+  }
+}
+
+// grad[co][ci][kh][kw] (=|+=) scale[co] * sum_s ws[s][co][kh][kw][ci]: threads walk the slabs
+// in their own order (4 consecutive input channels per thread, 16-byte loads, eight slabs in
+// flight, added in slice order) and scatter into the OIHW parameter layout
+__global__ void wgrad_unpack4_kernel(const float* ws, const float* scale, float* grad, int Co,
+                                     int Ci, int Cp, int KHW, int accumulate, int splits) {
+  const int c4 = Ci / 4;
+  const long total = (long)Co * KHW * c4;
+  const long slab = (long)Co * KHW * Cp;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % c4) * 4;
+    const long t = i / c4;
+    const int tap = (int)(t % KHW), co = (int)(t / KHW);
+    const float* src = ws + ((long)co * KHW + tap) * Cp + ci;
+    f32x4 v = *(const f32x4*)src;
+    int s = 1;
+    for (; s + 7 < splits; s += 8) {
+      f32x4 u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = *(const f32x4*)(src + (s + k) * slab);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v += u[k];
+    }
+    for (; s < splits; ++s) v += *(const f32x4*)(src + s * slab);
+    const float sc = scale ? scale[co] : 1.f;
+    float* dst = grad + ((long)co * Ci + ci) * KHW + tap;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x = v[e] * sc;
+      dst[(long)e * KHW] = accumulate ? dst[(long)e * KHW] + x : x;
     }
   }
 }
@@ -593,6 +638,13 @@ int retr_conv2d_wgrad_splits(int dtype, int Nb, int H, int W, int C, int Co, int
 int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,
                            int Cp, int KH, int KW, int accumulate, int splits, void* stream) {
   RETR_REQUIRE(splits >= 1, "conv_wgrad_unpack: splits=%d", splits);
+  if (Ci % 4 == 0 && Cp % 4 == 0 && ((uintptr_t)ws & 15) == 0) {
+    const long total = (long)Co * KH * KW * (Ci / 4);
+    const int grid = (int)(total / 256 + 1 < 8192 ? total / 256 + 1 : 8192);
+    hipLaunchKernelGGL(wgrad_unpack4_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws,
+                       scale, grad, Co, Ci, Cp, KH * KW, accumulate, splits);
+    return retr_check_launch("conv_wgrad_unpack4");
+  }
   long total = (long)Co * Ci * KH * KW;
   int grid = (int)(total / 256 + 1 < 4096 ? total / 256 + 1 : 4096);
   hipLaunchKernelGGL(wgrad_unpack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, scale,

@@ -292,11 +292,22 @@ RETR_DEVICE __attribute__((always_inline)) void gemm2_tile(const LA& la, const L
   }
 }
 
+template <class E, class = void>
+struct has_split_slot : std::false_type {};
+template <class E>
+struct has_split_slot<E, std::void_t<decltype(std::declval<E&>().split)>> : std::true_type {};
+
+// Split-K grids (weight gradients) are remapped split-major over the whole grid: every tile of
+// one K-slice lands on the same XCD, so the slice's operand rows are fetched into that XCD's L2
+// once and shared by all its tiles (a tile-only remap spread each slice over all eight L2s).
 template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB, class LA, class LB, class EP>
 __global__ void __launch_bounds__(WM * WN * 64)
 gemm2_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
-  gemm2_tile<FAM, BM, BN, WM, WN, S, EPB>(la, lb, ep, M, N, K, kchunk, tiles_n,
-                                          xcd_remap(blockIdx.x, gridDim.x), blockIdx.y);
+  const int tiles = gridDim.x;
+  const int r = xcd_remap(blockIdx.y * tiles + blockIdx.x, tiles * gridDim.y);
+  const int split = r / tiles, tile = r - split * tiles;
+  if constexpr (has_split_slot<EP>::value) ep.split = split;
+  gemm2_tile<FAM, BM, BN, WM, WN, S, EPB>(la, lb, ep, M, N, K, kchunk, tiles_n, tile, split);
 }
 
 // ---- grouped launch: up to G independent GEMMs with the same operand/epilogue types (the
@@ -316,11 +327,6 @@ struct GGroup {
   GProb<LA, LB, EP> p[G];
   int n;
 };
-
-template <class E, class = void>
-struct has_split_slot : std::false_type {};
-template <class E>
-struct has_split_slot<E, std::void_t<decltype(std::declval<E&>().split)>> : std::true_type {};
 
 template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB, class LA, class LB, class EP,
           int G>

@@ -22,7 +22,10 @@ SHAPES = [("fwd", 16, 160, 160, 64, 256, 1, 1, 0, 1), ("fwd", 16, 160, 160, 64, 
           ("fwd", 16, 160, 160, 256, 64, 1, 1, 0, 0), ("fwd", 16, 160, 160, 64, 64, 3, 1, 1, 0),
           ("fwd", 16, 640, 640, 8, 64, 7, 2, 3, 0),
           ("dgrad", 16, 40, 40, 1024, 256, 1, 1, 0, 1), ("dgrad", 16, 80, 80, 512, 128, 1, 1, 0, 1),
-          ("dgrad", 16, 80, 80, 512, 1024, 1, 2, 0, 1), ("dgrad", 16, 40, 40, 1024, 2048, 1, 2, 0, 1)]
+          ("dgrad", 16, 80, 80, 512, 1024, 1, 2, 0, 1), ("dgrad", 16, 40, 40, 1024, 2048, 1, 2, 0, 1),
+          ("wgrad", 16, 40, 40, 256, 256, 3, 1, 1, 0), ("wgrad", 16, 80, 80, 128, 128, 3, 1, 1, 0),
+          ("wgrad", 16, 20, 20, 512, 512, 3, 1, 1, 0), ("wgrad", 16, 40, 40, 256, 1024, 1, 1, 0, 0),
+          ("wgrad", 16, 80, 80, 128, 512, 1, 1, 0, 0)]
 
 
 VARIANTS = [(0, 0), (0, 1), (1, 0), (1, 1), (5, 0), (6, 0), (6, 1)]
@@ -60,6 +63,18 @@ def main():
             fn = lambda: call("retr_conv2d_fwd", BF, ptr(x), N, H, W, C, ptr(w), ptr(b),  # noqa: E731
                               ptr(res), ptr(y), Co, k, k, s, p, 1, 1, stream())
             nbytes = 2 * (x.numel() + y.numel() * (2 if extra else 1) + w.numel())
+        elif kind == "wgrad":
+            dy = torch.randn(N * OH * OW * Co, device=DEV).to(bf)
+            sp = load().retr_conv2d_wgrad_splits(BF, N, H, W, C, Co, k, k, s, p, 1)
+            ws = torch.empty(sp * Co * k * k * C, device=DEV)
+            grad = torch.empty(Co * C * k * k, device=DEV)
+
+            def fn():
+                call("retr_conv2d_wgrad", BF, ptr(dy), ptr(x), N, H, W, C, ptr(ws), Co, k, k, s,
+                     p, 1, stream())
+                call("retr_conv_wgrad_unpack", ptr(ws), None, ptr(grad), Co, C, C, k, k, 0, sp,
+                     stream())
+            nbytes = 2 * (dy.numel() + x.numel()) + 8 * ws.numel()
         else:
             dy = torch.randn(N * OH * OW * Co, device=DEV).to(bf)
             add = torch.randn(N * H * W * C, device=DEV).to(bf) if extra else None
@@ -69,7 +84,7 @@ def main():
             nbytes = 2 * (dy.numel() + dx.numel() * (2 if extra else 1) + w.numel())
         fl = 2.0 * N * OH * OW * Co * k * k * C
         out = []
-        for tile, nt in VARIANTS:
+        for tile, nt in (VARIANTS if kind != "wgrad" else [(0, 0)]):
             load().retr_tune(6, tile)
             load().retr_tune(7, nt)
             try:
