@@ -457,14 +457,17 @@ int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, in
     case 7: return launch_gemm2<FAM, 128, 128, 2, 2, 1, 1>(la, lb, ep, M, N, K, splits, st, what);
     default: break;
   }
-  if (K <= 128 && splits == 1 && N > 64 && t128 >= 160)   // small K: 4 blocks per CU
+  // small K (<= 4 K-steps): single-stage 128x128, 4 blocks per CU (tools/conv_micro.py:
+  // 1x1 convs with 256 input channels 46 -> 38 us); N = 64: the 64x64 two-stage tile (the stem
+  // 325 -> 280 us, 3x3 64-channel convs 82 -> 64 us)
+  if (K <= 256 && splits == 1 && N > 64 && t128 >= 160)
     return launch_gemm2<FAM, 128, 128, 2, 2, 1, 2>(la, lb, ep, M, N, K, splits, st, what);
   if (N >= 4096 && t256 >= 256)
     return launch_gemm2<FAM, 256, 256, 2, 4, 2>(la, lb, ep, M, N, K, splits, st, what);
   if (N > 64 && t128 >= 160)
     return launch_gemm2<FAM, 128, 128, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
   if (N <= 64 && t12864 >= 160)
-    return launch_gemm2<FAM, 128, 64, 2, 2, 3>(la, lb, ep, M, N, K, splits, st, what);
+    return launch_gemm2<FAM, 64, 64, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
   return launch_gemm<FAM, bf16, 64, 64>(la, lb, ep, M, N, K, splits, st, what);
 }
 

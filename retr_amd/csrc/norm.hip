@@ -44,6 +44,7 @@ ln_fwd_kernel(const float* x, long ldx, const float* gamma, const float* beta, f
 }
 
 // rows_per_block rows handled by 4 waves; per-column dgamma/dbeta partials reduced in LDS.
+constexpr int kLnBwdRows = 8;
 template <typename T, int PER>
 __global__ void __launch_bounds__(256)
 ln_bwd_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, const float* gamma,
@@ -58,7 +59,7 @@ ln_bwd_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, co
   int r1 = min(M, r0 + rows_per_block);
   // the wave's rows in batches of RB: every load of a batch is issued before the first
   // reduction, and the batch's independent shuffle chains interleave (latency-bound otherwise)
-  constexpr int RB = 4;
+  constexpr int RB = 2;
   for (int rb = r0 + wave; rb < r1; rb += 4 * RB) {
     float d[RB][PER], xv[RB][PER], ad[RB][PER], mu[RB], rs[RB];
 #pragma unroll
@@ -376,7 +377,7 @@ int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, co
   RETR_REQUIRE(mean && rstd && gamma && dx, "layernorm_bwd: missing saved statistics");
   RETR_REQUIRE(!(dgamma || dbeta) || workspace, "layernorm_bwd: dgamma/dbeta need a workspace");
   hipStream_t st = (hipStream_t)stream;
-  const int rpb = 16;  // 4 rows per wave: enough blocks to fill 256 CUs at M ~ 2k-6k rows
+  const int rpb = kLnBwdRows;  // 2 rows per wave: ~12 waves per CU at M = 6400
   dim3 grid(cdiv(M, rpb));
   float* part = (dgamma || dbeta) ? workspace : nullptr;
 #define LNB(P)                                                                                     \
@@ -398,7 +399,7 @@ int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, co
 }
 
 size_t retr_layernorm_bwd_workspace(int M, int C) {
-  return sizeof(float) * 2 * (size_t)C * (size_t)cdiv(M, 16);
+  return sizeof(float) * 2 * (size_t)C * (size_t)cdiv(M, kLnBwdRows);
 }
 
 int retr_embed_ln_fwd(const long long* tokens, int B, int T, int C, const float* word,

@@ -385,7 +385,7 @@ def k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, caus
 
 def ln_workspace(M, C, dev):
     """fp32 scratch for the LayerNorm backward's per-block dgamma/dbeta partials."""
-    n = (2 * C * ((M + 15) // 16))
+    n = _lib.load().retr_layernorm_bwd_workspace(M, C) // 4
     return torch.empty(n, dtype=torch.float32, device=dev)
 
 
