@@ -91,6 +91,29 @@ RETR_DEVICE bool attn_keep(uint32_t bits, uint32_t key, uint32_t thresh16) {
   return ((key & 1) ? (bits >> 16) : (bits & 0xffffu)) >= thresh16;
 }
 
+// Element dropout of row-major activations (residual branches, embeddings): the same
+// construction per (row, column pair) -- one 32-bit hash decides two columns -- instead of a
+// 64-bit mix per element (3 64-bit multiplies).  Used identically by the forward epilogues and
+// the backward's mask regeneration (retr_dropout_apply).
+RETR_DEVICE uint32_t drop_th16(uint32_t thresh) { return (thresh + 0x8000u) >> 16; }
+RETR_DEVICE uint32_t drop_row_key(uint64_t seed, uint32_t row) {
+  return attn_row_key(seed ^ 0xA5A5F00Dull, row);
+}
+RETR_DEVICE bool drop_keep(uint32_t row_key, uint32_t col, uint32_t th16) {
+  return attn_keep(attn_pair_bits(row_key, col), col, th16);
+}
+// keep bits of columns n .. n+7 (n even): bit e = column n + e
+RETR_DEVICE uint32_t drop_keep8(uint32_t row_key, uint32_t n, uint32_t th16) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const uint32_t b = attn_pair_bits(row_key, n + e);
+    m |= (uint32_t)((b & 0xffffu) >= th16) << e;
+    m |= (uint32_t)((b >> 16) >= th16) << (e + 1);
+  }
+  return m;
+}
+
 // ---- wave reductions (wave64) ------------------------------------------------------------------
 RETR_DEVICE float wave_sum(float v) {
 #pragma unroll

@@ -78,7 +78,9 @@ struct EpiFwd {
   RETR_DEVICE void apply(int m, int n, float v) const {
     if (bias) v += bias[n];
     if (relu == 1) v = fmaxf(v, 0.f);
-    if (dp.thresh) v = retr_keep(dp_seed(dp), (uint64_t)m * drop_ld + n, dp.thresh) ? v * dp.scale : 0.f;
+    if (dp.thresh)
+      v = drop_keep(drop_row_key(dp_seed(dp), (uint32_t)m), (uint32_t)n, drop_th16(dp.thresh))
+              ? v * dp.scale : 0.f;
     if (res) v += to_f(res[(long)m * ldr + n]);
     if (relu == 2) v = fmaxf(v, 0.f);
     out[(long)m * ldo + n] = from_f<TO>(v);
@@ -100,9 +102,10 @@ struct EpiFwd {
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
     if (dp.thresh) {
+      const uint32_t km = drop_keep8(drop_row_key(dp_seed(dp), (uint32_t)m), (uint32_t)n,
+                                     drop_th16(dp.thresh));
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        v[e] = retr_keep(dp_seed(dp), (uint64_t)m * drop_ld + n + e, dp.thresh) ? v[e] * dp.scale : 0.f;
+      for (int e = 0; e < 8; ++e) v[e] = ((km >> e) & 1u) ? v[e] * dp.scale : 0.f;
     }
     if (res) {
       float r[8];
@@ -138,9 +141,10 @@ struct EpiFwd {
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
     if (dp.thresh) {
+      const uint32_t km = drop_keep8(drop_row_key(dp_seed(dp), (uint32_t)m), (uint32_t)n,
+                                     drop_th16(dp.thresh));
 #pragma unroll
-      for (int e = 0; e < 8; ++e)
-        v[e] = retr_keep(dp_seed(dp), (uint64_t)m * drop_ld + n + e, dp.thresh) ? v[e] * dp.scale : 0.f;
+      for (int e = 0; e < 8; ++e) v[e] = ((km >> e) & 1u) ? v[e] * dp.scale : 0.f;
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += p.r[e];

@@ -116,14 +116,43 @@ __global__ void mask_nearest_kernel(const unsigned char* m, unsigned char* out, 
 template <typename TO>
 __global__ void dropout_apply_kernel(const float* x, long ldx, TO* y, long ldy, int M, int N,
                                      DropoutParams dp) {
-  long total = (long)M * N;
+  // 8 consecutive columns per thread (N % 8 == 0 and 16-byte aligned rows: vector path)
+  const int cpr = (N + 7) / 8;
+  const long total = (long)M * cpr;
+  const uint64_t seed = dp.thresh ? dp_seed(dp) : 0ull;
+  const uint32_t th16 = drop_th16(dp.thresh);
+  const bool vec = (N % 8 == 0) && (ldx % 4 == 0) && (ldy % 8 == 0);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    int n = i % N;
-    long m = i / N;
-    float v = x[m * ldx + n];
-    if (dp.thresh) v = retr_keep(dp_seed(dp), (uint64_t)m * N + n, dp.thresh) ? v * dp.scale : 0.f;
-    y[m * ldy + n] = from_f<TO>(v);
+    const int m = (int)(i / cpr), n = (int)(i - (long)m * cpr) * 8;
+    const uint32_t km = dp.thresh ? drop_keep8(drop_row_key(seed, (uint32_t)m), (uint32_t)n, th16)
+                                  : 0xffu;
+    const float* xr = x + (long)m * ldx + n;
+    TO* yr = y + (long)m * ldy + n;
+    if (vec) {
+      float v[8];
+      const f32x4 a = *(const f32x4*)xr, b = *(const f32x4*)(xr + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = a[e], v[e + 4] = b[e];
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        v[e] = ((km >> e) & 1u) ? (dp.thresh ? v[e] * dp.scale : v[e]) : 0.f;
+      if constexpr (sizeof(TO) == 2) {
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+        *(bf16x8*)yr = o;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) yr[e] = from_f<TO>(v[e]);
+      }
+    } else {
+      for (int e = 0; e < 8 && n + e < N; ++e) {
+        float v = xr[e];
+        if (dp.thresh) v = ((km >> e) & 1u) ? v * dp.scale : 0.f;
+        yr[e] = from_f<TO>(v);
+      }
+    }
   }
 }
 
@@ -196,8 +225,8 @@ int retr_mask_nearest(const unsigned char* m, unsigned char* out, int N, int H, 
 
 int retr_dropout_apply(int dtype_out, const float* x, long ldx, void* y, long ldy, int M, int N,
                        float drop_p, unsigned long long seed, void* stream) {
-  long total = (long)M * N;
-  if (total == 0) return 0;
+  if ((long)M * N == 0) return 0;
+  const long total = (long)M * ((N + 7) / 8);   // threads: 8 columns each
   hipStream_t st = (hipStream_t)stream;
   DropoutParams dp = make_dp(drop_p, seed);
   if (dtype_out == RETR_BF16)

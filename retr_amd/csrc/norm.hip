@@ -190,7 +190,9 @@ embed_ln_fwd_kernel(const long long* tok, int M, int T, int C, const float* word
   for (int i = 0; i < PER; ++i) {
     int c = lane + 64 * i;
     float o = (v[i] - mean) * rstd * gamma[c] + beta[c];
-    if (dp.thresh) o = retr_keep(dp_seed(dp), (uint64_t)row * C + c, dp.thresh) ? o * dp.scale : 0.f;
+    if (dp.thresh)
+      o = drop_keep(drop_row_key(dp_seed(dp), (uint32_t)row), (uint32_t)c, drop_th16(dp.thresh))
+              ? o * dp.scale : 0.f;
     y[(long)row * C + c] = o;
   }
   if (lane == 0) {
@@ -226,7 +228,9 @@ embed_ln_bwd_kernel(const long long* tok, int M, int T, int C, const float* word
     for (int i = 0; i < PER; ++i) {
       int c = lane + 64 * i;
       float d = dy[(long)row * C + c];
-      if (dp.thresh) d = retr_keep(dp_seed(dp), (uint64_t)row * C + c, dp.thresh) ? d * dp.scale : 0.f;
+      if (dp.thresh)
+        d = drop_keep(drop_row_key(dp_seed(dp), (uint32_t)row), (uint32_t)c, drop_th16(dp.thresh))
+                ? d * dp.scale : 0.f;
       xh[i] = (word[t * C + c] + posw[(long)p * C + c] - mu) * rs;
       pg[i] += d * xh[i];
       pb[i] += d;

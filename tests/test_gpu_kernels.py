@@ -607,3 +607,24 @@ def test_linear_splitk_fwd_dgrad(M, N, K):
     dx2 = torch.empty_like(dx)
     ops.k_linear_dgrad(dy, ops._TView(w.t().contiguous()), dx2, addend=add, gate=gate)
     assert torch.equal(dx, dx2)
+
+
+def test_linear_dropout_mask_regenerated_by_backward():
+    """The residual-branch dropout of a linear forward (GEMM epilogue) and the backward's
+    retr_dropout_apply draw the same keep mask from (seed, row, column); keep rate ~ 1 - p."""
+    M, N, K, p, seed = 3000, 256, 64, 0.1, 12345
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(M, K, generator=g).to(DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, generator=g).to(DEV).to(torch.bfloat16)
+    b = torch.full((N,), 10.0, device=DEV)                 # branch never exactly zero
+    res = torch.zeros(M, N, device=DEV)
+    y = torch.empty(M, N, device=DEV)
+    ops.k_linear_fwd(x, w, b, y, res=res, drop_p=p, seed=seed)
+    kept_fwd = y != 0
+    ones = torch.ones(M, N, device=DEV)
+    m = torch.empty(M, N, device=DEV)
+    ops.k_dropout_apply(ones, m, p, seed)
+    kept_bwd = m != 0
+    assert torch.equal(kept_fwd, kept_bwd)
+    assert abs(kept_bwd.float().mean().item() - (1 - p)) < 5e-3
+    assert torch.allclose(m[kept_bwd], torch.full_like(m[kept_bwd], 1 / (1 - p)))
