@@ -176,13 +176,16 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
       for (int e = 0; e < 16; ++e) mt = fmaxf(mt, S[sub][e]);
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float mn = fmaxf(m, mt);
-    const float alpha = (mn == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mn);
+    const float ms = (mn == -INFINITY) ? 0.f : mn;
+    const float alpha = __builtin_amdgcn_exp2f(m - ms);
     m = mn;
-    l *= alpha;
+    if (__any(alpha != 1.f)) {
+      l *= alpha;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) O[dt][e] *= alpha;
+        for (int e = 0; e < 16; ++e) O[dt][e] *= alpha;
+    }
     bf16x8 pf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -197,12 +200,9 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           const int e = 4 * g + e4;
-          float p = (mn == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(S[sub][e] - mn);
+          float p = __builtin_amdgcn_exp2f(S[sub][e] - ms);
           l += p;
-          if (drop) {
-            const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
-            p = kp ? p * dp.scale : 0.f;
-          }
+          if (drop) p = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? p : 0.f;
           pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
         }
       }
@@ -225,7 +225,9 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
 
   l += __shfl_xor(l, 32, 64);
   if (qi < Lq) {
-    const float inv = 1.f / l;      // fully masked row: 0 * inf = NaN (torch's all -inf softmax)
+    // fully masked row: 0 * inf = NaN (torch's all -inf softmax); kept probabilities were left
+    // unscaled, the dropout scale is applied here once
+    const float inv = (drop ? dp.scale : 1.f) / l;
     bf16* orow = o + ((long)b * Lq + qi) * ldo + h * HD;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -404,13 +406,18 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
       for (int e = 0; e < 16; ++e) mt = fmaxf(mt, S[sub][e]);
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float mn = fmaxf(m, mt);
-    const float alpha = (mn == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mn);
+    // a row with no valid key so far keeps m = -inf: exponentiate against 0 instead (every
+    // score is -inf then, so every p is 0) -- no per-element select
+    const float ms = (mn == -INFINITY) ? 0.f : mn;
+    const float alpha = __builtin_amdgcn_exp2f(m - ms);
     m = mn;
-    l *= alpha;
+    if (__any(alpha != 1.f)) {        // the running max moved for some row of the wave
+      l *= alpha;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) O[dt][e] *= alpha;
+        for (int e = 0; e < 16; ++e) O[dt][e] *= alpha;
+    }
     bf16x8 pf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -425,12 +432,9 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           const int e = 4 * g + e4;
-          float p = (mn == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(S[sub][e] - mn);
+          float p = __builtin_amdgcn_exp2f(S[sub][e] - ms);
           l += p;
-          if (drop) {
-            const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
-            p = kp ? p * dp.scale : 0.f;
-          }
+          if (drop) p = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? p : 0.f;
           pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
         }
       }
@@ -450,7 +454,7 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
 
   l += __shfl_xor(l, 32, 64);
   if (qi < Lq) {
-    const float inv = 1.f / l;
+    const float inv = (drop ? dp.scale : 1.f) / l;
     bf16* orow = o + ((long)b * Lq + qi) * ldo + h * HD;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -543,6 +547,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
     const char* Vl = Vs + t * L::TILE;
     const unsigned long long pmask = pm[t];
     const bool diag = causal && (key0 + 63 > q0);
+    const bool anym = pmask != 0ull || diag;      // wave-uniform: masking needed on this tile
     bf16x8 sf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -566,7 +571,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
-          const bool msk = ((pmask >> kl) & 1ull) || (diag && key0 + kl > qi);
+          const bool msk = anym && (((pmask >> kl) & 1ull) || (diag && key0 + kl > qi));
           const float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - lq2);
           float dpv = P[e];
           if (drop) dpv = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? dpv * dp.scale : 0.f;
@@ -828,10 +833,13 @@ int retr_attention_fwd2(const void* q, long ldq, const void* k, long ldk, const 
                         long ldv, void* o, long ldo, int B, int H, int Lq, int Lk, int hd,
                         const unsigned char* kpm, int causal, float p, unsigned long long seed,
                         float* lse, hipStream_t st) {
+  // forward: the streaming kernel (20 KB of LDS, up to 8 blocks per CU) beats the resident
+  // one (2 blocks per CU) at every cfg2 shape (tools/attn_micro.py: 400x400 24.8 vs 28.1 us);
+  // the resident forward stays selectable (RETR_TUNE_ATTN_MODE = 2) for sweeps
   const int mode = attn_res_mode();
   const int ntk = (Lk + 63) / 64;
   const bool fits = hd == 32 ? res_lds_fwd<32>(ntk) <= kResLdsMax : res_lds_fwd<64>(ntk) <= kResLdsMax;
-  if (mode != 1 && fits) {
+  if (mode == 2 && fits) {
     const int nw = pick_nw(B, H, Lq);
     if (hd == 32)
       return nw == 4 ? launch_fwd3<32, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, st)
@@ -959,6 +967,7 @@ attn_bwd_dq2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
     if (kpm && !pad) pad = kpm[(long)b * Lk + key0 + lane] != 0;
     const unsigned long long pmask = __ballot(pad);
     const bool diag = causal && (key0 + TL::KT - 1 > q0);
+    const bool anym = pmask != 0ull || diag;      // wave-uniform: masking needed on this tile
     bf16x8 sf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -982,7 +991,7 @@ attn_bwd_dq2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
-          const bool msk = ((pmask >> kl) & 1ull) || (diag && key0 + kl > qi);
+          const bool msk = anym && (((pmask >> kl) & 1ull) || (diag && key0 + kl > qi));
           const float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - lq2);
           float dpv = P[e];
           if (drop) dpv = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? dpv * dp.scale : 0.f;

@@ -84,8 +84,19 @@ RETR_DEVICE uint32_t mix32(uint32_t x) {
 RETR_DEVICE uint32_t attn_row_key(uint64_t seed, uint32_t row) {
   return mix32((uint32_t)seed ^ mix32(row * 0x9E3779B9u + (uint32_t)(seed >> 32)));
 }
+// per-element hash: the same xorshift-multiply finaliser on 24-bit multiplies
+// (v_mul_u32_u24, full rate; a 32-bit v_mul_lo_u32 is quarter rate) -- the xorshift before
+// each multiply folds bits 24..31 into the low 24, so no input bit is dropped
+RETR_DEVICE uint32_t mix24(uint32_t x) {
+  x ^= x >> 16;
+  x = __umul24(x, 0xEB352Du);
+  x ^= x >> 15;
+  x = __umul24(x, 0x6CA68Bu);
+  x ^= x >> 16;
+  return x;
+}
 RETR_DEVICE uint32_t attn_pair_bits(uint32_t row_key, uint32_t key) {
-  return mix32(row_key + (key >> 1) * 0x85EBCA77u);
+  return mix24(row_key + __umul24(key >> 1, 0xEBCA77u));
 }
 RETR_DEVICE bool attn_keep(uint32_t bits, uint32_t key, uint32_t thresh16) {
   return ((key & 1) ? (bits >> 16) : (bits & 0xffffu)) >= thresh16;

@@ -394,6 +394,17 @@ def _mix32(x):
     return x
 
 
+def _mix24(x):
+    """common.hpp mix24: the finaliser on 24-bit multiplies (v_mul_u32_u24)."""
+    x = x.astype(np.uint64) & 0xFFFFFFFF
+    x ^= x >> 16
+    x = ((x & 0xFFFFFF) * 0xEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = ((x & 0xFFFFFF) * 0x6CA68B) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
 def attn_keep_mask(seed, B, H, Lq, Lk, p):
     """numpy restatement of the fused attention kernels' dropout keep mask (csrc/common.hpp
     attn_row_key / attn_pair_bits / attn_keep): [B, H, Lq, Lk] bool."""
@@ -403,7 +414,7 @@ def attn_keep_mask(seed, B, H, Lq, Lk, p):
     s_lo, s_hi = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
     rk = _mix32(s_lo ^ _mix32((rows * 0x9E3779B9 + s_hi) & 0xFFFFFFFF))
     keys = np.arange(Lk, dtype=np.uint64)
-    bits = _mix32((rk[:, None] + (keys[None, :] >> 1) * 0x85EBCA77) & 0xFFFFFFFF)
+    bits = _mix24((rk[:, None] + ((keys[None, :] >> 1) & 0xFFFFFF) * 0xEBCA77) & 0xFFFFFFFF)
     half = np.where(keys[None, :] & 1, bits >> 16, bits & 0xFFFF)
     return torch.from_numpy((half >= th16).reshape(B, H, Lq, Lk))
 
