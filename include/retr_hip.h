@@ -232,6 +232,12 @@ int retr_ce_bwd(int dtype, const void* logits, long ld, int M, int V, const long
                 void* stream);
 int retr_argmax_rows(int dtype, const void* x, long ld, int M, int V, long long* out,
                      void* stream);
+/* the same first-index argmax for few long rows (decode logits): 16 segments per row in
+ * parallel, partials reduced by a second kernel.  workspace: retr_argmax_workspace(M) bytes;
+ * falls back to retr_argmax_rows for fp32 / short rows */
+size_t retr_argmax_workspace(int M);
+int retr_argmax_rows_ws(int dtype, const void* x, long ld, int M, int V, long long* out,
+                        void* workspace, void* stream);
 
 /* greedy bookkeeping for step i (eval_utils/decode.py:72-79) on device */
 /* ---- beam search (new capability; reference decode.py has greedy only) -------------------

@@ -103,6 +103,8 @@ _SIGS = {
     "retr_ce_fwd": [_I, _P, _L, _I, _I, _P, _P, _P, _P, _P],
     "retr_ce_bwd": [_I, _P, _L, _I, _I, _P, _P, _P, _F, _P, _L, _P],
     "retr_argmax_rows": [_I, _P, _L, _I, _I, _P, _P],
+    "retr_argmax_workspace": [_I],
+    "retr_argmax_rows_ws": [_I, _P, _L, _I, _I, _P, _P, _P],
     "retr_dropout_apply": [_I, _P, _L, _P, _L, _I, _I, _F, _U64, _P],
     "retr_cast": [_I, _P, _P, _L, _P],
     "retr_add_pos_fwd": [_I, _P, _L, _I, _I, _P, _I, _P, _P, _L, _P],
@@ -118,7 +120,7 @@ _SIGS = {
 }
 _RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
             "retr_layernorm_bwd_workspace": _SZ, "retr_embed_ln_bwd_workspace": _SZ,
-            "retr_linear_wgrad_group_workspace": _SZ,
+            "retr_linear_wgrad_group_workspace": _SZ, "retr_argmax_workspace": _SZ,
             "retr_set_deterministic": None,
             "retr_set_seed_base": None}
 

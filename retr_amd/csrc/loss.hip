@@ -124,9 +124,91 @@ argmax_kernel(const T* x, long ld, int V, long long* out) {
   }
 }
 
+// (value, first index, NaN wins) order of argmax_kernel as a comparison
+RETR_DEVICE bool am_better(float v2, int i2, float v1, int i1) {
+  const bool nan2 = v2 != v2, nan1 = v1 != v1;
+  return (nan2 && !nan1) || (nan2 == nan1 && (v2 > v1 || (v2 == v1 && i2 < i1)));
+}
+
+// Split argmax for few long rows (decode: 64 rows x 30522 logits): blockIdx.x = segment of the
+// row, blockIdx.y = row; every 16-byte load of a segment is in flight at once.  Partials
+// (value, index) go to ws[row][segment]; argmax_final_kernel reduces them per row.
+constexpr int kArgSeg = 16;
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+argmax_part_kernel(const T* x, long ld, int V, float* pv, int* pi) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int row = blockIdx.y, seg = blockIdx.x;
+  const T* xr = x + (long)row * ld;
+  const int V8 = V / 8;                               // 8-element chunks (ld % 8 == 0)
+  const int per = (V8 + kArgSeg - 1) / kArgSeg;
+  const int c0 = seg * per, c1 = min(V8, c0 + per);
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int c = c0 + threadIdx.x; c < c1; c += 256) {
+    const bf16x8 x8 = *(const bf16x8*)(xr + 8 * c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (am_better((float)x8[e], 8 * c + e, bv, bi)) bv = (float)x8[e], bi = 8 * c + e;
+  }
+  if (seg == kArgSeg - 1)                             // the ragged tail
+    for (int j = 8 * V8 + threadIdx.x; j < V; j += 256)
+      if (am_better(to_f(xr[j]), j, bv, bi)) bv = to_f(xr[j]), bi = j;
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(bv, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    if (am_better(v2, i2, bv, bi)) bv = v2, bi = i2;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) sv[w] = bv, si[w] = bi;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 4; ++i)
+      if (am_better(sv[i], si[i], bv, bi)) bv = sv[i], bi = si[i];
+    pv[row * kArgSeg + seg] = bv;
+    pi[row * kArgSeg + seg] = bi;
+  }
+}
+
+__global__ void argmax_final_kernel(const float* pv, const int* pi, int M, long long* out) {
+  const int row = blockIdx.x * (blockDim.x / kArgSeg) + threadIdx.x / kArgSeg;
+  const int s = threadIdx.x % kArgSeg;
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  if (row < M) bv = pv[row * kArgSeg + s], bi = pi[row * kArgSeg + s];
+  for (int o = kArgSeg / 2; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(bv, o, 64);
+    const int i2 = __shfl_xor(bi, o, 64);
+    if (am_better(v2, i2, bv, bi)) bv = v2, bi = i2;
+  }
+  if (row < M && s == 0) out[row] = bi;
+}
+
 }  // namespace
 
 extern "C" {
+
+int retr_argmax_rows(int dtype, const void* x, long ld, int M, int V, long long* out,
+                     void* stream);
+size_t retr_argmax_workspace(int M) { return (size_t)M * kArgSeg * 8; }
+
+int retr_argmax_rows_ws(int dtype, const void* x, long ld, int M, int V, long long* out,
+                        void* workspace, void* stream) {
+  if (M == 0) return 0;
+  if (dtype != RETR_BF16 || ld % 8 != 0 || V < 8 * kArgSeg * 256 / 4 || !workspace)
+    return retr_argmax_rows(dtype, x, ld, M, V, out, stream);
+  hipStream_t st = (hipStream_t)stream;
+  float* pv = (float*)workspace;
+  int* pi = (int*)(pv + (size_t)M * kArgSeg);
+  hipLaunchKernelGGL(argmax_part_kernel<bf16>, dim3(kArgSeg, M), dim3(256), 0, st, (const bf16*)x,
+                     ld, V, pv, pi);
+  if (int e = retr_check_launch("argmax_part")) return e;
+  hipLaunchKernelGGL(argmax_final_kernel, dim3(cdiv(M, 256 / kArgSeg)), dim3(256), 0, st, pv, pi,
+                     M, out);
+  return retr_check_launch("argmax_final");
+}
 
 int retr_ce_fwd(int dtype, const void* logits, long ld, int M, int V, const long long* targets,
                 float* lse, float* loss_rows, float* loss, void* stream) {

@@ -22,7 +22,7 @@ reference algorithm run by the CPU oracle (tests/test_gpu_model.py).
 import torch
 
 from .. import ops
-from .._lib import call, ptr
+from .._lib import call, load, ptr
 from ..ops import dcode, k_linear_fwd, _st
 
 
@@ -76,6 +76,8 @@ class _DecodeState:
         self.Vp = (V + 63) // 64 * 64
         self.logits = torch.empty(R, self.Vp, dtype=cd, device=dev)
         self.pred = torch.empty(R, dtype=torch.long, device=dev)
+        self.am_ws = torch.empty(max(1, load().retr_argmax_workspace(R) // 4),
+                                 dtype=torch.float32, device=dev)   # split argmax partials
         if K > 1:
             self.init_beam(dev)
         self.head_bias = None
@@ -251,7 +253,8 @@ class IncrementalGreedy:
     def _select(self, st, i, V, eos_token, s):
         """Greedy: first-index argmax + the reference's finished/early-exit bookkeeping."""
         cd = self.cdtype
-        call("retr_argmax_rows", dcode(cd), ptr(st.logits), st.Vp, st.B, V, ptr(st.pred), s)
+        call("retr_argmax_rows_ws", dcode(cd), ptr(st.logits), st.Vp, st.B, V, ptr(st.pred),
+             ptr(st.am_ws), s)
         call("retr_greedy_update", ptr(st.pred), st.B, st.T, i, int(eos_token), ptr(st.caption),
              ptr(st.finished), ptr(st.done), ptr(st.tok), s)
 

@@ -639,3 +639,23 @@ def test_linear_dropout_mask_regenerated_by_backward():
     assert torch.equal(kept_fwd, kept_bwd)
     assert abs(kept_bwd.float().mean().item() - (1 - p)) < 5e-3
     assert torch.allclose(m[kept_bwd], torch.full_like(m[kept_bwd], 1 / (1 - p)))
+
+
+def test_argmax_split_matches_single_pass():
+    """Split (16 segments per row) first-index argmax == the one-block-per-row kernel ==
+    torch.argmax on bf16 decode logits, incl. ties across segments and a NaN row."""
+    M, V, Vp = 64, 30522, 30528
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.randn(M, Vp, generator=g).to(torch.bfloat16)
+    x[:, V:] = 0
+    x[3, 100] = x[3, 25000] = 50.0                  # tie: first index wins
+    x[5, 29999] = float("nan")                      # NaN wins (torch semantics)
+    x = x.to(DEV)
+    ws = torch.empty(_lib.load().retr_argmax_workspace(M) // 4, device=DEV)
+    a = torch.empty(M, dtype=torch.long, device=DEV)
+    b = torch.empty(M, dtype=torch.long, device=DEV)
+    call("retr_argmax_rows_ws", 1, ptr(x), Vp, M, V, ptr(a), ptr(ws), ops._st())
+    call("retr_argmax_rows", 1, ptr(x), Vp, M, V, ptr(b), ops._st())
+    assert torch.equal(a, b)
+    assert torch.equal(a.cpu(), x[:, :V].float().cpu().argmax(1))
+    assert int(a[3]) == 100 and int(a[5]) == 29999
