@@ -106,54 +106,73 @@ dec_gemm_kernel(const bf16* a_plain, const bf16* a_pos, int R, const bf16* w, co
   }
 }
 
-// ---- dec_rows: residual update + LayerNorm, one wave per row ----------------------------------
+// ---- dec_rows: residual update + LayerNorm, one block per row ---------------------------------
 // x = xin (+ b2 + sum_j slabs[j], slabs in order); xout = x (if given); n = LN(x) (bf16),
-// npos = LN(x) + pos (bf16, if given).  The LN arithmetic of ln_fwd_kernel (norm.hip).
-template <int PER>
+// npos = LN(x) + pos (bf16, if given).
+// One 256-thread block per row: thread t owns columns t, t + 256 (C / 256 of them) and issues
+// all of its slab loads at once (a wave-per-row layout ran only R / 4 blocks and walked the
+// slabs in four dependent chunks); slabs are added in slab order per column.  The row's
+// LayerNorm statistics come from a wave butterfly plus a 4-wave LDS sum.
+template <int CPT>
 __global__ void __launch_bounds__(256)
-dec_rows_kernel(const float* xin, const float* slabs, int nslab, const float* b2, int R,
-                float* xout, const float* gamma, const float* beta, float eps, const float* pos,
-                bf16* n, bf16* npos) {
-  constexpr int C = PER * 64;
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= R) return;
+dec_rows_blk_kernel(const float* xin, const float* slabs, int nslab, const float* b2, int R,
+                    float* xout, const float* gamma, const float* beta, float eps,
+                    const float* pos, bf16* n, bf16* npos) {
+  constexpr int C = CPT * 256, MAXS = 64 / CPT;
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = blockIdx.x;
   const long RC = (long)R * C;
-  float v[PER];
+  float v[CPT];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) v[i] = xin[(long)r * C + lane + 64 * i];
+  for (int i = 0; i < CPT; ++i) v[i] = xin[(long)r * C + tid + 256 * i];
   if (slabs) {
-    float s[PER];
+    float s[CPT];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) s[i] = 0.f;
-    constexpr int CHUNK = 16;                      // CHUNK x PER loads in flight
-    for (int j0 = 0; j0 < nslab; j0 += CHUNK) {
-      float t[CHUNK][PER];
+    for (int i = 0; i < CPT; ++i) s[i] = 0.f;
+    for (int j0 = 0; j0 < nslab; j0 += MAXS) {
+      float t[MAXS][CPT];
 #pragma unroll
-      for (int u = 0; u < CHUNK; ++u)
+      for (int u = 0; u < MAXS; ++u)
 #pragma unroll
-        for (int i = 0; i < PER; ++i)
-          t[u][i] = j0 + u < nslab ? slabs[(long)(j0 + u) * RC + (long)r * C + lane + 64 * i] : 0.f;
+        for (int i = 0; i < CPT; ++i)
+          t[u][i] = j0 + u < nslab ? slabs[(long)(j0 + u) * RC + (long)r * C + tid + 256 * i] : 0.f;
 #pragma unroll
-      for (int u = 0; u < CHUNK; ++u)
+      for (int u = 0; u < MAXS; ++u)
 #pragma unroll
-        for (int i = 0; i < PER; ++i)
+        for (int i = 0; i < CPT; ++i)
           if (j0 + u < nslab) s[i] += t[u][i];
     }
 #pragma unroll
-    for (int i = 0; i < PER; ++i) v[i] = v[i] + (s[i] + b2[lane + 64 * i]);
+    for (int i = 0; i < CPT; ++i) v[i] = v[i] + (s[i] + b2[tid + 256 * i]);
   }
   if (xout) {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) xout[(long)r * C + lane + 64 * i] = v[i];
+    for (int i = 0; i < CPT; ++i) xout[(long)r * C + tid + 256 * i] = v[i];
   }
-  float o[PER];
-  ln_row_wave<PER>(v, gamma, beta, eps, C, lane, o);
+  float sm = 0.f;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = lane + 64 * i;
-    n[(long)r * C + c] = (bf16)o[i];
-    if (npos) npos[(long)r * C + c] = (bf16)(o[i] + pos[c]);
+  for (int i = 0; i < CPT; ++i) sm += v[i];
+  sm = wave_sum(sm);
+  if (lane == 0) red[0][wave] = sm;
+  __syncthreads();
+  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  q = wave_sum(q);
+  if (lane == 0) red[1][wave] = q;
+  __syncthreads();
+  const float rstd = 1.0f / sqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / C + eps);
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = tid + 256 * i;
+    const float o = (v[i] - mean) * rstd * gamma[c] + beta[c];
+    n[(long)r * C + c] = (bf16)o;
+    if (npos) npos[(long)r * C + c] = (bf16)(o + pos[c]);
   }
 }
 
@@ -387,14 +406,16 @@ dec_attn_row_kernel(AttnRowArgs a, float scale) {
 
 // ---- dec_ffn: FFN1 + ReLU + FFN2 over hidden units [32 j, 32 j + 32) -> slab j -----------------
 template <int PER>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(64)
 dec_ffn_kernel(const bf16* n3, int R, const bf16* w1, const float* b1, const bf16* w2, int F,
                float* slabs) {
+  // one wave = 16 rows per block: every wave loads its own weight fragments anyway, so
+  // single-wave blocks cost no extra traffic and put 4x the blocks on the GPU at R = 64
   constexpr int C = PER * 64;
   constexpr int HS = 32 + 8;
-  __shared__ __attribute__((aligned(16))) bf16 Hs[64 * HS];     // relu(h) [64 rows][32 units]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int j0 = blockIdx.x * 32, r0 = blockIdx.y * 64;
+  __shared__ __attribute__((aligned(16))) bf16 Hs[16 * HS];     // relu(h) [16 rows][32 units]
+  const int tid = threadIdx.x, lane = tid & 63, wave = 0;
+  const int j0 = blockIdx.x * 32, r0 = blockIdx.y * 16;
   constexpr int NT = C / 16;                     // output column tiles of FFN2
   // every fragment of both weight slices and of the wave's 16 input rows, before any MFMA
   u32x4 w1f[2][C / 32], af[C / 32], w2f[NT];
@@ -482,11 +503,11 @@ int retr_dec_rows(const float* xin, const float* slabs, int nslab, const float* 
   if (R == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (C == 256)
-    hipLaunchKernelGGL(dec_rows_kernel<4>, dim3(cdiv(R, 4)), dim3(256), 0, st, xin, slabs, nslab,
-                       b2, R, xout, gamma, beta, eps, pos, (bf16*)n, (bf16*)npos);
+    hipLaunchKernelGGL(dec_rows_blk_kernel<1>, dim3(R), dim3(256), 0, st, xin, slabs, nslab, b2,
+                       R, xout, gamma, beta, eps, pos, (bf16*)n, (bf16*)npos);
   else
-    hipLaunchKernelGGL(dec_rows_kernel<8>, dim3(cdiv(R, 4)), dim3(256), 0, st, xin, slabs, nslab,
-                       b2, R, xout, gamma, beta, eps, pos, (bf16*)n, (bf16*)npos);
+    hipLaunchKernelGGL(dec_rows_blk_kernel<2>, dim3(R), dim3(256), 0, st, xin, slabs, nslab, b2,
+                       R, xout, gamma, beta, eps, pos, (bf16*)n, (bf16*)npos);
   return retr_check_launch("dec_rows");
 }
 
@@ -524,12 +545,12 @@ int retr_dec_ffn(const void* n3, int R, int C, const void* w1, const float* b1, 
   RETR_REQUIRE((C == 256 || C == 512) && F % 32 == 0, "dec_ffn: C=%d F=%d", C, F);
   if (R == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid(F / 32, cdiv(R, 64));
+  dim3 grid(F / 32, cdiv(R, 16));
   if (C == 256)
-    hipLaunchKernelGGL(dec_ffn_kernel<4>, grid, dim3(256), 0, st, (const bf16*)n3, R,
+    hipLaunchKernelGGL(dec_ffn_kernel<4>, grid, dim3(64), 0, st, (const bf16*)n3, R,
                        (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
   else
-    hipLaunchKernelGGL(dec_ffn_kernel<8>, grid, dim3(256), 0, st, (const bf16*)n3, R,
+    hipLaunchKernelGGL(dec_ffn_kernel<8>, grid, dim3(64), 0, st, (const bf16*)n3, R,
                        (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
   return retr_check_launch("dec_ffn");
 }
