@@ -404,6 +404,147 @@ dec_attn_row_kernel(AttnRowArgs a, float scale) {
   for (int c = tid; c < C; c += NT) a.q2[(long)r * C + c] = (bf16)(yb[c] + a.bq[c]);
 }
 
+// Two waves per head (1024 threads, H = 8): each wave scores and accumulates one half of the
+// keys against its own running max; the halves merge through LDS (max, sum, 8 partial dims per
+// lane group) -- the per-head dependency chain (key loads, scores, softmax, P V) is half as
+// long as with one wave per head.  The out-projection / LayerNorm / next-query tail is the
+// 512-thread kernel's, on 32 half-waves.
+template <int PER, int HD, int MK>
+__global__ void __launch_bounds__(1024)
+dec_attn_row2_kernel(AttnRowArgs a, float scale) {
+  constexpr int C = PER * 64, H = C / HD, NT = 1024;
+  constexpr int MKH = MK / 2;                    // key groups of 64 per half
+  constexpr int NG = HD / 8, NPART = 64 / NG;
+  constexpr int NU = 64 * MK / NPART;            // value rows per lane over all keys
+  constexpr int NUH = NU / 2;                    // ... per half
+  static_assert(H * 2 == NT / 64 && MK % 2 == 0, "two waves per head");
+  __shared__ float qs[C];
+  __shared__ float ob[C];
+  __shared__ float yb[C];
+  __shared__ float pb[H][64 * MK];               // probabilities of each head (both halves)
+  __shared__ float hmx[H][2], hsum[H][2];
+  __shared__ float hacc[H][HD];                  // half 1's unnormalised P V
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = wave >> 1, half = wave & 1;
+  const int r = blockIdx.x;
+  constexpr bool kPre = C == 256;
+  GemvFrag<C, NT> wo;
+  if constexpr (kPre) wo.load(a.wo, tid);
+  for (int c = tid; c < C; c += NT) qs[c] = (float)(bf16)((float)a.q[(long)r * C + c] * scale);
+  const int kvb = r / a.kv_group;
+  const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
+  const unsigned char* km = a.kpm ? a.kpm + (long)kvb * a.Lk : nullptr;
+  const int Lk = a.Lk;
+  long krow[MKH];
+  bool kok[MKH];
+#pragma unroll
+  for (int m = 0; m < MKH; ++m) {
+    const int j = lane + 64 * (m + half * MKH);
+    kok[m] = j < Lk && !(km && km[j]);
+    krow[m] = j < Lk ? (ar ? (long)ar[j] : (long)kvb) * a.Lmax + j : 0;
+  }
+  bf16x8 kv[MKH][HD / 8];
+#pragma unroll
+  for (int m = 0; m < MKH; ++m)
+#pragma unroll
+    for (int d0 = 0; d0 < HD / 8; ++d0)
+      kv[m][d0] = kok[m] ? *(const bf16x8*)(a.k + krow[m] * C + h * HD + 8 * d0) : bf16x8{};
+  const int g = lane % NG, part = lane / NG;
+  bf16x8 vv[NUH];                                // this half's value rows, keys in order
+#pragma unroll
+  for (int u = 0; u < NUH; ++u) {
+    const int j = part + NPART * (u + half * NUH);
+    const long row = j < Lk ? (ar ? (long)ar[j] : (long)kvb) * a.Lmax + j : 0;
+    vv[u] = j < Lk ? *(const bf16x8*)(a.v + row * C + h * HD + 8 * g) : bf16x8{};
+  }
+  __syncthreads();
+  float sc[MKH];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int m = 0; m < MKH; ++m) {
+    float sv = -INFINITY;
+    if (kok[m]) {
+      sv = 0.f;
+#pragma unroll
+      for (int d0 = 0; d0 < HD / 8; ++d0)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sv += qs[h * HD + 8 * d0 + e] * (float)kv[m][d0][e];
+    }
+    sc[m] = sv;
+    mx = fmaxf(mx, sv);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  float* p = pb[h];
+#pragma unroll
+  for (int m = 0; m < MKH; ++m) {
+    const float e = (mx == -INFINITY || sc[m] == -INFINITY) ? 0.f : __expf(sc[m] - mx);
+    p[lane + 64 * (m + half * MKH)] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < NUH; ++u) {
+    const int j = part + NPART * (u + half * NUH);
+    const float pj = j < Lk ? p[j] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += pj * (float)vv[u][e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int o = NG; o < 64; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
+  if (lane == 0) {
+    hmx[h][half] = mx;
+    hsum[h][half] = sum;
+  }
+  if (half == 1 && part == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hacc[h][8 * g + e] = acc[e];
+  }
+  __syncthreads();
+  if (half == 0 && part == 0) {
+    const float m0 = hmx[h][0], m1 = hmx[h][1];
+    const float M = fmaxf(m0, m1);
+    const float e0 = (m0 == -INFINITY) ? 0.f : __expf(m0 - M);
+    const float e1 = (m1 == -INFINITY) ? 0.f : __expf(m1 - M);
+    const float inv = 1.f / (hsum[h][0] * e0 + hsum[h][1] * e1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      ob[h * HD + 8 * g + e] = (float)(bf16)((acc[e] * e0 + hacc[h][8 * g + e] * e1) * inv);
+  }
+  __syncthreads();
+  if constexpr (kPre) wo.dot(ob, yb, tid);
+  else gemv_rows<C, NT>(a.wo, ob, yb, tid);
+  GemvFrag<C, NT> wq;
+  if (kPre && a.wq) wq.load(a.wq, tid);
+  __syncthreads();
+  if (wave == 0) {
+    float v[PER], o[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = a.x[(long)r * C + c] + (yb[c] + a.bo[c]);
+      a.xo[(long)r * C + c] = v[i];
+    }
+    ln_row_wave<PER>(v, a.gamma, a.beta, a.eps, C, lane, o);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      const float t = (float)(bf16)(a.pos ? o[i] + a.pos[c] : o[i]);
+      if (a.wq) ob[c] = t;
+      else a.q2[(long)r * C + c] = (bf16)t;
+    }
+  }
+  if (!a.wq) return;
+  __syncthreads();
+  if constexpr (kPre) wq.dot(ob, yb, tid);
+  else gemv_rows<C, NT>(a.wq, ob, yb, tid);
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) a.q2[(long)r * C + c] = (bf16)(yb[c] + a.bq[c]);
+}
+
 // ---- dec_ffn: FFN1 + ReLU + FFN2 over hidden units [32 j, 32 j + 32) -> slab j -----------------
 template <int PER>
 __global__ void __launch_bounds__(64)
@@ -473,6 +614,15 @@ void set_lds(K kern, size_t bytes) {
   }
 }
 
+// eight heads: two waves per head (1024 threads); otherwise one wave per head
+template <int P, int HDV, int MKV>
+void launch_attn_row(const AttnRowArgs& a, float scale, int R, hipStream_t st) {
+  if constexpr (P * 64 / HDV == 8)
+    hipLaunchKernelGGL((dec_attn_row2_kernel<P, HDV, MKV>), dim3(R), dim3(1024), 0, st, a, scale);
+  else
+    hipLaunchKernelGGL((dec_attn_row_kernel<P, HDV, MKV>), dim3(R), dim3(512), 0, st, a, scale);
+}
+
 }  // namespace
 
 extern "C" {
@@ -525,8 +675,7 @@ int retr_dec_attn_row(const void* q, const void* k, const void* v, int R, int C,
                 (const bf16*)wo, bo, xo, gamma, beta, eps, pos, (const bf16*)wq, bq, (bf16*)q2};
   const float scale = 1.0f / sqrtf((float)hd);
   hipStream_t st = (hipStream_t)stream;
-#define ATT(P, HDV, MKV) \
-  hipLaunchKernelGGL((dec_attn_row_kernel<P, HDV, MKV>), dim3(R), dim3(512), 0, st, a, scale)
+#define ATT(P, HDV, MKV) launch_attn_row<P, HDV, MKV>(a, scale, R, st)
 #define ATT_MK(P, HDV)                 \
   if (Lk <= 128) ATT(P, HDV, 2);       \
   else if (Lk <= 256) ATT(P, HDV, 4);  \
