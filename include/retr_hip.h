@@ -143,6 +143,14 @@ int retr_conv_pack(int dtype, const float* w, const float* bn_w, const float* bn
                    const float* bn_rm, const float* bn_rv, const float* conv_bias, int Co, int Ci,
                    int KH, int KW, int Cp, void* w_out, void* wt_out, float* bias_out,
                    float* scale_out, void* stream);
+/* every conv's packing in one launch (up to 16 per kernel, more in further launches) */
+typedef struct {
+  const float *w, *bn_w, *bn_b, *bn_rm, *bn_rv, *conv_bias;   /* as retr_conv_pack */
+  void *w_out, *wt_out;
+  float *bias_out, *scale_out;
+  int Co, Ci, KH, KW, Cp, pad;
+} retr_conv_pack_desc;
+int retr_conv_pack_group(int dtype, int n, const retr_conv_pack_desc* d, void* stream);
 int retr_conv2d_fwd(int dtype, const void* x, int Nb, int H, int W, int C, const void* w,
                     const float* bias, const void* residual, void* y, int Co, int KH, int KW,
                     int stride, int pad, int dil, int relu, void* stream);

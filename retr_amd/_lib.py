@@ -43,6 +43,14 @@ class LinearWgradDesc(ctypes.Structure):
                 ("db", _P), ("M", _I), ("N", _I), ("K", _I), ("accumulate", _I)]
 
 
+class ConvPackDesc(ctypes.Structure):
+    """retr_conv_pack_desc"""
+    _fields_ = [("w", _P), ("bn_w", _P), ("bn_b", _P), ("bn_rm", _P), ("bn_rv", _P),
+                ("conv_bias", _P), ("w_out", _P), ("wt_out", _P), ("bias_out", _P),
+                ("scale_out", _P), ("Co", _I), ("Ci", _I), ("KH", _I), ("KW", _I), ("Cp", _I),
+                ("pad", _I)]
+
+
 _PFD = ctypes.POINTER(LinearFwdDesc)
 _PDD = ctypes.POINTER(LinearDgradDesc)
 _PWD = ctypes.POINTER(LinearWgradDesc)
@@ -70,6 +78,7 @@ _SIGS = {
     "retr_linear_wgrad_group_workspace": [_I, _PWD],
     "retr_linear_wgrad_group": [_I, _I, _PWD, _P, _P],
     "retr_conv_pack": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
+    "retr_conv_pack_group": [_I, _I, ctypes.POINTER(ConvPackDesc), _P],
     "retr_conv2d_fwd": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "retr_conv2d_dgrad": [_I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "retr_conv2d_wgrad": [_I, _P, _P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P],

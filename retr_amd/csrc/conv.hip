@@ -569,6 +569,113 @@ __global__ void wgrad_unpack_kernel(const float* ws, const float* scale, float* 
   }
 }
 
+// Grouped weight packing: every conv of the backbone in one launch (the per-conv launches were
+// ~42 small, latency-bound kernels per training step).  Block ranges per descriptor (block-
+// uniform descriptor lookup); the per-element arithmetic of conv_pack_kernel.
+constexpr int kPackGroup = 16;
+constexpr int kPackPerThread = 4;
+
+struct PackGroup {
+  retr_conv_pack_desc d[kPackGroup];
+  int blk0[kPackGroup + 1];
+  int n;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) conv_pack_group_kernel(PackGroup g) {
+  const int bid = blockIdx.x;
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < kPackGroup; ++i)
+    if (i < g.n && bid >= g.blk0[i]) p = i;
+  const retr_conv_pack_desc& d = g.d[p];
+  const int Co = d.Co, Ci = d.Ci, KH = d.KH, KW = d.KW, Cp = d.Cp;
+  const long total = (long)Co * KH * KW * Cp;
+  const long base = ((long)(bid - g.blk0[p]) * 256 + threadIdx.x) * kPackPerThread;
+  const float* bnw = d.bn_w;
+#pragma unroll
+  for (int u = 0; u < kPackPerThread; ++u) {
+    const long i = base + u;
+    if (i >= total) break;
+    const int ci = (int)(i % Cp);
+    long t = i / Cp;
+    const int kw = (int)(t % KW);
+    t /= KW;
+    const int kh = (int)(t % KH);
+    const int co = (int)(t / KH);
+    float scale = 1.f;
+    if (bnw) scale = bnw[co] * (1.0f / sqrtf(d.bn_rv[co] + 1e-5f));
+    const float v = ci < Ci ? d.w[(((long)co * Ci + ci) * KH + kh) * KW + kw] * scale : 0.f;
+    ((T*)d.w_out)[i] = from_f<T>(v);
+    if (d.wt_out) ((T*)d.wt_out)[(((long)ci * KH + kh) * KW + kw) * Co + co] = from_f<T>(v);
+    if (ci == 0 && kh == 0 && kw == 0) {
+      float b;
+      if (bnw) b = d.bn_b[co] - d.bn_rm[co] * scale;
+      else b = d.conv_bias ? d.conv_bias[co] : 0.f;
+      if (d.bias_out) d.bias_out[co] = b;
+      if (d.scale_out) d.scale_out[co] = scale;
+    }
+  }
+}
+
+// Tiled grouped packing for convs with Ci == Cp and 64 | Co, Cp: one block per (desc, 64 output
+// channels, 64 input channels, all KHW taps): the fp32 rows [co][ci0 .. ci0+63][taps] are read as
+// contiguous runs, folded and rounded into an LDS tile, and both images are written as 128-byte
+// runs ([co][tap][Cp] with ci fastest, [ci][tap][Co] with co fastest).
+template <typename T, int KHW>
+__global__ void __launch_bounds__(256) conv_pack_tiled_group_kernel(PackGroup g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* tile = (T*)smem;                            // [64 co][64 ci][KHW]
+  __shared__ float sc[64];
+  const int bid = blockIdx.x;
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < kPackGroup; ++i)
+    if (i < g.n && bid >= g.blk0[i]) p = i;
+  const retr_conv_pack_desc& d = g.d[p];
+  const int Co = d.Co, Cp = d.Cp;
+  const int t = bid - g.blk0[p], tn = Cp / 64;
+  const int co0 = (t / tn) * 64, ci0 = (t % tn) * 64;
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    const int co = co0 + tid;
+    float scale = 1.f;
+    if (d.bn_w) scale = d.bn_w[co] * (1.0f / sqrtf(d.bn_rv[co] + 1e-5f));
+    sc[tid] = scale;
+    if (ci0 == 0) {
+      float b;
+      if (d.bn_w) b = d.bn_b[co] - d.bn_rm[co] * scale;
+      else b = d.conv_bias ? d.conv_bias[co] : 0.f;
+      if (d.bias_out) d.bias_out[co] = b;
+      if (d.scale_out) d.scale_out[co] = scale;
+    }
+  }
+  __syncthreads();
+  constexpr int ROW = 64 * KHW;                  // one co row of the tile
+  constexpr int TOT = 64 * ROW;
+#pragma unroll 8
+  for (int e = tid; e < TOT; e += 256) {
+    const int r = e / ROW, j = e - r * ROW;
+    tile[e] = from_f<T>(d.w[((long)(co0 + r) * Cp + ci0) * KHW + j] * sc[r]);
+  }
+  __syncthreads();
+  T* wout = (T*)d.w_out;
+#pragma unroll 8
+  for (int e = tid; e < TOT; e += 256) {
+    const int ci = e & 63, q = e >> 6;
+    const int tap = q % KHW, r = q / KHW;
+    wout[((long)(co0 + r) * KHW + tap) * Cp + ci0 + ci] = tile[r * ROW + ci * KHW + tap];
+  }
+  if (!d.wt_out) return;
+  T* wt = (T*)d.wt_out;
+#pragma unroll 8
+  for (int e = tid; e < TOT; e += 256) {
+    const int r = e & 63, q = e >> 6;
+    const int tap = q % KHW, ci = q / KHW;
+    wt[((long)(ci0 + ci) * KHW + tap) * Co + co0 + r] = tile[r * ROW + ci * KHW + tap];
+  }
+}
+
 Geom make_geom(int Nb, int H, int W, int C, int Co, int KH, int KW, int s, int p, int d) {
   Geom g{Nb, H, W, C, Co, KH, KW, s, p, d, 0, 0};
   g.OH = (H + 2 * p - d * (KH - 1) - 1) / s + 1;
@@ -625,6 +732,67 @@ int retr_conv_pack(int dtype, const float* w, const float* bn_w, const float* bn
     hipLaunchKernelGGL(conv_pack_kernel<float>, dim3(grid), dim3(256), 0, st, w, bn_w, bn_b, bn_rm,
                        bn_rv, conv_bias, Co, Ci, KH, KW, Cp, (float*)w_out, (float*)wt_out, bias_out, scale_out);
   return retr_check_launch("conv_pack");
+}
+
+namespace {
+// launch one class of descriptors (tiled kernel with KHW taps, or the elementwise one: KHW = 0)
+template <typename T, int KHW>
+int pack_class(const retr_conv_pack_desc* const* d, int n, hipStream_t st) {
+  for (int i0 = 0; i0 < n; i0 += kPackGroup) {
+    PackGroup g{};
+    int blocks = 0;
+    for (int i = i0; i < n && g.n < kPackGroup; ++i) {
+      const retr_conv_pack_desc& q = *d[i];
+      g.d[g.n] = q;
+      g.blk0[g.n] = blocks;
+      if constexpr (KHW > 0) blocks += (q.Co / 64) * (q.Cp / 64);
+      else blocks += (int)cdiv((long)q.Co * q.KH * q.KW * q.Cp, 256L * kPackPerThread);
+      ++g.n;
+    }
+    g.blk0[g.n] = blocks;
+    if (blocks == 0) continue;
+    if constexpr (KHW > 0) {
+      constexpr size_t lds = (size_t)64 * 64 * KHW * sizeof(T);
+      auto kern = conv_pack_tiled_group_kernel<T, KHW>;
+      static bool attr = false;
+      if (lds > 65536 && !attr) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        attr = true;
+      }
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, st, g);
+    } else {
+      hipLaunchKernelGGL(conv_pack_group_kernel<T>, dim3(blocks), dim3(256), 0, st, g);
+    }
+    if (int e = retr_check_launch("conv_pack_group")) return e;
+  }
+  return 0;
+}
+
+template <typename T>
+int pack_all(int n, const retr_conv_pack_desc* d, hipStream_t st) {
+  // classes: 3x3 / 1x1 tiled (Ci == Cp, 64 | Co, 64 | Cp), everything else elementwise
+  const retr_conv_pack_desc* c9[256];
+  const retr_conv_pack_desc* c1[256];
+  const retr_conv_pack_desc* ce[256];
+  int n9 = 0, n1 = 0, ne = 0;
+  for (int i = 0; i < n; ++i) {
+    const retr_conv_pack_desc& q = d[i];
+    const bool tiled = q.Ci == q.Cp && q.Co % 64 == 0 && q.Cp % 64 == 0;
+    if (tiled && q.KH * q.KW == 9) c9[n9++] = &q;
+    else if (tiled && q.KH * q.KW == 1) c1[n1++] = &q;
+    else ce[ne++] = &q;
+  }
+  if (int e = pack_class<T, 9>(c9, n9, st)) return e;
+  if (int e = pack_class<T, 1>(c1, n1, st)) return e;
+  return pack_class<T, 0>(ce, ne, st);
+}
+}  // namespace
+
+int retr_conv_pack_group(int dtype, int n, const retr_conv_pack_desc* d, void* stream) {
+  RETR_REQUIRE(n >= 0 && n <= 256, "conv_pack_group: n=%d (0..256)", n);
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == RETR_BF16 ? pack_all<bf16>(n, d, st) : pack_all<float>(n, d, st);
 }
 
 int retr_conv2d_wgrad_splits(int dtype, int Nb, int H, int W, int C, int Co, int KH, int KW,

@@ -108,6 +108,40 @@ class _PackCache:
         return out
 
 
+    def prepare(self, specs, dtype):
+        """Pack every stale conv of ``specs`` in one grouped launch (retr_conv_pack_group)."""
+        todo = []
+        for spec in specs:
+            w, bn = spec.conv.weight, spec.bn
+            ver = (w._version, w.data_ptr(), dtype) + tuple(
+                (b._version, b.data_ptr()) for b in (bn.weight, bn.bias, bn.running_mean,
+                                                     bn.running_var))
+            ent = self._d.get(id(spec))
+            if ent is None or ent[0] != ver:
+                todo.append((spec, ver))
+        if not todo:
+            return
+        arr = (_lib.ConvPackDesc * len(todo))()
+        keep = []
+        for i, (spec, ver) in enumerate(todo):
+            w, bn = spec.conv.weight, spec.bn
+            co, ci, k = spec.cout, spec.cin, spec.k
+            dev = w.device
+            wp = torch.empty(co, k, k, spec.cp, dtype=dtype, device=dev)
+            wt = torch.empty(spec.cp, k, k, co, dtype=dtype, device=dev)
+            bias = torch.empty(co, dtype=torch.float32, device=dev)
+            scale = torch.empty(co, dtype=torch.float32, device=dev)
+            wd = w.detach().contiguous()
+            keep.append(wd)
+            d = arr[i]
+            d.w, d.bn_w, d.bn_b = ptr(wd), ptr(bn.weight), ptr(bn.bias)
+            d.bn_rm, d.bn_rv, d.conv_bias = ptr(bn.running_mean), ptr(bn.running_var), None
+            d.w_out, d.wt_out, d.bias_out, d.scale_out = ptr(wp), ptr(wt), ptr(bias), ptr(scale)
+            d.Co, d.Ci, d.KH, d.KW, d.Cp = co, ci, k, k, spec.cp
+            self._d[id(spec)] = (ver, (wp, wt, bias, scale))
+        call("retr_conv_pack_group", dcode(dtype), len(todo), arr, _st())
+
+
 PACKS = _PackCache()
 
 
@@ -155,6 +189,7 @@ class _Backbone(torch.autograd.Function):
     def forward(ctx, images, runner, *weights):
         stem, blocks, cdtype = runner.stem, runner.blocks, runner.cdtype
         _lib.require_device(images)
+        PACKS.prepare(runner.specs, cdtype)      # every stale conv packed in one launch
         N, C, H, W = images.shape
         x = torch.empty(N, H, W, stem.cp, dtype=cdtype, device=images.device)
         img = images.detach().float().contiguous()
@@ -257,6 +292,8 @@ class BackboneRunner:
         for b in self.blocks:
             ws.extend(b.params())
         self.weights = ws
+        self.specs = [self.stem] + [c for b in self.blocks
+                                    for c in b.convs + ([b.ds] if b.ds is not None else [])]
 
     def run(self, images):
         # activations are only kept when autograd will call backward
