@@ -261,6 +261,11 @@ int retr_beam_select(const int* cand_tok, const float* cand_lp, int B, int K, in
 int retr_greedy_update(const long long* pred, int B, int T, int i, long long eos,
                        long long* caption, unsigned char* finished, int* done, long long* tok,
                        void* stream);
+/* retr_argmax_rows_ws + retr_greedy_update with the per-row reduction and the bookkeeping in
+ * one launch (pred is written too); workspace: retr_argmax_workspace(B) bytes */
+int retr_greedy_select(int dtype, const void* logits, long ld, int B, int V, void* workspace,
+                       int T, int i, long long eos, long long* pred, long long* caption,
+                       unsigned char* finished, int* done, long long* tok, void* stream);
 
 /* ---- elementwise helpers --------------------------------------------------------------- */
 /* Encoder output without a final LayerNorm (pre_norm=False; models/ConcatTransformer.py:24,
@@ -312,6 +317,12 @@ int retr_dec_gemm(const void* a_plain, const void* a_pos, int R, int C, const vo
 int retr_dec_rows(const float* xin, const float* slabs, int nslab, const float* b2, int R, int C,
                   float* xout, const float* gamma, const float* beta, float eps, const float* pos,
                   void* n, void* npos, void* stream);
+/* decode-step input rows: x = LN_e(word[tok[r]] + qpos) (fp32, the retr_embed_ln_fwd
+ * arithmetic, DecoderEmbeddings models/ConcatTransformer.py:224-243 at one position), then
+ * n = LN1(x), npos = LN1(x) + qpos (bf16, the retr_dec_rows arithmetic) */
+int retr_dec_embed_rows(const long long* tok, int R, int C, const float* word, const float* qpos,
+                        const float* ge, const float* be, float epse, float* x, const float* g1,
+                        const float* b1, float eps1, void* n, void* npos, void* stream);
 /* per query row: multi-head attention over Lk cache/memory rows ((anc ? anc[r][j] : r/kv_group)
  * * Lmax + j; kpm [R/kv_group][Lk]), xo = x + o Wo^T + bo, then LN(xo) (+pos) -> q2 = (.) Wq^T
  * + bq, or q2 = LN(xo) when wq is NULL */

@@ -625,7 +625,7 @@ __global__ void __launch_bounds__(256) conv_pack_group_kernel(PackGroup g) {
 template <typename T, int KHW>
 __global__ void __launch_bounds__(256) conv_pack_tiled_group_kernel(PackGroup g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* tile = (T*)smem;                            // [64 co][64 ci][KHW]
+  T* tile = (T*)smem;                            // [64 co][64 ci][KHW] (+2 pad per co)
   __shared__ float sc[64];
   const int bid = blockIdx.x;
   int p = 0;
@@ -652,11 +652,12 @@ __global__ void __launch_bounds__(256) conv_pack_tiled_group_kernel(PackGroup g)
   }
   __syncthreads();
   constexpr int ROW = 64 * KHW;                  // one co row of the tile
-  constexpr int TOT = 64 * ROW;
+  constexpr int LDR = ROW + 2;                   // odd dword stride: the co-fastest reads below
+  constexpr int TOT = 64 * ROW;                  // hit 64 distinct banks
 #pragma unroll 8
   for (int e = tid; e < TOT; e += 256) {
     const int r = e / ROW, j = e - r * ROW;
-    tile[e] = from_f<T>(d.w[((long)(co0 + r) * Cp + ci0) * KHW + j] * sc[r]);
+    tile[r * LDR + j] = from_f<T>(d.w[((long)(co0 + r) * Cp + ci0) * KHW + j] * sc[r]);
   }
   __syncthreads();
   T* wout = (T*)d.w_out;
@@ -664,7 +665,7 @@ __global__ void __launch_bounds__(256) conv_pack_tiled_group_kernel(PackGroup g)
   for (int e = tid; e < TOT; e += 256) {
     const int ci = e & 63, q = e >> 6;
     const int tap = q % KHW, r = q / KHW;
-    wout[((long)(co0 + r) * KHW + tap) * Cp + ci0 + ci] = tile[r * ROW + ci * KHW + tap];
+    wout[((long)(co0 + r) * KHW + tap) * Cp + ci0 + ci] = tile[r * LDR + ci * KHW + tap];
   }
   if (!d.wt_out) return;
   T* wt = (T*)d.wt_out;
@@ -672,7 +673,7 @@ __global__ void __launch_bounds__(256) conv_pack_tiled_group_kernel(PackGroup g)
   for (int e = tid; e < TOT; e += 256) {
     const int r = e & 63, q = e >> 6;
     const int tap = q % KHW, ci = q / KHW;
-    wt[((long)(ci0 + ci) * KHW + tap) * Co + co0 + r] = tile[r * ROW + ci * KHW + tap];
+    wt[((long)(ci0 + ci) * KHW + tap) * Co + co0 + r] = tile[r * LDR + ci * KHW + tap];
   }
 }
 
@@ -734,6 +735,8 @@ int retr_conv_pack(int dtype, const float* w, const float* bn_w, const float* bn
   return retr_check_launch("conv_pack");
 }
 
+}  // extern "C"
+
 namespace {
 // launch one class of descriptors (tiled kernel with KHW taps, or the elementwise one: KHW = 0)
 template <typename T, int KHW>
@@ -752,7 +755,7 @@ int pack_class(const retr_conv_pack_desc* const* d, int n, hipStream_t st) {
     g.blk0[g.n] = blocks;
     if (blocks == 0) continue;
     if constexpr (KHW > 0) {
-      constexpr size_t lds = (size_t)64 * 64 * KHW * sizeof(T);
+      constexpr size_t lds = (size_t)64 * (64 * KHW + 2) * sizeof(T);
       auto kern = conv_pack_tiled_group_kernel<T, KHW>;
       static bool attr = false;
       if (lds > 65536 && !attr) {
@@ -788,6 +791,8 @@ int pack_all(int n, const retr_conv_pack_desc* d, hipStream_t st) {
   return pack_class<T, 0>(ce, ne, st);
 }
 }  // namespace
+
+extern "C" {
 
 int retr_conv_pack_group(int dtype, int n, const retr_conv_pack_desc* d, void* stream) {
   RETR_REQUIRE(n >= 0 && n <= 256, "conv_pack_group: n=%d (0..256)", n);

@@ -15,6 +15,8 @@
 // bf16 operands, fp32 accumulation and residual stream, exactly the roundings of the unfused
 // path (bf16 GEMM inputs, bf16 q/k/v/attention output, fp32 residual).  Every kernel is
 // latency-bound at R = 64: the point is fewer dependent launches per step.
+#include <type_traits>
+
 #include "common.hpp"
 #include "../../include/retr_hip.h"
 
@@ -27,26 +29,20 @@ RETR_DEVICE f4 mfma16(const u32x4& a, const u32x4& b, f4 acc) {
                                                  __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
 }
 
-// ---- LayerNorm of one row by one wave: the arithmetic of ln_fwd_kernel (norm.hip) ----------
-template <int PER>
-RETR_DEVICE void ln_row_wave(const float (&v)[PER], const float* gamma, const float* beta,
-                             float eps, int C, int lane, float (&o)[PER]) {
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) s += v[i];
-  const float mean = wave_sum(s) / C;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const float d = v[i] - mean;
-    q += d * d;
-  }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = lane + 64 * i;
-    o[i] = (v[i] - mean) * rstd * gamma[c] + beta[c];
-  }
+// Sum over aligned groups of G lanes (G = 4 or 8) by DPP: quad xor 1, quad xor 2 and, for 8,
+// the half-row mirror (lane i <- 7 - i within 8).  Every lane of a group ends with the sum.
+template <int CTRL>
+RETR_DEVICE float dpp_mov(float s) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s),
+                                                               CTRL, 0xF, 0xF, false));
+}
+template <int G>
+RETR_DEVICE float group_sum(float s) {
+  static_assert(G == 4 || G == 8, "group of 4 or 8 lanes");
+  s += dpp_mov<0xB1>(s);
+  s += dpp_mov<0x4E>(s);
+  if constexpr (G == 8) s += dpp_mov<0x141>(s);
+  return s;
 }
 
 // ---- dec_gemm ---------------------------------------------------------------------------------
@@ -83,6 +79,12 @@ dec_gemm_kernel(const bf16* a_plain, const bf16* a_pos, int R, const bf16* w, co
   for (int ks = 0; ks < C / 32; ++ks)
     af[ks] = ar < R ? *(const u32x4*)(A + (long)ar * C + 32 * ks + 8 * (lane >> 4))
                     : u32x4{0u, 0u, 0u, 0u};
+  float bn[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + 16 * j + (lane & 15);
+    bn[j] = (bias && n < N) ? bias[n] : 0.f;
+  }
   f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
   for (int ks = 0; ks < C / 32; ++ks) {
@@ -93,7 +95,7 @@ dec_gemm_kernel(const bf16* a_plain, const bf16* a_pos, int R, const bf16* w, co
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + 16 * j + (lane & 15);
     if (n >= N) continue;
-    const float b = bias ? bias[n] : 0.f;
+    const float b = bn[j];
     bf16* dst = segs.base[seg] + (n - seg * segw);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -123,9 +125,16 @@ dec_rows_blk_kernel(const float* xin, const float* slabs, int nslab, const float
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = blockIdx.x;
   const long RC = (long)R * C;
-  float v[CPT];
+  float v[CPT], bb[CPT], gm[CPT], bt[CPT], ps[CPT];   // per-column operands, loaded up front
 #pragma unroll
-  for (int i = 0; i < CPT; ++i) v[i] = xin[(long)r * C + tid + 256 * i];
+  for (int i = 0; i < CPT; ++i) {
+    const int c = tid + 256 * i;
+    v[i] = xin[(long)r * C + c];
+    bb[i] = slabs ? b2[c] : 0.f;
+    gm[i] = gamma[c];
+    bt[i] = beta[c];
+    ps[i] = npos ? pos[c] : 0.f;
+  }
   if (slabs) {
     float s[CPT];
 #pragma unroll
@@ -144,7 +153,7 @@ dec_rows_blk_kernel(const float* xin, const float* slabs, int nslab, const float
           if (j0 + u < nslab) s[i] += t[u][i];
     }
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) v[i] = v[i] + (s[i] + b2[tid + 256 * i]);
+    for (int i = 0; i < CPT; ++i) v[i] = v[i] + (s[i] + bb[i]);
   }
   if (xout) {
 #pragma unroll
@@ -170,11 +179,99 @@ dec_rows_blk_kernel(const float* xin, const float* slabs, int nslab, const float
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
     const int c = tid + 256 * i;
-    const float o = (v[i] - mean) * rstd * gamma[c] + beta[c];
+    const float o = (v[i] - mean) * rstd * gm[i] + bt[i];
     n[(long)r * C + c] = (bf16)o;
-    if (npos) npos[(long)r * C + c] = (bf16)(o + pos[c]);
+    if (npos) npos[(long)r * C + c] = (bf16)(o + ps[i]);
   }
 }
+
+// ---- dec_embed_rows: token embedding + its LayerNorm, then the first decoder LN1 -----------
+// Wave 0 computes LN_e(word[t] + qpos) with embed_ln_fwd_kernel's lane layout and reductions
+// (norm.hip), the block then runs dec_rows_blk_kernel's LN on the result (same rounding as the
+// two launches it replaces).
+template <int CPT>
+__global__ void __launch_bounds__(256)
+dec_embed_rows_kernel(const long long* tok, const float* word, const float* qpos, const float* ge,
+                      const float* be, float epse, float* xout, const float* g1, const float* b1,
+                      float eps1, bf16* n, bf16* npos) {
+  constexpr int C = CPT * 256, PER = C / 64;
+  __shared__ float xs[C];
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = blockIdx.x;
+  float gm[CPT], bt[CPT], ps[CPT];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = tid + 256 * i;
+    gm[i] = g1[c];
+    bt[i] = b1[c];
+    ps[i] = qpos[c];
+  }
+  if (wave == 0) {
+    const long t = tok[r];
+    float v[PER], s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = word[t * C + c] + qpos[c];
+      s += v[i];
+    }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const float d = v[i] - mean;
+      q += d * d;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + epse);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      const float o = (v[i] - mean) * rstd * ge[c] + be[c];
+      xs[c] = o;
+      xout[(long)r * C + c] = o;
+    }
+  }
+  __syncthreads();
+  float v[CPT];
+  float sm = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    v[i] = xs[tid + 256 * i];
+    sm += v[i];
+  }
+  sm = wave_sum(sm);
+  if (lane == 0) red[0][wave] = sm;
+  __syncthreads();
+  const float mean = (red[0][0] + red[0][1] + red[0][2] + red[0][3]) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  q = wave_sum(q);
+  if (lane == 0) red[1][wave] = q;
+  __syncthreads();
+  const float rstd = 1.0f / sqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / C + eps1);
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = tid + 256 * i;
+    const float o = (v[i] - mean) * rstd * gm[i] + bt[i];
+    n[(long)r * C + c] = (bf16)o;
+    npos[(long)r * C + c] = (bf16)(o + ps[i]);
+  }
+}
+
+// Phase timestamps of block 0 / wave 0 for tools/dec_phase.py (a separate -DRETR_DEC_TIMING
+// build of the library; compiled out of the product build).
+#ifdef RETR_DEC_TIMING
+__device__ long long g_dec_t[16];
+#define DEC_T(i) \
+  if (blockIdx.x == 0 && threadIdx.x == 0) g_dec_t[i] = wall_clock64();
+#else
+#define DEC_T(i)
+#endif
 
 // ---- dec_attn_row ----------------------------------------------------------------------------
 // One block per query row r.  Multi-head attention of q[r] over Lk keys (self: cache rows
@@ -267,6 +364,100 @@ struct GemvFrag {
   }
 };
 
+// The residual + LayerNorm tail of dec_attn_row (the ln_fwd_kernel arithmetic), with every
+// operand it reads from global memory (residual row, out-proj bias, LN parameters, position row)
+// loaded at kernel start by wave 0: they do not depend on the attention, and loading them after
+// it cost a dependent HBM round trip per launch.
+template <int PER>
+struct RowTail {
+  static constexpr int C = PER * 64;
+  // LDS-DMA (global_load_lds, 4 bytes per lane) of the tail operands into sm [5][C]: no
+  // registers held while the attention loads are in flight; read after a __syncthreads (which
+  // waits for vmcnt(0))
+  RETR_DEVICE static void load(const AttnRowArgs& a, int r, int lane, float* sm) {
+    auto g4 = [](const float* src, float* dst) {
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
+    };
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      g4(a.x + (long)r * C + c, sm + 64 * i);
+      g4(a.bo + c, sm + C + 64 * i);
+      g4(a.gamma + c, sm + 2 * C + 64 * i);
+      g4(a.beta + c, sm + 3 * C + 64 * i);
+      if (a.pos) g4(a.pos + c, sm + 4 * C + 64 * i);
+    }
+  }
+  // xo = x + (y + bo); t = bf16(LN(xo) (+pos)) -> ob (when a W_q2 follows) or q2
+  RETR_DEVICE static void run(const AttnRowArgs& a, int r, int lane, const float* sm,
+                              const float* yb, float* ob) {
+    float v[PER];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = sm[c] + (yb[c] + sm[C + c]);
+      a.xo[(long)r * C + c] = v[i];
+      s += v[i];
+    }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const float d = v[i] - mean;
+      q += d * d;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + a.eps);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      const float o = (v[i] - mean) * rstd * sm[2 * C + c] + sm[3 * C + c];
+      const float t = (float)(bf16)(a.pos ? o + sm[4 * C + c] : o);
+      if (a.wq) ob[c] = t;
+      else a.q2[(long)r * C + c] = (bf16)t;
+    }
+  }
+};
+
+// 1024-thread GEMV for C = 256, two passes of 128 outputs: thread t owns output
+// n = 128 p + t / 8 and the 16-byte chunks sub, sub + 8, sub + 16, sub + 24 of its row
+// (sub = t % 8): every load instruction reads 128 contiguous bytes per row; the 8 partial sums
+// meet through three DPP adds (quad xor 1, quad xor 2, half-row mirror).  (One output row per
+// half-wave needed five dependent cross-lane shuffles per row: 2-3 us per GEMV.)
+struct Gemv256 {
+  bf16x8 wv[2][4];
+  RETR_DEVICE void load(const bf16* W, int tid) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const bf16* src = W + (long)(128 * p + (tid >> 3)) * 256 + 8 * (tid & 7);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wv[p][c] = *(const bf16x8*)(src + 64 * c);
+    }
+  }
+  // out[n] = sum_k W[n][k] a[k]
+  RETR_DEVICE void dot(const float* a, float* out, int tid) const {
+    const float* av = a + 8 * (tid & 7);
+    float s[2] = {0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f4 a0 = *(const f4*)(av + 64 * c), a1 = *(const f4*)(av + 64 * c + 4);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[p] += (float)wv[p][c][e] * a0[e];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[p] += (float)wv[p][c][4 + e] * a1[e];
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const float v = group_sum<8>(s[p]);
+      if ((tid & 7) == 0) out[128 * p + (tid >> 3)] = v;
+    }
+  }
+};
+
 template <int PER, int HD, int MK>
 __global__ void __launch_bounds__(512)
 dec_attn_row_kernel(AttnRowArgs a, float scale) {
@@ -275,23 +466,32 @@ dec_attn_row_kernel(AttnRowArgs a, float scale) {
   __shared__ float qs[C];                        // scaled, rounded query
   __shared__ float ob[C];                        // attention output (bf16-rounded) / LN output
   __shared__ float yb[C];                        // GEMV result
+  __shared__ float tsm[5 * C];                   // RowTail operands
   __shared__ float pb[NW][64 * MK];              // probabilities of the wave's current head
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = blockIdx.x;
   constexpr bool kPre = C == 256;                // out-proj rows prefetched during attention
   GemvFrag<C, NT> wo;
   if constexpr (kPre) wo.load(a.wo, tid);
+  if (wave == 0) RowTail<PER>::load(a, r, lane, tsm);
+  float bq[(C + NT - 1) / NT];
+#pragma unroll
+  for (int u = 0; u < (C + NT - 1) / NT; ++u) {
+    const int c = tid + NT * u;
+    bq[u] = (a.wq && c < C) ? a.bq[c] : 0.f;
+  }
   for (int c = tid; c < C; c += NT) qs[c] = (float)(bf16)((float)a.q[(long)r * C + c] * scale);
   const int kvb = r / a.kv_group;
   const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
   const unsigned char* km = a.kpm ? a.kpm + (long)kvb * a.Lk : nullptr;
   const int Lk = a.Lk;
   long krow[MK];                                 // cache / memory row of key lane + 64 m
-  bool kok[MK];
+  bool kin[MK], kok[MK];                         // key exists / key exists and is not masked
 #pragma unroll
   for (int m = 0; m < MK; ++m) {
     const int j = lane + 64 * m;
-    kok[m] = j < Lk && !(km && km[j]);
+    kin[m] = j < Lk;
+    kok[m] = kin[m] && !(km && km[j]);
     krow[m] = j < Lk ? (ar ? (long)ar[j] : (long)kvb) * a.Lmax + j : 0;
   }
   __syncthreads();
@@ -305,7 +505,7 @@ dec_attn_row_kernel(AttnRowArgs a, float scale) {
     for (int m = 0; m < MK; ++m)
 #pragma unroll
       for (int d0 = 0; d0 < HD / 8; ++d0)
-        kv[m][d0] = kok[m] ? *(const bf16x8*)(a.k + krow[m] * C + h * HD + 8 * d0) : bf16x8{};
+        kv[m][d0] = kin[m] ? *(const bf16x8*)(a.k + krow[m] * C + h * HD + 8 * d0) : bf16x8{};
     // first 8 value rows of this lane's PV share, loaded before the scores are reduced
     constexpr int NG = HD / 8, NPART = 64 / NG;
     const int g = lane % NG, part = lane / NG;
@@ -379,29 +579,17 @@ dec_attn_row_kernel(AttnRowArgs a, float scale) {
   if (kPre && a.wq) wq.load(a.wq, tid);           // in flight across the residual + LN
   __syncthreads();
   // residual (fp32) and the next LayerNorm, one wave (the ln_fwd_kernel arithmetic)
-  if (wave == 0) {
-    float v[PER], o[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = lane + 64 * i;
-      v[i] = a.x[(long)r * C + c] + (yb[c] + a.bo[c]);
-      a.xo[(long)r * C + c] = v[i];
-    }
-    ln_row_wave<PER>(v, a.gamma, a.beta, a.eps, C, lane, o);
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = lane + 64 * i;
-      const float t = (float)(bf16)(a.pos ? o[i] + a.pos[c] : o[i]);
-      if (a.wq) ob[c] = t;
-      else a.q2[(long)r * C + c] = (bf16)t;
-    }
-  }
+  if (wave == 0) RowTail<PER>::run(a, r, lane, tsm, yb, ob);
   if (!a.wq) return;
   __syncthreads();
   if constexpr (kPre) wq.dot(ob, yb, tid);
   else gemv_rows<C, NT>(a.wq, ob, yb, tid);
   __syncthreads();
-  for (int c = tid; c < C; c += NT) a.q2[(long)r * C + c] = (bf16)(yb[c] + a.bq[c]);
+#pragma unroll
+  for (int u = 0; u < (C + NT - 1) / NT; ++u) {
+    const int c = tid + NT * u;
+    if (c < C) a.q2[(long)r * C + c] = (bf16)(yb[c] + bq[u]);
+  }
 }
 
 // Two waves per head (1024 threads, H = 8): each wave scores and accumulates one half of the
@@ -413,84 +601,110 @@ template <int PER, int HD, int MK>
 __global__ void __launch_bounds__(1024)
 dec_attn_row2_kernel(AttnRowArgs a, float scale) {
   constexpr int C = PER * 64, H = C / HD, NT = 1024;
-  constexpr int MKH = MK / 2;                    // key groups of 64 per half
   constexpr int NG = HD / 8, NPART = 64 / NG;
   constexpr int NU = 64 * MK / NPART;            // value rows per lane over all keys
   constexpr int NUH = NU / 2;                    // ... per half
   static_assert(H * 2 == NT / 64 && MK % 2 == 0, "two waves per head");
-  __shared__ float qs[C];
-  __shared__ float ob[C];
+  __shared__ __attribute__((aligned(16))) float qs[C];
+  __shared__ __attribute__((aligned(16))) float ob[C];
   __shared__ float yb[C];
-  __shared__ float pb[H][64 * MK];               // probabilities of each head (both halves)
+  __shared__ float tsm[5 * C];                   // RowTail operands
   __shared__ float hmx[H][2], hsum[H][2];
   __shared__ float hacc[H][HD];                  // half 1's unnormalised P V
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = wave >> 1, half = wave & 1;
   const int r = blockIdx.x;
+  DEC_T(0)
   constexpr bool kPre = C == 256;
-  GemvFrag<C, NT> wo;
-  if constexpr (kPre) wo.load(a.wo, tid);
-  for (int c = tid; c < C; c += NT) qs[c] = (float)(bf16)((float)a.q[(long)r * C + c] * scale);
+  // C = 256: both GEMV weight slices (out-proj, next query) in flight from the start
+  using Frag = std::conditional_t<kPre, Gemv256, GemvFrag<C, NT>>;
+  constexpr bool kPreQ = kPre && MK <= 2;         // (MK = 4 would spill; cross has no W_q2)
+  Frag wo, wq;
+  float bq[(C + NT - 1) / NT];
+#pragma unroll
+  for (int u = 0; u < (C + NT - 1) / NT; ++u) {
+    const int c = tid + NT * u;
+    bq[u] = (a.wq && c < C) ? a.bq[c] : 0.f;
+  }
+  bf16 qv[(C + NT - 1) / NT];
+#pragma unroll
+  for (int u = 0; u < (C + NT - 1) / NT; ++u) {
+    const int c = tid + NT * u;
+    qv[u] = c < C ? a.q[(long)r * C + c] : bf16(0.f);
+  }
+  // (the tail's LDS-DMA is issued here: placed after the key / value loads it trips an
+  // "incorrect register class" error in the gfx950 backend)
+  if (wave == 0) RowTail<PER>::load(a, r, lane, tsm);
   const int kvb = r / a.kv_group;
   const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
   const unsigned char* km = a.kpm ? a.kpm + (long)kvb * a.Lk : nullptr;
   const int Lk = a.Lk;
-  long krow[MKH];
-  bool kok[MKH];
-#pragma unroll
-  for (int m = 0; m < MKH; ++m) {
-    const int j = lane + 64 * (m + half * MKH);
-    kok[m] = j < Lk && !(km && km[j]);
-    krow[m] = j < Lk ? (ar ? (long)ar[j] : (long)kvb) * a.Lmax + j : 0;
-  }
-  bf16x8 kv[MKH][HD / 8];
-#pragma unroll
-  for (int m = 0; m < MKH; ++m)
-#pragma unroll
-    for (int d0 = 0; d0 < HD / 8; ++d0)
-      kv[m][d0] = kok[m] ? *(const bf16x8*)(a.k + krow[m] * C + h * HD + 8 * d0) : bf16x8{};
+  // lane = (dim group g of 8 dims, key part): keys j = part + NPART u (+ this half's offset);
+  // every load instruction reads NPART rows x HD contiguous bytes pieces (the per-CU load
+  // pipeline is the limit at one row per block), and the lane's scores are exactly the
+  // probabilities its P V share needs (no LDS round trip for P)
   const int g = lane % NG, part = lane / NG;
-  bf16x8 vv[NUH];                                // this half's value rows, keys in order
+  bool kok[NUH];
+  bf16x8 kk[NUH], vv[NUH];
+#pragma unroll
+  for (int u = 0; u < NUH; ++u) {
+    const int j = part + NPART * (u + half * NUH);
+    const long row = j < Lk ? (ar ? (long)ar[j] : (long)kvb) * a.Lmax + j : 0;
+    kk[u] = j < Lk ? *(const bf16x8*)(a.k + row * C + h * HD + 8 * g) : bf16x8{};
+    kok[u] = j < Lk && !(km && km[j]);
+  }
 #pragma unroll
   for (int u = 0; u < NUH; ++u) {
     const int j = part + NPART * (u + half * NUH);
     const long row = j < Lk ? (ar ? (long)ar[j] : (long)kvb) * a.Lmax + j : 0;
     vv[u] = j < Lk ? *(const bf16x8*)(a.v + row * C + h * HD + 8 * g) : bf16x8{};
   }
-  __syncthreads();
-  float sc[MKH];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int m = 0; m < MKH; ++m) {
-    float sv = -INFINITY;
-    if (kok[m]) {
-      sv = 0.f;
-#pragma unroll
-      for (int d0 = 0; d0 < HD / 8; ++d0)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sv += qs[h * HD + 8 * d0 + e] * (float)kv[m][d0][e];
-    }
-    sc[m] = sv;
-    mx = fmaxf(mx, sv);
+  // load order = need order (the CU's load bandwidth is the limit at one row per block): query,
+  // keys, values, then the GEMV weights, which stream in during the attention
+  constexpr bool kEarlyWo = MK <= 2;             // (MK = 4: after the scores, or it spills)
+  if constexpr (kPre && kEarlyWo) wo.load(a.wo, tid);
+  if constexpr (kPreQ) {
+    if (a.wq) wq.load(a.wq, tid);
   }
+  // the query goes to LDS only after every key / value load has been issued (the store waits
+  // for the query load)
+#pragma unroll
+  for (int u = 0; u < (C + NT - 1) / NT; ++u) {
+    const int c = tid + NT * u;
+    if (c < C) qs[c] = (float)(bf16)((float)qv[u] * scale);
+  }
+  DEC_T(1)
+  __syncthreads();
+  DEC_T(2)
+  float sc[NUH];
+  float mx = -INFINITY;
+  {
+    const f4 q0 = *(const f4*)(qs + h * HD + 8 * g), q1 = *(const f4*)(qs + h * HD + 8 * g + 4);
+#pragma unroll
+    for (int u = 0; u < NUH; ++u) {
+      float sv = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sv += q0[e] * (float)kk[u][e];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sv += q1[e] * (float)kk[u][4 + e];
+      sv = group_sum<NG>(sv);
+      sc[u] = kok[u] ? sv : -INFINITY;
+      mx = fmaxf(mx, sc[u]);
+    }
+  }
+  if constexpr (kPre && !kEarlyWo) wo.load(a.wo, tid);
   mx = wave_max(mx);
   float sum = 0.f;
-  float* p = pb[h];
-#pragma unroll
-  for (int m = 0; m < MKH; ++m) {
-    const float e = (mx == -INFINITY || sc[m] == -INFINITY) ? 0.f : __expf(sc[m] - mx);
-    p[lane + 64 * (m + half * MKH)] = e;
-    sum += e;
-  }
-  sum = wave_sum(sum);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < NUH; ++u) {
-    const int j = part + NPART * (u + half * NUH);
-    const float pj = j < Lk ? p[j] : 0.f;
+    const float e = (mx == -INFINITY || sc[u] == -INFINITY) ? 0.f : __expf(sc[u] - mx);
+    sum += e;                                    // NG copies of every key: divided out below
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] += pj * (float)vv[u][e];
+    for (int d = 0; d < 8; ++d) acc[d] += e * (float)vv[u][d];
   }
+  sum = wave_sum(sum) * (1.0f / NG);
+  DEC_T(3)
 #pragma unroll
   for (int e = 0; e < 8; ++e)
 #pragma unroll
@@ -503,6 +717,7 @@ dec_attn_row2_kernel(AttnRowArgs a, float scale) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) hacc[h][8 * g + e] = acc[e];
   }
+  DEC_T(4)
   __syncthreads();
   if (half == 0 && part == 0) {
     const float m0 = hmx[h][0], m1 = hmx[h][1];
@@ -515,34 +730,29 @@ dec_attn_row2_kernel(AttnRowArgs a, float scale) {
       ob[h * HD + 8 * g + e] = (float)(bf16)((acc[e] * e0 + hacc[h][8 * g + e] * e1) * inv);
   }
   __syncthreads();
+  DEC_T(5)
   if constexpr (kPre) wo.dot(ob, yb, tid);
   else gemv_rows<C, NT>(a.wo, ob, yb, tid);
-  GemvFrag<C, NT> wq;
-  if (kPre && a.wq) wq.load(a.wq, tid);
-  __syncthreads();
-  if (wave == 0) {
-    float v[PER], o[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = lane + 64 * i;
-      v[i] = a.x[(long)r * C + c] + (yb[c] + a.bo[c]);
-      a.xo[(long)r * C + c] = v[i];
-    }
-    ln_row_wave<PER>(v, a.gamma, a.beta, a.eps, C, lane, o);
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = lane + 64 * i;
-      const float t = (float)(bf16)(a.pos ? o[i] + a.pos[c] : o[i]);
-      if (a.wq) ob[c] = t;
-      else a.q2[(long)r * C + c] = (bf16)t;
-    }
+  if constexpr (kPre && !kPreQ) {
+    if (a.wq) wq.load(a.wq, tid);                // in flight across the residual + LN
   }
+  __syncthreads();
+  DEC_T(6)
+  if (wave == 0) RowTail<PER>::run(a, r, lane, tsm, yb, ob);
+  DEC_T(7)
   if (!a.wq) return;
   __syncthreads();
   if constexpr (kPre) wq.dot(ob, yb, tid);
   else gemv_rows<C, NT>(a.wq, ob, yb, tid);
+  DEC_T(8)
   __syncthreads();
-  for (int c = tid; c < C; c += NT) a.q2[(long)r * C + c] = (bf16)(yb[c] + a.bq[c]);
+  DEC_T(9)
+#pragma unroll
+  for (int u = 0; u < (C + NT - 1) / NT; ++u) {
+    const int c = tid + NT * u;
+    if (c < C) a.q2[(long)r * C + c] = (bf16)(yb[c] + bq[u]);
+  }
+  DEC_T(10)
 }
 
 // ---- dec_ffn: FFN1 + ReLU + FFN2 over hidden units [32 j, 32 j + 32) -> slab j -----------------
@@ -574,6 +784,7 @@ dec_ffn_kernel(const bf16* n3, int R, const bf16* w1, const float* b1, const bf1
   for (int ks = 0; ks < C / 32; ++ks)
     af[ks] = ar < R ? *(const u32x4*)(n3 + (long)ar * C + 32 * ks + 8 * (lane >> 4))
                     : u32x4{0u, 0u, 0u, 0u};
+  const float b1v[2] = {b1[j0 + (lane & 15)], b1[j0 + 16 + (lane & 15)]};
   f4 h[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
   for (int ks = 0; ks < C / 32; ++ks) {
@@ -583,7 +794,7 @@ dec_ffn_kernel(const bf16* n3, int R, const bf16* w1, const float* b1, const bf1
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int jj = 16 * t + (lane & 15);
-    const float b = b1[j0 + jj];
+    const float b = b1v[t];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       Hs[(16 * wave + 4 * (lane >> 4) + e) * HS + jj] = (bf16)fmaxf(h[t][e] + b, 0.f);
@@ -661,6 +872,21 @@ int retr_dec_rows(const float* xin, const float* slabs, int nslab, const float* 
   return retr_check_launch("dec_rows");
 }
 
+int retr_dec_embed_rows(const long long* tok, int R, int C, const float* word, const float* qpos,
+                        const float* ge, const float* be, float epse, float* x, const float* g1,
+                        const float* b1, float eps1, void* n, void* npos, void* stream) {
+  RETR_REQUIRE(C == 256 || C == 512, "dec_embed_rows: C=%d (256 | 512)", C);
+  if (R == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (C == 256)
+    hipLaunchKernelGGL(dec_embed_rows_kernel<1>, dim3(R), dim3(256), 0, st, tok, word, qpos, ge,
+                       be, epse, x, g1, b1, eps1, (bf16*)n, (bf16*)npos);
+  else
+    hipLaunchKernelGGL(dec_embed_rows_kernel<2>, dim3(R), dim3(256), 0, st, tok, word, qpos, ge,
+                       be, epse, x, g1, b1, eps1, (bf16*)n, (bf16*)npos);
+  return retr_check_launch("dec_embed_rows");
+}
+
 int retr_dec_attn_row(const void* q, const void* k, const void* v, int R, int C, int H, int Lk,
                       int Lmax, int kv_group, const int* anc, const unsigned char* kpm,
                       const float* x, const void* wo, const float* bo, float* xo,
@@ -703,5 +929,11 @@ int retr_dec_ffn(const void* n3, int R, int C, const void* w1, const float* b1, 
                        (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
   return retr_check_launch("dec_ffn");
 }
+
+#ifdef RETR_DEC_TIMING
+int retr_dec_timing_read(long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dec_t), sizeof(long long) * 16);
+}
+#endif
 
 }  // extern "C"

@@ -280,6 +280,70 @@ __global__ void greedy_update_kernel(const long long* pred, int B, int T, int i,
   if (threadIdx.x == 0 && prev_done < 0 && all_fin) *done = i;
 }
 
+// argmax_final_kernel + greedy_update_kernel in one block: thread t reduces segment t % 16 of
+// row (t / 16) (rows in groups of 64), the row winners go to pred and an LDS copy, then the
+// bookkeeping above runs on them.  One launch fewer per decode step.
+__global__ void __launch_bounds__(1024)
+greedy_select_kernel(const float* pv, const int* pi, int B, int T, int i, long long eos,
+                     long long* pred, long long* caption, unsigned char* finished, int* done,
+                     long long* tok) {
+  __shared__ int all_fin;
+  __shared__ long long sp[1024];
+  if (threadIdx.x == 0) all_fin = 1;
+  const int s = threadIdx.x % kArgSeg;
+  for (int r0 = 0; r0 < B; r0 += 1024 / kArgSeg) {
+    const int row = r0 + threadIdx.x / kArgSeg;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    if (row < B) bv = pv[row * kArgSeg + s], bi = pi[row * kArgSeg + s];
+    for (int o = kArgSeg / 2; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(bv, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (am_better(v2, i2, bv, bi)) bv = v2, bi = i2;
+    }
+    if (row < B && s == 0) {
+      pred[row] = bi;
+      if (row < 1024) sp[row] = bi;
+    }
+  }
+  __syncthreads();
+  const int prev_done = *done;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const long long pb = b < 1024 ? sp[b] : pred[b];
+    unsigned char f = finished[b] | (pb == eos ? 1 : 0);
+    finished[b] = f;
+    if (!f) atomicAnd(&all_fin, 0);
+  }
+  __syncthreads();
+  const bool stop = prev_done >= 0 || all_fin;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const long long pb = b < 1024 ? sp[b] : pred[b];
+    if (!stop) caption[(long)b * T + i + 1] = pb;
+    tok[b] = pb;
+  }
+  if (threadIdx.x == 0 && prev_done < 0 && all_fin) *done = i;
+}
+
+extern "C" int retr_greedy_select(int dtype, const void* logits, long ld, int B, int V,
+                                  void* workspace, int T, int i, long long eos, long long* pred,
+                                  long long* caption, unsigned char* finished, int* done,
+                                  long long* tok, void* stream) {
+  if (B == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype != RETR_BF16 || ld % 8 != 0 || V < 8 * kArgSeg * 256 / 4 || !workspace || B > 1024) {
+    if (int e = retr_argmax_rows(dtype, logits, ld, B, V, pred, stream)) return e;
+    return retr_greedy_update(pred, B, T, i, eos, caption, finished, done, tok, stream);
+  }
+  float* pv = (float*)workspace;
+  int* pi = (int*)(pv + (size_t)B * kArgSeg);
+  hipLaunchKernelGGL(argmax_part_kernel<bf16>, dim3(kArgSeg, B), dim3(256), 0, st,
+                     (const bf16*)logits, ld, V, pv, pi);
+  if (int e = retr_check_launch("argmax_part")) return e;
+  hipLaunchKernelGGL(greedy_select_kernel, dim3(1), dim3(1024), 0, st, pv, pi, B, T, i, eos, pred,
+                     caption, finished, done, tok);
+  return retr_check_launch("greedy_select");
+}
+
 extern "C" int retr_greedy_update(const long long* pred, int B, int T, int i, long long eos,
                                   long long* caption, unsigned char* finished, int* done,
                                   long long* tok, void* stream) {

@@ -204,12 +204,10 @@ class IncrementalGreedy:
         qp = emb.position_embeddings.weight.detach()[i]
         s = _st()
         x, xa = st.y, st.y2
-        call("retr_embed_ln_fwd", ptr(st.tok), R, 1, C, ptr(emb.word_embeddings.weight), ptr(qp),
-             ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias), float(emb.LayerNorm.eps), 0.0, 0,
-             ptr(x), ptr(st.mean), ptr(st.rstd), s)
         n0 = layers[0].tgt_self_attn.norm
-        call("retr_dec_rows", ptr(x), None, 0, None, R, C, None, ptr(n0.weight), ptr(n0.bias),
-             float(n0.eps), ptr(qp), ptr(st.n), ptr(st.npos), s)
+        call("retr_dec_embed_rows", ptr(st.tok), R, C, ptr(emb.word_embeddings.weight), ptr(qp),
+             ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias), float(emb.LayerNorm.eps), ptr(x),
+             ptr(n0.weight), ptr(n0.bias), float(n0.eps), ptr(st.n), ptr(st.npos), s)
         anc = ptr(st.anc) if self.beam else None
         nslab = F // 32
         for li, layer in enumerate(layers):
@@ -253,10 +251,9 @@ class IncrementalGreedy:
     def _select(self, st, i, V, eos_token, s):
         """Greedy: first-index argmax + the reference's finished/early-exit bookkeeping."""
         cd = self.cdtype
-        call("retr_argmax_rows_ws", dcode(cd), ptr(st.logits), st.Vp, st.B, V, ptr(st.pred),
-             ptr(st.am_ws), s)
-        call("retr_greedy_update", ptr(st.pred), st.B, st.T, i, int(eos_token), ptr(st.caption),
-             ptr(st.finished), ptr(st.done), ptr(st.tok), s)
+        call("retr_greedy_select", dcode(cd), ptr(st.logits), st.Vp, st.B, V, ptr(st.am_ws),
+             st.T, i, int(eos_token), ptr(st.pred), ptr(st.caption), ptr(st.finished),
+             ptr(st.done), ptr(st.tok), s)
 
     # -- state handling (overridden by IncrementalBeam) --------------------------------------
     def _new_state(self, B, S, T, C, F, L, V, cd, dev):

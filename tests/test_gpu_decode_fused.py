@@ -193,3 +193,64 @@ def test_fused_decode_matches_unfused_cfg5():
     # graphs vs eager launches of the fused step: bitwise
     ids_e = IncrementalGreedy(model, use_graphs=False, fused=True)(s, T, 101, 102)
     assert torch.equal(ids_f, ids_e)
+
+
+@pytest.mark.parametrize("C", [256, 512])
+def test_dec_embed_rows_matches_two_launches(C):
+    """dec_embed_rows == retr_embed_ln_fwd (one position) followed by retr_dec_rows (LN1 + pos):
+    bit-identical x, n and npos."""
+    R, V = 70, 1000
+    g = _g(C)
+    tok = torch.randint(0, V, (R,), generator=g).to(DEV)
+    word = torch.randn(V, C, generator=g).to(DEV)
+    qp = torch.randn(C, generator=g).to(DEV)
+    ge, be = (torch.rand(C, generator=g) + 0.5).to(DEV), torch.randn(C, generator=g).to(DEV)
+    g1, b1 = (torch.rand(C, generator=g) + 0.5).to(DEV), torch.randn(C, generator=g).to(DEV)
+    x0, x1 = torch.empty(R, C, device=DEV), torch.empty(R, C, device=DEV)
+    mean, rstd = torch.empty(R, device=DEV), torch.empty(R, device=DEV)
+    n0, p0 = (torch.empty(R, C, dtype=torch.bfloat16, device=DEV) for _ in range(2))
+    n1, p1 = (torch.empty(R, C, dtype=torch.bfloat16, device=DEV) for _ in range(2))
+    st = ops._st()
+    call("retr_embed_ln_fwd", ptr(tok), R, 1, C, ptr(word), ptr(qp), ptr(ge), ptr(be), 1e-12, 0.0,
+         0, ptr(x0), ptr(mean), ptr(rstd), st)
+    call("retr_dec_rows", ptr(x0), None, 0, None, R, C, None, ptr(g1), ptr(b1), 1e-5, ptr(qp),
+         ptr(n0), ptr(p0), st)
+    call("retr_dec_embed_rows", ptr(tok), R, C, ptr(word), ptr(qp), ptr(ge), ptr(be), 1e-12,
+         ptr(x1), ptr(g1), ptr(b1), 1e-5, ptr(n1), ptr(p1), st)
+    assert torch.equal(x0, x1) and torch.equal(n0, n1) and torch.equal(p0, p1)
+
+
+@pytest.mark.parametrize("B", [3, 64, 100])
+def test_greedy_select_matches_argmax_and_update(B):
+    """retr_greedy_select == retr_argmax_rows_ws + retr_greedy_update (pred, caption, finished,
+    done, tok), including ties (first index wins), rows that hit EOS and the all-finished step."""
+    from retr_amd import _lib
+    V, Vp, T, eos = 30522, 30528, 16, 102
+    g = _g(B)
+    logits = torch.randn(B, Vp, generator=g).to(DEV).bfloat16()
+    logits[0, 500] = logits[0, 900] = 50.0                     # tie -> 500
+    logits[1, eos] = 60.0                                       # finishes
+    ws = torch.empty(_lib.load().retr_argmax_workspace(B), dtype=torch.uint8, device=DEV)
+    st = ops._st()
+
+    def state():
+        cap = torch.zeros(B, T, dtype=torch.long, device=DEV)
+        fin = torch.zeros(B, dtype=torch.uint8, device=DEV)
+        fin[2 % B] = 1
+        done = torch.full((1,), -1, dtype=torch.int32, device=DEV)
+        return cap, fin, done, torch.zeros(B, dtype=torch.long, device=DEV), \
+            torch.empty(B, dtype=torch.long, device=DEV)
+
+    for step, all_eos in ((3, False), (4, True)):
+        if all_eos:
+            logits[:, eos] = 70.0
+        a, b = state(), state()
+        call("retr_argmax_rows_ws", 1, ptr(logits), Vp, B, V, ptr(a[4]), ptr(ws), st)
+        call("retr_greedy_update", ptr(a[4]), B, T, step, eos, ptr(a[0]), ptr(a[1]), ptr(a[2]),
+             ptr(a[3]), st)
+        call("retr_greedy_select", 1, ptr(logits), Vp, B, V, ptr(ws), T, step, eos, ptr(b[4]),
+             ptr(b[0]), ptr(b[1]), ptr(b[2]), ptr(b[3]), st)
+        for u, v in zip(a, b):
+            assert torch.equal(u, v)
+        assert int(b[4][0]) == (eos if all_eos else 500)
+        assert int(b[2][0]) == (step if all_eos else -1)
