@@ -91,7 +91,9 @@ enum {
                                    3 256x256, 4 128x64 S3, 5 reg-staged 64x64, 6 64x64 S2,
                                    7 128x128 S1 one epilogue band */
   RETR_TUNE_NT_STORE = 7,       /* 1: non-temporal GEMM output stores */
-  RETR_TUNE_COUNT = 8
+  RETR_TUNE_CONV_WGRAD_SPLITS = 8, /* conv weight-gradient split-K: 1 legacy ceil(512 / tiles),
+                                      >= 2 that many slices (capped by the K-steps) */
+  RETR_TUNE_COUNT = 9
 };
 int retr_tune(int knob, int value);
 

@@ -332,12 +332,30 @@ WgradPlan wgrad_plan(int R, int Ncols, int Mp) {
   const int bn = bm;
   const long tiles = (long)cdiv(R, bm) * cdiv(Ncols, bn);
   const int ksteps = cdiv(Mp, BK);
-  // about two blocks per CU (the 128x128 kernel runs 2 per CU), >= 8 K-steps per slice,
-  // <= 128 slabs (tools/gemm_tune: 8-32 slices within 10 % of the best on 16-36 tiles; the
-  // 1-2 tile GEMMs of 1x1 convs over 160x160 maps need more)
-  long s = (512 + tiles - 1) / tiles;
-  if (s > ksteps / 8) s = ksteps / 8;
-  if (s > 128) s = 128;
+  // <= 128 slabs, >= 8 K-steps per slice.  The 128x128 kernel runs two blocks per CU (512
+  // slots): pick the slice count by a cost model, rounds x K-steps per slice (a grid of 540
+  // blocks runs two rounds, so 14 slices of 29 K-steps beat 15 of 27) plus the slab traffic of
+  // the extra slices (tiles x 64 KB written + read per slice, ~0.016 K-step-times per tile).
+  const int tune = retr_tune_get(RETR_TUNE_CONV_WGRAD_SPLITS);
+  long smax = ksteps / 8;
+  if (smax > 128) smax = 128;
+  if (smax < 1) smax = 1;
+  long s;
+  if (tune >= 2) {
+    s = tune < smax ? tune : smax;
+  } else if (tune == 1 || p.tile != 128) {
+    s = (512 + tiles - 1) / tiles;
+    if (s > smax) s = smax;
+  } else {
+    s = 1;
+    double best = 1e30;
+    for (long c = 1; c <= smax; ++c) {
+      const long kc = cdiv(ksteps, (int)c);
+      const long rounds = (tiles * cdiv(ksteps, (int)kc) + 511) / 512;
+      const double cost = (double)rounds * (kc + 2) + 0.016 * (double)tiles * c;
+      if (cost < best) { best = cost; s = c; }
+    }
+  }
   if (s < 1) s = 1;
   // the launcher rounds the slice length up to whole K-steps: report the slices it will use
   const int kchunk = cdiv(ksteps, (int)s) * BK;

@@ -25,10 +25,12 @@ SHAPES = [("fwd", 16, 160, 160, 64, 256, 1, 1, 0, 1), ("fwd", 16, 160, 160, 64, 
           ("dgrad", 16, 80, 80, 512, 1024, 1, 2, 0, 1), ("dgrad", 16, 40, 40, 1024, 2048, 1, 2, 0, 1),
           ("wgrad", 16, 40, 40, 256, 256, 3, 1, 1, 0), ("wgrad", 16, 80, 80, 128, 128, 3, 1, 1, 0),
           ("wgrad", 16, 20, 20, 512, 512, 3, 1, 1, 0), ("wgrad", 16, 40, 40, 256, 1024, 1, 1, 0, 0),
+          ("wgrad", 16, 40, 40, 512, 512, 3, 2, 1, 0), ("wgrad", 16, 80, 80, 256, 256, 3, 2, 1, 0),
           ("wgrad", 16, 80, 80, 128, 512, 1, 1, 0, 0)]
 
 
 VARIANTS = [(0, 0), (0, 1), (1, 0), (1, 1), (5, 0), (6, 0), (6, 1)]
+WGRAD_PLANS = [0, 1, 7, 10, 12, 14, 16]
 
 
 def timeit(fn, n=20):
@@ -51,8 +53,11 @@ def timeit(fn, n=20):
 
 
 def main():
+    only = sys.argv[1] if len(sys.argv) > 1 else None
     bf = torch.bfloat16
     for kind, N, H, W, C, Co, k, s, p, extra in SHAPES:
+        if only and kind != only:
+            continue
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         x = torch.randn(N * H * W * C, device=DEV).to(bf)
         w = (torch.randn(Co * k * k * C, device=DEV) * 0.05).to(bf)
@@ -65,16 +70,19 @@ def main():
             nbytes = 2 * (x.numel() + y.numel() * (2 if extra else 1) + w.numel())
         elif kind == "wgrad":
             dy = torch.randn(N * OH * OW * Co, device=DEV).to(bf)
-            sp = load().retr_conv2d_wgrad_splits(BF, N, H, W, C, Co, k, k, s, p, 1)
-            ws = torch.empty(sp * Co * k * k * C, device=DEV)
             grad = torch.empty(Co * C * k * k, device=DEV)
 
-            def fn():
-                call("retr_conv2d_wgrad", BF, ptr(dy), ptr(x), N, H, W, C, ptr(ws), Co, k, k, s,
-                     p, 1, stream())
-                call("retr_conv_wgrad_unpack", ptr(ws), None, ptr(grad), Co, C, C, k, k, 0, sp,
-                     stream())
-            nbytes = 2 * (dy.numel() + x.numel()) + 8 * ws.numel()
+            def make_fn():
+                sp = load().retr_conv2d_wgrad_splits(BF, N, H, W, C, Co, k, k, s, p, 1)
+                ws = torch.empty(sp * Co * k * k * C, device=DEV)
+
+                def fn():
+                    call("retr_conv2d_wgrad", BF, ptr(dy), ptr(x), N, H, W, C, ptr(ws), Co, k, k,
+                         s, p, 1, stream())
+                    call("retr_conv_wgrad_unpack", ptr(ws), None, ptr(grad), Co, C, C, k, k, 0,
+                         sp, stream())
+                return fn, sp
+            nbytes = 2 * (dy.numel() + x.numel())
         else:
             dy = torch.randn(N * OH * OW * Co, device=DEV).to(bf)
             add = torch.randn(N * H * W * C, device=DEV).to(bf) if extra else None
@@ -84,7 +92,15 @@ def main():
             nbytes = 2 * (dy.numel() + dx.numel() * (2 if extra else 1) + w.numel())
         fl = 2.0 * N * OH * OW * Co * k * k * C
         out = []
-        for tile, nt in (VARIANTS if kind != "wgrad" else [(0, 0)]):
+        if kind == "wgrad":
+            # split-K plan: 0 cost model (default), 1 legacy ceil(512 / tiles), >= 2 forced
+            for plan in WGRAD_PLANS:
+                load().retr_tune(8, plan)
+                fn, sp = make_fn()
+                t = timeit(fn)
+                out.append(f"plan{plan}/s{sp}:{t:7.1f}us {fl / t / 1e6:4.0f}TF")
+            load().retr_tune(8, 0)
+        for tile, nt in (VARIANTS if kind != "wgrad" else []):
             load().retr_tune(6, tile)
             load().retr_tune(7, nt)
             try:
