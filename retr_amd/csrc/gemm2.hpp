@@ -443,7 +443,7 @@ int launch_gemm2(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, 
 // weight-gradient GEMMs (split over the pixel / token reduction).
 template <int FAM, class LA, class LB, class EP>
 int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits,
-               hipStream_t st, const char* what) {
+               hipStream_t st, const char* what, bool prefer64 = false) {
   const long t256 = (long)cdiv(M, 256) * cdiv(N, 256) * splits;
   const long t128 = (long)cdiv(M, 128) * cdiv(N, 128) * splits;
   const long t12864 = (long)cdiv(M, 128) * cdiv(N, 64) * splits;
@@ -457,6 +457,9 @@ int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, in
     case 7: return launch_gemm2<FAM, 128, 128, 2, 2, 1, 1>(la, lb, ep, M, N, K, splits, st, what);
     default: break;
   }
+  // caller's choice of the 64x64 two-stage tile (conv shapes where 4x the blocks win: the
+  // 20x20 maps of layer 4 and the 1x1 convolutions to / from 1024 channels at 40x40)
+  if (prefer64) return launch_gemm2<FAM, 64, 64, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
   // small K (<= 4 K-steps): single-stage 128x128, 4 blocks per CU (tools/conv_micro.py:
   // 1x1 convs with 256 input channels 46 -> 38 us); N = 64: the 64x64 two-stage tile (the stem
   // 325 -> 280 us, 3x3 64-channel convs 82 -> 64 us)

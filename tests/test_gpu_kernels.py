@@ -179,6 +179,13 @@ BIG_CONVS = [
     (8, 128, 81, 128, 3, 2, 1, 1),
     (8, 256, 30, 256, 3, 1, 2, 2),
     (16, 256, 41, 512, 1, 2, 0, 1),
+    # 64x64-tile rule (conv.hip prefer_tile64): layer-4 sized maps, stride-2 phases, 1x1 to / from
+    # 1024 channels
+    (16, 512, 20, 512, 3, 1, 1, 1),
+    (16, 512, 40, 512, 3, 2, 1, 1),
+    (8, 1024, 40, 256, 1, 1, 0, 1),
+    (8, 256, 40, 1024, 1, 1, 0, 1),
+    (16, 512, 20, 2048, 1, 1, 0, 1),
 ]
 
 

@@ -21,6 +21,10 @@ SHAPES = [("fwd", 16, 160, 160, 64, 256, 1, 1, 0, 1), ("fwd", 16, 160, 160, 64, 
           ("fwd", 16, 80, 80, 128, 512, 1, 1, 0, 1), ("fwd", 16, 40, 40, 256, 1024, 1, 1, 0, 1),
           ("fwd", 16, 160, 160, 256, 64, 1, 1, 0, 0), ("fwd", 16, 160, 160, 64, 64, 3, 1, 1, 0),
           ("fwd", 16, 640, 640, 8, 64, 7, 2, 3, 0),
+          ("fwd", 16, 20, 20, 512, 512, 3, 1, 1, 0), ("fwd", 16, 20, 20, 2048, 512, 1, 1, 0, 0),
+          ("fwd", 16, 20, 20, 512, 2048, 1, 1, 0, 1), ("fwd", 16, 40, 40, 512, 512, 3, 2, 1, 0),
+          ("dgrad", 16, 20, 20, 512, 512, 3, 1, 1, 0), ("dgrad", 16, 20, 20, 512, 2048, 1, 1, 0, 1),
+          ("dgrad", 16, 20, 20, 2048, 512, 1, 1, 0, 1),
           ("dgrad", 16, 40, 40, 1024, 256, 1, 1, 0, 1), ("dgrad", 16, 80, 80, 512, 128, 1, 1, 0, 1),
           ("dgrad", 16, 80, 80, 512, 1024, 1, 2, 0, 1), ("dgrad", 16, 40, 40, 1024, 2048, 1, 2, 0, 1),
           ("wgrad", 16, 40, 40, 256, 256, 3, 1, 1, 0), ("wgrad", 16, 80, 80, 128, 128, 3, 1, 1, 0),
@@ -29,8 +33,32 @@ SHAPES = [("fwd", 16, 160, 160, 64, 256, 1, 1, 0, 1), ("fwd", 16, 160, 160, 64, 
           ("wgrad", 16, 80, 80, 128, 512, 1, 1, 0, 0)]
 
 
-VARIANTS = [(0, 0), (0, 1), (1, 0), (1, 1), (5, 0), (6, 0), (6, 1)]
+VARIANTS = [(0, 0), (1, 0), (2, 0), (4, 0), (5, 0), (6, 0)]
 WGRAD_PLANS = [0, 1, 7, 10, 12, 14, 16]
+
+
+def r50_shapes(N=16, res=640):
+    """Every distinct forward / data-gradient convolution of the cfg2 ResNet-50 step (layer1
+    frozen: forward only), with residual / addend where the model fuses one."""
+    out = set()
+    H = res // 4
+    cin = 64
+    for li, (planes, blocks, stride) in enumerate(((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))):
+        train = li > 0
+        for b in range(blocks):
+            s = stride if b == 0 else 1
+            Ho = H // s
+            convs = [(cin, planes, 1, 1, 0, H, 0), (planes, planes, 3, s, 1, H, 0),
+                     (planes, planes * 4, 1, 1, 0, Ho, 1)]
+            if b == 0:
+                convs.append((cin, planes * 4, 1, s, 0, H, 0))
+            for C, Co, k, st, pd, Hin, res_ in convs:
+                out.add(("fwd", N, Hin, Hin, C, Co, k, st, pd, res_))
+                if train:
+                    out.add(("dgrad", N, Hin, Hin, C, Co, k, st, pd, 1))
+            cin = planes * 4
+            H = Ho
+    return sorted(out, key=lambda t: (t[0], -t[2], t[4], t[5]))
 
 
 def timeit(fn, n=20):
@@ -54,9 +82,17 @@ def timeit(fn, n=20):
 
 def main():
     only = sys.argv[1] if len(sys.argv) > 1 else None
+    small = len(sys.argv) > 2  # only the 20x20 / 40x40 (layer4) shapes
     bf = torch.bfloat16
-    for kind, N, H, W, C, Co, k, s, p, extra in SHAPES:
-        if only and kind != only:
+    global VARIANTS
+    shapes = SHAPES
+    if only == "r50":
+        shapes = r50_shapes()
+        VARIANTS = [(0, 0), (4, 0), (6, 0)]
+    for kind, N, H, W, C, Co, k, s, p, extra in shapes:
+        if only and only not in ("all", "r50") and kind != only:
+            continue
+        if small and H > 40:
             continue
         OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         x = torch.randn(N * H * W * C, device=DEV).to(bf)
