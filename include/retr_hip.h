@@ -156,6 +156,11 @@ int retr_conv_pack_group(int dtype, int n, const retr_conv_pack_desc* d, void* s
 int retr_conv2d_fwd(int dtype, const void* x, int Nb, int H, int W, int C, const void* w,
                     const float* bias, const void* residual, void* y, int Co, int KH, int KW,
                     int stride, int pad, int dil, int relu, void* stream);
+/* retr_conv2d_fwd over an explicit output extent OH x OW (<= the conv's own; used by the
+ * space-to-depth stem, a 4x4 pad-2 conv whose 321st row / column torchvision never computes) */
+int retr_conv2d_fwd_out(int dtype, const void* x, int Nb, int H, int W, int C, const void* w,
+                        const float* bias, const void* residual, void* y, int Co, int KH, int KW,
+                        int stride, int pad, int dil, int OH, int OW, int relu, void* stream);
 int retr_conv2d_dgrad(int dtype, const void* dy, int Nb, int H, int W, int C, const void* wt,
                       void* dx, int Co, int KH, int KW, int stride, int pad, int dil,
                       const void* addend, const void* gate, void* stream);
@@ -172,6 +177,14 @@ int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int
 /* NCHW fp32 image -> NHWC (channels zero-padded to Cp) */
 int retr_nchw_to_nhwc(int dtype, const float* x, void* y, int N, int C, int H, int W, int Cp,
                       void* stream);
+/* bf16 space-to-depth stem input (models/backbone.py:85-95 -> torchvision conv1, 7x7 stride 2
+ * pad 3): y[n][Y][X][(dy*2+dx)*3+c] = x[n][c][2Y+dy][2X+dx], 12 channels + 4 zero (C == 3,
+ * H and W even) */
+int retr_nchw_to_s2d16(const float* x, void* y, int N, int C, int H, int W, void* stream);
+/* the stem's packed [Co][7][7][Cp] bf16 weights re-laid for that input: [Co][4][4][16],
+ * w2[co][i][j][(dy*2+dx)*3+c] = wp[co][2i+dy-1][2j+dx-1][c] (zero off the 7x7 taps); the conv
+ * is then retr_conv2d_fwd_out(k 4, stride 1, pad 2, OH = H/2, OW = W/2) */
+int retr_stem_s2d_weights(const void* wp, void* w2, int Co, int Cp, void* stream);
 /* MaxPool2d(3, 2, 1) on NHWC (torchvision stem) */
 int retr_maxpool3x3s2(int dtype, const void* x, void* y, int N, int H, int W, int C, int OH,
                       int OW, void* stream);

@@ -85,6 +85,10 @@ _SIGS = {
     "retr_conv_wgrad_unpack": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "retr_conv2d_wgrad_splits": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
     "retr_nchw_to_nhwc": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
+    "retr_nchw_to_s2d16": [_P, _P, _I, _I, _I, _I, _P],
+    "retr_stem_s2d_weights": [_P, _P, _I, _I, _P],
+    "retr_conv2d_fwd_out": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I,
+                            _I, _I, _P],
     "retr_maxpool3x3s2": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
     "retr_mask_nearest": [_P, _P, _I, _I, _I, _I, _I, _P],
     "retr_layernorm_fwd": [_I, _P, _L, _P, _P, _F, _I, _I, _P, _L, _P, _P, _I, _P, _P, _P],

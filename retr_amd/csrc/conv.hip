@@ -728,6 +728,20 @@ int retr_conv2d_fwd(int dtype, const void* x, int Nb, int H, int W, int C, const
   return conv_fwd_t<float>(x, g, w, bias, residual, y, relu, (hipStream_t)stream);
 }
 
+int retr_conv2d_fwd_out(int dtype, const void* x, int Nb, int H, int W, int C, const void* w,
+                        const float* bias, const void* residual, void* y, int Co, int KH, int KW,
+                        int stride, int pad, int dil, int OH, int OW, int relu, void* stream) {
+  Geom g = make_geom(Nb, H, W, C, Co, KH, KW, stride, pad, dil);
+  int epc = dtype == RETR_BF16 ? 8 : 4;
+  RETR_REQUIRE(C % epc == 0, "conv2d_fwd_out: C=%d must be a multiple of %d", C, epc);
+  RETR_REQUIRE(OH > 0 && OW > 0 && OH <= g.OH && OW <= g.OW,
+               "conv2d_fwd_out: output %dx%d outside the conv's %dx%d", OH, OW, g.OH, g.OW);
+  g.OH = OH;
+  g.OW = OW;
+  if (dtype == RETR_BF16) return conv_fwd_t<bf16>(x, g, w, bias, residual, y, relu, (hipStream_t)stream);
+  return conv_fwd_t<float>(x, g, w, bias, residual, y, relu, (hipStream_t)stream);
+}
+
 int retr_conv2d_dgrad(int dtype, const void* dy, int Nb, int H, int W, int C, const void* wt,
                       void* dx, int Co, int KH, int KW, int stride, int pad, int dil,
                       const void* addend, const void* gate, void* stream) {

@@ -35,6 +35,51 @@ __global__ void nchw_to_nhwc8_kernel(const float* x, bf16* y, int N, int C, int 
   }
 }
 
+// bf16 space-to-depth stem input: y[n][Y][X][(dy * 2 + dx) * 3 + c] = x[n][c][2Y + dy][2X + dx]
+// (12 channels, 4 zero pad channels -> one 32-byte pixel).  The 7x7 stride-2 stem becomes a 4x4
+// stride-1 conv over 16 channels (K = 256 instead of 7 * 7 * 8 = 392) on half the input bytes.
+__global__ void nchw_to_s2d16_kernel(const float* x, bf16* y, int N, int H, int W) {
+  constexpr int C = 3;
+  const int H2 = H / 2, W2 = W / 2;
+  const long HW = (long)H * W, P2 = (long)H2 * W2, total = (long)N * P2;
+  for (long pix = blockIdx.x * (long)blockDim.x + threadIdx.x; pix < total;
+       pix += (long)gridDim.x * blockDim.x) {
+    const long n = pix / P2, rem = pix - n * P2;
+    const int Y = (int)(rem / W2), X = (int)(rem - (long)Y * W2);
+    bf16x8 o[2];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[1][e] = (bf16)0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int dy = 0; dy < 2; ++dy) {
+        const float2 v = *(const float2*)(x + (n * C + c) * HW + (long)(2 * Y + dy) * W + 2 * X);
+        const int q0 = (dy * 2) * C + c, q1 = (dy * 2 + 1) * C + c;
+        o[q0 >> 3][q0 & 7] = (bf16)v.x;
+        o[q1 >> 3][q1 & 7] = (bf16)v.y;
+      }
+    bf16x8* dst = (bf16x8*)(y + pix * 16);
+    dst[0] = o[0];
+    dst[1] = o[1];
+  }
+}
+
+// the stem's packed 7x7 weights [Co][7][7][Cp] re-laid for the space-to-depth input:
+// w2[co][i][j][(dy * 2 + dx) * 3 + c] = wp[co][2i + dy - 1][2j + dx - 1][c] (0 off the taps)
+__global__ void stem_s2d_weights_kernel(const bf16* wp, bf16* w2, int Co, int Cp) {
+  const int total = Co * 4 * 4 * 16;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int ch = i & 15, j = (i >> 4) & 3, ii = (i >> 6) & 3, co = i >> 8;
+    float v = 0.f;
+    if (ch < 12) {
+      const int q = ch / 3, c = ch - 3 * q;
+      const int kh = 2 * ii + (q >> 1) - 1, kw = 2 * j + (q & 1) - 1;
+      if (kh >= 0 && kw >= 0 && kh < 7 && kw < 7) v = (float)wp[((co * 7 + kh) * 7 + kw) * Cp + c];
+    }
+    w2[i] = (bf16)v;
+  }
+}
+
 // bf16 MaxPool2d(3, 2, 1) NHWC, C % 8 == 0: one thread per (output pixel, 8 channels), 16-byte
 // loads of the 3x3 window and one 16-byte store
 __global__ void maxpool8_kernel(const bf16* x, bf16* y, int N, int H, int W, int C, int OH,
@@ -197,6 +242,23 @@ int retr_nchw_to_nhwc(int dtype, const float* x, void* y, int N, int C, int H, i
   else
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x, (float*)y, N, C, H, W, Cp);
   return retr_check_launch("nchw_to_nhwc");
+}
+
+int retr_nchw_to_s2d16(const float* x, void* y, int N, int C, int H, int W, void* stream) {
+  RETR_REQUIRE(C == 3 && H % 2 == 0 && W % 2 == 0, "nchw_to_s2d16: C=%d H=%d W=%d", C, H, W);
+  const long pixels = (long)N * (H / 2) * (W / 2);
+  if (pixels == 0) return 0;
+  hipLaunchKernelGGL(nchw_to_s2d16_kernel, dim3(grid_for(pixels)), dim3(256), 0,
+                     (hipStream_t)stream, x, (bf16*)y, N, H, W);
+  return retr_check_launch("nchw_to_s2d16");
+}
+
+int retr_stem_s2d_weights(const void* wp, void* w2, int Co, int Cp, void* stream) {
+  RETR_REQUIRE(Cp >= 3 && Co > 0, "stem_s2d_weights: Co=%d Cp=%d", Co, Cp);
+  const int total = Co * 256;
+  hipLaunchKernelGGL(stem_s2d_weights_kernel, dim3((total + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, (const bf16*)wp, (bf16*)w2, Co, Cp);
+  return retr_check_launch("stem_s2d_weights");
 }
 
 int retr_maxpool3x3s2(int dtype, const void* x, void* y, int N, int H, int W, int C, int OH,

@@ -14,6 +14,8 @@ Backward (only blocks whose parameters require grad — the reference freezes st
   dW1 = wgrad(G1, x)  * s1 ;  dWds = wgrad(G3, x) * sds
   G3_prev = (dgrad(G1, W1eff) + [G3 | dgrad(G3, Wdseff)]) * (x > 0)
 """
+import os
+
 import torch
 
 from . import _lib
@@ -184,6 +186,28 @@ def _conv_wgrad(spec, g, x, in_shape):
     return grad
 
 
+def _stem_s2d(runner, img):
+    """bf16 stem as a space-to-depth conv: the 3-channel image becomes [N, H/2, W/2, 16]
+    (2x2 pixel blocks, 12 channels + 4 zero), the 7x7 stride-2 pad-3 kernel a 4x4 stride-1 pad-2
+    one (retr_stem_s2d_weights) -- the same bf16 operands and products as torchvision's conv1
+    (models/backbone.py:85-95), K = 256 instead of 392 and half the input bytes."""
+    stem = runner.stem
+    N, C, H, W = img.shape
+    wp, _, bias, _ = PACKS.get(stem, runner.cdtype)
+    if runner._s2d_w is None or runner._s2d_w[0] is not wp:
+        w2 = torch.empty(stem.cout, 4, 4, 16, dtype=runner.cdtype, device=img.device)
+        call("retr_stem_s2d_weights", ptr(wp), ptr(w2), stem.cout, stem.cp, _st())
+        runner._s2d_w = (wp, w2)
+    w2 = runner._s2d_w[1]
+    h2, w2_ = H // 2, W // 2
+    x = torch.empty(N, h2, w2_, 16, dtype=runner.cdtype, device=img.device)
+    call("retr_nchw_to_s2d16", ptr(img), ptr(x), N, C, H, W, _st())
+    y = torch.empty(N, h2, w2_, stem.cout, dtype=runner.cdtype, device=img.device)
+    call("retr_conv2d_fwd_out", dcode(runner.cdtype), ptr(x), N, h2, w2_, 16, ptr(w2), ptr(bias),
+         None, ptr(y), stem.cout, 4, 4, 1, 2, 1, h2, w2_, 1, _st())
+    return y, (N, h2, w2_, stem.cout)
+
+
 class _Backbone(torch.autograd.Function):
     @staticmethod
     def forward(ctx, images, runner, *weights):
@@ -191,10 +215,13 @@ class _Backbone(torch.autograd.Function):
         _lib.require_device(images)
         PACKS.prepare(runner.specs, cdtype)      # every stale conv packed in one launch
         N, C, H, W = images.shape
-        x = torch.empty(N, H, W, stem.cp, dtype=cdtype, device=images.device)
         img = images.detach().float().contiguous()
-        call("retr_nchw_to_nhwc", dcode(cdtype), ptr(img), ptr(x), N, C, H, W, stem.cp, _st())
-        s, sh = _conv_fwd(stem, x, (N, H, W, stem.cp), relu=True)
+        if runner.s2d_stem(C, H, W):
+            s, sh = _stem_s2d(runner, img)
+        else:
+            x = torch.empty(N, H, W, stem.cp, dtype=cdtype, device=images.device)
+            call("retr_nchw_to_nhwc", dcode(cdtype), ptr(img), ptr(x), N, C, H, W, stem.cp, _st())
+            s, sh = _conv_fwd(stem, x, (N, H, W, stem.cp), relu=True)
         ph, pw = (sh[1] + 2 - 3) // 2 + 1, (sh[2] + 2 - 3) // 2 + 1
         x = torch.empty(N, ph, pw, sh[3], dtype=cdtype, device=images.device)
         call("retr_maxpool3x3s2", dcode(cdtype), ptr(s), ptr(x), N, sh[1], sh[2], sh[3], ph, pw,
@@ -294,6 +321,16 @@ class BackboneRunner:
         self.weights = ws
         self.specs = [self.stem] + [c for b in self.blocks
                                     for c in b.convs + ([b.ds] if b.ds is not None else [])]
+        self._s2d_w = None
+        self.use_s2d = os.environ.get("RETR_S2D_STEM", "1") != "0"
+
+    def s2d_stem(self, c, h, w):
+        """bf16 torchvision stem (7x7, stride 2, pad 3, RGB) on even-sized images: run it as the
+        space-to-depth conv (_stem_s2d)."""
+        st = self.stem
+        return (self.use_s2d and self.cdtype == torch.bfloat16 and st.k == 7 and st.s == 2
+                and st.p == 3 and st.d == 1 and st.cin == 3 and c == 3 and h % 2 == 0
+                and w % 2 == 0)
 
     def run(self, images):
         # activations are only kept when autograd will call backward

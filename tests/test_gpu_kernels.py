@@ -694,3 +694,38 @@ def test_conv_pack_group_matches_single():
     for o, r in zip(outs, refs):
         for a, b in zip(o, r):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 64, 64), (3, 38, 50), (16, 224, 224)])
+def test_stem_space_to_depth(N, H, W):
+    """bf16 stem as a 4x4 stride-1 conv over the space-to-depth image (retr_nchw_to_s2d16 +
+    retr_stem_s2d_weights + retr_conv2d_fwd_out) == the 7x7 stride-2 conv over NHWC8: same bf16
+    operands and products (only the fp32 summation order differs), and both against fp32 torch."""
+    bf = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(N * H + W)
+    img = torch.randn(N, 3, H, W, generator=g)
+    w = torch.randn(64, 3, 7, 7, generator=g) / math.sqrt(147)
+    wp, _, bias, _, cp, _ = _pack(w.to(DEV), bf)
+    imd = img.to(DEV)
+    OH, OW = H // 2, W // 2
+    x8 = torch.empty(N, H, W, 8, dtype=bf, device=DEV)
+    call("retr_nchw_to_nhwc", ops.dcode(bf), ptr(imd), ptr(x8), N, 3, H, W, 8, ops._st())
+    y_ref = torch.empty(N, OH, OW, 64, dtype=bf, device=DEV)
+    call("retr_conv2d_fwd", ops.dcode(bf), ptr(x8), N, H, W, 8, ptr(wp), ptr(bias), None,
+         ptr(y_ref), 64, 7, 7, 2, 3, 1, 1, ops._st())
+    xs = torch.full((N, OH, OW, 16), float("nan"), dtype=bf, device=DEV)
+    call("retr_nchw_to_s2d16", ptr(imd), ptr(xs), N, 3, H, W, ops._st())
+    assert torch.equal(xs[..., 12:].float(), torch.zeros(N, OH, OW, 4, device=DEV))
+    ref_s2d = imd.to(bf).view(N, 3, OH, 2, OW, 2).permute(0, 2, 4, 3, 5, 1).reshape(N, OH, OW, 12)
+    assert torch.equal(xs[..., :12], ref_s2d)
+    w2 = torch.empty(64, 4, 4, 16, dtype=bf, device=DEV)
+    call("retr_stem_s2d_weights", ptr(wp), ptr(w2), 64, cp, ops._st())
+    y = torch.empty(N, OH, OW, 64, dtype=bf, device=DEV)
+    call("retr_conv2d_fwd_out", ops.dcode(bf), ptr(xs), N, OH, OW, 16, ptr(w2), ptr(bias), None,
+         ptr(y), 64, 4, 4, 1, 2, 1, OH, OW, 1, ops._st())
+    torch.cuda.synchronize()
+    assert rel_err(y.float(), y_ref.float()) < 2e-3
+    weff = wp.float()[..., :3].permute(0, 3, 1, 2).cpu()
+    ref = torch.relu(F.conv2d(img.to(bf).float(), weff, stride=2, padding=3)
+                     + bias.cpu().view(1, -1, 1, 1))
+    assert rel_err(y.permute(0, 3, 1, 2).float().cpu(), ref) < 1e-2

@@ -80,11 +80,44 @@ def timeit(fn, n=20):
     return best
 
 
+def stem(N=16, H=640):
+    """Legacy stem (NHWC8 + 7x7 stride-2) vs the space-to-depth stem (s2d16 + 4x4 stride-1),
+    conversion + conv per variant of the big-GEMM tile."""
+    bf = torch.bfloat16
+    img = torch.randn(N, 3, H, H, device=DEV)
+    w = (torch.randn(64 * 7 * 7 * 8, device=DEV) * 0.05).to(bf)
+    w2 = (torch.randn(64 * 4 * 4 * 16, device=DEV) * 0.05).to(bf)
+    b = torch.randn(64, device=DEV)
+    x8 = torch.empty(N * H * H * 8, dtype=bf, device=DEV)
+    xs = torch.empty(N * H * H * 4, dtype=bf, device=DEV)
+    OH = H // 2
+    y = torch.empty(N * OH * OH * 64, dtype=bf, device=DEV)
+    fl = 2.0 * N * OH * OH * 64 * 147
+    cases = {
+        "nhwc8": lambda: call("retr_nchw_to_nhwc", BF, ptr(img), ptr(x8), N, 3, H, H, 8, stream()),
+        "s2d16": lambda: call("retr_nchw_to_s2d16", ptr(img), ptr(xs), N, 3, H, H, stream()),
+    }
+    for name, fn in cases.items():
+        print(f"stem  {name:6s} conversion {timeit(fn):7.1f}us", flush=True)
+    for tile in (0, 1, 2, 4, 6):
+        load().retr_tune(6, tile)
+        t7 = timeit(lambda: call("retr_conv2d_fwd", BF, ptr(x8), N, H, H, 8, ptr(w), ptr(b), None,
+                                 ptr(y), 64, 7, 7, 2, 3, 1, 1, stream()))
+        t4 = timeit(lambda: call("retr_conv2d_fwd_out", BF, ptr(xs), N, OH, OH, 16, ptr(w2),
+                                 ptr(b), None, ptr(y), 64, 4, 4, 1, 2, 1, OH, OH, 1, stream()))
+        print(f"stem  t{tile}: 7x7s2 {t7:7.1f}us {fl / t7 / 1e6:4.0f}TF | s2d 4x4 {t4:7.1f}us "
+              f"{fl / t4 / 1e6:4.0f}TF", flush=True)
+    load().retr_tune(6, 0)
+
+
 def main():
     only = sys.argv[1] if len(sys.argv) > 1 else None
     small = len(sys.argv) > 2  # only the 20x20 / 40x40 (layer4) shapes
     bf = torch.bfloat16
     global VARIANTS
+    if only == "stem":
+        stem()
+        return
     shapes = SHAPES
     if only == "r50":
         shapes = r50_shapes()
