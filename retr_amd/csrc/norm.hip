@@ -43,6 +43,155 @@ ln_fwd_kernel(const float* x, long ldx, const float* gamma, const float* beta, f
   }
 }
 
+// ---- C % 256 == 0: lanes own 4 consecutive columns per 256-column chunk (16-byte fp32 /
+// 8-byte bf16 accesses, one load instruction per operand and chunk) ---------------------------
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+RETR_DEVICE f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+RETR_DEVICE f32x4 ld4(const bf16* p) {
+  const bf16x4 v = *(const bf16x4*)p;
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+RETR_DEVICE void st4(float* p, f32x4 v) { *(f32x4*)p = v; }
+RETR_DEVICE void st4(bf16* p, f32x4 v) {
+  *(bf16x4*)p = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+}
+
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256)
+ln_fwd4_kernel(const float* x, long ldx, const float* gamma, const float* beta, float eps, int M,
+               T* y, long ldy, T* y2, const float* pos, int period, float* mean_out,
+               float* rstd_out) {
+  constexpr int C = 256 * NCH;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (long)row * ldx + 4 * lane;
+  f32x4 v[NCH];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    v[j] = ld4(xr + 256 * j);
+    s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+  }
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[j][e] - mean;
+      q += d * d;
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+  const float* pr = pos ? pos + (long)(row % period) * C + 4 * lane : nullptr;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = 4 * lane + 256 * j;
+    const f32x4 g = ld4(gamma + c), b = ld4(beta + c);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mean) * rstd * g[e] + b[e];
+    if (y) st4(y + (long)row * ldy + c, o);
+    if (y2) st4(y2 + (long)row * ldy + c, o + ld4(pr + 256 * j));
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+// NW waves per block, 2 rows per wave in flight; per-column dgamma / dbeta partials summed over
+// the block's waves in wave order (deterministic) -> part[block][2][C]
+template <typename T, int NCH, int NW>
+__global__ void __launch_bounds__(NW * 64)
+ln_bwd4_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, const float* gamma,
+               const float* mean, const float* rstd, int M, float* dx, long lddx,
+               const float* addend, float* part, int rows_per_block) {
+  constexpr int C = 256 * NCH;
+  __shared__ f32x4 red[2][NW][64 * NCH];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  f32x4 pg[NCH], pb[NCH], gm[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    pg[j] = pb[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    gm[j] = ld4(gamma + 4 * lane + 256 * j);
+  }
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  constexpr int RB = 2;
+  for (int rb = r0 + wave; rb < r1; rb += NW * RB) {
+    f32x4 d[RB][NCH], xv[RB][NCH], ad[RB][NCH];
+    float mu[RB], rs[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int row = rb + NW * u;
+      const bool ok = row < r1;
+      mu[u] = ok ? mean[row] : 0.f;
+      rs[u] = ok ? rstd[row] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        const int c = 4 * lane + 256 * j;
+        f32x4 t = (ok && dy) ? ld4(dy + (long)row * lddy + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if (ok && dy2) t += ld4(dy2 + (long)row * lddy + c);
+        d[u][j] = t;
+        xv[u][j] = ok ? ld4(x + (long)row * ldx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        ad[u][j] = (ok && addend) ? ld4(addend + (long)row * ldx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    float s1[RB], s2[RB];
+    f32x4 g[RB][NCH], xh[RB][NCH];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      s1[u] = 0.f;
+      s2[u] = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        xh[u][j] = (xv[u][j] - mu[u]) * rs[u];
+        pg[j] += d[u][j] * xh[u][j];
+        pb[j] += d[u][j];
+        g[u][j] = d[u][j] * gm[j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s1[u] += g[u][j][e];
+          s2[u] += g[u][j][e] * xh[u][j][e];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      s1[u] = wave_sum(s1[u]) / C;
+      s2[u] = wave_sum(s2[u]) / C;
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int row = rb + NW * u;
+      if (row >= r1) continue;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        f32x4 o = rs[u] * (g[u][j] - s1[u] - xh[u][j] * s2[u]);
+        if (addend) o += ad[u][j];
+        st4(dx + (long)row * lddx + 4 * lane + 256 * j, o);
+      }
+    }
+  }
+  if (!part) return;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    red[0][wave][lane + 64 * j] = pg[j];
+    red[1][wave][lane + 64 * j] = pb[j];
+  }
+  __syncthreads();
+  float* pw = part + (long)blockIdx.x * 2 * C;
+  for (int q = threadIdx.x; q < 2 * 64 * NCH; q += NW * 64) {
+    const int which = q / (64 * NCH), cq = q - which * 64 * NCH;
+    f32x4 t = red[which][0][cq];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) t += red[which][w][cq];
+    // chunk cq = lane + 64 j holds columns 4 lane + 256 j .. + 3
+    const int ln = cq % 64, j = cq / 64;
+    st4(pw + which * C + 4 * ln + 256 * j, t);
+  }
+}
+
 // rows_per_block rows handled by 4 waves; per-column dgamma/dbeta partials reduced in LDS.
 constexpr int kLnBwdRows = 8;
 template <typename T, int PER>
@@ -359,6 +508,26 @@ int retr_layernorm_fwd(int dtype, const float* x, long ldx, const float* gamma,
   RETR_REQUIRE(C % 64 == 0, "layernorm: C=%d must be a multiple of 64", C);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(cdiv(M, 4));
+  const bool v4 = C % 256 == 0 && C <= 1024 && ldx % 4 == 0 && ldy % 4 == 0 &&
+                  ((uintptr_t)x & 15) == 0 && (!y || ((uintptr_t)y & 7) == 0) &&
+                  (!y2 || ((uintptr_t)y2 & 7) == 0) && (!pos || ((uintptr_t)pos & 15) == 0) &&
+                  ((uintptr_t)gamma & 15) == 0 && ((uintptr_t)beta & 15) == 0;
+  if (v4) {
+#define LNF4(NC)                                                                                 \
+    if (dtype == RETR_BF16)                                                                       \
+      hipLaunchKernelGGL((ln_fwd4_kernel<bf16, NC>), grid, dim3(256), 0, st, x, ldx, gamma, beta, \
+                         eps, M, (bf16*)y, ldy, (bf16*)y2, pos, period, mean, rstd);              \
+    else                                                                                          \
+      hipLaunchKernelGGL((ln_fwd4_kernel<float, NC>), grid, dim3(256), 0, st, x, ldx, gamma, beta,\
+                         eps, M, (float*)y, ldy, (float*)y2, pos, period, mean, rstd);
+    switch (C / 256) {
+      case 1: LNF4(1); break;
+      case 2: LNF4(2); break;
+      default: LNF4(4); break;
+    }
+#undef LNF4
+    return retr_check_launch("layernorm_fwd4");
+  }
 #define LNF(P)                                                                                   \
   if (dtype == RETR_BF16)                                                                         \
     hipLaunchKernelGGL((ln_fwd_kernel<bf16, P>), grid, dim3(256), 0, st, x, ldx, gamma, beta, eps, \
@@ -381,9 +550,41 @@ int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, co
   RETR_REQUIRE(mean && rstd && gamma && dx, "layernorm_bwd: missing saved statistics");
   RETR_REQUIRE(!(dgamma || dbeta) || workspace, "layernorm_bwd: dgamma/dbeta need a workspace");
   hipStream_t st = (hipStream_t)stream;
+  float* part = (dgamma || dbeta) ? workspace : nullptr;
+  const bool v4 = C % 256 == 0 && C <= 512 && lddy % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0 &&
+                  (((uintptr_t)x | (uintptr_t)dx | (uintptr_t)gamma |
+                    (uintptr_t)(addend ? addend : x)) & 15) == 0 &&
+                  (((uintptr_t)(dy ? dy : dy2) | (uintptr_t)(dy2 ? dy2 : dy)) &
+                   (dtype == RETR_BF16 ? 7 : 15)) == 0;
+  if (v4) {
+    // >= 4096 rows: 16 waves x 2 rows per block (1/4 the partial rows of 8-row blocks for the
+    // parameter reduction); fewer rows: 4 waves x 2 rows (enough blocks to spread over the CUs)
+    const bool big = M >= 4096;
+    const int rpb = big ? 32 : 8;
+    dim3 grid(cdiv(M, rpb));
+#define LNB4(NC, NW)                                                                               \
+    if (dtype == RETR_BF16)                                                                        \
+      hipLaunchKernelGGL((ln_bwd4_kernel<bf16, NC, NW>), grid, dim3(NW * 64), 0, st,               \
+                         (const bf16*)dy, (const bf16*)dy2, lddy, x, ldx, gamma, mean, rstd, M,    \
+                         dx, lddx, addend, part, rpb);                                             \
+    else                                                                                           \
+      hipLaunchKernelGGL((ln_bwd4_kernel<float, NC, NW>), grid, dim3(NW * 64), 0, st,              \
+                         (const float*)dy, (const float*)dy2, lddy, x, ldx, gamma, mean, rstd, M,  \
+                         dx, lddx, addend, part, rpb);
+    if (C == 256) {
+      if (big) { LNB4(1, 16) } else { LNB4(1, 4) }
+    } else {
+      if (big) { LNB4(2, 16) } else { LNB4(2, 4) }
+    }
+#undef LNB4
+    if (int e = retr_check_launch("layernorm_bwd4")) return e;
+    if (!part) return 0;
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(2 * C, 64)), dim3(1024), 0, st, part,
+                       (int)grid.x, C, dgamma, dbeta);
+    return retr_check_launch("layernorm_param_reduce");
+  }
   const int rpb = kLnBwdRows;  // 2 rows per wave: ~12 waves per CU at M = 6400
   dim3 grid(cdiv(M, rpb));
-  float* part = (dgamma || dbeta) ? workspace : nullptr;
 #define LNB(P)                                                                                     \
   if (dtype == RETR_BF16)                                                                          \
     hipLaunchKernelGGL((ln_bwd_kernel<bf16, P>), grid, dim3(256), 0, st, (const bf16*)dy,          \

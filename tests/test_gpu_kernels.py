@@ -244,7 +244,7 @@ def _check_conv(dtype, tol, cfg):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
-@pytest.mark.parametrize("M,C", [(37, 64), (512, 256), (130, 512)])
+@pytest.mark.parametrize("M,C", [(37, 64), (512, 256), (130, 512), (6400, 256), (4100, 512)])
 def test_layernorm(dtype, tol, M, C):
     g = torch.Generator(device="cpu").manual_seed(M * C)
     x = (torch.randn(M, C, generator=g) * 3 + 1).to(DEV)

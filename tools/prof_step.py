@@ -20,7 +20,7 @@ def main():
          "d.workgroup_size_x from rocpd_kernel_dispatch d join rocpd_info_kernel_symbol s "
          "on d.kernel_id = s.id order by d.start")
     rows = list(c.execute(q))
-    marks = [i for i, r in enumerate(rows) if "nchw_to_nhwc" in r[0]]
+    marks = [i for i, r in enumerate(rows) if "nchw_to_nhwc" in r[0] or "nchw_to_s2d" in r[0]]
     w = rows[marks[step]:marks[step + 1]]
     span = (w[-1][2] - w[0][1]) / 1e6
     busy = sum(r[2] - r[1] for r in w) / 1e6
