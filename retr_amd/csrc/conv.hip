@@ -570,6 +570,56 @@ __global__ void wgrad_unpack4_kernel(const float* ws, const float* scale, float*
   }
 }
 
+// Same sum with the slices spread over NW waves: the 64 lanes of a wave take 64 consecutive
+// 4-channel chunks (coalesced 1 KB per load), wave w adds slices w, w + NW, ... (up to 8 loads in
+// flight), and wave 0 adds the NW partial sums in wave order -- a fixed order, so still
+// deterministic.  (One thread per chunk walking all slices left the 3x3 / 56-slice and 1x1 /
+// 124-slice unpacks at ~150 blocks, latency-bound at ~10 us.)
+template <int NW>
+__global__ void __launch_bounds__(NW * 64)
+wgrad_unpack4w_kernel(const float* ws, const float* scale, float* grad, int Co, int Ci, int Cp,
+                      int KHW, int accumulate, int splits) {
+  __shared__ f32x4 red[NW][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c4 = Ci / 4;
+  const long total = (long)Co * KHW * c4;
+  const long slab = (long)Co * KHW * Cp;
+  const long i = (long)blockIdx.x * 64 + lane;
+  int ci = 0, tap = 0, co = 0;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (i < total) {
+    ci = (int)(i % c4) * 4;
+    const long t = i / c4;
+    tap = (int)(t % KHW);
+    co = (int)(t / KHW);
+    const float* src = ws + ((long)co * KHW + tap) * Cp + ci;
+    int s = w;
+    for (; s + 7 * NW < splits; s += 8 * NW) {
+      f32x4 u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = *(const f32x4*)(src + (long)(s + k * NW) * slab);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v += u[k];
+    }
+    for (; s < splits; s += NW) v += *(const f32x4*)(src + (long)s * slab);
+  }
+  if constexpr (NW > 1) {
+    red[w][lane] = v;
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int k = 1; k < NW; ++k) v += red[k][lane];
+  }
+  if (i >= total) return;
+  const float sc = scale ? scale[co] : 1.f;
+  float* dst = grad + ((long)co * Ci + ci) * KHW + tap;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float x = v[e] * sc;
+    dst[(long)e * KHW] = accumulate ? dst[(long)e * KHW] + x : x;
+  }
+}
+
 __global__ void wgrad_unpack_kernel(const float* ws, const float* scale, float* grad, int Co,
                                     int Ci, int Cp, int KH, int KW, int accumulate, int splits) {
   const long total = (long)Co * Ci * KH * KW;
@@ -856,6 +906,17 @@ int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int
   RETR_REQUIRE(splits >= 1, "conv_wgrad_unpack: splits=%d", splits);
   if (Ci % 4 == 0 && Cp % 4 == 0 && ((uintptr_t)ws & 15) == 0) {
     const long total = (long)Co * KH * KW * (Ci / 4);
+    if (splits >= 8) {
+      const dim3 grid((unsigned)cdiv(total, 64));
+      hipStream_t st = (hipStream_t)stream;
+#define UNPW(NW) hipLaunchKernelGGL(wgrad_unpack4w_kernel<NW>, grid, dim3(NW * 64), 0, st, ws, \
+                                    scale, grad, Co, Ci, Cp, KH * KW, accumulate, splits)
+      if (splits >= 64) UNPW(16);
+      else if (splits >= 24) UNPW(8);
+      else UNPW(4);
+#undef UNPW
+      return retr_check_launch("conv_wgrad_unpack4w");
+    }
     const int grid = (int)(total / 256 + 1 < 8192 ? total / 256 + 1 : 8192);
     hipLaunchKernelGGL(wgrad_unpack4_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws,
                        scale, grad, Co, Ci, Cp, KH * KW, accumulate, splits);

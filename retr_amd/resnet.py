@@ -25,7 +25,7 @@ from .ops import dcode, _st
 
 
 class ConvSpec:
-    __slots__ = ("conv", "bn", "k", "s", "p", "d", "cin", "cout", "cp")
+    __slots__ = ("conv", "bn", "k", "s", "p", "d", "cin", "cout", "cp", "pack")
 
     def __init__(self, conv, bn, stride=1, padding=0, dilation=1):
         self.conv, self.bn = conv, bn
@@ -33,6 +33,7 @@ class ConvSpec:
         self.s, self.p, self.d = stride, padding, dilation
         self.cout, self.cin = conv.weight.shape[0], conv.weight.shape[1]
         self.cp = max(8, (self.cin + 7) // 8 * 8)
+        self.pack = None            # (version key, packed tensors): _PackCache
 
     def out_hw(self, h, w):
         oh = (h + 2 * self.p - self.d * (self.k - 1) - 1) // self.s + 1
@@ -82,10 +83,10 @@ def build_plan(body):
 
 
 class _PackCache:
-    """Folded compute-dtype weights per conv, refreshed when the weight or a BN buffer changes."""
-
-    def __init__(self):
-        self._d = {}
+    """Folded compute-dtype weights per conv, refreshed when the weight or a BN buffer changes.
+    The entry lives on the ConvSpec itself (it dies with its model): a dict keyed by id(spec)
+    could hand a new model, whose spec reuses a dead one's id and whose tensors reuse its
+    addresses, the dead model's packed weights."""
 
     def get(self, spec, dtype):
         w = spec.conv.weight
@@ -93,7 +94,7 @@ class _PackCache:
         ver = (w._version, w.data_ptr(), dtype) + tuple(
             (b._version, b.data_ptr()) for b in (bn.weight, bn.bias, bn.running_mean,
                                                  bn.running_var))
-        ent = self._d.get(id(spec))
+        ent = spec.pack
         if ent is not None and ent[0] == ver:
             return ent[1]
         co, ci, k = spec.cout, spec.cin, spec.k
@@ -106,7 +107,7 @@ class _PackCache:
              ptr(bn.running_mean), ptr(bn.running_var), None, co, ci, k, k, spec.cp, ptr(wp),
              ptr(wt), ptr(bias), ptr(scale), _st())
         out = (wp, wt, bias, scale)
-        self._d[id(spec)] = (ver, out)
+        spec.pack = (ver, out)
         return out
 
 
@@ -118,7 +119,7 @@ class _PackCache:
             ver = (w._version, w.data_ptr(), dtype) + tuple(
                 (b._version, b.data_ptr()) for b in (bn.weight, bn.bias, bn.running_mean,
                                                      bn.running_var))
-            ent = self._d.get(id(spec))
+            ent = spec.pack
             if ent is None or ent[0] != ver:
                 todo.append((spec, ver))
         if not todo:
@@ -140,7 +141,7 @@ class _PackCache:
             d.bn_rm, d.bn_rv, d.conv_bias = ptr(bn.running_mean), ptr(bn.running_var), None
             d.w_out, d.wt_out, d.bias_out, d.scale_out = ptr(wp), ptr(wt), ptr(bias), ptr(scale)
             d.Co, d.Ci, d.KH, d.KW, d.Cp = co, ci, k, k, spec.cp
-            self._d[id(spec)] = (ver, (wp, wt, bias, scale))
+            spec.pack = (ver, (wp, wt, bias, scale))
         call("retr_conv_pack_group", dcode(dtype), len(todo), arr, _st())
 
 

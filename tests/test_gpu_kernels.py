@@ -729,3 +729,25 @@ def test_stem_space_to_depth(N, H, W):
     ref = torch.relu(F.conv2d(img.to(bf).float(), weff, stride=2, padding=3)
                      + bias.cpu().view(1, -1, 1, 1))
     assert rel_err(y.permute(0, 3, 1, 2).float().cpu(), ref) < 1e-2
+
+
+def test_conv_pack_cache_lives_on_the_spec():
+    """Packed conv weights are cached on each ConvSpec (they die with the model): a dict keyed by
+    id(spec) served a later model -- whose specs reused dead ids and whose tensors reused the
+    same addresses -- the dead model's packed weights (intermittent test_gpu_optim failure)."""
+    from tests.helpers import make_config
+    from retr_amd.models.caption import build_model
+    from retr_amd.models.utils import NestedTensor
+    from retr_amd.synthetic import synthetic_images
+    assert not hasattr(resnet.PACKS, "_d")
+    model, _ = build_model(make_config())
+    model.to(DEV).eval()
+    img, mask = synthetic_images(1, 64, seed=3)
+    with torch.no_grad():
+        model(NestedTensor(img.to(DEV), mask.to(DEV)),
+              torch.zeros(1, 16, dtype=torch.long, device=DEV),
+              torch.zeros(1, 16, dtype=torch.bool, device=DEV))
+    specs = [s for m in model.modules() if isinstance(getattr(m, "_runner", None),
+                                                       resnet.BackboneRunner)
+             for s in m._runner.specs]
+    assert specs and all(s.pack is not None for s in specs)
