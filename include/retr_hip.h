@@ -89,11 +89,13 @@ enum {
   RETR_TUNE_ATTN_MODE = 5,      /* bf16 attention: 1 streaming K/V tiles, 2 LDS-resident */
   RETR_TUNE_BIG_TILE = 6,       /* large bf16 GEMMs (convs): 1 128x128 S1, 2 128x128 S2,
                                    3 256x256, 4 128x64 S3, 5 reg-staged 64x64, 6 64x64 S2,
-                                   7 128x128 S1 one epilogue band */
+                                   7 128x128 S1 one epilogue band, 8 64x64 S4, 9 64x128 S3 */
   RETR_TUNE_NT_STORE = 7,       /* 1: non-temporal GEMM output stores */
   RETR_TUNE_CONV_WGRAD_SPLITS = 8, /* conv weight-gradient split-K: 1 legacy ceil(512 / tiles),
                                       >= 2 that many slices (capped by the K-steps) */
-  RETR_TUNE_COUNT = 9
+  RETR_TUNE_CONV_WGRAD_TILE = 9, /* conv weight-gradient tile (bf16): 1 always 64x64 LDS-DMA,
+                                    2 never (0: the built-in shape rule) */
+  RETR_TUNE_COUNT = 10
 };
 int retr_tune(int knob, int value);
 

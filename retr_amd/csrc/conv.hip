@@ -330,16 +330,24 @@ int launch_auto(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, i
 // and made split-K the cost of these GEMMs); retr_conv_wgrad_unpack adds the slabs in order
 // while it re-lays the gradient out to OIHW, so the result is deterministic.
 struct WgradPlan {
-  int tile;     // 128: gemm2 128x128 (LDS-DMA), 129: reg-staged 128x128, 64: 64x64
+  int tile;     // 128: gemm2 128x128 (LDS-DMA), 65: gemm2 64x64, 129: reg-staged 128x128,
+                // 64: reg-staged 64x64
   int splits;
 };
 
 template <typename T>
-WgradPlan wgrad_plan(int R, int Ncols, int Mp) {
+WgradPlan wgrad_plan(int R, int Ncols, int Mp, bool dense1x1) {
   constexpr int BK = Elem<T>::BK;
   WgradPlan p{64, 1};
   if (R >= 128 && Ncols >= 128) p.tile = sizeof(T) == 2 ? 128 : 129;
-  const int bm = p.tile == 64 ? 64 : 128;
+  // 64x64 LDS-DMA tile for the 1x1 stride-1 weight gradients with a <= 128-wide side or
+  // <= 8192 pixels (tools/conv_micro.py wtile, profiles/r2_conv_wgrad_tiles.txt: 3-14 % faster;
+  // 3x3, strided and 256 x 512 ones are faster on 128x128); knob 1 forces it, 2 forbids it
+  const int tt = retr_tune_get(RETR_TUNE_CONV_WGRAD_TILE);
+  if (sizeof(T) == 2 && R >= 64 && Ncols >= 64 &&
+      (tt == 1 || (tt == 0 && dense1x1 && (R <= 128 || Ncols <= 128 || Mp <= 8192))))
+    p.tile = 65;
+  const int bm = (p.tile == 64 || p.tile == 65) ? 64 : 128;
   const int bn = bm;
   const long tiles = (long)cdiv(R, bm) * cdiv(Ncols, bn);
   const int ksteps = cdiv(Mp, BK);
@@ -354,16 +362,19 @@ WgradPlan wgrad_plan(int R, int Ncols, int Mp) {
   long s;
   if (tune >= 2) {
     s = tune < smax ? tune : smax;
-  } else if (tune == 1 || p.tile != 128) {
+  } else if (tune == 1 || (p.tile != 128 && p.tile != 65)) {
     s = (512 + tiles - 1) / tiles;
     if (s > smax) s = smax;
   } else {
+    // (the 64x64 tile: ~4 blocks per CU, a quarter of the slab bytes per tile)
+    const long slots = p.tile == 65 ? 1024 : 512;
+    const double slab_cost = p.tile == 65 ? 0.004 : 0.016;
     s = 1;
     double best = 1e30;
     for (long c = 1; c <= smax; ++c) {
       const long kc = cdiv(ksteps, (int)c);
-      const long rounds = (tiles * cdiv(ksteps, (int)kc) + 511) / 512;
-      const double cost = (double)rounds * (kc + 2) + 0.016 * (double)tiles * c;
+      const long rounds = (tiles * cdiv(ksteps, (int)kc) + slots - 1) / slots;
+      const double cost = (double)rounds * (kc + 2) + slab_cost * (double)tiles * c;
       if (cost < best) { best = cost; s = c; }
     }
   }
@@ -376,14 +387,15 @@ WgradPlan wgrad_plan(int R, int Ncols, int Mp) {
 
 template <int FAM, typename T, class LA, class LB>
 int launch_wgrad(const LA& la, const LB& lb, float* ws, long ldws, int R, int Ncols, int Mp,
-                 hipStream_t st, const char* what) {
-  const WgradPlan p = wgrad_plan<T>(R, Ncols, Mp);
+                 hipStream_t st, const char* what, bool dense1x1) {
+  const WgradPlan p = wgrad_plan<T>(R, Ncols, Mp, dense1x1);
   const int s = p.splits;
   EpiAccF32 ep{ws, ldws, 0, 0, 1, nullptr};
   ep.split_stride = s > 1 ? (long)R * ldws : 0;
   ep.set_vec();
   if constexpr (sizeof(T) == 2) {
     if (p.tile == 128) return launch_gemm2<FAM, 128, 128, 2, 2, 2>(la, lb, ep, R, Ncols, Mp, s, st, what);
+    if (p.tile == 65) return launch_gemm2<FAM, 64, 64, 2, 2, 2>(la, lb, ep, R, Ncols, Mp, s, st, what);
   } else {
     if (p.tile == 129) return launch_gemm<FAM, T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, what);
   }
@@ -499,10 +511,11 @@ int conv_wgrad_t(const void* dy, const void* x, Geom g, float* ws, hipStream_t s
   DenseT<T> la{(const T*)dy, (long)g.Co, R, Mp};
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseT<T> lb{(const T*)x, (long)g.C, Ncols, Mp};
-    return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st, "conv_wgrad_1x1");
+    return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st, "conv_wgrad_1x1",
+                                          true);
   }
   ConvWgradB<T> lb{(const T*)x, g, Ncols, Mp, Elem<T>::BK / g.OW, Elem<T>::BK % g.OW};
-  return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st, "conv_wgrad");
+  return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st, "conv_wgrad", false);
 }
 
 // ---- weight packing: fp32 OIHW (+ FrozenBN buffers) -> folded [Co][KH][KW][Cp] and the
@@ -897,8 +910,9 @@ int retr_conv2d_wgrad_splits(int dtype, int Nb, int H, int W, int C, int Co, int
                              int stride, int pad, int dil) {
   Geom g = make_geom(Nb, H, W, C, Co, KH, KW, stride, pad, dil);
   const int Mp = g.Nb * g.OH * g.OW, Ncols = g.KH * g.KW * g.C;
-  return dtype == RETR_BF16 ? wgrad_plan<bf16>(g.Co, Ncols, Mp).splits
-                            : wgrad_plan<float>(g.Co, Ncols, Mp).splits;
+  const bool d1 = g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0;
+  return dtype == RETR_BF16 ? wgrad_plan<bf16>(g.Co, Ncols, Mp, d1).splits
+                            : wgrad_plan<float>(g.Co, Ncols, Mp, d1).splits;
 }
 
 int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,

@@ -455,8 +455,18 @@ int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, in
     case 5: return launch_gemm<FAM, bf16, 64, 64>(la, lb, ep, M, N, K, splits, st, what);
     case 6: return launch_gemm2<FAM, 64, 64, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
     case 7: return launch_gemm2<FAM, 128, 128, 2, 2, 1, 1>(la, lb, ep, M, N, K, splits, st, what);
+    case 8: return launch_gemm2<FAM, 64, 64, 2, 2, 4>(la, lb, ep, M, N, K, splits, st, what);
+    case 9: return launch_gemm2<FAM, 64, 128, 2, 2, 3>(la, lb, ep, M, N, K, splits, st, what);
     default: break;
   }
+  // skinny GEMMs over a wide N (the decode step's vocabulary projection, M = 64 caption rows /
+  // 320 beam rows, N = 30528): weight streaming is the cost -- 64x64 with a 4-deep ring at
+  // M <= 64 (12.4 -> 8.7 us), single-stage 128x128 up to 512 rows (30.3 -> 26.1 us;
+  // tools/head_micro.py, profiles/r2_head_tiles.txt)
+  if (M <= 64 && N >= 4096)
+    return launch_gemm2<FAM, 64, 64, 2, 2, 4>(la, lb, ep, M, N, K, splits, st, what);
+  if (M <= 512 && N >= 4096 && K >= 256)
+    return launch_gemm2<FAM, 128, 128, 2, 2, 1, 2>(la, lb, ep, M, N, K, splits, st, what);
   // caller's choice of the 64x64 two-stage tile (conv shapes where 4x the blocks win: the
   // 20x20 maps of layer 4 and the 1x1 convolutions to / from 1024 channels at 40x40)
   if (prefer64) return launch_gemm2<FAM, 64, 64, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);

@@ -122,8 +122,11 @@ def main():
     if only == "r50":
         shapes = r50_shapes()
         VARIANTS = [(0, 0), (4, 0), (6, 0)]
+    if only == "wtile":   # every cfg2 weight-gradient conv, 128x128 vs 64x64 tile
+        shapes = sorted({("wgrad",) + t[1:9] + (0,) for t in r50_shapes() if t[0] == "dgrad"},
+                        key=lambda t: (-t[2], t[4], t[5]))
     for kind, N, H, W, C, Co, k, s, p, extra in shapes:
-        if only and only not in ("all", "r50") and kind != only:
+        if only and only not in ("all", "r50", "wtile") and kind != only:
             continue
         if small and H > 40:
             continue
@@ -163,12 +166,16 @@ def main():
         out = []
         if kind == "wgrad":
             # split-K plan: 0 cost model (default), 1 legacy ceil(512 / tiles), >= 2 forced
-            for plan in WGRAD_PLANS:
-                load().retr_tune(8, plan)
-                fn, sp = make_fn()
-                t = timeit(fn)
-                out.append(f"plan{plan}/s{sp}:{t:7.1f}us {fl / t / 1e6:4.0f}TF")
+            for tile in (2, 1):
+                for plan in (WGRAD_PLANS if only != "wtile" else [0]):
+                    load().retr_tune(8, plan)
+                    load().retr_tune(9, tile)
+                    fn, sp = make_fn()
+                    t = timeit(fn)
+                    out.append(f"{'t64' if tile == 1 else 't128'}/plan{plan}/s{sp}:{t:7.1f}us "
+                               f"{fl / t / 1e6:4.0f}TF")
             load().retr_tune(8, 0)
+            load().retr_tune(9, 0)
         for tile, nt in (VARIANTS if kind != "wgrad" else []):
             load().retr_tune(6, tile)
             load().retr_tune(7, nt)
