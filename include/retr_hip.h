@@ -187,6 +187,31 @@ int retr_nchw_to_s2d16(const float* x, void* y, int N, int C, int H, int W, void
  * w2[co][i][j][(dy*2+dx)*3+c] = wp[co][2i+dy-1][2j+dx-1][c] (zero off the 7x7 taps); the conv
  * is then retr_conv2d_fwd_out(k 4, stride 1, pad 2, OH = H/2, OW = W/2) */
 int retr_stem_s2d_weights(const void* wp, void* w2, int Co, int Cp, void* stream);
+/* RefCOCO encoder-input pipeline (data_utils/refcoco.py:131-178, data_utils/utils.py:161-252):
+ * one descriptor per item; coefficient / window tables computed on the host as Pillow /
+ * torchvision do (retr_amd/data_pipeline.py). */
+typedef struct {
+  long long src_off;            /* byte offset of the item's HxWx3 uint8 image in src */
+  long long tmp_off;            /* byte offset of its horizontal-pass buffer [D][S][3] in tmp */
+  int H, W;                     /* source image size */
+  int x0, y0, rw, rh;           /* pasted region: source origin and size */
+  int bx, by, bw, bh;           /* context: zeroed / masked box in region coordinates (bw 0: none) */
+  int D, ox, oy;                /* padded side, image paste offsets (ImageOps.pad rounding) */
+  int mx, my;                   /* mask paste offsets (pad_mask_to_max: floor) */
+  int coef_off, ksize;          /* ints into coef: bounds [S][2] (xmin, count), then [S][ksize] */
+  int win_off;                  /* ints into win: mask tap windows [S][2] (lo, hi) */
+  int ops;                      /* ColorJitter ops, 4 bits per slot in order: 1 brightness,
+                                   2 contrast, 3 saturation, 0 end */
+  float f[3];                   /* their factors */
+  int pad_[2];
+} retr_pipe_item;
+/* crop/pad/resize (+ jitter) + normalise n items to fp32 [n][3][S][S] (u8: [n][S][S][3]
+ * scratch, tmp: sum of D*S*3 bytes) and, when mask != null, their resized masks [n][S][S];
+ * src, items, coef, win, tmp, u8, out, mask are device pointers, mean / std_ host float[3] */
+int retr_pipe_run(const unsigned char* src, const retr_pipe_item* items, int n, const int* coef,
+                  const int* win, unsigned char* tmp, int max_d, unsigned char* u8, float* out,
+                  unsigned char* mask, int S, const float* mean, const float* std_,
+                  void* stream);
 /* MaxPool2d(3, 2, 1) on NHWC (torchvision stem) */
 int retr_maxpool3x3s2(int dtype, const void* x, void* y, int N, int H, int W, int C, int OH,
                       int OW, void* stream);

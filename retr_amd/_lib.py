@@ -86,6 +86,7 @@ _SIGS = {
     "retr_conv2d_wgrad_splits": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
     "retr_nchw_to_nhwc": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "retr_nchw_to_s2d16": [_P, _P, _I, _I, _I, _I, _P],
+    "retr_pipe_run": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _P],
     "retr_stem_s2d_weights": [_P, _P, _I, _I, _P],
     "retr_conv2d_fwd_out": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I,
                             _I, _I, _P],
