@@ -308,17 +308,20 @@ struct EpiPhaseRows {
 // output pixels (layer 4 at cfg2, incl. stride-2 dgrad phases) unless both N and K exceed 512,
 // and 1x1 stride-1 convs into >= 1024 channels from <= 512 (40x40 maps).  A retr_tune
 // RETR_TUNE_BIG_TILE override still wins.
-inline bool prefer_tile64(int M, int N, int K, bool dense1x1) {
+inline bool prefer_tile64(int M, int N, int K, bool dense1x1, bool res_small_k) {
   if (retr_tune_get(RETR_TUNE_BIG_TILE) != 0) return false;
+  if (res_small_k) return true;   // 1x1 K <= 64 with a residual (layer 1): 117 -> 106 us
   if (M <= 8192 && (N <= 512 || K <= 512)) return true;
   return dense1x1 && N >= 1024 && K <= 512 && M <= 32768;
 }
 
 template <int FAM, typename T, class LA, class LB, class EP>
 int launch_auto(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, int splits,
-                hipStream_t st, const char* what, bool dense1x1 = false) {
+                hipStream_t st, const char* what, bool dense1x1 = false,
+                bool res_small_k = false) {
   if constexpr (sizeof(T) == 2) {
-    return launch_big<FAM>(la, lb, ep, M, N, K, splits, st, what, prefer_tile64(M, N, K, dense1x1));
+    return launch_big<FAM>(la, lb, ep, M, N, K, splits, st, what,
+                           prefer_tile64(M, N, K, dense1x1, res_small_k));
   } else {
     if (N >= 128 && M >= 4096) return launch_gemm<FAM, T, 128, 128>(la, lb, ep, M, N, K, splits, st, what);
     return launch_gemm<FAM, T, 64, 64>(la, lb, ep, M, N, K, splits, st, what);
@@ -411,7 +414,8 @@ int conv_fwd_t(const void* x, Geom g, const void* w, const float* bias, const vo
   ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseK<T> la{(const T*)x, (long)g.C, M, K};
-    return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd_1x1", true);
+    return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd_1x1", true,
+                                       res != nullptr && K <= 64);
   }
   ConvFwdA<T> la{(const T*)x, g, M, K};
   return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd");
