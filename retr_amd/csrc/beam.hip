@@ -36,32 +36,27 @@ template <> RETR_DEVICE void load8f<float>(const float* p, float (&v)[8]) {
 // One block per logits row: log-sum-exp and the K best (value, index), first index on ties.
 // Each thread keeps a sorted private list over its 8-wide chunks, then K rounds of a block-wide
 // (value desc, index asc) reduction pop the global best.
-template <typename T>
+template <typename T, int K>
 __global__ void __launch_bounds__(kThreads)
-topk_kernel(const T* x, long ld, int V, int K, int* idx_out, float* lp_out) {
+topk_kernel(const T* x, long ld, int V, int* idx_out, float* lp_out) {
   __shared__ float rv[kThreads / 64];
   __shared__ int ri[kThreads / 64], rt[kThreads / 64];
   __shared__ float red[2 * kThreads / 64];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const T* xr = x + (long)row * ld;
-  float tv[kMaxK];
-  int ti[kMaxK];
+  float tv[K];
+  int ti[K];
 #pragma unroll
-  for (int k = 0; k < kMaxK; ++k) tv[k] = -INFINITY, ti[k] = 0x7fffffff;
+  for (int k = 0; k < K; ++k) tv[k] = -INFINITY, ti[k] = 0x7fffffff;
   float mx = -INFINITY, sum = 0.f;   // online log-sum-exp
-  auto offer = [&](float v, int i) {
-    if (v > mx) {
-      sum = sum * __expf(mx - v) + 1.f;
-      mx = v;
-    } else {
-      sum += __expf(v - mx);
-    }
-    // insertion into the sorted private list (static indices only: registers, no scratch)
+  // sorted private list insertion (K is a compile-time constant: static indices, registers)
+  auto insert = [&](float v, int i) {
+    if (!better(v, i, tv[K - 1], ti[K - 1])) return;
     float cv = v;
     int ci = i;
 #pragma unroll
-    for (int k = 0; k < kMaxK; ++k) {
-      if (k < K && better(cv, ci, tv[k], ti[k])) {
+    for (int k = 0; k < K; ++k) {
+      if (better(cv, ci, tv[k], ti[k])) {
         const float tvk = tv[k];
         const int tik = ti[k];
         tv[k] = cv;
@@ -71,12 +66,49 @@ topk_kernel(const T* x, long ld, int V, int K, int* idx_out, float* lp_out) {
       }
     }
   };
-  const int V8 = V / 8;
-  for (int c = tid; c < V8; c += kThreads) {
-    float v[8];
-    load8f<T>(xr + 8 * c, v);
+  auto offer = [&](float v, int i) {
+    if (v > mx) {
+      sum = sum * __expf(mx - v) + 1.f;
+      mx = v;
+    } else {
+      sum += __expf(v - mx);
+    }
+    insert(v, i);
+  };
+  // 8-element chunks: one running-max rescale per chunk (no per-element divergent branch), and
+  // the insertion only for chunks whose max reaches the current K-th best (after the first few
+  // chunks almost none do) -- the per-element compare-and-shift chain made this kernel
+  // VALU-bound at ~40 us for 320 rows of 30522 words
+  auto offer8 = [&](const float (&v)[8], int base) {
+    float cm = v[0];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) offer(v[e], 8 * c + e);
+    for (int e = 1; e < 8; ++e) cm = fmaxf(cm, v[e]);
+    if (cm > mx) {
+      sum = mx == -INFINITY ? 0.f : sum * __expf(mx - cm);
+      mx = cm;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sum += __expf(v[e] - mx);
+    if (cm >= tv[K - 1]) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) insert(v[e], base + e);
+    }
+  };
+  // 8 chunks per thread in flight before any is offered
+  const int V8 = V / 8;
+  constexpr int U = 8;
+  for (int c0 = tid; c0 < V8; c0 += U * kThreads) {
+    float v[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u * kThreads;
+      if (c < V8) load8f<T>(xr + 8 * c, v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u * kThreads;
+      if (c < V8) offer8(v[u], 8 * c);
+    }
   }
   for (int i = 8 * V8 + tid; i < V; i += kThreads) offer(to_f(xr[i]), i);
   // block log-sum-exp
@@ -111,12 +143,12 @@ topk_kernel(const T* x, long ld, int V, int K, int* idx_out, float* lp_out) {
     if (tid == bw) {
       // pop: shift the private list (static indexing keeps it in registers)
 #pragma unroll
-      for (int q = 0; q < kMaxK - 1; ++q) {
+      for (int q = 0; q < K - 1; ++q) {
         tv[q] = tv[q + 1];
         ti[q] = ti[q + 1];
       }
-      tv[kMaxK - 1] = -INFINITY;
-      ti[kMaxK - 1] = 0x7fffffff;
+      tv[K - 1] = -INFINITY;
+      ti[K - 1] = 0x7fffffff;
     }
     if (tid == 0) {
       idx_out[(long)row * K + k] = bi;
@@ -141,34 +173,39 @@ beam_select_kernel(const int* cand_tok, const float* cand_lp, int B, int K, int 
   const int b = blockIdx.x, tid = threadIdx.x;
   if (*done >= 0) return;      // the decode already ended (reference contract: no more writes)
   const int r0 = b * K;
-  if (tid == 0) {
-    // candidates in (beam, rank) order; a stable selection of the K best by score
-    float cs[kMaxK * kMaxK];
-    int cp[kMaxK * kMaxK], ct[kMaxK * kMaxK], n = 0;
-    for (int k = 0; k < K; ++k) {
-      if (i == 0 && k > 0) break;                 // all beams start identical: expand one
-      const bool fin = i > 0 && finished[r0 + k];
+  // candidate c = (beam k, rank j) on thread c = k K + j (K <= 8: <= 64 candidates, one wave);
+  // its place in the stable order (score desc, then (k, j)) is the number of candidates ahead
+  // of it, so the K survivors are the candidates of rank < K -- the serial "pick the first best
+  // unused candidate K times" selection, without a single-thread loop over scratch arrays
+  {
+    __shared__ float cs_s[kMaxK * kMaxK];
+    __shared__ int ok_s[kMaxK * kMaxK];
+    const int k = tid / K, j = tid - k * K;
+    bool ok = tid < K * K && !(i == 0 && k > 0);
+    const bool fin = ok && i > 0 && finished[r0 + k];
+    if (fin && j > 0) ok = false;                  // a finished beam offers one continuation
+    float sc = -INFINITY;
+    int tk = 0;
+    if (ok) {
       const float base = i > 0 ? scores[r0 + k] : 0.f;
-      const int m = fin ? 1 : K;
-      for (int j = 0; j < m; ++j) {
-        cs[n] = fin ? base : base + cand_lp[(long)(r0 + k) * K + j];
-        cp[n] = k;
-        ct[n] = cand_tok[(long)(r0 + k) * K + j];
-        ++n;
-      }
+      sc = fin ? base : base + cand_lp[(long)(r0 + k) * K + j];
+      tk = cand_tok[(long)(r0 + k) * K + j];
     }
-    bool used[kMaxK * kMaxK];
-    for (int c = 0; c < n; ++c) used[c] = false;
-    for (int s = 0; s < K; ++s) {
-      int best = -1;
-      for (int c = 0; c < n; ++c)
-        if (!used[c] && (best < 0 || cs[c] > cs[best])) best = c;   // first index on ties
-      used[best] = true;
-      par[s] = cp[best];
-      ntok[s] = ct[best];
-      nsc[s] = cs[best];
-      const bool pf = i > 0 && finished[r0 + cp[best]];
-      nfin[s] = (pf || ct[best] == eos) ? 1 : 0;
+    if (tid < kMaxK * kMaxK) {
+      cs_s[tid] = sc;
+      ok_s[tid] = ok;
+    }
+    __syncthreads();
+    if (ok) {
+      int rank = 0;
+      for (int c = 0; c < K * K; ++c)
+        if (ok_s[c] && (cs_s[c] > sc || (cs_s[c] == sc && c < tid))) ++rank;
+      if (rank < K) {
+        par[rank] = k;
+        ntok[rank] = tk;
+        nsc[rank] = sc;
+        nfin[rank] = (fin || (long long)tk == eos) ? 1 : 0;
+      }
     }
   }
   // stage old rows
@@ -220,12 +257,24 @@ int retr_topk_rows(int dtype, const void* x, long ld, int M, int V, int K, int* 
   RETR_REQUIRE(ld % 8 == 0 && V >= K, "topk_rows: row stride %%8 and V >= K");
   if (M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == RETR_BF16)
-    hipLaunchKernelGGL(topk_kernel<bf16>, dim3(M), dim3(kThreads), 0, st, (const bf16*)x, ld, V,
-                       K, idx, logprob);
-  else
-    hipLaunchKernelGGL(topk_kernel<float>, dim3(M), dim3(kThreads), 0, st, (const float*)x, ld,
-                       V, K, idx, logprob);
+#define TOPK(KK)                                                                                 \
+  if (dtype == RETR_BF16)                                                                        \
+    hipLaunchKernelGGL((topk_kernel<bf16, KK>), dim3(M), dim3(kThreads), 0, st, (const bf16*)x,  \
+                       ld, V, idx, logprob);                                                     \
+  else                                                                                           \
+    hipLaunchKernelGGL((topk_kernel<float, KK>), dim3(M), dim3(kThreads), 0, st,                 \
+                       (const float*)x, ld, V, idx, logprob);
+  switch (K) {
+    case 1: TOPK(1) break;
+    case 2: TOPK(2) break;
+    case 3: TOPK(3) break;
+    case 4: TOPK(4) break;
+    case 5: TOPK(5) break;
+    case 6: TOPK(6) break;
+    case 7: TOPK(7) break;
+    default: TOPK(8) break;
+  }
+#undef TOPK
   return retr_check_launch("topk_rows");
 }
 
