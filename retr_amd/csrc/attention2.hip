@@ -44,6 +44,28 @@ RETR_DEVICE bf16x8 join(const s16x4& lo, const s16x4& hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// XCD-aware block order: the hardware deals workgroups round-robin to the 8 XCDs (each with its
+// own L2) in linear-id order, so the blocks of one (b, h) -- which all read the same K/V (or
+// Q/dO) slice -- landed on different XCDs and each fetched the slice from HBM (the resident
+// kernels' prologue, 512 blocks loading at once, took 7-10 us of a 35 us dq pass;
+// tools/attn_phase.py).  Physical id p runs logical id (p % 8) * (n / 8) + p / 8 (n % 8 == 0):
+// consecutive logical ids -- the blocks of one (b, h) -- share an XCD and its L2.
+struct BlockXYZ {
+  int x, y, z;
+};
+RETR_DEVICE BlockXYZ xcd_block() {
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int n = gx * gy * gridDim.z;
+  int p = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if ((n & 7) == 0) p = (p & 7) * (n >> 3) + (p >> 3);
+  BlockXYZ r;
+  r.x = p % gx;
+  const int t = p / gx;
+  r.y = t % gy;
+  r.z = t / gy;
+  return r;
+}
+
 template <int HD>
 struct Tile {
   static constexpr int KT = 64;              // keys per LDS stage
@@ -96,8 +118,9 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int qblk = blockIdx.x * (32 * NW);
+  const BlockXYZ bxyz = xcd_block();
+  const int b = bxyz.z, h = bxyz.y;
+  const int qblk = bxyz.x * (32 * NW);
   const int q0 = qblk + wave * 32;
   const int qi = q0 + r;                          // this lane's query
   const bf16* kb = k + (long)b * kbr * ldk + h * HD;
@@ -325,8 +348,9 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int qblk = blockIdx.x * (32 * NW);
+  const BlockXYZ bxyz = xcd_block();
+  const int b = bxyz.z, h = bxyz.y;
+  const int qblk = bxyz.x * (32 * NW);
   const int q0 = qblk + wave * 32;
   const int qi = q0 + r;
   const bf16* kb = k + (long)b * kbr * ldk + h * HD;
@@ -470,6 +494,19 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
   }
 }
 
+// Per-block timestamps (start, LDS-DMA drained, tile loop done) of the resident backward
+// kernels for tools/attn_phase.py: a separate -DRETR_ATTN_TIMING build in tools/_timing_attn/.
+#ifdef RETR_ATTN_TIMING
+__device__ long long g_attn_t[2][8192][3];
+#define ATTN_T(K, i)                                                                          \
+  if (threadIdx.x == 0) {                                                                     \
+    const int blk_ = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;          \
+    if (blk_ < 8192) g_attn_t[K][blk_][i] = wall_clock64();                                   \
+  }
+#else
+#define ATTN_T(K, i)
+#endif
+
 template <int HD, int NW>
 __global__ void __launch_bounds__(NW * 64)
 attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
@@ -482,14 +519,16 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int qblk = blockIdx.x * (32 * NW);
+  const BlockXYZ bxyz = xcd_block();
+  const int b = bxyz.z, h = bxyz.y;
+  const int qblk = bxyz.x * (32 * NW);
   const int q0 = qblk + wave * 32;
   const int qi = q0 + r;
   const int qc = qi < Lq ? qi : Lq - 1;
   const bf16* kb = k + (long)b * Lk * ldk + h * HD;
   const bf16* vb = v + (long)b * Lk * ldv + h * HD;
   const long srow = ((long)b * H + h) * Lq + qc;
+  ATTN_T(0, 0)
 
   int kend = Lk;
   if (causal) kend = min(Lk, qblk + 32 * NW);
@@ -539,6 +578,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
 #pragma unroll
     for (int e = 0; e < 16; ++e) G[dt][e] = 0.f;
   dma_drain_barrier();
+  ATTN_T(0, 1)
 
   const int wtiles = causal ? min(ntiles, (q0 + 32 + 63) / 64) : ntiles;
   for (int t = 0; t < wtiles; ++t) {
@@ -591,6 +631,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
       }
     }
   }
+  ATTN_T(0, 2)
   if (qi < Lq) {
     bf16* row = dq + ((long)b * Lq + qi) * lddq + h * HD;
 #pragma unroll
@@ -618,8 +659,9 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int kblk = blockIdx.x * (32 * NW);
+  const BlockXYZ bxyz = xcd_block();
+  const int b = bxyz.z, h = bxyz.y;
+  const int kblk = bxyz.x * (32 * NW);
   const int kj = kblk + wave * 32 + r;
   const int kc = kj < Lk ? kj : Lk - 1;
   const bf16* qb = q + (long)b * Lq * ldq + h * HD;
@@ -627,6 +669,7 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
   const long sbase = ((long)b * H + h) * Lq;
   const bool drop = dp.thresh != 0;
   const uint64_t seed = drop ? dp_seed(dp) : 0ull;
+  ATTN_T(1, 0)
 
   // queries [qstart, Lq) resident: tiles are numbered from qstart (causal skips the rows no key
   // of this block sees)
@@ -669,6 +712,7 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
 #pragma unroll
     for (int e = 0; e < 16; ++e) GK[dt][e] = 0.f, GV[dt][e] = 0.f;
   dma_drain_barrier();
+  ATTN_T(1, 1)
 
   // a wave's keys see no query below its first key (causal): skip those tiles
   const int wt0 = causal ? max(0, (kblk + wave * 32 - qstart) / 64) : 0;
@@ -727,6 +771,7 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
       }
     }
   }
+  ATTN_T(1, 2)
   if (kj < Lk) {
     bf16* krow = dk + ((long)b * Lk + kj) * lddk + h * HD;
     bf16* vrow = dv + ((long)b * Lk + kj) * lddv + h * HD;
@@ -909,8 +954,9 @@ attn_bwd_dq2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int qblk = blockIdx.x * (32 * NW);
+  const BlockXYZ bxyz = xcd_block();
+  const int b = bxyz.z, h = bxyz.y;
+  const int qblk = bxyz.x * (32 * NW);
   const int q0 = qblk + wave * 32;
   const int qi = q0 + r;
   const int qc = qi < Lq ? qi : Lq - 1;
@@ -1041,8 +1087,9 @@ attn_bwd_dkdv2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int b = blockIdx.z, h = blockIdx.y;
-  const int kblk = blockIdx.x * (32 * NW);
+  const BlockXYZ bxyz = xcd_block();
+  const int b = bxyz.z, h = bxyz.y;
+  const int kblk = bxyz.x * (32 * NW);
   const int kj = kblk + wave * 32 + r;          // this lane's key
   const int kc = kj < Lk ? kj : Lk - 1;
   const bf16* qb = q + (long)b * Lq * ldq + h * HD;
@@ -1178,6 +1225,12 @@ int launch_bwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
                      (bf16*)dk, lddk, (bf16*)dv, lddv, H, Lq, Lk, kpm, causal, cs, scale, dp);
   return retr_check_launch("attention_bwd_dkdv2");
 }
+
+#ifdef RETR_ATTN_TIMING
+extern "C" int retr_attn_timing_read(long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_attn_t), sizeof(long long) * 2 * 8192 * 3);
+}
+#endif
 
 int retr_attention_bwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
                         long ldv, const void* o, long ldo, const void* dout, long lddo,
