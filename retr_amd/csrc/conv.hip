@@ -809,6 +809,25 @@ int retr_conv2d_fwd_out(int dtype, const void* x, int Nb, int H, int W, int C, c
   return conv_fwd_t<float>(x, g, w, bias, residual, y, relu, (hipStream_t)stream);
 }
 
+int retr_conv1x1_fwd_cat(int dtype, const void* x1, int C1, const void* x2, int C2, int M,
+                         const void* w, const float* bias, void* y, int Co, int relu,
+                         void* stream) {
+  RETR_REQUIRE(dtype == RETR_BF16, "conv1x1_fwd_cat: bf16 only");
+  RETR_REQUIRE(C1 % 8 == 0 && C2 % 8 == 0 && C1 > 0 && C2 > 0 && Co % 8 == 0 && M > 0,
+               "conv1x1_fwd_cat: C1=%d C2=%d Co=%d must be positive multiples of 8", C1, C2, Co);
+  const int K = C1 + C2;
+  DenseK2<bf16> la{(const bf16*)x1, (long)C1, (const bf16*)x2, (long)C2, C1, M, K};
+  DenseK<bf16> lb{(const bf16*)w, (long)K, Co, K};
+  EpiFwd<bf16, bf16> ep{(bf16*)y, (long)Co, bias, nullptr, (long)Co, relu ? 2 : 0,
+                        DropoutParams{0, 0, 1.f}, 0};
+  ep.set_vec();
+  // built-in tile rule without the residual-conv 64x64 preference: at layer 1 (K = 128) the
+  // single-stage 128x128 tile runs 105 us vs 145 us for 64x64 (tools/cat_micro.py,
+  // profiles/r2_cat_micro.txt; unfused pair 212 us)
+  return launch_auto<kFamConvFwd, bf16>(la, lb, ep, M, Co, K, 1, (hipStream_t)stream,
+                                        "conv_fwd_1x1_cat", true, false);
+}
+
 int retr_conv2d_dgrad(int dtype, const void* dy, int Nb, int H, int W, int C, const void* wt,
                       void* dx, int Co, int KH, int KW, int stride, int pad, int dil,
                       const void* addend, const void* gate, void* stream) {

@@ -399,6 +399,31 @@ struct DenseK {
   }
 };
 
+// Two row-major operands side by side along K: element (r, k) = p1[r*ld1 + k] for k < K1,
+// p2[r*ld2 + k - K1] after (a 1x1 conv over channel-concatenated inputs, without writing the
+// concatenation).  K1 % EPC == 0, so no 16-byte chunk straddles the seam.
+template <typename T>
+struct DenseK2 {
+  static constexpr bool kContig = true;
+  static constexpr int EPC = Elem<T>::EPC;
+  const T* p1;
+  long ld1;
+  const T* p2;
+  long ld2;
+  int K1, rows, K;
+  struct Ctx { const T* r1; const T* r2; bool ok; };
+  struct KCur { int k; };
+  RETR_DEVICE Ctx row_ctx(int r) const {
+    return Ctx{p1 + (long)r * ld1, p2 + (long)r * ld2 - K1, r < rows};
+  }
+  RETR_DEVICE KCur kcur(int k) const { return KCur{k}; }
+  RETR_DEVICE void advance(KCur& c, int d) const { c.k += d; }
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& k) const {
+    if (!c.ok || k.k >= K) return nullptr;
+    return (k.k < K1 ? c.r1 : c.r2) + k.k;
+  }
+};
+
 // Operand stored [k][ld] (rows contiguous): element (r, k) = p[k*ld + r]; chunks along rows.
 // Requires rows % EPC == 0 or zero-padding beyond `rows` inside the chunk's row range.
 template <typename T>

@@ -31,6 +31,9 @@ def flops_of(name, a):
         _, _, n, h, w, c, _, _, _, _, co, kh, kw, s, p, d = a[:16]
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
         return "conv_fwd", 2.0 * n * oh * ow * co * kh * kw * c
+    if name == "retr_conv1x1_fwd_cat":
+        c1, c2, m, co = a[2], a[4], a[5], a[9]
+        return "conv_fwd", 2.0 * m * co * (c1 + c2)
     if name == "retr_conv2d_dgrad":
         _, _, n, h, w, c, _, _, co, kh, kw, s, p, d = a[:14]
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
@@ -73,6 +76,8 @@ def shape_of(name, a):
         return "group " + " + ".join(f"M{arr[i].M} N{arr[i].N} K{arr[i].K}" for i in range(n))
     if name == "retr_conv2d_fwd":
         return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} ->{a[10]} k{a[11]} s{a[13]} d{a[15]}"
+    if name == "retr_conv1x1_fwd_cat":
+        return f"M{a[5]} [{a[2]}|{a[4]}] ->{a[9]} k1 cat"
     if name == "retr_conv2d_dgrad":
         return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} <-{a[8]} k{a[9]} s{a[11]} d{a[13]}"
     if name == "retr_conv2d_wgrad":
@@ -94,7 +99,7 @@ def shape_of(name, a):
     return ""
 
 
-TRACKED = ("retr_conv2d_fwd", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
+TRACKED = ("retr_conv2d_fwd", "retr_conv1x1_fwd_cat", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
            "retr_linear_fwd_splitk",
            "retr_linear_dgrad", "retr_linear_dgrad_splitk", "retr_linear_wgrad",
            "retr_linear_fwd_group", "retr_linear_dgrad_group", "retr_linear_wgrad_group",

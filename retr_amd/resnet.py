@@ -187,6 +187,24 @@ def _conv_wgrad(spec, g, x, in_shape):
     return grad
 
 
+def _conv_tail_cat(runner, blk, h2, s2, x, xshape):
+    """relu(conv3(h2) + downsample(x)) as one 1x1 conv over the channel concatenation
+    (BackboneRunner.cat_tail); weights [W3eff | Wdseff] and bias b3 + bds cached per pack."""
+    c3, ds = blk.convs[2], blk.ds
+    wp3, _, b3, _ = PACKS.get(c3, h2.dtype)
+    wpd, _, bd, _ = PACKS.get(ds, h2.dtype)
+    ent = runner._cat_w.get(blk.name)
+    if ent is None or ent[0] is not wp3 or ent[1] is not wpd:
+        wcat = torch.cat([wp3.view(c3.cout, -1), wpd.view(ds.cout, -1)], 1).contiguous()
+        ent = (wp3, wpd, wcat, b3 + bd)
+        runner._cat_w[blk.name] = ent
+    n, oh, ow, c1 = s2
+    y = torch.empty(n, oh, ow, c3.cout, dtype=h2.dtype, device=h2.device)
+    call("retr_conv1x1_fwd_cat", dcode(h2.dtype), ptr(h2), c1, ptr(x), xshape[3], n * oh * ow,
+         ptr(ent[2]), ptr(ent[3]), ptr(y), c3.cout, 1, _st())
+    return y, (n, oh, ow, c3.cout)
+
+
 def _stem_s2d(runner, img):
     """bf16 stem as a space-to-depth conv: the 3-channel image becomes [N, H/2, W/2, 16]
     (2x2 pixel blocks, 12 channels + 4 zero), the 7x7 stride-2 pad-3 kernel a 4x4 stride-1 pad-2
@@ -237,8 +255,11 @@ class _Backbone(torch.autograd.Function):
                 c1, c2, c3 = blk.convs
                 h1, s1 = _conv_fwd(c1, inp, ishape, True)
                 h2, s2 = _conv_fwd(c2, h1, s1, True)
-                idt = _conv_fwd(blk.ds, inp, ishape, False)[0] if blk.ds is not None else inp
-                out, oshape = _conv_fwd(c3, h2, s2, True, residual=idt)
+                if runner.cat_tail(blk, ishape, s2):
+                    out, oshape = _conv_tail_cat(runner, blk, h2, s2, inp, ishape)
+                else:
+                    idt = _conv_fwd(blk.ds, inp, ishape, False)[0] if blk.ds is not None else inp
+                    out, oshape = _conv_fwd(c3, h2, s2, True, residual=idt)
                 acts = (inp, ishape, h1, s1, h2, s2)
             else:
                 c1, c2 = blk.convs
@@ -324,6 +345,21 @@ class BackboneRunner:
                                     for c in b.convs + ([b.ds] if b.ds is not None else [])]
         self._s2d_w = None
         self.use_s2d = os.environ.get("RETR_S2D_STEM", "1") != "0"
+        self._cat_w = {}
+        self.use_cat = os.environ.get("RETR_CAT_TAIL", "1") != "0"
+
+    def cat_tail(self, blk, ishape, s2):
+        """bf16 bottleneck whose downsample is a stride-1 1x1 conv (layer1.0; layer4.0 with
+        dilation): conv3 + downsample + residual add + ReLU as one 1x1 conv over [h2 | x]
+        (retr_conv1x1_fwd_cat) -- the downsample output is never written or re-read.  Backward
+        never needs it (the block's backward reads x, h1, h2 and the output gradient only)."""
+        ds = blk.ds
+        if not (self.use_cat and self.cdtype == torch.bfloat16 and blk.kind == "bottleneck"
+                and ds is not None):
+            return False
+        c3 = blk.convs[2]
+        return (ds.k == 1 and ds.s == 1 and ds.p == 0 and c3.k == 1 and c3.s == 1 and c3.p == 0
+                and ishape[1:3] == s2[1:3] and ishape[3] == ds.cp and s2[3] == c3.cp)
 
     def s2d_stem(self, c, h, w):
         """bf16 torchvision stem (7x7, stride 2, pad 3, RGB) on even-sized images: run it as the

@@ -751,3 +751,37 @@ def test_conv_pack_cache_lives_on_the_spec():
                                                        resnet.BackboneRunner)
              for s in m._runner.specs]
     assert specs and all(s.pack is not None for s in specs)
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2,Co", [(2, 20, 20, 64, 64, 256), (3, 7, 9, 64, 64, 256),
+                                            (1, 28, 28, 512, 1024, 2048),
+                                            (16, 160, 160, 64, 64, 256)])
+def test_conv1x1_fwd_cat(N, H, W, C1, C2, Co):
+    """retr_conv1x1_fwd_cat (bottleneck conv3 + stride-1 1x1 downsample + residual + ReLU as one
+    conv over [h2 | x]) against fp32 torch, and against the unfused pair (downsample conv, then
+    conv3 with the downsample output as its residual: differs by that output's bf16 rounding)."""
+    bf = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(N * H * W + C2)
+    M = N * H * W
+    x1 = torch.randn(M, C1, generator=g).to(DEV, bf)
+    x2 = torch.randn(M, C2, generator=g).to(DEV, bf)
+    w1 = (torch.randn(Co, C1, generator=g) / math.sqrt(C1)).to(DEV, bf)
+    w2 = (torch.randn(Co, C2, generator=g) / math.sqrt(C2)).to(DEV, bf)
+    b1 = torch.randn(Co, generator=g).to(DEV)
+    b2 = torch.randn(Co, generator=g).to(DEV)
+    wcat = torch.cat([w1, w2], 1).contiguous()
+    bcat = b1 + b2
+    y = torch.full((M, Co), float("nan"), dtype=bf, device=DEV)
+    call("retr_conv1x1_fwd_cat", ops.dcode(bf), ptr(x1), C1, ptr(x2), C2, M, ptr(wcat),
+         ptr(bcat), ptr(y), Co, 1, ops._st())
+    ref = torch.relu(x1.float() @ w1.float().t() + x2.float() @ w2.float().t() + bcat)
+    assert rel_err(y.float(), ref) < 1e-2
+    yd = torch.empty(M, Co, dtype=bf, device=DEV)
+    call("retr_conv2d_fwd", ops.dcode(bf), ptr(x2), N, H, W, C2, ptr(w2), ptr(b2), None, ptr(yd),
+         Co, 1, 1, 1, 0, 1, 0, ops._st())
+    yu = torch.empty(M, Co, dtype=bf, device=DEV)
+    call("retr_conv2d_fwd", ops.dcode(bf), ptr(x1), N, H, W, C1, ptr(w1), ptr(b1), ptr(yd),
+         ptr(yu), Co, 1, 1, 1, 0, 1, 1, ops._st())
+    torch.cuda.synchronize()
+    assert rel_err(y.float(), yu.float()) < 1e-2
+    assert torch.isfinite(y.float()).all()

@@ -157,3 +157,48 @@ def test_hip_path_matches_reference_goldens(case):
             ids = greedy(samples, model, max_len=cfg.max_position_embeddings, bos_token=101,
                          eos_token=int(eos))
             np.testing.assert_array_equal(ids.cpu().numpy(), g[f"greedy/eos{i}"])
+
+
+def test_cat_tail_matches_unfused():
+    """bf16 backbone with the fused bottleneck tail (retr_conv1x1_fwd_cat on layer1.0 and, with
+    dilation, layer4.0) vs the unfused downsample + residual path: logits and loss within bf16
+    tolerance of each other, and every gradient no further from the fp32 model's than the
+    unfused path's is (the fused path skips one bf16 rounding of the downsample output; in a
+    micro bf16 backbone either rounding moves deep weight gradients by a few percent)."""
+    _, m32, crit32, _, images, mask, caps, cap_mask = _setup("micro_r50_dil", dtype="fp32")
+    cfg, model, crit, sd, *_ = _setup("micro_r50_dil", dtype="bf16")
+    bb = next(m for m in model.modules() if hasattr(m, "runner") and hasattr(m, "body"))
+    runner = bb.runner(torch.bfloat16)
+    fused = [b.name for b in runner.blocks
+             if runner.cat_tail(b, (1, 8, 8, b.ds.cp) if b.ds is not None else (1, 8, 8, 0),
+                                (1, 8, 8, b.convs[-1].cp))]
+    assert fused == ["layer1.0", "layer4.0"], fused
+    samples = NestedTensor(images.to(DEV), mask.to(DEV))
+
+    def run(mdl, cr):
+        mdl.zero_grad(set_to_none=True)
+        out = mdl(samples, caps[:, :-1].to(DEV), cap_mask[:, :-1].to(DEV))
+        loss = cr(out.permute(0, 2, 1), caps[:, 1:].to(DEV))
+        loss.backward()
+        return (out.detach().float().clone(), loss.item(),
+                {n: p.grad.detach().double().clone() for n, p in mdl.named_parameters()
+                 if p.grad is not None})
+
+    o32, l32, g32 = run(m32, crit32)
+    runner.use_cat = True
+    o1, l1, g1 = run(model, crit)
+    runner.use_cat = False
+    o0, l0, g0 = run(model, crit)
+    runner.use_cat = True
+    assert _max_rel(o1, o0) < 2e-2
+    assert abs(l1 - l0) < 1e-2 * abs(l0)
+    assert g1.keys() == g0.keys() == g32.keys() and len(g1) > 0
+
+    def err(g, n):
+        return ((g[n] - g32[n]).norm() / (g32[n].norm() + 1e-30)).item()
+
+    e1 = sum(err(g1, n) for n in g1) / len(g1)
+    e0 = sum(err(g0, n) for n in g0) / len(g0)
+    assert e1 <= 1.25 * e0 + 1e-3, (e1, e0)
+    for n in g1:
+        assert err(g1, n) <= 2.0 * err(g0, n) + 2e-2, (n, err(g1, n), err(g0, n))
