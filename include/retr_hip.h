@@ -163,13 +163,15 @@ int retr_conv2d_fwd(int dtype, const void* x, int Nb, int H, int W, int C, const
 int retr_conv2d_fwd_out(int dtype, const void* x, int Nb, int H, int W, int C, const void* w,
                         const float* bias, const void* residual, void* y, int Co, int KH, int KW,
                         int stride, int pad, int dil, int OH, int OW, int relu, void* stream);
-/* Bottleneck tail with a stride-1 1x1 downsample (torchvision Bottleneck.forward:
+/* Bottleneck tail with its 1x1 downsample folded in (torchvision Bottleneck.forward:
  * relu(bn3(conv3(h)) + bn_ds(conv_ds(x))), models/backbone.py:65) as ONE 1x1 conv over the
- * channel concatenation [x1 | x2] (never materialised): y[M][Co] = act([x1 x2] . w^T + bias),
- * w [Co][C1 + C2] = [W3eff | Wdseff], bias = b3 + bds.  bf16 only. */
-int retr_conv1x1_fwd_cat(int dtype, const void* x1, int C1, const void* x2, int C2, int M,
-                         const void* w, const float* bias, void* y, int Co, int relu,
-                         void* stream);
+ * channel concatenation [x1 | x2] (never materialised): y[Nb*OH*OW][Co] =
+ * act([x1 x2'] . w^T + bias), x1 [Nb*OH*OW][C1] (h), x2 [Nb][H2][W2][C2] (the block input)
+ * sampled at stride2 (x2' = x2[:, ::s, ::s]), w [Co][C1 + C2] = [W3eff | Wdseff],
+ * bias = b3 + bds.  bf16 only. */
+int retr_conv1x1_fwd_cat(int dtype, const void* x1, int C1, const void* x2, int C2, int Nb,
+                         int OH, int OW, int H2, int W2, int stride2, const void* w,
+                         const float* bias, void* y, int Co, int relu, void* stream);
 int retr_conv2d_dgrad(int dtype, const void* dy, int Nb, int H, int W, int C, const void* wt,
                       void* dx, int Co, int KH, int KW, int stride, int pad, int dil,
                       const void* addend, const void* gate, void* stream);

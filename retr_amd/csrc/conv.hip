@@ -809,14 +809,19 @@ int retr_conv2d_fwd_out(int dtype, const void* x, int Nb, int H, int W, int C, c
   return conv_fwd_t<float>(x, g, w, bias, residual, y, relu, (hipStream_t)stream);
 }
 
-int retr_conv1x1_fwd_cat(int dtype, const void* x1, int C1, const void* x2, int C2, int M,
-                         const void* w, const float* bias, void* y, int Co, int relu,
-                         void* stream) {
+int retr_conv1x1_fwd_cat(int dtype, const void* x1, int C1, const void* x2, int C2, int Nb,
+                         int OH, int OW, int H2, int W2, int stride2, const void* w,
+                         const float* bias, void* y, int Co, int relu, void* stream) {
   RETR_REQUIRE(dtype == RETR_BF16, "conv1x1_fwd_cat: bf16 only");
-  RETR_REQUIRE(C1 % 8 == 0 && C2 % 8 == 0 && C1 > 0 && C2 > 0 && Co % 8 == 0 && M > 0,
+  RETR_REQUIRE(C1 % 8 == 0 && C2 % 8 == 0 && C1 > 0 && C2 > 0 && Co % 8 == 0,
                "conv1x1_fwd_cat: C1=%d C2=%d Co=%d must be positive multiples of 8", C1, C2, Co);
-  const int K = C1 + C2;
-  DenseK2<bf16> la{(const bf16*)x1, (long)C1, (const bf16*)x2, (long)C2, C1, M, K};
+  RETR_REQUIRE(Nb > 0 && OH > 0 && OW > 0 && stride2 >= 1 && (OH - 1) * stride2 < H2 &&
+               (OW - 1) * stride2 < W2 && (stride2 != 1 || (H2 == OH && W2 == OW)),
+               "conv1x1_fwd_cat: %dx%d output of a stride-%d 1x1 conv over %dx%d", OH, OW,
+               stride2, H2, W2);
+  const int K = C1 + C2, M = Nb * OH * OW;
+  DenseK2<bf16> la{(const bf16*)x1, (long)C1, (const bf16*)x2, (long)C2, C1, M, K,
+                   OH, OW, H2, W2, stride2};
   DenseK<bf16> lb{(const bf16*)w, (long)K, Co, K};
   EpiFwd<bf16, bf16> ep{(bf16*)y, (long)Co, bias, nullptr, (long)Co, relu ? 2 : 0,
                         DropoutParams{0, 0, 1.f}, 0};

@@ -399,9 +399,11 @@ struct DenseK {
   }
 };
 
-// Two row-major operands side by side along K: element (r, k) = p1[r*ld1 + k] for k < K1,
-// p2[r*ld2 + k - K1] after (a 1x1 conv over channel-concatenated inputs, without writing the
-// concatenation).  K1 % EPC == 0, so no 16-byte chunk straddles the seam.
+// Two row-major operands side by side along K: element (r, k) = p1[r*ld1 + k] for k < K1, and
+// for k >= K1 the 1x1 stride-s2 conv input of output pixel r = (n, oh, ow) of an OH x OW map:
+// p2[((n*H2 + oh*s2)*W2 + ow*s2)*ld2 + k - K1] (s2 = 1: row r of p2).  A bottleneck's conv3 over
+// [h2 | x] with its downsample folded in, without writing the concatenation.  K1 % EPC == 0, so
+// no 16-byte chunk straddles the seam.
 template <typename T>
 struct DenseK2 {
   static constexpr bool kContig = true;
@@ -411,10 +413,19 @@ struct DenseK2 {
   const T* p2;
   long ld2;
   int K1, rows, K;
+  int OH, OW, H2, W2, s2;
   struct Ctx { const T* r1; const T* r2; bool ok; };
   struct KCur { int k; };
   RETR_DEVICE Ctx row_ctx(int r) const {
-    return Ctx{p1 + (long)r * ld1, p2 + (long)r * ld2 - K1, r < rows};
+    const int rr = r < rows ? r : 0;
+    long px = rr;
+    if (s2 != 1) {
+      const int hw = OH * OW;
+      const int n = rr / hw, rem = rr - n * hw;
+      const int oh = rem / OW, ow = rem - oh * OW;
+      px = ((long)n * H2 + (long)oh * s2) * W2 + (long)ow * s2;
+    }
+    return Ctx{p1 + (long)rr * ld1, p2 + px * ld2 - K1, r < rows};
   }
   RETR_DEVICE KCur kcur(int k) const { return KCur{k}; }
   RETR_DEVICE void advance(KCur& c, int d) const { c.k += d; }

@@ -32,7 +32,7 @@ def flops_of(name, a):
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
         return "conv_fwd", 2.0 * n * oh * ow * co * kh * kw * c
     if name == "retr_conv1x1_fwd_cat":
-        c1, c2, m, co = a[2], a[4], a[5], a[9]
+        c1, c2, m, co = a[2], a[4], a[5] * a[6] * a[7], a[14]
         return "conv_fwd", 2.0 * m * co * (c1 + c2)
     if name == "retr_conv2d_dgrad":
         _, _, n, h, w, c, _, _, co, kh, kw, s, p, d = a[:14]
@@ -77,7 +77,7 @@ def shape_of(name, a):
     if name == "retr_conv2d_fwd":
         return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} ->{a[10]} k{a[11]} s{a[13]} d{a[15]}"
     if name == "retr_conv1x1_fwd_cat":
-        return f"M{a[5]} [{a[2]}|{a[4]}] ->{a[9]} k1 cat"
+        return f"N{a[5]} {a[6]}x{a[7]} [{a[2]}|{a[4]} s{a[10]}] ->{a[14]} k1 cat"
     if name == "retr_conv2d_dgrad":
         return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} <-{a[8]} k{a[9]} s{a[11]} d{a[13]}"
     if name == "retr_conv2d_wgrad":

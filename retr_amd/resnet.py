@@ -200,8 +200,9 @@ def _conv_tail_cat(runner, blk, h2, s2, x, xshape):
         runner._cat_w[blk.name] = ent
     n, oh, ow, c1 = s2
     y = torch.empty(n, oh, ow, c3.cout, dtype=h2.dtype, device=h2.device)
-    call("retr_conv1x1_fwd_cat", dcode(h2.dtype), ptr(h2), c1, ptr(x), xshape[3], n * oh * ow,
-         ptr(ent[2]), ptr(ent[3]), ptr(y), c3.cout, 1, _st())
+    call("retr_conv1x1_fwd_cat", dcode(h2.dtype), ptr(h2), c1, ptr(x), xshape[3], n, oh, ow,
+         xshape[1], xshape[2], ds.s, ptr(ent[2]), ptr(ent[3]), ptr(y), c3.cout, 1, _st())
+    runner.cat_used.append(blk.name)
     return y, (n, oh, ow, c3.cout)
 
 
@@ -248,6 +249,7 @@ class _Backbone(torch.autograd.Function):
         shape = (N, ph, pw, sh[3])
         del s
         saved = []
+        runner.cat_used = []
         grad_on = runner.save
         for blk in blocks:
             inp, ishape = x, shape
@@ -346,20 +348,22 @@ class BackboneRunner:
         self._s2d_w = None
         self.use_s2d = os.environ.get("RETR_S2D_STEM", "1") != "0"
         self._cat_w = {}
+        self.cat_used = []          # blocks that took the fused tail in the last forward
         self.use_cat = os.environ.get("RETR_CAT_TAIL", "1") != "0"
 
     def cat_tail(self, blk, ishape, s2):
-        """bf16 bottleneck whose downsample is a stride-1 1x1 conv (layer1.0; layer4.0 with
-        dilation): conv3 + downsample + residual add + ReLU as one 1x1 conv over [h2 | x]
-        (retr_conv1x1_fwd_cat) -- the downsample output is never written or re-read.  Backward
-        never needs it (the block's backward reads x, h1, h2 and the output gradient only)."""
+        """bf16 bottleneck with a 1x1 downsample (the first block of every layer): conv3 +
+        downsample + residual add + ReLU as one 1x1 conv over [h2 | x sampled at the downsample
+        stride] (retr_conv1x1_fwd_cat) -- the downsample output is never written or re-read.
+        Backward never needs it (the block's backward reads x, h1, h2 and the output gradient)."""
         ds = blk.ds
         if not (self.use_cat and self.cdtype == torch.bfloat16 and blk.kind == "bottleneck"
                 and ds is not None):
             return False
         c3 = blk.convs[2]
-        return (ds.k == 1 and ds.s == 1 and ds.p == 0 and c3.k == 1 and c3.s == 1 and c3.p == 0
-                and ishape[1:3] == s2[1:3] and ishape[3] == ds.cp and s2[3] == c3.cp)
+        return (ds.k == 1 and ds.p == 0 and ds.d == 1 and c3.k == 1 and c3.s == 1 and c3.p == 0
+                and ds.out_hw(ishape[1], ishape[2]) == tuple(s2[1:3]) and ishape[3] == ds.cp
+                and s2[3] == c3.cp)
 
     def s2d_stem(self, c, h, w):
         """bf16 torchvision stem (7x7, stride 2, pad 3, RGB) on even-sized images: run it as the

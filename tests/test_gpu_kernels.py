@@ -753,18 +753,24 @@ def test_conv_pack_cache_lives_on_the_spec():
     assert specs and all(s.pack is not None for s in specs)
 
 
-@pytest.mark.parametrize("N,H,W,C1,C2,Co", [(2, 20, 20, 64, 64, 256), (3, 7, 9, 64, 64, 256),
-                                            (1, 28, 28, 512, 1024, 2048),
-                                            (16, 160, 160, 64, 64, 256)])
-def test_conv1x1_fwd_cat(N, H, W, C1, C2, Co):
-    """retr_conv1x1_fwd_cat (bottleneck conv3 + stride-1 1x1 downsample + residual + ReLU as one
-    conv over [h2 | x]) against fp32 torch, and against the unfused pair (downsample conv, then
-    conv3 with the downsample output as its residual: differs by that output's bf16 rounding)."""
+@pytest.mark.parametrize("N,H,W,C1,C2,Co,s", [(2, 20, 20, 64, 64, 256, 1),
+                                              (3, 7, 9, 64, 64, 256, 1),
+                                              (1, 28, 28, 512, 1024, 2048, 1),
+                                              (16, 160, 160, 64, 64, 256, 1),
+                                              (2, 10, 10, 128, 256, 512, 2),
+                                              (3, 5, 7, 256, 512, 1024, 2),
+                                              (16, 80, 80, 128, 256, 512, 2)])
+def test_conv1x1_fwd_cat(N, H, W, C1, C2, Co, s):
+    """retr_conv1x1_fwd_cat (bottleneck conv3 + 1x1 downsample of stride s + residual + ReLU as
+    one conv over [h2 | x[:, ::s, ::s]]) against fp32 torch, and against the unfused pair
+    (downsample conv, then conv3 with its output as the residual: differs by that output's
+    bf16 rounding).  H2 = s * H (even) or s * H - 1 (odd input rows, as torchvision's)."""
     bf = torch.bfloat16
-    g = torch.Generator(device="cpu").manual_seed(N * H * W + C2)
+    g = torch.Generator(device="cpu").manual_seed(N * H * W + C2 + s)
     M = N * H * W
+    H2, W2 = (s * H, s * W - (1 if s > 1 else 0))
     x1 = torch.randn(M, C1, generator=g).to(DEV, bf)
-    x2 = torch.randn(M, C2, generator=g).to(DEV, bf)
+    x2 = torch.randn(N, H2, W2, C2, generator=g).to(DEV, bf)
     w1 = (torch.randn(Co, C1, generator=g) / math.sqrt(C1)).to(DEV, bf)
     w2 = (torch.randn(Co, C2, generator=g) / math.sqrt(C2)).to(DEV, bf)
     b1 = torch.randn(Co, generator=g).to(DEV)
@@ -772,13 +778,14 @@ def test_conv1x1_fwd_cat(N, H, W, C1, C2, Co):
     wcat = torch.cat([w1, w2], 1).contiguous()
     bcat = b1 + b2
     y = torch.full((M, Co), float("nan"), dtype=bf, device=DEV)
-    call("retr_conv1x1_fwd_cat", ops.dcode(bf), ptr(x1), C1, ptr(x2), C2, M, ptr(wcat),
-         ptr(bcat), ptr(y), Co, 1, ops._st())
-    ref = torch.relu(x1.float() @ w1.float().t() + x2.float() @ w2.float().t() + bcat)
+    call("retr_conv1x1_fwd_cat", ops.dcode(bf), ptr(x1), C1, ptr(x2), C2, N, H, W, H2, W2, s,
+         ptr(wcat), ptr(bcat), ptr(y), Co, 1, ops._st())
+    xs = x2[:, ::s, ::s, :].reshape(M, C2)
+    ref = torch.relu(x1.float() @ w1.float().t() + xs.float() @ w2.float().t() + bcat)
     assert rel_err(y.float(), ref) < 1e-2
     yd = torch.empty(M, Co, dtype=bf, device=DEV)
-    call("retr_conv2d_fwd", ops.dcode(bf), ptr(x2), N, H, W, C2, ptr(w2), ptr(b2), None, ptr(yd),
-         Co, 1, 1, 1, 0, 1, 0, ops._st())
+    call("retr_conv2d_fwd", ops.dcode(bf), ptr(x2), N, H2, W2, C2, ptr(w2), ptr(b2), None,
+         ptr(yd), Co, 1, 1, s, 0, 1, 0, ops._st())
     yu = torch.empty(M, Co, dtype=bf, device=DEV)
     call("retr_conv2d_fwd", ops.dcode(bf), ptr(x1), N, H, W, C1, ptr(w1), ptr(b1), ptr(yd),
          ptr(yu), Co, 1, 1, 1, 0, 1, 1, ops._st())
