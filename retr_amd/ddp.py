@@ -24,6 +24,8 @@ the captured forward/backward graph and the captured optimizer graph.
 import torch
 import torch.distributed as dist
 
+from .optim import _round
+
 
 class GradSync:
     def __init__(self, params, bucket_mb=64, group=None, optimizer=None, defer=False):
@@ -71,6 +73,7 @@ class GradSync:
         self.pending = [0] * len(self.buckets)
         self.handles = [None] * len(self.buckets)
         self.foreign = set()
+        self.on_ready = None                  # deferred mode: callback(bucket) at completion
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
         self.reset()
 
@@ -94,6 +97,22 @@ class GradSync:
     def zero_copy(self):
         return self.arena is not None
 
+    def _mark_dirty(self):
+        """G now holds values the optimizer's arena bookkeeping did not hand out (a copied-in
+        gradient, or the all-reduce's in-place result): make its next reset zero G."""
+        a = getattr(self.arena, "arena", None)
+        if a is not None:
+            a.dirty = True
+
+    def all_finite(self, finite):
+        """True iff ``finite`` holds on every rank (one MAX all-reduce of a flag)."""
+        dev = self.params[0].device if self.params else torch.device("cpu")
+        if self.avg_supported and dev.type != "cuda":
+            dev = torch.device("cuda", torch.cuda.current_device())
+        t = torch.tensor([0.0 if finite else 1.0], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t.item() == 0.0
+
     def reset(self):
         self.pending = [len(ps) for ps in self.buckets]
         self.handles = [None] * len(self.buckets)
@@ -112,11 +131,15 @@ class GradSync:
             if p.grad.data_ptr() != view.data_ptr():     # produced outside the arena
                 view.copy_(p.grad)
                 self.foreign.add(p)
+                self._mark_dirty()
         else:
             self.flat[bi][off:off + p.numel()].copy_(p.grad.reshape(-1))
         self.pending[bi] -= 1
-        if self.pending[bi] == 0 and not self.defer:
-            self._launch(bi)
+        if self.pending[bi] == 0:
+            if not self.defer:
+                self._launch(bi)
+            elif self.on_ready is not None:
+                self.on_ready(bi)
 
     def synchronize(self):
         """Wait for every bucket (launching the ones not launched yet: deferred mode, or
@@ -136,6 +159,7 @@ class GradSync:
             if not self.avg_supported:
                 flat.div_(self.world)
             if self.arena is not None:
+                self._mark_dirty()
                 for p in ps:
                     if p.grad is None or p in self.foreign:
                         p.grad = p._retr_grad_view.view(p.shape)
@@ -149,10 +173,6 @@ class GradSync:
                     p.grad.copy_(g)
         self.foreign.clear()
         self.reset()
-
-
-def _round(n, a=16):
-    return (n + a - 1) // a * a
 
 
 def broadcast_parameters(module, src=0, group=None):

@@ -5,7 +5,8 @@
 Differences (all on the MI355X path, none observable in results):
   * ``nlgeval`` is imported lazily inside ``eval_model`` (the reference imports it at module
     top, ``engine.py:14-17``, which makes the module unimportable without the submodule);
-  * under data parallelism (``retr_amd.ddp``) gradients are all-reduced before clipping.
+  * under data parallelism (``retr_amd.ddp``) gradients are all-reduced before clipping, and
+    the non-finite-loss exit is agreed over ranks (one all-reduce of a flag per step).
 """
 import math
 import sys
@@ -84,10 +85,16 @@ class GraphedTrainStep:
     convolution weights, captured decode graphs) never serve values from before the replay,
     and FusedAdamW's host step counters advance with the device counter.
 
-    Data parallel (``grad_sync``): the step is captured as two graphs -- forward + backward,
-    then clip + optimizer -- and every replay runs the bucketed RCCL all-reduces of
-    ``grad_sync`` (deferred mode: in place on FusedAdamW's gradient arena) between them, so no
-    collective is captured inside a graph.
+    Data parallel (``grad_sync``): forward + backward is captured as a chain of SEGMENT graphs
+    cut where a gradient bucket becomes complete (the bucket's last post-accumulate-grad hook
+    ends the running capture and begins the next, on the same capture stream and memory
+    pool), then clip + optimizer as one more graph.  A replay runs segment 0, enqueues the RCCL
+    all-reduce (AVG, in place on FusedAdamW's gradient arena) of every bucket that completed
+    in it, runs segment 1 -- concurrently with those all-reduces on RCCL's stream -- and so on;
+    the optimizer graph waits for every bucket.  No collective is captured inside a graph, so
+    the all-reduces stay plain eager RCCL calls (the same ones the eager hook path issues)
+    while still overlapping the rest of backward.  ``order`` records the replay's enqueue
+    sequence (("segment", k) / ("allreduce", bucket)) for tests.
 
     Requirements: ``optimizer`` built with ``capturable=True`` (or a retr_amd FusedAdamW, whose
     step counter and lr live on the device); fixed batch shapes.
@@ -98,9 +105,14 @@ class GraphedTrainStep:
         self.max_norm, self.grad_sync, self.warmup = max_norm, grad_sync, warmup
         self.graph = None
         self.graph_opt = None
+        self.segments = []        # DP: forward/backward segment graphs (segments[0] is graph)
+        self.after = []           # DP: buckets whose all-reduce follows segment k
+        self.order = []           # DP: enqueue order of the last replay
         self.static = None
         self.loss = None
         self._active = None
+        self._cap_stream = None
+        self._tick = None
 
     def _step(self):
         s_img, s_mask, s_caps, s_cm = self.static
@@ -121,19 +133,67 @@ class GraphedTrainStep:
             with torch.cuda.graph(self.graph, capture_error_mode=mode):
                 self.loss = self._step().detach()
             return
+        self._capture_segmented()
+
+    def _capture_segmented(self):
+        """Forward + backward as segment graphs cut at bucket completions (see class doc).
+        A cut happens inside a post-accumulate-grad hook, i.e. on autograd's device thread,
+        while the main thread began the capture: "relaxed" capture mode is the one that lets a
+        capture end on another thread than the one that began it."""
+        import gc
         gs = self.grad_sync
         defer = gs.defer
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self._tick = torch.zeros(1, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        gc.collect()
+        torch.cuda.empty_cache()
+        cs = self._cap_stream = torch.cuda.Stream(device=dev)
+        cs.wait_stream(torch.cuda.current_stream())
         gs.defer = True                      # hooks only route gradients while capturing
+        gs.on_ready = self._cut
+        self.segments, self.after = [self.graph], [[]]
+        self._pool = torch.cuda.graph_pool_handle()   # shared by every segment + the optimizer
+        capturing = False
         try:
-            with torch.cuda.graph(self.graph, capture_error_mode=mode):
+            with torch.cuda.stream(cs):
+                self.graph.capture_begin(pool=self._pool, capture_error_mode="relaxed")
+                capturing = True
                 self.loss = self._fb().detach()
-            gs.synchronize()                 # eager: p.grad -> bucket views for the 2nd graph
+                capturing = False
+                self.segments[-1].capture_end()
+        except BaseException:
+            if capturing:                    # leave no stream capturing behind the error
+                with torch.cuda.stream(cs):
+                    try:
+                        self.segments[-1].capture_end()
+                    except Exception:
+                        pass
+            gs.defer = defer
+            raise
+        finally:
+            gs.on_ready = None
+        torch.cuda.current_stream().wait_stream(cs)
+        try:
+            gs.synchronize()                 # eager: p.grad -> bucket views for the last graph
             self.graph_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_opt, pool=self.graph.pool(),
-                                  capture_error_mode=mode):
+            with torch.cuda.graph(self.graph_opt, pool=self._pool, stream=cs,
+                                  capture_error_mode="thread_local"):
                 clip_and_step(self.model, self.optimizer, self.max_norm)
         finally:
             gs.defer = defer
+
+    def _cut(self, bucket):
+        """Bucket ``bucket`` is complete: end the running segment (its all-reduce will follow
+        that segment's replay) and begin the next one."""
+        with torch.cuda.stream(self._cap_stream):
+            self.segments[-1].capture_end()
+            self.after[-1].append(bucket)
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin(pool=self._pool, capture_error_mode="relaxed")
+            self.segments.append(g)
+            self.after.append([])
+            self._tick.zero_()               # one node, so no segment is ever empty
 
     def _params(self):
         return [p for g in self.optimizer.param_groups for p in g["params"]]
@@ -208,9 +268,18 @@ class GraphedTrainStep:
             self._restore(snap)
         if hasattr(self.optimizer, "sync_hyper"):
             self.optimizer.sync_hyper()      # lr schedule changes reach the captured kernels
-        self.graph.replay()
-        if self.graph_opt is not None:
-            self.grad_sync.synchronize()     # RCCL all-reduce of every bucket, then the update
+        if self.graph_opt is None:
+            self.graph.replay()
+        else:
+            gs = self.grad_sync
+            self.order = []
+            for k, g in enumerate(self.segments):
+                g.replay()
+                self.order.append(("segment", k))
+                for b in self.after[k]:
+                    gs._launch(b)            # RCCL stream waits for segment k only
+                    self.order.append(("allreduce", b))
+            gs.synchronize()                 # any bucket not launched yet; stream waits on all
             self.graph_opt.replay()
         if hasattr(self.optimizer, "_advance_host"):
             self.optimizer._advance_host(self._active)
@@ -236,7 +305,12 @@ def train_one_epoch(model, criterion, data_loader, optimizer, device, epoch, max
             loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
             loss_value = loss.item()
             epoch_loss += loss_value
-            if not math.isfinite(loss_value):
+            finite = math.isfinite(loss_value)
+            if grad_sync is not None:
+                # every rank takes the same decision: a rank that exits alone would leave the
+                # others blocked in the gradient all-reduce of this step
+                finite = grad_sync.all_finite(finite)
+            if not finite:
                 print(f"Loss is {loss_value}, stopping training")
                 sys.exit(1)
             optimizer.zero_grad()

@@ -16,6 +16,10 @@ import torch
 
 from . import _lib
 
+PEAK_FLOPS = 2.5e15    # MI355X dense bf16 MFMA (MI355X_MICROARCH.md), FLOP/s
+PEAK_BYTES = 8.0e12    # HBM3E, B/s
+RIDGE = PEAK_FLOPS / PEAK_BYTES   # 312.5 FLOP/B: below it a launch is HBM-bound
+
 
 def _conv_out(h, k, s, p, d):
     return (h + 2 * p - d * (k - 1) - 1) // s + 1
@@ -27,9 +31,11 @@ def _conv_variant(k, s, p):
 
 def flops_of(name, a):
     """(family key, algorithmic FLOPs) of one C-ABI call (2 FLOP per MAC)."""
-    if name == "retr_conv2d_fwd":
+    if name in ("retr_conv2d_fwd", "retr_conv2d_fwd_out"):
         _, _, n, h, w, c, _, _, _, _, co, kh, kw, s, p, d = a[:16]
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
+        if name == "retr_conv2d_fwd_out":
+            oh, ow = a[16], a[17]
         return "conv_fwd", 2.0 * n * oh * ow * co * kh * kw * c
     if name == "retr_conv1x1_fwd_cat":
         c1, c2, m, co = a[2], a[4], a[5] * a[6] * a[7], a[14]
@@ -69,12 +75,75 @@ _GROUPS = {"retr_linear_fwd_group": ("linear_fwd", 3), "retr_linear_dgrad_group"
            "retr_linear_wgrad_group": ("linear_wgrad", 2)}
 
 
+def _esz(dtype):
+    return 2 if dtype == 1 else 4
+
+
+def bytes_of(name, a):
+    """Algorithmic (compulsory) HBM bytes of one C-ABI call: every operand read once and every
+    output written once in its storage type (bf16 operands, fp32 weight gradients / fp32
+    outputs where the call says so).  Split-K slabs, re-reads and padding are implementation
+    traffic and are NOT counted here -- the rocprofv3 --pmc passes measure those."""
+    e = _esz(a[0])
+    if name in ("retr_conv2d_fwd", "retr_conv2d_fwd_out"):
+        _, _, n, h, w, c, _, _, res, _, co, kh, kw, s, p, d = a[:16]
+        oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
+        if name == "retr_conv2d_fwd_out":
+            oh, ow = a[16], a[17]
+        out = n * oh * ow * co * e
+        return e * (n * h * w * c + co * kh * kw * c) + out * (2 if res else 1)
+    if name == "retr_conv1x1_fwd_cat":
+        c1, c2, n, oh, ow, co = a[2], a[4], a[5], a[6], a[7], a[14]
+        m = n * oh * ow
+        return e * (m * (c1 + c2) + co * (c1 + c2) + m * co)
+    if name == "retr_conv2d_dgrad":
+        _, _, n, h, w, c, _, _, co, kh, kw, s, p, d, addend, gate = a[:16]
+        oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
+        dx = n * h * w * c * e
+        return e * (n * oh * ow * co + co * kh * kw * c) + dx * (1 + bool(addend) + bool(gate))
+    if name == "retr_conv2d_wgrad":
+        _, _, _, n, h, w, c, _, co, kh, kw, s, p, d = a[:14]
+        oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
+        return e * (n * oh * ow * co + n * h * w * c) + 4 * co * kh * kw * c
+    if name in ("retr_linear_fwd", "retr_linear_fwd_splitk"):
+        yf32, m, n, k, res = a[8], a[9], a[10], a[11], a[13]
+        return e * (m * k + n * k) + m * n * (4 if yf32 else e) + (4 * m * n if res else 0)
+    if name in ("retr_linear_dgrad", "retr_linear_dgrad_splitk"):
+        dxf32, m, n, k, addend, af32, gate = a[7], a[8], a[9], a[10], a[11], a[12], a[14]
+        return (e * (m * n + n * k) + m * k * (4 if dxf32 else e)
+                + (m * k * (4 if af32 else e) if addend else 0) + (m * k * e if gate else 0))
+    if name == "retr_linear_wgrad":
+        m, n, k, acc = a[7], a[8], a[9], a[11]
+        return e * (m * n + m * k) + 4 * n * k * (2 if acc else 1)
+    if name == "retr_linear_fwd_group":
+        yf32, cnt, arr = a[1], a[2], a[3]
+        return sum(e * (d.M * d.K + d.N * d.K) + d.M * d.N * (4 if yf32 else e)
+                   + (4 * d.M * d.N if d.residual else 0) for d in (arr[i] for i in range(cnt)))
+    if name == "retr_linear_dgrad_group":
+        dxf32, af32, cnt, arr = a[1], a[2], a[4], a[5]
+        return sum(e * (d.M * d.N + d.N * d.K) + d.M * d.K * (4 if dxf32 else e)
+                   + (d.M * d.K * (4 if af32 else e) if d.addend else 0)
+                   + (d.M * d.K * e if d.gate else 0) for d in (arr[i] for i in range(cnt)))
+    if name == "retr_linear_wgrad_group":
+        cnt, arr = a[1], a[2]
+        return sum(e * (d.M * d.N + d.M * d.K) + 4 * d.N * d.K * (2 if d.accumulate else 1)
+                   for d in (arr[i] for i in range(cnt)))
+    if name == "retr_attention_fwd":
+        b, h, lq, lk, hd = a[9], a[10], a[11], a[12], a[13]
+        return e * b * h * hd * (2 * lq + 2 * lk) + 4 * b * h * lq
+    if name == "retr_attention_bwd":
+        b, h, lq, lk, hd = a[18], a[19], a[20], a[21], a[22]
+        # read q k v o dO (+lse), write dq dk dv
+        return e * b * h * hd * (3 * lq + 2 * lk + lq + 2 * lk) + 4 * b * h * lq
+    return 0
+
+
 def shape_of(name, a):
     """Short shape tag of a call (for the per-shape breakdown)."""
     if name in _GROUPS:
         n, arr = a[_GROUPS[name][1] - 1], a[_GROUPS[name][1]]
         return "group " + " + ".join(f"M{arr[i].M} N{arr[i].N} K{arr[i].K}" for i in range(n))
-    if name == "retr_conv2d_fwd":
+    if name in ("retr_conv2d_fwd", "retr_conv2d_fwd_out"):
         return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} ->{a[10]} k{a[11]} s{a[13]} d{a[15]}"
     if name == "retr_conv1x1_fwd_cat":
         return f"N{a[5]} {a[6]}x{a[7]} [{a[2]}|{a[4]} s{a[10]}] ->{a[14]} k1 cat"
@@ -99,7 +168,7 @@ def shape_of(name, a):
     return ""
 
 
-TRACKED = ("retr_conv2d_fwd", "retr_conv1x1_fwd_cat", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
+TRACKED = ("retr_conv2d_fwd", "retr_conv2d_fwd_out", "retr_conv1x1_fwd_cat", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
            "retr_linear_fwd_splitk",
            "retr_linear_dgrad", "retr_linear_dgrad_splitk", "retr_linear_wgrad",
            "retr_linear_fwd_group", "retr_linear_dgrad_group", "retr_linear_wgrad_group",
@@ -135,13 +204,14 @@ class Probe:
         self.names = set(names)
         self.detail = detail
         self.spin_us = spin_us
-        self.records = []     # (key, flops, ev0, ev1)
+        self.records = []     # (key, flops, bytes, ev0, ev1)
         self.active = False
 
     def wrap(self, name, args, fn):
         if not self.active:
             return fn()
         key, fl = flops_of(name, args)
+        by = bytes_of(name, args)
         if self.detail:
             key = f"{key} | {shape_of(name, args)}"
         e0 = torch.cuda.Event(enable_timing=True)
@@ -151,20 +221,24 @@ class Probe:
         e0.record()
         fn()
         e1.record()
-        self.records.append((key, fl, e0, e1))
+        self.records.append((key, fl, by, e0, e1))
 
-    def summary(self):
-        """{key: {launches, ms_total, ms_avg, tflops}} (call after synchronising)."""
+    def summary(self, peak_flops=PEAK_FLOPS, peak_bytes=PEAK_BYTES):
+        """{key: {launches, ms_total, ms_avg, tflops, flops, bytes, attainable_ms}} (call after
+        synchronising).  ``attainable_ms`` = sum over launches of max(FLOP / MFMA peak,
+        algorithmic bytes / HBM peak): the time each launch would take at its own roofline."""
         out = {}
-        for key, fl, e0, e1 in self.records:
+        for key, fl, by, e0, e1 in self.records:
             ms = e0.elapsed_time(e1)
-            d = out.setdefault(key, {"launches": 0, "ms_total": 0.0, "flops": 0.0})
+            d = out.setdefault(key, {"launches": 0, "ms_total": 0.0, "flops": 0.0,
+                                     "bytes": 0.0, "attainable_ms": 0.0})
             d["launches"] += 1
             d["ms_total"] += ms
             d["flops"] += fl
+            d["bytes"] += by
+            d["attainable_ms"] += max(fl / peak_flops, by / peak_bytes) * 1e3
         for d in out.values():
-            d["ms_avg"] = d["ms_total"] / max(1, d["launches"])
-            d["tflops"] = d["flops"] / (d["ms_total"] * 1e-3) / 1e12 if d["ms_total"] else 0.0
+            finish(d)
         return out
 
     def __enter__(self):
@@ -175,3 +249,14 @@ class Probe:
     def __exit__(self, *exc):
         self.active = False
         _lib.set_probe(None)
+
+
+def finish(d):
+    """Derived rates of a summary entry (after its sums changed)."""
+    d["ms_avg"] = d["ms_total"] / max(1, d["launches"])
+    t = d["ms_total"] * 1e-3
+    d["tflops"] = d["flops"] / t / 1e12 if t else 0.0
+    d["gbs"] = d["bytes"] / t / 1e9 if t else 0.0
+    d["intensity"] = d["flops"] / d["bytes"] if d["bytes"] else float("inf")
+    d["attainable_frac"] = d["attainable_ms"] / d["ms_total"] if d["ms_total"] else 0.0
+    return d

@@ -9,8 +9,11 @@ Differences from main.py, all forced by data parallelism or the MI355X optimizer
     main.py:19-21: the same is kept for the data-side RNGs);
   * the optimizer is ``FusedAdamW`` over the same two parameter groups (main.py:30-39) and the
     gradients are averaged in place on its arena by ``GradSync`` (retr_amd/ddp.py);
-  * epoch / validation losses are averaged over ranks; rank 0 prints and writes checkpoints
-    (train_utils/checkpoints.py format).
+  * the epoch loss is averaged over ranks; the validation loss is the reference's evaluate()
+    over the whole validation set (SequentialSampler, main.py:52) run on rank 0 and broadcast;
+    rank 0 prints and writes checkpoints (train_utils/checkpoints.py format);
+  * a non-finite loss on any rank stops every rank (engine.train_one_epoch agrees on it with
+    one all-reduce), so no rank is left waiting in a collective.
 The CIDEr evaluation (eval_model, nlgeval + BERT tokenizer) and early stopping stay with the
 caller: they need network-fetched assets outside the hot path.
 """
@@ -43,12 +46,24 @@ def build_loaders(config, dataset_train, dataset_val, rank, world):
     loader_train = DataLoader(dataset_train, batch_sampler=batch_sampler_train,
                               num_workers=config.num_workers)
     loader_val = None
-    if dataset_val is not None:
-        sampler_val = DistributedSampler(dataset_val, num_replicas=world, rank=rank,
-                                         shuffle=False, drop_last=False)
-        loader_val = DataLoader(dataset_val, config.batch_size, sampler=sampler_val,
+    if dataset_val is not None and rank == 0:
+        # the reference's own validation loader (main.py:52,61-62), on rank 0 only: a sharded
+        # DistributedSampler would pad the set with repeats and change the batch partition,
+        # so the rank-averaged loss would not be evaluate()'s value over the exact val set
+        loader_val = DataLoader(dataset_val, config.batch_size,
+                                sampler=torch.utils.data.SequentialSampler(dataset_val),
                                 drop_last=False, num_workers=config.num_workers)
     return loader_train, loader_val, sampler_train
+
+
+def _from_rank0(v, device, world):
+    """Rank 0's value on every rank (the validation loss is computed on rank 0 only)."""
+    if world == 1:
+        return v
+    t = torch.tensor([float("nan") if v is None else float(v)], dtype=torch.float64,
+                     device=device)
+    dist.broadcast(t, 0)
+    return t.item()
 
 
 def _mean_over_ranks(v, device, world):
@@ -107,9 +122,10 @@ def main(config, dataset_train, dataset_val=None, epochs=None, checkpoint_dir=No
         lr_scheduler.step()
         epoch_loss = _mean_over_ranks(epoch_loss, device, world)
         val_loss = None
-        if loader_val is not None:
-            val_loss = _mean_over_ranks(evaluate(model, criterion, loader_val, device), device,
-                                        world)
+        if dataset_val is not None:
+            if loader_val is not None:
+                val_loss = evaluate(model, criterion, loader_val, device)
+            val_loss = _from_rank0(val_loss, device, world)
         if rank == 0:
             print(f"Training Loss: {epoch_loss}")
             if val_loss is not None:

@@ -8,7 +8,9 @@
   (hipGraph replay == eager launches, == the full-recompute reference algorithm on the GPU
   wherever the recompute's top-2 logit margin is above bf16 rounding), and fp32 at batch 2
   bit-exact against the oracle's reference algorithm.
-cfg3 is cfg2 under data parallelism (tests/test_ddp_*.py); cfg1 is in test_gpu_model.py.
+* cfg4 per-GPU slice at full size (batch 8, 800x800, bf16): fwd + bwd vs the fp32 forward.
+cfg3 is cfg2 under data parallelism (tests/test_ddp_*.py, tests/test_gpu_ddp.py); cfg1 is in
+test_gpu_model.py.
 """
 import pytest
 import torch
@@ -153,3 +155,58 @@ def test_cfg5_greedy_fp32_batch2_bit_exact_vs_oracle():
         ids_o = orc.greedy(lambda c, m: orc.caption_forward(sd, cfg, images, mask, c, m), B, T,
                            101, 102)
     assert torch.equal(ids.cpu(), ids_o)
+
+
+def test_cfg4_bf16_full_slice_step():
+    """cfg4's per-GPU slice at full size (R101 6/6 d512 nhead 8, 800x800, batch 8, bf16):
+    forward + backward through the hd = 64 attention path at S = 625; loss within 1e-2 of the
+    fp32 model's (forward only, same weights and inputs), every gradient finite.
+    Reference shapes: models/backbone.py:86-91, models/ConcatTransformer.py:259-269."""
+    B = 8
+    images, mask = synthetic_images(B, 800, seed=11)
+    cfg, m16, crit, _ = _model(CFG4, "bf16")
+    caps, cap_mask = synthetic_captions(B, cfg.max_position_embeddings, cfg.vocab_size, seed=12)
+    samples = NestedTensor(images.to(DEV), mask.to(DEV))
+    m16.train()
+    out = m16(samples, caps[:, :-1].to(DEV), cap_mask[:, :-1].to(DEV))
+    assert out.shape == (B, 128, 30522)
+    loss16 = crit(out.permute(0, 2, 1), caps[:, 1:].to(DEV))
+    loss16.backward()
+    for n, p in m16.named_parameters():
+        if p.requires_grad:
+            assert p.grad is not None and torch.isfinite(p.grad).all(), n
+    del m16, out
+    torch.cuda.empty_cache()
+    _, m32, _, _ = _model(CFG4, "fp32")
+    m32.train()                      # dropout 0: train() only selects the training code path
+    with torch.no_grad():
+        out32 = m32(samples, caps[:, :-1].to(DEV), cap_mask[:, :-1].to(DEV))
+        loss32 = crit(out32.permute(0, 2, 1), caps[:, 1:].to(DEV))
+    l16, l32 = loss16.item(), loss32.item()
+    assert torch.isfinite(torch.tensor([l16, l32])).all()
+    assert abs(l16 - l32) <= 1e-2 * abs(l32), (l16, l32)
+
+
+def test_cfg5_greedy_fp32_batch64_graphs_eager_recompute_bitwise():
+    """Parity mode (fp32, exact-f32 MFMA) at the decode config's batch: hipGraph replay ==
+    eager launches == the reference's full-recompute algorithm (decode.py:53-81, 127 full
+    forwards) on the GPU, token for token.  (The B=2 test above pins the same ids to the CPU
+    oracle.)"""
+    cfg, model, _, _ = _model(CFG5, "fp32")
+    model.eval()
+    B, T = 64, cfg.max_position_embeddings
+    images, mask = synthetic_images(B, 224, seed=9, pad_band=True)
+    samples = [NestedTensor(images.to(DEV), mask.to(DEV))]
+    ids = greedy(samples, model, max_len=T, bos_token=101, eos_token=102)        # hipGraphs
+    ids_eager = IncrementalGreedy(model, use_graphs=False)(samples[0], T, 101, 102)
+    assert torch.equal(ids, ids_eager)
+    ids_full = greedy_reference_algorithm(samples, model, T, 101, 102)
+    diff = (ids != ids_full).any(1).nonzero().flatten().tolist()
+    if diff:
+        margins = _recompute_margins(model, samples, ids_full)
+        info = []
+        for b in diff:
+            j = int((ids[b] != ids_full[b]).nonzero()[0])
+            info.append((b, j, float(margins[b, j - 1])))
+        raise AssertionError(f"rows differing from the reference algorithm (row, first "
+                             f"column, top-2 margin there): {info}")

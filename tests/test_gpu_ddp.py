@@ -119,3 +119,61 @@ def test_train_dp_launcher(pg, tmp_path):
     ck = torch.load(tmp_path / f"{cfg.transformer_type}_{cfg.prefix}_checkpoint_1.pth",
                     map_location="cpu", weights_only=True)
     assert ck["epoch"] == 1 and "model_state_dict" in ck and "optimizer_state_dict" in ck
+
+
+def test_segmented_dp_step_cfg2_equals_single_graph_bitwise(pg):
+    """bench.py's N>1 objects at the full cfg2 shape (R50 6/6 d256, 640x640, batch 16, bf16,
+    dropout 0.1, FusedAdamW, GradSync with the bench's 64 MB buckets): the segmented capture
+    (forward/backward cut at bucket completions, each bucket's RCCL all-reduce enqueued
+    right after the segment it completed in) gives bitwise the same losses and weights as the
+    single-graph non-DP step (world 1: AVG over one rank is the identity).  Deterministic
+    reductions on both sides so the comparison can be bitwise."""
+    from bench import build, cfg2, make_optimizer
+    from retr_amd import ops
+    from retr_amd.ddp import GradSync
+    from retr_amd.engine import GraphedTrainStep
+    from retr_amd.synthetic import synthetic_captions, synthetic_images
+    cfg = cfg2()
+    cfg.deterministic = True
+    try:
+        m1, crit = build(cfg, DEV)
+        m2, _ = build(cfg, DEV)
+        o1 = make_optimizer(m1, cfg, capturable=True, fused=True)
+        o2 = make_optimizer(m2, cfg, capturable=True, fused=True)
+        gs = GradSync([p for p in m1.parameters() if p.requires_grad],
+                      bucket_mb=cfg.grad_bucket_mb, optimizer=o1)
+        s1 = GraphedTrainStep(m1, crit, o1, cfg.clip_max_norm, gs)
+        s2 = GraphedTrainStep(m2, crit, o2, cfg.clip_max_norm)
+        img, mask = synthetic_images(16, 640, seed=1000)
+        caps, cm = synthetic_captions(16, cfg.max_position_embeddings, cfg.vocab_size, seed=2000)
+        samples = (NestedTensor(img.to(DEV), mask.to(DEV)),)
+        caps, cm = caps.to(DEV), cm.to(DEV)
+        m1.train()
+        m2.train()
+        for _ in range(3):
+            # the same dropout streams on both sides: device step seed and host per-op counter
+            seed, ctr = ops.seed_base().clone(), ops._seed_state["ctr"]
+            l1 = s1(samples, caps, cm).clone()
+            ops.seed_base().copy_(seed)
+            ops._seed_state["ctr"] = ctr
+            l2 = s2(samples, caps, cm).clone()
+            torch.cuda.synchronize()
+            assert torch.isfinite(l1).all()
+            assert torch.equal(l1, l2), (l1.item(), l2.item())
+        assert torch.equal(o1.P, o2.P)
+        assert torch.equal(o1.M, o2.M) and torch.equal(o1.V, o2.V)
+        # the schedule: several segments, every bucket all-reduced exactly once, each right
+        # after the segment it completed in and before the next segment's replay
+        nb = len(gs.buckets)
+        assert nb >= 3 and len(s1.segments) >= 2
+        seen = [b for kind, b in s1.order if kind == "allreduce"]
+        assert sorted(seen) == list(range(nb)), s1.order
+        for i, (kind, v) in enumerate(s1.order):
+            if kind == "allreduce":
+                k = max(j for j in range(i) if s1.order[j][0] == "segment")
+                assert v in s1.after[s1.order[k][1]]
+        # overlap exists: at least one all-reduce is enqueued before the last segment's replay
+        last = max(i for i, (kind, _) in enumerate(s1.order) if kind == "segment")
+        assert any(kind == "allreduce" for kind, _ in s1.order[:last]), s1.order
+    finally:
+        ops.set_deterministic(False)
