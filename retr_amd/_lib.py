@@ -10,6 +10,9 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libretr_hip.so")
+# A/B measurements only (tools/*_micro.py): time a baseline build of the same C-ABI
+if os.environ.get("RETR_AB_LIB"):
+    LIB_PATH = os.environ["RETR_AB_LIB"]
 
 F32, BF16 = 0, 1
 

@@ -66,6 +66,31 @@ RETR_DEVICE BlockXYZ xcd_block() {
   return r;
 }
 
+// Key-padding / causal masking of one 64-key score tile without per-element branches (the
+// short-circuit form compiled to an exec-mask branch per score: ~70 s_and_saveexec per tile).
+// Score element e of sub-tile sub holds key key0 + kc + 4 hh, kc = sub*32 + (e&3) + 8*(e>>2)
+// (a compile-time constant); the ballot is shifted once to this lane's key phase and tested at
+// constant bit positions; the causal test is one compare against lim = qi - key0 - 4 hh.
+template <int E>
+RETR_DEVICE constexpr int tile_kc(int sub) { return sub * 32 + (E & 3) + 8 * (E >> 2); }
+
+RETR_DEVICE bool key_masked(uint32_t lo, uint32_t hi, int kc, bool diag, int lim) {
+  const uint32_t bit = (kc < 32 ? (lo >> kc) : (hi >> (kc - 32))) & 1u;
+  return (bit != 0u) | (diag & (kc > lim));
+}
+
+RETR_DEVICE void mask_tile(f32x16 (&S)[2], unsigned long long pmask, bool diag, int lim, int hh) {
+  const unsigned long long pm = pmask >> (4 * hh);
+  const uint32_t lo = (uint32_t)pm, hi = (uint32_t)(pm >> 32);
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int kc = sub * 32 + (e & 3) + 8 * (e >> 2);
+      S[sub][e] = key_masked(lo, hi, kc, diag, lim) ? -INFINITY : S[sub][e];
+    }
+}
+
 template <int HD>
 struct Tile {
   static constexpr int KT = 64;              // keys per LDS stage
@@ -182,15 +207,7 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
         S[sub] = mfma32(a, qf[s], S[sub]);
       }
     }
-    if (pmask || diag) {
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int kl = sub * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if (((pmask >> kl) & 1ull) || (diag && key0 + kl > qi)) S[sub][e] = -INFINITY;
-        }
-    }
+    if (pmask || diag) mask_tile(S, pmask, diag, qi - key0 - 4 * hh, hh);
     // online softmax (log2 domain)
     float mt = -INFINITY;
 #pragma unroll
@@ -414,15 +431,7 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
         S[sub] = mfma32(a, qf[s], S[sub]);
       }
     }
-    if (pmask || diag) {
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int kl = sub * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-          if (((pmask >> kl) & 1ull) || (diag && key0 + kl > qi)) S[sub][e] = -INFINITY;
-        }
-    }
+    if (pmask || diag) mask_tile(S, pmask, diag, qi - key0 - 4 * hh, hh);
     float mt = -INFINITY;
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
@@ -588,6 +597,9 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
     const unsigned long long pmask = pm[t];
     const bool diag = causal && (key0 + 63 > q0);
     const bool anym = pmask != 0ull || diag;      // wave-uniform: masking needed on this tile
+    const unsigned long long pml = pmask >> (4 * hh);
+    const uint32_t pmlo = (uint32_t)pml, pmhi = (uint32_t)(pml >> 32);
+    const int mlim = qi - key0 - 4 * hh;
     bf16x8 sf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -611,7 +623,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
-          const bool msk = anym && (((pmask >> kl) & 1ull) || (diag && key0 + kl > qi));
+          const bool msk = anym & key_masked(pmlo, pmhi, kl - 4 * hh, diag, mlim);
           const float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - lq2);
           float dpv = P[e];
           if (drop) dpv = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? dpv * dp.scale : 0.f;
@@ -1014,6 +1026,9 @@ attn_bwd_dq2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
     const unsigned long long pmask = __ballot(pad);
     const bool diag = causal && (key0 + TL::KT - 1 > q0);
     const bool anym = pmask != 0ull || diag;      // wave-uniform: masking needed on this tile
+    const unsigned long long pml = pmask >> (4 * hh);
+    const uint32_t pmlo = (uint32_t)pml, pmhi = (uint32_t)(pml >> 32);
+    const int mlim = qi - key0 - 4 * hh;
     bf16x8 sf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -1037,7 +1052,7 @@ attn_bwd_dq2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
-          const bool msk = anym && (((pmask >> kl) & 1ull) || (diag && key0 + kl > qi));
+          const bool msk = anym & key_masked(pmlo, pmhi, kl - 4 * hh, diag, mlim);
           const float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - lq2);
           float dpv = P[e];
           if (drop) dpv = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? dpv * dp.scale : 0.f;

@@ -79,6 +79,72 @@ struct ConvFwdA {  // A(m = n,oh,ow ; k = kh,kw,ci)
   }
 };
 
+// ConvFwdA for C % 64 == 0 (every conv but the stem): a 64-deep K step never leaves one
+// (kh, kw) tap, so the K cursor is wave-uniform (kUniformK: SGPRs) and the address of a chunk is
+// the row's pixel pointer at tap (0, 0) plus the cursor's tap offset; the padding test is one
+// bit of a per-row mask of in-bounds taps (built once).  No 64-bit multiplies, divisions or
+// branches per DMA (ConvFwdA: ~25 vector instructions per chunk, this: ~6).
+template <typename T>
+struct ConvFwdAU {  // A(m = n,oh,ow ; k = kh,kw,ci)
+  static constexpr bool kContig = true;
+  static constexpr bool kUniformK = true;
+  const T* x;
+  Geom g;
+  int M, K;
+  struct Ctx { const T* base; unsigned mask; };
+  struct KCur { int c0, t, kh, kw, off; };     // off = (kh d W + kw d) C + c0 (elements)
+  RETR_DEVICE Ctx row_ctx_c(int r, int coff) const {
+    Ctx c;
+    const bool ok = r < M;
+    const int rr = ok ? r : 0;
+    const int hw = g.OH * g.OW;
+    const int n = rr / hw, rem = rr - n * hw;
+    const int oh = rem / g.OW, ow = rem - oh * g.OW;
+    const int ihb = oh * g.s - g.p, iwb = ow * g.s - g.p;
+    c.base = x + (((long)n * g.H + ihb) * g.W + iwb) * g.C + coff;
+    unsigned m = 0;
+    if (ok) {
+      for (int kh = 0; kh < g.KH; ++kh)
+        for (int kw = 0; kw < g.KW; ++kw)
+          if ((unsigned)(ihb + kh * g.d) < (unsigned)g.H &&
+              (unsigned)(iwb + kw * g.d) < (unsigned)g.W)
+            m |= 1u << (kh * g.KW + kw);
+    }
+    c.mask = m;
+    return c;
+  }
+  RETR_DEVICE Ctx row_ctx(int r) const { return row_ctx_c(r, 0); }
+  RETR_DEVICE void set_off(KCur& t) const { t.off = (t.kh * g.d * g.W + t.kw * g.d) * g.C + t.c0; }
+  RETR_DEVICE KCur kcur(int k) const {
+    KCur t;
+    t.t = k / g.C;
+    t.c0 = k - t.t * g.C;
+    t.kh = t.t / g.KW;
+    t.kw = t.t - t.kh * g.KW;
+    set_off(t);
+    return t;
+  }
+  RETR_DEVICE void advance(KCur& t, int d) const {
+    t.c0 += d;
+    if (t.c0 >= g.C) {                 // d <= 64 <= C: at most one tap per step
+      t.c0 -= g.C;
+      ++t.t;
+      if (++t.kw == g.KW) {
+        t.kw = 0;
+        ++t.kh;
+      }
+    }
+    set_off(t);
+  }
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& t) const {
+    if (!((c.mask >> t.t) & 1u)) return nullptr;   // padding, rows >= M, taps past K
+    return c.base + t.off;
+  }
+  RETR_DEVICE const void* addr_or(const Ctx& c, const KCur& t, const void* fb) const {
+    return ((c.mask >> t.t) & 1u) ? (const void*)(c.base + t.off) : fb;
+  }
+};
+
 template <typename T>
 struct ConvDgradA {  // A(m = n,ih,iw ; k = kh,kw,co) = G[n, (ih+p-kh d)/s, (iw+p-kw d)/s, co]
   static constexpr bool kContig = true;
@@ -113,6 +179,72 @@ struct ConvDgradA {  // A(m = n,ih,iw ; k = kh,kw,co) = G[n, (ih+p-kh d)/s, (iw+
     }
     if (oh >= g.OH || ow >= g.OW) return nullptr;
     return c.img + ((long)oh * g.OW + ow) * g.Co + t.c;
+  }
+};
+
+// ConvDgradA for stride 1 with Co % 64 == 0: as ConvFwdAU, the tap of a 64-deep K step is
+// wave-uniform; chunk address = the pixel pointer of G at (ih + p, iw + p) minus the tap offset
+// (kh d OW + kw d) Co, padding test = one bit of the row's in-bounds-tap mask.
+template <typename T>
+struct ConvDgradAU {  // A(m = n,ih,iw ; k = kh,kw,co) = G[n, ih+p-kh d, iw+p-kw d, co]
+  static constexpr bool kContig = true;
+  static constexpr bool kUniformK = true;
+  const T* gr;
+  Geom g;
+  int M, K;
+  struct Ctx { const T* base; unsigned mask; };
+  struct KCur { int c0, t, kh, kw, off; };     // off = c0 - (kh d OW + kw d) Co
+  RETR_DEVICE Ctx row_ctx_c(int r, int coff) const {
+    Ctx c;
+    const bool ok = r < M;
+    const int rr = ok ? r : 0;
+    const int hw = g.H * g.W;
+    const int n = rr / hw, rem = rr - n * hw;
+    const int ih = rem / g.W, iw = rem - ih * g.W;
+    const int ihp = ih + g.p, iwp = iw + g.p;
+    c.base = gr + (((long)n * g.OH + ihp) * g.OW + iwp) * g.Co + coff;
+    unsigned m = 0;
+    if (ok) {
+      for (int kh = 0; kh < g.KH; ++kh)
+        for (int kw = 0; kw < g.KW; ++kw)
+          if ((unsigned)(ihp - kh * g.d) < (unsigned)g.OH &&
+              (unsigned)(iwp - kw * g.d) < (unsigned)g.OW)
+            m |= 1u << (kh * g.KW + kw);
+    }
+    c.mask = m;
+    return c;
+  }
+  RETR_DEVICE Ctx row_ctx(int r) const { return row_ctx_c(r, 0); }
+  RETR_DEVICE void set_off(KCur& t) const {
+    t.off = t.c0 - (t.kh * g.d * g.OW + t.kw * g.d) * g.Co;
+  }
+  RETR_DEVICE KCur kcur(int k) const {
+    KCur t;
+    t.t = k / g.Co;
+    t.c0 = k - t.t * g.Co;
+    t.kh = t.t / g.KW;
+    t.kw = t.t - t.kh * g.KW;
+    set_off(t);
+    return t;
+  }
+  RETR_DEVICE void advance(KCur& t, int d) const {
+    t.c0 += d;
+    if (t.c0 >= g.Co) {
+      t.c0 -= g.Co;
+      ++t.t;
+      if (++t.kw == g.KW) {
+        t.kw = 0;
+        ++t.kh;
+      }
+    }
+    set_off(t);
+  }
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& t) const {
+    if (!((c.mask >> t.t) & 1u)) return nullptr;
+    return c.base + t.off;
+  }
+  RETR_DEVICE const void* addr_or(const Ctx& c, const KCur& t, const void* fb) const {
+    return ((c.mask >> t.t) & 1u) ? (const void*)(c.base + t.off) : fb;
   }
 };
 
@@ -237,6 +369,117 @@ struct ConvDgradPhaseA {  // A(m = n,i',j' ; k = ti,tj,co) = G[n, i' + ch(ti), j
     const int ow = c.j + ((ph.iw0 + g.p - ph.b) >> 1) - t.tj;
     if ((unsigned)oh >= (unsigned)g.OH || (unsigned)ow >= (unsigned)g.OW) return nullptr;
     return c.img + ((long)oh * g.OW + ow) * g.Co + t.c;
+  }
+};
+
+// Uniform-K versions of the two phase loaders (Co % 64 == 0): tap (ti, tj) and channel base
+// in SGPRs; A's chunk = the row's G pointer at (i + ch0, j + cw0) minus (ti OW + tj) Co, with a
+// per-row mask of in-bounds taps (nkh * nkw <= 32).
+template <typename T>
+struct ConvDgradPhaseAU {
+  static constexpr bool kContig = true;
+  static constexpr bool kUniformK = true;
+  const T* gr;
+  Geom g;
+  Phase ph;
+  int M, K;
+  struct Ctx { const T* base; unsigned mask; };
+  struct KCur { int c0, t, ti, tj, off; };
+  RETR_DEVICE Ctx row_ctx_c(int r, int coff) const {
+    Ctx c;
+    const bool ok = r < M;
+    const int rr = ok ? r : 0;
+    const int hw = ph.Hp * ph.Wp;
+    const int n = rr / hw, rem = rr - n * hw;
+    const int i = rem / ph.Wp, j = rem - i * ph.Wp;
+    const int oh0 = i + ((ph.ih0 + g.p - ph.a) >> 1), ow0 = j + ((ph.iw0 + g.p - ph.b) >> 1);
+    c.base = gr + (((long)n * g.OH + oh0) * g.OW + ow0) * g.Co + coff;
+    unsigned m = 0;
+    if (ok) {
+      for (int ti = 0; ti < ph.nkh; ++ti)
+        for (int tj = 0; tj < ph.nkw; ++tj)
+          if ((unsigned)(oh0 - ti) < (unsigned)g.OH && (unsigned)(ow0 - tj) < (unsigned)g.OW)
+            m |= 1u << (ti * ph.nkw + tj);
+    }
+    c.mask = m;
+    return c;
+  }
+  RETR_DEVICE Ctx row_ctx(int r) const { return row_ctx_c(r, 0); }
+  RETR_DEVICE void set_off(KCur& t) const { t.off = t.c0 - (t.ti * g.OW + t.tj) * g.Co; }
+  RETR_DEVICE KCur kcur(int k) const {
+    KCur t;
+    t.t = k / g.Co;
+    t.c0 = k - t.t * g.Co;
+    t.ti = t.t / ph.nkw;
+    t.tj = t.t - t.ti * ph.nkw;
+    set_off(t);
+    return t;
+  }
+  RETR_DEVICE void advance(KCur& t, int d) const {
+    t.c0 += d;
+    if (t.c0 >= g.Co) {
+      t.c0 -= g.Co;
+      ++t.t;
+      if (++t.tj == ph.nkw) {
+        t.tj = 0;
+        ++t.ti;
+      }
+    }
+    set_off(t);
+  }
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& t) const {
+    if (!((c.mask >> t.t) & 1u)) return nullptr;
+    return c.base + t.off;
+  }
+  RETR_DEVICE const void* addr_or(const Ctx& c, const KCur& t, const void* fb) const {
+    return ((c.mask >> t.t) & 1u) ? (const void*)(c.base + t.off) : fb;
+  }
+};
+
+template <typename T>
+struct DgradPhaseWU {  // B(row = ci ; k = ti,tj,co) = Wt[ci][a + 2ti][b + 2tj][co]
+  static constexpr bool kContig = true;
+  static constexpr bool kUniformK = true;
+  const T* wt;
+  Geom g;
+  Phase ph;
+  int rows, K;
+  struct Ctx { const T* row; int klim; };
+  struct KCur { int k, c0, ti, tj, off; };
+  RETR_DEVICE Ctx row_ctx_c(int r, int coff) const {
+    return Ctx{wt + (long)(r < rows ? r : 0) * g.KH * g.KW * g.Co + coff, r < rows ? K : 0};
+  }
+  RETR_DEVICE Ctx row_ctx(int r) const { return row_ctx_c(r, 0); }
+  RETR_DEVICE void set_off(KCur& t) const {
+    t.off = ((ph.a + 2 * t.ti) * g.KW + ph.b + 2 * t.tj) * g.Co + t.c0;
+  }
+  RETR_DEVICE KCur kcur(int k) const {
+    KCur t;
+    t.k = k;
+    const int tap = k / g.Co;
+    t.c0 = k - tap * g.Co;
+    t.ti = tap / ph.nkw;
+    t.tj = tap - t.ti * ph.nkw;
+    set_off(t);
+    return t;
+  }
+  RETR_DEVICE void advance(KCur& t, int d) const {
+    t.k += d;
+    t.c0 += d;
+    if (t.c0 >= g.Co) {
+      t.c0 -= g.Co;
+      if (++t.tj == ph.nkw) {
+        t.tj = 0;
+        ++t.ti;
+      }
+    }
+    set_off(t);
+  }
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& t) const {
+    return t.k < c.klim ? (const void*)(c.row + t.off) : nullptr;
+  }
+  RETR_DEVICE const void* addr_or(const Ctx& c, const KCur& t, const void* fb) const {
+    return t.k < c.klim ? (const void*)(c.row + t.off) : fb;
   }
 };
 
@@ -417,6 +660,11 @@ int conv_fwd_t(const void* x, Geom g, const void* w, const float* bias, const vo
     return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd_1x1", true,
                                        res != nullptr && K <= 64);
   }
+  // (1x1 strided convs keep ConvFwdA: a single tap gains nothing and measured slower)
+  if (sizeof(T) == 2 && g.C % 64 == 0 && g.KH * g.KW > 1 && g.KH * g.KW <= 32) {
+    ConvFwdAU<T> la{(const T*)x, g, M, K};
+    return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd");
+  }
   ConvFwdA<T> la{(const T*)x, g, M, K};
   return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd");
 }
@@ -496,13 +744,24 @@ int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* a
         const int Mp = g.Nb * ph.Hp * ph.Wp, Kp = ph.nkh * ph.nkw * g.Co;
         if (Mp == 0) continue;
         if (Kp == 0 && (zmask >> (ph.ih0 * 2 + ph.iw0) & 1)) continue;
+        EpiPhaseRows<EpiDgrad<T, T, T>> pe{ep, ph.Hp, ph.Wp, g.H, g.W, ph.ih0, ph.iw0};
+        if (sizeof(T) == 2 && g.Co % 64 == 0 && ph.nkh * ph.nkw <= 32) {
+          ConvDgradPhaseAU<T> pa{(const T*)dy, g, ph, Mp, Kp};
+          DgradPhaseWU<T> pb{(const T*)wt, g, ph, N, Kp};
+          if (int e = launch_auto<kFamConvDgrad, T>(pa, pb, pe, Mp, N, Kp, 1, st, "conv_dgrad_s2"))
+            return e;
+          continue;
+        }
         ConvDgradPhaseA<T> pa{(const T*)dy, g, ph, Mp, Kp};
         DgradPhaseW<T> pb{(const T*)wt, g, ph, N, Kp};
-        EpiPhaseRows<EpiDgrad<T, T, T>> pe{ep, ph.Hp, ph.Wp, g.H, g.W, ph.ih0, ph.iw0};
         if (int e = launch_auto<kFamConvDgrad, T>(pa, pb, pe, Mp, N, Kp, 1, st, "conv_dgrad_s2"))
           return e;
       }
     return 0;
+  }
+  if (sizeof(T) == 2 && g.s == 1 && g.Co % 64 == 0 && g.KH * g.KW <= 32) {
+    ConvDgradAU<T> la{(const T*)dy, g, M, K};
+    return launch_auto<kFamConvDgrad, T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad");
   }
   ConvDgradA<T> la{(const T*)dy, g, M, K};
   return launch_auto<kFamConvDgrad, T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad");

@@ -381,21 +381,29 @@ static inline int pick_splits(int M, int N, int K, int BM, int BN, int BK, int m
 // ----------------------------------------------------------------------------------------------
 
 // Row-major [rows][ld] operand, K contiguous (activations X[M][K], weights W[N][K]).
+// kUniformK (gemm2.hpp GStager): the K cursor is the block's (wave-uniform, SGPRs); the
+// thread's chunk offset lives in the row context (row pointer and remaining-K limit).
 template <typename T>
 struct DenseK {
   static constexpr bool kContig = true;
+  static constexpr bool kUniformK = true;
   static constexpr int EPC = Elem<T>::EPC;
   const T* p;
   long ld;
   int rows, K;
-  struct Ctx { const T* row; bool ok; };
+  struct Ctx { const T* row; int klim; };     // klim = K - chunk offset (0: row out of range)
   struct KCur { int k; };
-  RETR_DEVICE Ctx row_ctx(int r) const { return Ctx{p + (long)r * ld, r < rows}; }
+  RETR_DEVICE Ctx row_ctx_c(int r, int coff) const {
+    return Ctx{p + (long)r * ld + coff, r < rows ? K - coff : 0};
+  }
+  RETR_DEVICE Ctx row_ctx(int r) const { return row_ctx_c(r, 0); }
   RETR_DEVICE KCur kcur(int k) const { return KCur{k}; }
   RETR_DEVICE void advance(KCur& c, int d) const { c.k += d; }
   RETR_DEVICE const void* addr(const Ctx& c, const KCur& k) const {
-    if (!c.ok || k.k >= K) return nullptr;
-    return c.row + k.k;
+    return k.k < c.klim ? (const void*)(c.row + k.k) : nullptr;
+  }
+  RETR_DEVICE const void* addr_or(const Ctx& c, const KCur& k, const void* fb) const {
+    return k.k < c.klim ? (const void*)(c.row + k.k) : fb;
   }
 };
 
@@ -437,21 +445,29 @@ struct DenseK2 {
 
 // Operand stored [k][ld] (rows contiguous): element (r, k) = p[k*ld + r]; chunks along rows.
 // Requires rows % EPC == 0 or zero-padding beyond `rows` inside the chunk's row range.
+// kUniformK (gemm2.hpp GStager): the thread's k-row offset is baked into each row context
+// (pointer and remaining-K limit), the block cursor (k, k*ld) stays wave-uniform.
 template <typename T>
 struct DenseT {
   static constexpr bool kContig = false;
+  static constexpr bool kUniformK = true;
   static constexpr int EPC = Elem<T>::EPC;
   const T* p;
   long ld;
   int rows, K;
-  struct Ctx { const T* col; bool ok; };
+  struct Ctx { const T* col; int klim; };
   struct KCur { int k; long off; };
-  RETR_DEVICE Ctx row_ctx(int r) const { return Ctx{p + r, r < rows}; }
+  RETR_DEVICE Ctx row_ctx_c(int r, int koff) const {
+    return Ctx{p + r + (long)koff * ld, r < rows ? K - koff : 0};
+  }
+  RETR_DEVICE Ctx row_ctx(int r) const { return row_ctx_c(r, 0); }
   RETR_DEVICE KCur kcur(int k) const { return KCur{k, (long)k * ld}; }
   RETR_DEVICE void advance(KCur& c, int d) const { c.k += d; c.off += (long)d * ld; }
   RETR_DEVICE const void* addr(const Ctx& c, const KCur& k) const {
-    if (!c.ok || k.k >= K) return nullptr;
-    return c.col + k.off;
+    return k.k < c.klim ? (const void*)(c.col + k.off) : nullptr;
+  }
+  RETR_DEVICE const void* addr_or(const Ctx& c, const KCur& k, const void* fb) const {
+    return k.k < c.klim ? (const void*)(c.col + k.off) : fb;
   }
 };
 

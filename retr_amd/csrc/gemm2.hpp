@@ -43,6 +43,34 @@ RETR_DEVICE void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Loaders with kUniformK = true keep the K cursor wave-uniform (it only depends on the block's
+// K range, so the compiler holds it in SGPRs): the per-thread 16-byte chunk offset goes into
+// the row context instead (row_ctx_c(r, coff)), and kcur(kb) takes the block's K start.
+template <class L, class = void>
+struct uniform_k : std::false_type {};
+template <class L>
+struct uniform_k<L, std::void_t<decltype(L::kUniformK)>> : std::integral_constant<bool, L::kUniformK> {};
+
+// Loaders with addr_or(ctx, cursor, fallback) return `fallback` (the zero page) themselves for
+// a chunk outside the operand: one select instead of a null result re-tested by the stager.
+template <class L, class = void>
+struct has_addr_or : std::false_type {};
+template <class L>
+struct has_addr_or<L, std::void_t<decltype(std::declval<const L&>().addr_or(
+                          std::declval<const typename L::Ctx&>(),
+                          std::declval<const typename L::KCur&>(), (const void*)nullptr))>>
+    : std::true_type {};
+
+template <class L>
+RETR_DEVICE const void* chunk_src(const L& l, const typename L::Ctx& c, const typename L::KCur& k) {
+  if constexpr (has_addr_or<L>::value) {
+    return l.addr_or(c, k, (const void*)g_zero_page);
+  } else {
+    const void* p = l.addr(c, k);
+    return p ? p : (const void*)g_zero_page;
+  }
+}
+
 // LDS-DMA stager of one ROWS x BK operand tile (bf16) for an NT-thread block.
 template <int ROWS, int NT, class L>
 struct GStager {
@@ -52,16 +80,23 @@ struct GStager {
   static_assert(NCH >= 1 && (ROWS * 8) % NT == 0, "tile too small for the block");
   static_assert(L::kContig || ((8 * NT / ROWS) % 16 == 0 && NT % CPR == 0),
                 "k-major image: thread's k rows must share one swizzle phase");
-  typename L::Ctx ctx[L::kContig ? NCH : 1];
-  typename L::KCur kc[L::kContig ? 1 : NCH];
+  static constexpr bool kU = uniform_k<L>::value;
+  typename L::Ctx ctx[(L::kContig || kU) ? NCH : 1];
+  typename L::KCur kc[(L::kContig || kU) ? 1 : NCH];
 
   RETR_DEVICE void init(const L& l, int row0, int tid, int kb) {
     if constexpr (L::kContig) {
       // linear slot (row r = tid/8 + (NT/8) i, slot tid%8) holds chunk slot ^ ((r>>1)&7)
       const int c = (tid & 7) ^ ((tid >> 4) & 7);
+      if constexpr (uniform_k<L>::value) {
 #pragma unroll
-      for (int i = 0; i < NCH; ++i) ctx[i] = l.row_ctx(row0 + (tid >> 3) + (NT / 8) * i);
-      kc[0] = l.kcur(kb + c * EPC);
+        for (int i = 0; i < NCH; ++i) ctx[i] = l.row_ctx_c(row0 + (tid >> 3) + (NT / 8) * i, c * EPC);
+        kc[0] = l.kcur(kb);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) ctx[i] = l.row_ctx(row0 + (tid >> 3) + (NT / 8) * i);
+        kc[0] = l.kcur(kb + c * EPC);
+      }
     } else {
       // linear slot (k = tid/CPR + (NT/CPR) i, slot tid%CPR) holds row-chunk slot ^ (f(k)/2)
       const int k0 = tid / CPR, slot = tid % CPR;
@@ -69,20 +104,27 @@ struct GStager {
       if constexpr (ROWS >= 128) f = 4 * ((k0 & 3) | (((k0 >> 3) & 1) << 2));
       else f = 4 * (((k0 >> 1) & 1) | (((k0 >> 3) & 1) << 1));
       const int c = slot ^ (f >> 1);
-      ctx[0] = l.row_ctx(row0 + c * EPC);
+      if constexpr (uniform_k<L>::value) {
+        // one row context per k row of the thread (its k offset baked in), one block cursor
 #pragma unroll
-      for (int i = 0; i < NCH; ++i) kc[i] = l.kcur(kb + k0 + (NT / CPR) * i);
+        for (int i = 0; i < NCH; ++i) ctx[i] = l.row_ctx_c(row0 + c * EPC, k0 + (NT / CPR) * i);
+        kc[0] = l.kcur(kb);
+      } else {
+        ctx[0] = l.row_ctx(row0 + c * EPC);
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) kc[i] = l.kcur(kb + k0 + (NT / CPR) * i);
+      }
     }
   }
   // issue the tile at the cursors into the image at `lds`, then advance the cursors
   RETR_DEVICE void issue(const L& l, char* lds, int wave) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const void* p = L::kContig ? l.addr(ctx[i], kc[0]) : l.addr(ctx[0], kc[i]);
-      glds16(p ? p : (const void*)g_zero_page, lds + (NT * i + wave * 64) * 16);
-      if constexpr (!L::kContig) l.advance(kc[i], BK);
+      const void* p = (L::kContig || kU) ? chunk_src(l, ctx[i], kc[0]) : chunk_src(l, ctx[0], kc[i]);
+      glds16(p, lds + (NT * i + wave * 64) * 16);
+      if constexpr (!L::kContig && !kU) l.advance(kc[i], BK);
     }
-    if constexpr (L::kContig) l.advance(kc[0], BK);
+    if constexpr (L::kContig || kU) l.advance(kc[0], BK);
   }
 };
 
@@ -138,7 +180,11 @@ RETR_DEVICE __attribute__((always_inline)) void gemm2_tile(const LA& la, const L
   constexpr int LPT = SA::NCH + SB::NCH;        // DMA instructions per wave per tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the wave id through readfirstlane: the compiler then knows every LDS-DMA destination
+  // (wave-uniform base, M0) is uniform and sets M0 from an SGPR instead of one
+  // v_readfirstlane per DMA instruction
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
   const int kb = split * kchunk;
