@@ -640,6 +640,10 @@ int launch_wgrad(const LA& la, const LB& lb, float* ws, long ldws, int R, int Nc
   ep.split_stride = s > 1 ? (long)R * ldws : 0;
   ep.set_vec();
   if constexpr (sizeof(T) == 2) {
+    // 8 waves (4 x 2) for the 3x3 / strided weight gradients, 4 waves (2 x 2) for the dense
+    // 1x1 ones with long split-K plans (tools/conv_micro.py wtile, profiles/r3_gemm_depth.txt)
+    if (p.tile == 128 && !dense1x1)
+      return launch_gemm2<FAM, 128, 128, 4, 2, 2>(la, lb, ep, R, Ncols, Mp, s, st, what);
     if (p.tile == 128) return launch_gemm2<FAM, 128, 128, 2, 2, 2>(la, lb, ep, R, Ncols, Mp, s, st, what);
     if (p.tile == 65) return launch_gemm2<FAM, 64, 64, 2, 2, 2>(la, lb, ep, R, Ncols, Mp, s, st, what);
   } else {

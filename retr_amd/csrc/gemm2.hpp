@@ -523,8 +523,11 @@ int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, in
     return launch_gemm2<FAM, 128, 128, 2, 2, 1, 2>(la, lb, ep, M, N, K, splits, st, what);
   if (N >= 4096 && t256 >= 256)
     return launch_gemm2<FAM, 256, 256, 2, 4, 2>(la, lb, ep, M, N, K, splits, st, what);
+  // 128x128 over 8 waves (4 x 2, 32x64 per wave), two blocks per CU: 4 waves per SIMD hide the
+  // per-K-step load latency better than 4 waves of 64x64 (tools/gemm_tune deep,
+  // profiles/r3_gemm_depth.txt: conv-shaped GEMMs 3-8 % faster; deeper rings at 1 block/CU lose)
   if (N > 64 && t128 >= 160)
-    return launch_gemm2<FAM, 128, 128, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
+    return launch_gemm2<FAM, 128, 128, 4, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
   if (N <= 64 && t12864 >= 160)
     return launch_gemm2<FAM, 64, 64, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
   return launch_gemm<FAM, bf16, 64, 64>(la, lb, ep, M, N, K, splits, st, what);

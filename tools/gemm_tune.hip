@@ -35,6 +35,7 @@ __global__ void fill_kernel(bf16* p, long n, unsigned seed) {
 struct Shape { int M, N, K; bool trans; const char* what; };
 
 int main(int argc, char** argv) {
+  const bool deep = argc > 1 && std::string(argv[1]) == "deep";
   std::vector<Shape> shapes = {
       {4096, 4096, 4096, false, "dense 4k"},
       {25600, 256, 2304, false, "conv3x3 40x40 256"},
@@ -69,6 +70,7 @@ int main(int argc, char** argv) {
   CHK(hipEventCreate(&e1));
 
   for (auto& s : shapes) {
+    if (deep && s.trans) continue;
     const int M = s.M, N = s.N, K = s.K;
     const double flop = 2.0 * M * N * K;
     std::vector<std::pair<std::string, std::function<int(float*)>>> vars;
@@ -82,6 +84,18 @@ int main(int argc, char** argv) {
       vars.push_back({"g128x128s2e2", [=](float* o) { return launch_gemm2<0, 128, 128, 2, 2, 2, 2>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
       vars.push_back({"g256x256s2", [=](float* o) { return launch_gemm2<0, 256, 256, 2, 4, 2>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
       vars.push_back({"g128x64s3", [=](float* o) { return launch_gemm2<0, 128, 64, 2, 2, 3>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
+      if (deep) {
+        // pipeline depth vs blocks per CU (tiles in flight per CU = blocks x (S - 1))
+        vars.push_back({"g128x128s3", [=](float* o) { return launch_gemm2<0, 128, 128, 2, 2, 3>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
+        vars.push_back({"g128x128s4", [=](float* o) { return launch_gemm2<0, 128, 128, 2, 2, 4>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
+        vars.push_back({"g128x128w8s2", [=](float* o) { return launch_gemm2<0, 128, 128, 4, 2, 2>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
+        vars.push_back({"g128x128w8s3", [=](float* o) { return launch_gemm2<0, 128, 128, 4, 2, 3>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
+        vars.push_back({"g128x128w8s4", [=](float* o) { return launch_gemm2<0, 128, 128, 4, 2, 4>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
+        vars.push_back({"g256x128w8s2", [=](float* o) { return launch_gemm2<0, 256, 128, 4, 2, 2>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
+        vars.push_back({"g256x128w8s3", [=](float* o) { return launch_gemm2<0, 256, 128, 4, 2, 3>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
+        vars.push_back({"g128x256w8s3", [=](float* o) { return launch_gemm2<0, 128, 256, 2, 4, 3>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
+        vars.push_back({"g64x128s4", [=](float* o) { return launch_gemm2<0, 64, 128, 2, 2, 4>(la, lb, ep(o), M, N, K, 1, 0, "v"); }});
+      }
     } else {
       // weight-gradient form: both operands row-contiguous ([k][rows]), split-K partial slabs
       DenseT<bf16> la{A, (long)M, M, K};
