@@ -185,6 +185,16 @@ int retr_conv2d_wgrad_splits(int dtype, int Nb, int H, int W, int C, int Co, int
 /* grad[Co][Ci][KH][KW] (=|+=) scale[co] * sum_s ws[s] (slices added in order: deterministic) */
 int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,
                            int Cp, int KH, int KW, int accumulate, int splits, void* stream);
+/* Fused stride-1 bottleneck forward for the frozen layer1 (torchvision Bottleneck,
+ * models/backbone.py:65; frozen by models/backbone.py:58-60, so backward needs none of its
+ * activations): y = relu(conv1x1_64->256(relu(conv3x3(relu(conv1x1(x))))) + residual), all BN
+ * folded.  ds = 0: identity residual (Cin = 256, w3 [256][64]); ds = 1: the 1x1 stride-1
+ * downsample folded in (Cin = 64, w3 = [W3 | Wds] [256][128], b3 = b3 + bds).  w1 [64][Cin],
+ * w2 [64][3][3][64] packed (retr_conv_pack layout), NHWC bf16, H % 8 == 0, W % 16 == 0.
+ * Bitwise equal to retr_conv2d_fwd x 3 (or x 2 + retr_conv1x1_fwd_cat). */
+int retr_bottleneck_s1_fwd(int dtype, const void* x, int N, int H, int W, int Cin,
+                           const void* w1, const float* b1, const void* w2, const float* b2,
+                           const void* w3, const float* b3, int ds, void* y, void* stream);
 /* NCHW fp32 image -> NHWC (channels zero-padded to Cp) */
 int retr_nchw_to_nhwc(int dtype, const float* x, void* y, int N, int C, int H, int W, int Cp,
                       void* stream);

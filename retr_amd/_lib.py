@@ -93,6 +93,7 @@ _SIGS = {
     "retr_stem_s2d_weights": [_P, _P, _I, _I, _P],
     "retr_conv2d_fwd_out": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I,
                             _I, _I, _P],
+    "retr_bottleneck_s1_fwd": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P],
     "retr_conv1x1_fwd_cat": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I,
                              _P],
     "retr_maxpool3x3s2": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],

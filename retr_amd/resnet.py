@@ -191,19 +191,45 @@ def _conv_tail_cat(runner, blk, h2, s2, x, xshape):
     """relu(conv3(h2) + downsample(x)) as one 1x1 conv over the channel concatenation
     (BackboneRunner.cat_tail); weights [W3eff | Wdseff] and bias b3 + bds cached per pack."""
     c3, ds = blk.convs[2], blk.ds
-    wp3, _, b3, _ = PACKS.get(c3, h2.dtype)
-    wpd, _, bd, _ = PACKS.get(ds, h2.dtype)
+    wcat, bcat = _cat_weights(runner, blk, h2.dtype)
+    n, oh, ow, c1 = s2
+    y = torch.empty(n, oh, ow, c3.cout, dtype=h2.dtype, device=h2.device)
+    call("retr_conv1x1_fwd_cat", dcode(h2.dtype), ptr(h2), c1, ptr(x), xshape[3], n, oh, ow,
+         xshape[1], xshape[2], ds.s, ptr(wcat), ptr(bcat), ptr(y), c3.cout, 1, _st())
+    runner.cat_used.append(blk.name)
+    return y, (n, oh, ow, c3.cout)
+
+
+def _cat_weights(runner, blk, dtype):
+    """[W3eff | Wdseff] and b3 + bds of a block with a 1x1 downsample, cached per pack."""
+    c3, ds = blk.convs[2], blk.ds
+    wp3, _, b3, _ = PACKS.get(c3, dtype)
+    wpd, _, bd, _ = PACKS.get(ds, dtype)
     ent = runner._cat_w.get(blk.name)
     if ent is None or ent[0] is not wp3 or ent[1] is not wpd:
         wcat = torch.cat([wp3.view(c3.cout, -1), wpd.view(ds.cout, -1)], 1).contiguous()
         ent = (wp3, wpd, wcat, b3 + bd)
         runner._cat_w[blk.name] = ent
-    n, oh, ow, c1 = s2
-    y = torch.empty(n, oh, ow, c3.cout, dtype=h2.dtype, device=h2.device)
-    call("retr_conv1x1_fwd_cat", dcode(h2.dtype), ptr(h2), c1, ptr(x), xshape[3], n, oh, ow,
-         xshape[1], xshape[2], ds.s, ptr(ent[2]), ptr(ent[3]), ptr(y), c3.cout, 1, _st())
-    runner.cat_used.append(blk.name)
-    return y, (n, oh, ow, c3.cout)
+    return ent[2], ent[3]
+
+
+def _bottleneck_fused(runner, blk, x, xshape):
+    """The whole stride-1 bottleneck in one launch (retr_bottleneck_s1_fwd): h1 / h2 stay in
+    LDS, x is read once.  Only for blocks whose activations backward never needs (the frozen
+    layer1, models/backbone.py:58-60)."""
+    c1, c2, c3 = blk.convs
+    n, h, w, cin = xshape
+    wp1, _, b1, _ = PACKS.get(c1, x.dtype)
+    wp2, _, b2, _ = PACKS.get(c2, x.dtype)
+    if blk.ds is not None:
+        w3, b3 = _cat_weights(runner, blk, x.dtype)
+    else:
+        w3, _, b3, _ = PACKS.get(c3, x.dtype)
+    y = torch.empty(n, h, w, c3.cout, dtype=x.dtype, device=x.device)
+    call("retr_bottleneck_s1_fwd", dcode(x.dtype), ptr(x), n, h, w, cin, ptr(wp1), ptr(b1),
+         ptr(wp2), ptr(b2), ptr(w3), ptr(b3), int(blk.ds is not None), ptr(y), _st())
+    runner.fused_used.append(blk.name)
+    return y, (n, h, w, c3.cout)
 
 
 def _stem_s2d(runner, img):
@@ -250,9 +276,14 @@ class _Backbone(torch.autograd.Function):
         del s
         saved = []
         runner.cat_used = []
+        runner.fused_used = []
         grad_on = runner.save
         for blk in blocks:
             inp, ishape = x, shape
+            keep = grad_on and blk.trainable()
+            if not keep and runner.fused_block(blk, ishape):
+                x, shape = _bottleneck_fused(runner, blk, inp, ishape)
+                continue
             if blk.kind == "bottleneck":
                 c1, c2, c3 = blk.convs
                 h1, s1 = _conv_fwd(c1, inp, ishape, True)
@@ -269,7 +300,7 @@ class _Backbone(torch.autograd.Function):
                 idt = _conv_fwd(blk.ds, inp, ishape, False)[0] if blk.ds is not None else inp
                 out, oshape = _conv_fwd(c2, h1, s1, True, residual=idt)
                 acts = (inp, ishape, h1, s1, None, None)
-            if grad_on and blk.trainable():
+            if keep:
                 saved.append((blk, acts))
             x, shape = out, oshape
         ctx.runner = runner
@@ -350,6 +381,28 @@ class BackboneRunner:
         self._cat_w = {}
         self.cat_used = []          # blocks that took the fused tail in the last forward
         self.use_cat = os.environ.get("RETR_CAT_TAIL", "1") != "0"
+        self.fused_used = []        # blocks run by retr_bottleneck_s1_fwd in the last forward
+        self.use_fused = os.environ.get("RETR_FUSED_BOTTLENECK", "1") != "0"
+
+    def fused_block(self, blk, ishape):
+        """bf16 stride-1 bottleneck of width 64 -> 256 (ResNet-50/101 layer1) on a map with
+        H % 8 == 0 and W % 16 == 0: one retr_bottleneck_s1_fwd launch.  The caller only asks
+        for blocks whose activations backward does not need."""
+        if not (self.use_fused and self.cdtype == torch.bfloat16 and blk.kind == "bottleneck"):
+            return False
+        c1, c2, c3 = blk.convs
+        n, h, w, cin = ishape
+        ok = (c1.k == 1 and c1.s == 1 and c1.cout == 64 and c1.cp == cin
+              and c2.k == 3 and c2.s == 1 and c2.p == 1 and c2.d == 1 and c2.cin == 64
+              and c2.cout == 64 and c3.k == 1 and c3.s == 1 and c3.cin == 64
+              and c3.cout == 256 and h % 8 == 0 and w % 16 == 0)
+        if not ok:
+            return False
+        if blk.ds is None:
+            return cin == 256
+        ds = blk.ds
+        return (cin == 64 and ds.k == 1 and ds.s == 1 and ds.p == 0 and ds.cp == 64
+                and ds.cout == 256)
 
     def cat_tail(self, blk, ishape, s2):
         """bf16 bottleneck with a 1x1 downsample (the first block of every layer): conv3 +

@@ -792,3 +792,52 @@ def test_conv1x1_fwd_cat(N, H, W, C1, C2, Co, s):
     torch.cuda.synchronize()
     assert rel_err(y.float(), yu.float()) < 1e-2
     assert torch.isfinite(y.float()).all()
+
+
+@pytest.mark.parametrize("N,H,W,ds", [(2, 16, 32, False), (2, 24, 48, True), (1, 40, 16, False),
+                                      (3, 8, 16, True)])
+def test_bottleneck_s1_fused_equals_three_launches(N, H, W, ds):
+    """retr_bottleneck_s1_fwd (the frozen layer1 block in one launch, h1 / h2 in LDS) equals the
+    unfused path bitwise: conv1 + conv2 (retr_conv2d_fwd) and conv3 with the identity residual
+    (retr_conv2d_fwd) or with the 1x1 downsample folded in (retr_conv1x1_fwd_cat)."""
+    bf = torch.bfloat16
+    cin = 64 if ds else 256
+    g = torch.Generator(device="cpu").manual_seed(N * 1000 + H + W + int(ds))
+    x = torch.randn(N, H, W, cin, generator=g).to(DEV).to(bf)
+    w1 = (torch.randn(64, cin, generator=g) / math.sqrt(cin)).to(DEV).to(bf)
+    w2 = (torch.randn(64, 3, 3, 64, generator=g) / 24).to(DEV).to(bf)
+    k3 = 64 + (cin if ds else 0)
+    w3 = (torch.randn(256, k3, generator=g) / math.sqrt(k3)).to(DEV).to(bf)
+    b1, b2, b3 = (torch.randn(c, generator=g).to(DEV) * 0.1 for c in (64, 64, 256))
+    st = ops._st()
+    # unfused
+    h1 = torch.empty(N, H, W, 64, dtype=bf, device=DEV)
+    h2 = torch.empty_like(h1)
+    y0 = torch.empty(N, H, W, 256, dtype=bf, device=DEV)
+    call("retr_conv2d_fwd", 1, ptr(x), N, H, W, cin, ptr(w1), ptr(b1), None, ptr(h1), 64, 1, 1,
+         1, 0, 1, 1, st)
+    call("retr_conv2d_fwd", 1, ptr(h1), N, H, W, 64, ptr(w2), ptr(b2), None, ptr(h2), 64, 3, 3,
+         1, 1, 1, 1, st)
+    if ds:
+        call("retr_conv1x1_fwd_cat", 1, ptr(h2), 64, ptr(x), cin, N, H, W, H, W, 1, ptr(w3),
+             ptr(b3), ptr(y0), 256, 1, st)
+    else:
+        call("retr_conv2d_fwd", 1, ptr(h2), N, H, W, 64, ptr(w3), ptr(b3), ptr(x), ptr(y0), 256,
+             1, 1, 1, 0, 1, 1, st)
+    y1 = torch.full_like(y0, float("nan"))
+    call("retr_bottleneck_s1_fwd", 1, ptr(x), N, H, W, cin, ptr(w1), ptr(b1), ptr(w2), ptr(b2),
+         ptr(w3), ptr(b3), int(ds), ptr(y1), st)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y1.float()).all()
+    assert torch.equal(y1, y0), (y1.float() - y0.float()).abs().max().item()
+    # and against an fp32 reference of the same bf16 operands (rounding of h1 / h2 included)
+    xf = x.float().permute(0, 3, 1, 2)
+    r1 = torch.relu(F.conv2d(xf, w1.float().view(64, cin, 1, 1)) + b1.view(1, -1, 1, 1))
+    r1 = r1.to(bf).float()
+    r2 = torch.relu(F.conv2d(r1, w2.float().permute(0, 3, 1, 2), padding=1) + b2.view(1, -1, 1, 1))
+    r2 = r2.to(bf).float()
+    if ds:
+        r3 = F.conv2d(torch.cat([r2, xf], 1), w3.float().view(256, k3, 1, 1)) + b3.view(1, -1, 1, 1)
+    else:
+        r3 = F.conv2d(r2, w3.float().view(256, 64, 1, 1)) + b3.view(1, -1, 1, 1) + xf
+    assert rel_err(y1.permute(0, 3, 1, 2), torch.relu(r3)) < 1e-2

@@ -169,6 +169,7 @@ def test_cat_tail_matches_unfused():
     cfg, model, crit, sd, *_ = _setup("micro_r50_dil", dtype="bf16")
     bb = next(m for m in model.modules() if hasattr(m, "runner") and hasattr(m, "body"))
     runner = bb.runner(torch.bfloat16)
+    runner.use_fused = False          # this test is about the fused tail of the unfused blocks
     samples = NestedTensor(images.to(DEV), mask.to(DEV))
 
     def run(mdl, cr):
@@ -199,3 +200,31 @@ def test_cat_tail_matches_unfused():
     assert e1 <= 1.25 * e0 + 1e-3, (e1, e0)
     for n in g1:
         assert err(g1, n) <= 2.0 * err(g0, n) + 2e-2, (n, err(g1, n), err(g0, n))
+
+
+def test_fused_layer1_bottlenecks_bitwise_in_model():
+    """The cfg2-shaped bf16 model (ResNet-50, 640x640, batch 2): the frozen layer1 blocks run as
+    retr_bottleneck_s1_fwd launches, and the training forward's logits and loss are bitwise
+    those of the unfused block path (three conv launches, or two + the fused tail)."""
+    from bench import build, cfg2
+    cfg = cfg2()
+    cfg.dropout = 0.0
+    model, crit = build(cfg, DEV)
+    model.train()
+    bb = next(m for m in model.modules() if hasattr(m, "runner") and hasattr(m, "body"))
+    runner = bb.runner(torch.bfloat16)
+    img, mask = synthetic_images(2, 640, seed=21)
+    caps, cm = synthetic_captions(2, cfg.max_position_embeddings, cfg.vocab_size, seed=22)
+    s = NestedTensor(img.to(DEV), mask.to(DEV))
+    outs = []
+    for fused in (True, False):
+        runner.use_fused = fused
+        with torch.no_grad():
+            out = model(s, caps[:, :-1].to(DEV), cm[:, :-1].to(DEV))
+            loss = crit(out.permute(0, 2, 1), caps[:, 1:].to(DEV)).item()
+        outs.append((out.float().clone(), loss))
+        expect = ["layer1.0", "layer1.1", "layer1.2"] if fused else []
+        assert runner.fused_used == expect, runner.fused_used
+    runner.use_fused = True
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1]
