@@ -140,6 +140,18 @@ typedef struct {
 size_t retr_linear_wgrad_group_workspace(int n, const retr_linear_wgrad_desc* d);
 int retr_linear_wgrad_group(int dtype, int n, const retr_linear_wgrad_desc* d, void* workspace,
                             void* stream);
+/* extra fixed-order partial sums folded into the weight-gradient group's slab-sum launch:
+ * dst[c] (=|+=) sum_{s < nparts} parts[s * stride + c], c < cols (e.g. a LayerNorm's
+ * dgamma / dbeta partial rows from retr_layernorm_bwd2) */
+typedef struct {
+  const float* parts;
+  long stride;
+  int nparts, cols;
+  float* dst;
+  int accumulate;
+} retr_slab_sum_desc;
+int retr_linear_wgrad_group2(int dtype, int n, const retr_linear_wgrad_desc* d, void* workspace,
+                             int nx, const retr_slab_sum_desc* x, void* stream);
 
 /* ---- ResNet convolutions (torchvision conv stack via models/backbone.py:65-69, FrozenBN
  * models/backbone.py:41-51 folded into the weights) --------------------------------------- */
@@ -251,6 +263,18 @@ int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, co
                        int C, float* dx, long lddx, const float* addend, float* dgamma,
                        float* dbeta, float* workspace, void* stream);
 size_t retr_layernorm_bwd_workspace(int M, int C);
+/* retr_layernorm_bwd plus two fusions of the transformer blocks' backward (ops._ln_bwd):
+ *  - dxd != NULL: also writes dxd = bf16(dropout(dx)) with the (drop_p, seed) mask of the
+ *    residual dropout that PRODUCED this LayerNorm's input (the previous block's
+ *    retr_dropout_apply of its incoming gradient, models/transformer_modules.py:44-46);
+ *  - nparts != NULL: the dgamma/dbeta partial rows are left in `workspace` ([*nparts][2C]:
+ *    dgamma partials in columns [0, C), dbeta in [C, 2C)) for the caller's slab sum
+ *    (retr_linear_wgrad_group2) instead of a reduction launch. */
+int retr_layernorm_bwd2(int dtype, const void* dy, const void* dy2, long lddy, const float* x,
+                        long ldx, const float* gamma, const float* mean, const float* rstd, int M,
+                        int C, float* dx, long lddx, const float* addend, float* dgamma,
+                        float* dbeta, float* workspace, void* dxd, long lddxd, float drop_p,
+                        unsigned long long seed, int* nparts, void* stream);
 
 /* ---- DecoderEmbeddings: word[caps] + pos[t] -> LayerNorm(eps) -> dropout
  * (models/transformer_modules.py:113-129) ------------------------------------------------- */

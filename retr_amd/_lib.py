@@ -54,6 +54,12 @@ class ConvPackDesc(ctypes.Structure):
                 ("pad", _I)]
 
 
+class SlabSumDesc(ctypes.Structure):
+    """retr_slab_sum_desc"""
+    _fields_ = [("parts", _P), ("stride", _L), ("nparts", _I), ("cols", _I), ("dst", _P),
+                ("accumulate", _I)]
+
+
 _PFD = ctypes.POINTER(LinearFwdDesc)
 _PDD = ctypes.POINTER(LinearDgradDesc)
 _PWD = ctypes.POINTER(LinearWgradDesc)
@@ -80,6 +86,7 @@ _SIGS = {
     "retr_linear_dgrad_group": [_I, _I, _I, _I, _I, _PDD, _P],
     "retr_linear_wgrad_group_workspace": [_I, _PWD],
     "retr_linear_wgrad_group": [_I, _I, _PWD, _P, _P],
+    "retr_linear_wgrad_group2": [_I, _I, _PWD, _P, _I, ctypes.POINTER(SlabSumDesc), _P],
     "retr_conv_pack": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "retr_conv_pack_group": [_I, _I, ctypes.POINTER(ConvPackDesc), _P],
     "retr_conv2d_fwd": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
@@ -102,6 +109,8 @@ _SIGS = {
     "retr_layernorm_bwd": [_I, _P, _P, _L, _P, _L, _P, _P, _P, _I, _I, _P, _L, _P, _P, _P, _P,
                            _P],
     "retr_layernorm_bwd_workspace": [_I, _I],
+    "retr_layernorm_bwd2": [_I, _P, _P, _L, _P, _L, _P, _P, _P, _I, _I, _P, _L, _P, _P, _P, _P,
+                            _P, _L, _F, _U64, _P, _P],
     "retr_embed_ln_fwd": [_P, _I, _I, _I, _P, _P, _P, _P, _F, _F, _U64, _P, _P, _P, _P],
     "retr_embed_ln_bwd": [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _U64, _P, _P, _P, _P, _I,
                           _P, _P],

@@ -125,6 +125,18 @@ RETR_DEVICE uint32_t drop_keep8(uint32_t row_key, uint32_t n, uint32_t th16) {
   return m;
 }
 
+// keep bits of columns n .. n+3 (n even): bit e = column n + e
+RETR_DEVICE uint32_t drop_keep4(uint32_t row_key, uint32_t n, uint32_t th16) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int e = 0; e < 4; e += 2) {
+    const uint32_t b = attn_pair_bits(row_key, n + e);
+    m |= (uint32_t)((b & 0xffffu) >= th16) << e;
+    m |= (uint32_t)((b >> 16) >= th16) << (e + 1);
+  }
+  return m;
+}
+
 // ---- wave reductions (wave64) ------------------------------------------------------------------
 RETR_DEVICE float wave_sum(float v) {
 #pragma unroll

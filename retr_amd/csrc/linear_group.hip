@@ -184,11 +184,16 @@ struct SlabSum {
   float* dst;
   long ld;        // dst row stride
   long slab;      // floats per slab (rows * cols)
+  long sstride;   // floats between consecutive slabs (>= slab)
   int rows, cols, splits, accumulate, blk0, nblk, vec;
+  int rowpar;     // many short slabs (LayerNorm partial rows): 64 columns per block, the four
+                  // waves take every fourth slab, 8 loads in flight, summed in wave order
 };
 
+constexpr int kMaxExtra = 4;   // extra partial-row sums per launch (two LayerNorms' dgamma/dbeta)
+
 struct SlabGroup {
-  SlabSum p[2 * kMaxWgrad];
+  SlabSum p[2 * kMaxWgrad + kMaxExtra];
   int n;
 };
 
@@ -199,9 +204,34 @@ __global__ void __launch_bounds__(256) slab_sum_group_kernel(SlabGroup g) {
   const int bid = blockIdx.x;
   int p = 0;
 #pragma unroll
-  for (int i = 1; i < 2 * kMaxWgrad; ++i)
+  for (int i = 1; i < 2 * kMaxWgrad + kMaxExtra; ++i)
     if (i < g.n && bid >= g.p[i].blk0) p = i;
   const SlabSum& d = g.p[p];
+  if (d.rowpar) {
+    __shared__ float red[4][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = (bid - d.blk0) * 64 + lane;
+    float v = 0.f;
+    if (c < d.cols) {
+      const float* src = d.ws + c;
+      int s = w;
+      for (; s + 28 < d.splits; s += 32) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = src[(long)(s + 4 * u) * d.sstride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += t[u];
+      }
+      for (; s < d.splits; s += 4) v += src[(long)s * d.sstride];
+    }
+    red[w][lane] = v;
+    __syncthreads();
+    if (w == 0 && c < d.cols) {
+      const float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+      d.dst[c] = d.accumulate ? d.dst[c] + t : t;
+    }
+    return;
+  }
   const long e0 = ((long)(bid - d.blk0) * 256 + threadIdx.x) * kSlabPerThread;
   if (e0 >= d.slab) return;
   float v[kSlabPerThread] = {0.f, 0.f, 0.f, 0.f};
@@ -210,14 +240,14 @@ __global__ void __launch_bounds__(256) slab_sum_group_kernel(SlabGroup g) {
     for (; s + 3 < d.splits; s += 4) {
       f32x4 t[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) t[u] = *(const f32x4*)(d.ws + (long)(s + u) * d.slab + e0);
+      for (int u = 0; u < 4; ++u) t[u] = *(const f32x4*)(d.ws + (long)(s + u) * d.sstride + e0);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] += t[u][e];
     }
     for (; s < d.splits; ++s) {
-      const f32x4 t = *(const f32x4*)(d.ws + (long)s * d.slab + e0);
+      const f32x4 t = *(const f32x4*)(d.ws + (long)s * d.sstride + e0);
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += t[e];
     }
@@ -235,7 +265,7 @@ __global__ void __launch_bounds__(256) slab_sum_group_kernel(SlabGroup g) {
     const long i = e0 + e;
     if (i >= d.slab) break;
     float t = 0.f;
-    for (int s = 0; s < d.splits; ++s) t += d.ws[(long)s * d.slab + i];
+    for (int s = 0; s < d.splits; ++s) t += d.ws[(long)s * d.sstride + i];
     const long r = i / d.cols, c = i - r * d.cols;
     float* o = d.dst + r * d.ld + c;
     *o = d.accumulate ? *o + t : t;
@@ -326,8 +356,21 @@ size_t retr_linear_wgrad_group_workspace(int n, const retr_linear_wgrad_desc* d)
 
 int retr_linear_wgrad_group(int dtype, int n, const retr_linear_wgrad_desc* d, void* workspace,
                             void* stream) {
+  return retr_linear_wgrad_group2(dtype, n, d, workspace, 0, nullptr, stream);
+}
+
+int retr_linear_wgrad_group2(int dtype, int n, const retr_linear_wgrad_desc* d, void* workspace,
+                             int nx, const retr_slab_sum_desc* x, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   RETR_REQUIRE(n >= 0 && n <= kMaxWgrad, "linear_wgrad_group: n=%d (max %d)", n, kMaxWgrad);
+  RETR_REQUIRE(nx >= 0 && nx <= kMaxExtra && (nx == 0 || x), "linear_wgrad_group: nx=%d", nx);
+  SlabGroup sg{};
+  int blocks = 0;
+  auto push = [&](SlabSum& s) {
+    s.blk0 = blocks;
+    s.nblk = s.rowpar ? (int)cdiv(s.cols, 64) : (int)cdiv(s.slab, 256L * kSlabPerThread);
+    blocks += s.nblk;
+  };
   if (dtype != RETR_BF16) {
     for (int i = 0; i < n; ++i) {
       const retr_linear_wgrad_desc& q = d[i];
@@ -335,46 +378,62 @@ int retr_linear_wgrad_group(int dtype, int n, const retr_linear_wgrad_desc* d, v
                                 q.db, q.accumulate, stream);
       if (e) return e;
     }
-    return 0;
-  }
-  for (int i = 0; i < n; ++i)
-    RETR_REQUIRE(d[i].M >= 0 && d[i].N > 0 && d[i].K > 0 && d[i].K % 8 == 0 &&
-                     d[i].lddy % 8 == 0 && d[i].ldx % 8 == 0 && d[i].lddy >= (d[i].N + 7) / 8 * 8,
-                 "linear_wgrad_group[%d]: bad shape M=%d N=%d K=%d", i, d[i].M, d[i].N, d[i].K);
-  const WPlan p = wgrad_plan(n, d);
-  if (p.n == 0) return 0;
-  RETR_REQUIRE(workspace != nullptr, "linear_wgrad_group: workspace required");
-  float* ws = (float*)workspace;
-  int e;
-  if (p.tile == 128) e = p.stages == 3 ? wgrad_group_gemm<128, 3>(p, d, ws, st)
-                                       : wgrad_group_gemm<128, 2>(p, d, ws, st);
-  else e = p.stages == 4 ? wgrad_group_gemm<64, 4>(p, d, ws, st)
-                         : wgrad_group_gemm<64, 2>(p, d, ws, st);
-  if (e) return e;
-  SlabGroup sg{};
-  int blocks = 0;
-  for (int j = 0; j < p.n; ++j) {
-    const retr_linear_wgrad_desc& q = d[p.src[j]];
-    SlabSum& s = sg.p[sg.n++];
-    s.ws = ws + p.ws_off[j];
-    s.rows = q.N;
-    s.cols = p.bias[j] ? 1 : q.K;
-    s.dst = p.bias[j] ? q.db : q.dw;
-    s.ld = p.bias[j] ? 1 : q.lddw;
-    s.slab = (long)s.rows * s.cols;
-    s.splits = p.splits[j];
-    s.accumulate = q.accumulate;
-    s.vec = (s.cols % 4 == 0 && s.ld % 4 == 0 && ((uintptr_t)s.dst & 15) == 0) ||
-            (s.cols == 1 && s.rows % 4 == 0 && ((uintptr_t)s.dst & 15) == 0);
-    if (s.cols == 1) {   // a bias vector: one row of N elements
-      s.cols = s.rows;
-      s.rows = 1;
-      s.ld = s.cols;
+  } else {
+    for (int i = 0; i < n; ++i)
+      RETR_REQUIRE(d[i].M >= 0 && d[i].N > 0 && d[i].K > 0 && d[i].K % 8 == 0 &&
+                       d[i].lddy % 8 == 0 && d[i].ldx % 8 == 0 && d[i].lddy >= (d[i].N + 7) / 8 * 8,
+                   "linear_wgrad_group[%d]: bad shape M=%d N=%d K=%d", i, d[i].M, d[i].N, d[i].K);
+    const WPlan p = wgrad_plan(n, d);
+    if (p.n > 0) {
+      RETR_REQUIRE(workspace != nullptr, "linear_wgrad_group: workspace required");
+      float* ws = (float*)workspace;
+      int e;
+      if (p.tile == 128) e = p.stages == 3 ? wgrad_group_gemm<128, 3>(p, d, ws, st)
+                                           : wgrad_group_gemm<128, 2>(p, d, ws, st);
+      else e = p.stages == 4 ? wgrad_group_gemm<64, 4>(p, d, ws, st)
+                             : wgrad_group_gemm<64, 2>(p, d, ws, st);
+      if (e) return e;
+      for (int j = 0; j < p.n; ++j) {
+        const retr_linear_wgrad_desc& q = d[p.src[j]];
+        SlabSum& s = sg.p[sg.n++];
+        s.ws = ws + p.ws_off[j];
+        s.rows = q.N;
+        s.cols = p.bias[j] ? 1 : q.K;
+        s.dst = p.bias[j] ? q.db : q.dw;
+        s.ld = p.bias[j] ? 1 : q.lddw;
+        s.slab = (long)s.rows * s.cols;
+        s.sstride = s.slab;
+        s.splits = p.splits[j];
+        s.accumulate = q.accumulate;
+        s.vec = (s.cols % 4 == 0 && s.ld % 4 == 0 && ((uintptr_t)s.dst & 15) == 0) ||
+                (s.cols == 1 && s.rows % 4 == 0 && ((uintptr_t)s.dst & 15) == 0);
+        if (s.cols == 1) {   // a bias vector: one row of N elements
+          s.cols = s.rows;
+          s.rows = 1;
+          s.ld = s.cols;
+        }
+        push(s);
+      }
     }
-    s.blk0 = blocks;
-    s.nblk = (int)cdiv(s.slab, 256L * kSlabPerThread);
-    blocks += s.nblk;
   }
+  for (int i = 0; i < nx; ++i) {
+    const retr_slab_sum_desc& q = x[i];
+    if (!q.dst || q.nparts <= 0 || q.cols <= 0) continue;
+    SlabSum& s = sg.p[sg.n++];
+    s.ws = q.parts;
+    s.dst = q.dst;
+    s.rows = 1;
+    s.cols = q.cols;
+    s.ld = q.cols;
+    s.slab = q.cols;
+    s.sstride = q.stride;
+    s.splits = q.nparts;
+    s.accumulate = q.accumulate;
+    s.vec = 0;
+    s.rowpar = 1;
+    push(s);
+  }
+  if (blocks == 0) return 0;
   hipLaunchKernelGGL(slab_sum_group_kernel, dim3(blocks), dim3(256), 0, st, sg);
   return retr_check_launch("linear_wgrad_group sum");
 }

@@ -105,7 +105,8 @@ template <typename T, int NCH, int NW>
 __global__ void __launch_bounds__(NW * 64)
 ln_bwd4_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, const float* gamma,
                const float* mean, const float* rstd, int M, float* dx, long lddx,
-               const float* addend, float* part, int rows_per_block) {
+               const float* addend, float* part, int rows_per_block, bf16* dxd, long lddxd,
+               DropoutParams dpd) {
   constexpr int C = 256 * NCH;
   __shared__ f32x4 red[2][NW][64 * NCH];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -170,6 +171,16 @@ ln_bwd4_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, c
         f32x4 o = rs[u] * (g[u][j] - s1[u] - xh[u][j] * s2[u]);
         if (addend) o += ad[u][j];
         st4(dx + (long)row * lddx + 4 * lane + 256 * j, o);
+        if (dxd) {   // the producing block's residual dropout applied to dx, in bf16
+          f32x4 od = o;
+          if (dpd.thresh) {
+            const uint32_t km = drop_keep4(drop_row_key(dp_seed(dpd), (uint32_t)row),
+                                           (uint32_t)(4 * lane + 256 * j), drop_th16(dpd.thresh));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) od[e] = ((km >> e) & 1u) ? o[e] * dpd.scale : 0.f;
+          }
+          st4(dxd + (long)row * lddxd + 4 * lane + 256 * j, od);
+        }
       }
     }
   }
@@ -544,13 +555,27 @@ int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, co
                        long ldx, const float* gamma, const float* mean, const float* rstd, int M,
                        int C, float* dx, long lddx, const float* addend, float* dgamma,
                        float* dbeta, float* workspace, void* stream) {
+  return retr_layernorm_bwd2(dtype, dy, dy2, lddy, x, ldx, gamma, mean, rstd, M, C, dx, lddx,
+                             addend, dgamma, dbeta, workspace, nullptr, 0, 0.f, 0ull, nullptr,
+                             stream);
+}
+
+int retr_layernorm_bwd2(int dtype, const void* dy, const void* dy2, long lddy, const float* x,
+                        long ldx, const float* gamma, const float* mean, const float* rstd, int M,
+                        int C, float* dx, long lddx, const float* addend, float* dgamma,
+                        float* dbeta, float* workspace, void* dxd, long lddxd, float drop_p,
+                        unsigned long long seed, int* nparts, void* stream) {
+  if (nparts) *nparts = 0;
   if (M == 0) return 0;
+  RETR_REQUIRE(!nparts || workspace, "layernorm_bwd: deferred parameter sums need a workspace");
+  if (nparts) dgamma = dbeta = nullptr;
   RETR_REQUIRE(C % 64 == 0, "layernorm: C=%d must be a multiple of 64", C);
   RETR_REQUIRE(dy || dy2, "layernorm_bwd: no incoming gradient");
   RETR_REQUIRE(mean && rstd && gamma && dx, "layernorm_bwd: missing saved statistics");
   RETR_REQUIRE(!(dgamma || dbeta) || workspace, "layernorm_bwd: dgamma/dbeta need a workspace");
   hipStream_t st = (hipStream_t)stream;
-  float* part = (dgamma || dbeta) ? workspace : nullptr;
+  float* part = (dgamma || dbeta || nparts) ? workspace : nullptr;
+  const DropoutParams dpd = make_dp(drop_p, seed);
   const bool v4 = C % 256 == 0 && C <= 512 && lddy % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0 &&
                   (((uintptr_t)x | (uintptr_t)dx | (uintptr_t)gamma |
                     (uintptr_t)(addend ? addend : x)) & 15) == 0 &&
@@ -566,11 +591,11 @@ int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, co
     if (dtype == RETR_BF16)                                                                        \
       hipLaunchKernelGGL((ln_bwd4_kernel<bf16, NC, NW>), grid, dim3(NW * 64), 0, st,               \
                          (const bf16*)dy, (const bf16*)dy2, lddy, x, ldx, gamma, mean, rstd, M,    \
-                         dx, lddx, addend, part, rpb);                                             \
+                         dx, lddx, addend, part, rpb, (bf16*)dxd, lddxd, dpd);                     \
     else                                                                                           \
       hipLaunchKernelGGL((ln_bwd4_kernel<float, NC, NW>), grid, dim3(NW * 64), 0, st,              \
                          (const float*)dy, (const float*)dy2, lddy, x, ldx, gamma, mean, rstd, M,  \
-                         dx, lddx, addend, part, rpb);
+                         dx, lddx, addend, part, rpb, (bf16*)dxd, lddxd, dpd);
     if (C == 256) {
       if (big) { LNB4(1, 16) } else { LNB4(1, 4) }
     } else {
@@ -579,6 +604,10 @@ int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, co
 #undef LNB4
     if (int e = retr_check_launch("layernorm_bwd4")) return e;
     if (!part) return 0;
+    if (nparts) {   // the caller sums the partial rows (e.g. in its weight-gradient slab sum)
+      *nparts = (int)grid.x;
+      return 0;
+    }
     hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(2 * C, 64)), dim3(1024), 0, st, part,
                        (int)grid.x, C, dgamma, dbeta);
     return retr_check_launch("layernorm_param_reduce");
@@ -597,7 +626,13 @@ int retr_layernorm_bwd(int dtype, const void* dy, const void* dy2, long lddy, co
   PER_SWITCH(C, LNB)
 #undef LNB
   if (int e = retr_check_launch("layernorm_bwd")) return e;
+  if (dxd && retr_dropout_apply(RETR_BF16, dx, lddx, dxd, lddxd, M, C, drop_p, seed, stream))
+    return 1;
   if (!part) return 0;
+  if (nparts) {
+    *nparts = (int)grid.x;
+    return 0;
+  }
   hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(2 * C, 64)), dim3(1024), 0, st, part,
                      (int)grid.x, C, dgamma, dbeta);
   return retr_check_launch("layernorm_param_reduce");

@@ -156,6 +156,8 @@ class ConcatTransformer(nn.Module):
 
     def run(self, src_rows, B, S, src_mask, tgt, tgt_mask, cdtype, return_attention=False):
         """Hot path.  Returns (hs [B*T, C] compute dtype, att dict or {})."""
+        from .. import ops
+        ops.begin_pass()
         kpm_src = src_mask.reshape(B, S).contiguous().view(torch.uint8)
         mem, mem_pos, att_e = self.encode(src_rows, B, S, kpm_src, cdtype, return_attention)
         hs, att_s, att_x = self.decode(mem, mem_pos, B, S, kpm_src, tgt, tgt_mask, cdtype,

@@ -337,9 +337,11 @@ def k_linear_dgrad_group(items):
          int(a0 is not None and a0.dtype == torch.float32), w_trans, n, arr, _st())
 
 
-def k_linear_wgrad_group(items):
+def k_linear_wgrad_group(items, extra=()):
     """One GEMM launch + one ordered slab-sum launch for the weight (and bias) gradients of
-    several projections: items of (dy, x, dw, db, accumulate)."""
+    several projections: items of (dy, x, dw, db, accumulate).  ``extra``: further partial-row
+    sums (parts, stride, nparts, cols, dst, accumulate) folded into the same slab-sum launch
+    (the block's LayerNorm dgamma / dbeta partials, _ln_bwd_fused)."""
     n = len(items)
     arr = (_lib.LinearWgradDesc * n)()
     for i, (dy, x, dw, db, acc) in enumerate(items):
@@ -349,7 +351,15 @@ def k_linear_wgrad_group(items):
         d.M, d.N, d.K, d.accumulate = dy.shape[0], dw.shape[0], x.shape[1], int(acc)
     nbytes = _lib.load().retr_linear_wgrad_group_workspace(n, arr)
     ws = torch.empty(max(1, nbytes // 4), dtype=torch.float32, device=items[0][0].device)
-    call("retr_linear_wgrad_group", dcode(items[0][0].dtype), n, arr, ptr(ws), _st())
+    if not extra:
+        call("retr_linear_wgrad_group", dcode(items[0][0].dtype), n, arr, ptr(ws), _st())
+        return
+    xa = (_lib.SlabSumDesc * len(extra))()
+    for i, (parts, stride, nparts, cols, dst, acc) in enumerate(extra):
+        xa[i].parts, xa[i].stride, xa[i].nparts = ptr(parts), stride, nparts
+        xa[i].cols, xa[i].dst, xa[i].accumulate = cols, ptr(dst), int(acc)
+    call("retr_linear_wgrad_group2", dcode(items[0][0].dtype), n, arr, ptr(ws), len(extra), xa,
+         _st())
 
 
 def _empty(*shape, dev):
@@ -501,6 +511,76 @@ def _ln_bwd(x, gamma, beta, mean, rstd, dy, dy2, addend, pos=None, period=1, nee
     return dx, dgamma, dbeta, dpos
 
 
+# Fused backward of the transformer blocks (bf16 compute): a block's LayerNorm backward also
+#  * writes the bf16 dropout(dx) of the residual dropout of the block that produced its input --
+#    exactly that block's first backward launch (retr_dropout_apply of its incoming gradient),
+#    which then finds it in _DBR instead of launching it;
+#  * leaves its dgamma / dbeta partial rows for the block's weight-gradient slab sum instead of
+#    a separate reduction launch.
+_DBR = {}   # data_ptr of dx -> ((drop_p, seed) of the producing block, dx._version, bf16 copy)
+FUSE_LN_BWD = True   # tests switch the fused path off to compare against the unfused launches
+FUSE_LN_PARAMS = True   # dgamma / dbeta partials into the wgrad slab sum (else their own launch)
+DBR_STATS = {"hit": 0, "miss": 0}
+
+
+def begin_pass():
+    """Forget the previous pass's unused fused dropout-gradient copies."""
+    _DBR.clear()
+
+
+def _tag_drop(out, drop_p, seed):
+    """Mark a block's fp32 output with its residual dropout (read by the next block)."""
+    out._retr_drop = (float(drop_p), int(seed))
+    return out
+
+
+def _take_dbr(dout, drop_p, seed, cdtype):
+    """bf16 dropout(dout) for a block's residual dropout: the copy the following block's fused
+    LayerNorm backward wrote (same pointer, unmodified since: version check), else one
+    retr_dropout_apply launch."""
+    ent = _DBR.pop(dout.data_ptr(), None)
+    if (ent is not None and ent[0] == (float(drop_p), int(seed)) and ent[1] == dout._version
+            and ent[2].shape == dout.shape and ent[2].dtype == cdtype):
+        DBR_STATS["hit"] += 1
+        return ent[2]
+    DBR_STATS["miss"] += 1
+    dbr = torch.empty(dout.shape, dtype=cdtype, device=dout.device)
+    k_dropout_apply(dout, dbr, drop_p, seed)
+    return dbr
+
+
+def _ln_bwd_fused(x, gamma, beta, mean, rstd, dy, dy2, addend, prev, cdtype, pos=None, period=1,
+                  need_dpos=False):
+    """_ln_bwd for the bf16 blocks: returns (dx, dgamma, dbeta, dpos, extra) where ``extra``
+    are the dgamma / dbeta partial-row sums for k_linear_wgrad_group; with ``prev`` = (drop_p,
+    seed) of the block that produced x, also caches bf16 dropout(dx) for that block."""
+    import ctypes
+    M, C = x.shape
+    ref = dy if dy is not None else dy2
+    if dy is not None and dy2 is not None and dy.dtype != dy2.dtype:
+        dy2 = dy2.to(dy.dtype)
+    dx = torch.empty(M, C, dtype=torch.float32, device=x.device)
+    dgamma, _ = grad_buffer(gamma)
+    dbeta, _ = grad_buffer(beta)
+    ws = ln_workspace(M, C, x.device)
+    dxd = torch.empty(M, C, dtype=cdtype, device=x.device) if prev is not None else None
+    nparts = ctypes.c_int(0)
+    call("retr_layernorm_bwd2", dcode(ref.dtype), ptr(dy), ptr(dy2), C, ptr(x), x.stride(0),
+         ptr(gamma), ptr(mean), ptr(rstd), M, C, ptr(dx), dx.stride(0), ptr(addend),
+         ptr(dgamma), ptr(dbeta), ptr(ws), ptr(dxd), C, prev[0] if prev else 0.0,
+         prev[1] if prev else 0, ctypes.addressof(nparts) if FUSE_LN_PARAMS else None, _st())
+    if dxd is not None:
+        _DBR[dx.data_ptr()] = (prev, dx._version, dxd)
+    n = nparts.value
+    extra = [(ws, 2 * C, n, C, dgamma, 1), (ws[C:], 2 * C, n, C, dbeta, 1)] if n > 0 else []
+    dpos = None
+    if need_dpos and dy2 is not None:
+        dpos, _ = grad_buffer(pos)
+        call("retr_pos_grad", dcode(dy2.dtype), ptr(dy2), dy2.stride(0), M, C, int(period),
+             ptr(dpos), _st())
+    return dx, dgamma, dbeta, dpos, extra
+
+
 # ---------------------------------------------------------------------------------------------
 # attention sub-layers
 # ---------------------------------------------------------------------------------------------
@@ -538,6 +618,8 @@ class _SelfAttnBlock(torch.autograd.Function):
         ctx.gparams = (w_in, b_in, w_out, b_out)
         ctx.ln = (ln_w, ln_b, pos, period)
         ctx.cfg = (B, L, H, causal, drop_attn, drop_res, s_att, s_res, cdtype)
+        ctx.prev = getattr(x, "_retr_drop", None)
+        _tag_drop(out, drop_res, s_res)
         if want_probs:
             ctx.mark_non_differentiable(probs)
             return out, probs
@@ -553,8 +635,12 @@ class _SelfAttnBlock(torch.autograd.Function):
         dout = dout.contiguous()
         wint = WEIGHTS.get_t(w_in, cdtype)
         woutt = WEIGHTS.get_t(w_out, cdtype)
-        dbr = torch.empty(M, C, dtype=cdtype, device=dev)
-        k_dropout_apply(dout, dbr, drop_res, s_res)
+        fused = cdtype == torch.bfloat16 and FUSE_LN_BWD
+        if fused:
+            dbr = _take_dbr(dout, drop_res, s_res, cdtype)
+        else:
+            dbr = torch.empty(M, C, dtype=cdtype, device=dev)
+            k_dropout_apply(dout, dbr, drop_res, s_res)
         (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
         do = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
@@ -565,13 +651,20 @@ class _SelfAttnBlock(torch.autograd.Function):
         dnpos = torch.empty(M, C, dtype=cdtype, device=dev)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad_group([(dqk, wint[:, : 2 * C], dnpos), (dv, wint[:, 2 * C:], dn)])
-        # the block's three weight gradients (+ biases): one grouped GEMM + one slab sum
-        k_linear_wgrad_group([(dbr, o, dw_out, db_out, True),
-                              (dqk, npos, dw_in[: 2 * C], db_in[: 2 * C], True),
-                              (dv, n, dw_in[2 * C:], db_in[2 * C:], True)])
         _, ln_b, pos, period = ctx.ln
-        dx, dlw, dlb, dpos = _ln_bwd(x, ln_w, ln_b, mean, rstd, dn, dnpos, dout, pos, period,
-                                     ctx.needs_input_grad[3])
+        # the block's three weight gradients (+ biases): one grouped GEMM + one slab sum (with
+        # the LayerNorm's parameter partials in it on the fused path)
+        wg = [(dbr, o, dw_out, db_out, True), (dqk, npos, dw_in[: 2 * C], db_in[: 2 * C], True),
+              (dv, n, dw_in[2 * C:], db_in[2 * C:], True)]
+        if fused:
+            dx, dlw, dlb, dpos, extra = _ln_bwd_fused(x, ln_w, ln_b, mean, rstd, dn, dnpos, dout,
+                                                      ctx.prev, cdtype, pos, period,
+                                                      ctx.needs_input_grad[3])
+            k_linear_wgrad_group(wg, extra)
+        else:
+            k_linear_wgrad_group(wg)
+            dx, dlw, dlb, dpos = _ln_bwd(x, ln_w, ln_b, mean, rstd, dn, dnpos, dout, pos, period,
+                                         ctx.needs_input_grad[3])
         return (dx, dlw, dlb, dpos, None, None, dw_in, db_in, dw_out, db_out) + (None,) * 9
 
 
@@ -610,6 +703,8 @@ class _CrossAttnBlock(torch.autograd.Function):
         ctx.gparams = (w_in, b_in, w_out, b_out)
         ctx.ln = (ln_w, ln_b, qp, period)
         ctx.cfg = (B, Lq, Lk, H, drop_attn, drop_res, s_att, s_res, cdtype)
+        ctx.prev = getattr(y, "_retr_drop", None)
+        _tag_drop(out, drop_res, s_res)
         if want_probs:
             ctx.mark_non_differentiable(probs)
             return out, probs
@@ -627,8 +722,12 @@ class _CrossAttnBlock(torch.autograd.Function):
         dout = dout.contiguous()
         wint = WEIGHTS.get_t(w_in, cdtype)
         woutt = WEIGHTS.get_t(w_out, cdtype)
-        dbr = torch.empty(Mq, C, dtype=cdtype, device=dev)
-        k_dropout_apply(dout, dbr, drop_res, s_res)
+        fused = cdtype == torch.bfloat16 and FUSE_LN_BWD
+        if fused:
+            dbr = _take_dbr(dout, drop_res, s_res, cdtype)
+        else:
+            dbr = torch.empty(Mq, C, dtype=cdtype, device=dev)
+            k_dropout_apply(dout, dbr, drop_res, s_res)
         (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
         do = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
@@ -642,13 +741,19 @@ class _CrossAttnBlock(torch.autograd.Function):
         dmem = torch.empty(Mk, C, dtype=cdtype, device=dev)
         k_linear_dgrad_group([(dq, wint[:, :C], dqpos), (dk, wint[:, C: 2 * C], dmem_pos),
                               (dv, wint[:, 2 * C:], dmem)])
-        k_linear_wgrad_group([(dbr, o, dw_out, db_out, True),
-                              (dq, qpos, dw_in[:C], db_in[:C], True),
-                              (dk, mem_pos, dw_in[C: 2 * C], db_in[C: 2 * C], True),
-                              (dv, mem, dw_in[2 * C:], db_in[2 * C:], True)])
+        wg = [(dbr, o, dw_out, db_out, True), (dq, qpos, dw_in[:C], db_in[:C], True),
+              (dk, mem_pos, dw_in[C: 2 * C], db_in[C: 2 * C], True),
+              (dv, mem, dw_in[2 * C:], db_in[2 * C:], True)]
         _, ln_b, qp, period = ctx.ln
-        dy, dlw, dlb, dqp = _ln_bwd(y, ln_w, ln_b, mean, rstd, None, dqpos, dout, qp, period,
-                                    ctx.needs_input_grad[3])
+        if fused:
+            dy, dlw, dlb, dqp, extra = _ln_bwd_fused(y, ln_w, ln_b, mean, rstd, None, dqpos, dout,
+                                                     ctx.prev, cdtype, qp, period,
+                                                     ctx.needs_input_grad[3])
+            k_linear_wgrad_group(wg, extra)
+        else:
+            k_linear_wgrad_group(wg)
+            dy, dlw, dlb, dqp = _ln_bwd(y, ln_w, ln_b, mean, rstd, None, dqpos, dout, qp, period,
+                                        ctx.needs_input_grad[3])
         return (dy, dlw, dlb, dqp, None, None, dmem_pos, dmem, dw_in, db_in, dw_out,
                 db_out) + (None,) * 9
 
@@ -675,7 +780,8 @@ class _FFNBlock(torch.autograd.Function):
         ctx.gparams = (w1, b1, w2, b2)
         ctx.ln_b = ln_b
         ctx.cfg = (drop_res, seed, cdtype)
-        return out
+        ctx.prev = getattr(x, "_retr_drop", None)
+        return _tag_drop(out, drop_res, seed)
 
     @staticmethod
     def backward(ctx, dout):
@@ -686,15 +792,25 @@ class _FFNBlock(torch.autograd.Function):
         dev = n.device
         dout = dout.contiguous()
         w1t, w2t = WEIGHTS.get_t(w1, cdtype), WEIGHTS.get_t(w2, cdtype)
-        dbr = torch.empty(M, C, dtype=cdtype, device=dev)
-        k_dropout_apply(dout, dbr, drop_res, seed)
+        fused = cdtype == torch.bfloat16 and FUSE_LN_BWD
+        if fused:
+            dbr = _take_dbr(dout, drop_res, seed, cdtype)
+        else:
+            dbr = torch.empty(M, C, dtype=cdtype, device=dev)
+            k_dropout_apply(dout, dbr, drop_res, seed)
         (dw1, _), (db1, _), (dw2, _), (db2, _) = map(grad_buffer, ctx.gparams)
         dh = torch.empty(M, F, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, w2t, dh, gate=h)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dh, w1t, dn)
-        k_linear_wgrad_group([(dbr, h, dw2, db2, True), (dh, n, dw1, db1, True)])
-        dx, dlw, dlb, _ = _ln_bwd(x, ln_w, ctx.ln_b, mean, rstd, dn, None, dout)
+        wg = [(dbr, h, dw2, db2, True), (dh, n, dw1, db1, True)]
+        if fused:
+            dx, dlw, dlb, _, extra = _ln_bwd_fused(x, ln_w, ctx.ln_b, mean, rstd, dn, None, dout,
+                                                   ctx.prev, cdtype)
+            k_linear_wgrad_group(wg, extra)
+        else:
+            k_linear_wgrad_group(wg)
+            dx, dlw, dlb, _ = _ln_bwd(x, ln_w, ctx.ln_b, mean, rstd, dn, None, dout)
         return dx, dlw, dlb, None, dw1, db1, dw2, db2, None, None
 
 

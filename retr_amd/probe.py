@@ -31,6 +31,7 @@ def _conv_variant(k, s, p):
 
 def flops_of(name, a):
     """(family key, algorithmic FLOPs) of one C-ABI call (2 FLOP per MAC)."""
+    name = _ALIAS.get(name, name)
     if name in ("retr_conv2d_fwd", "retr_conv2d_fwd_out"):
         _, _, n, h, w, c, _, _, _, _, co, kh, kw, s, p, d = a[:16]
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
@@ -74,9 +75,13 @@ def flops_of(name, a):
     return name, 0.0
 
 
+# entry points measured as another one (same leading arguments; extras are tiny sums)
+_ALIAS = {"retr_linear_wgrad_group2": "retr_linear_wgrad_group"}
+
 # grouped launches: name -> (family, index of the descriptor array in the call's arguments)
 _GROUPS = {"retr_linear_fwd_group": ("linear_fwd", 3), "retr_linear_dgrad_group": ("linear_dgrad", 5),
-           "retr_linear_wgrad_group": ("linear_wgrad", 2)}
+           "retr_linear_wgrad_group": ("linear_wgrad", 2),
+           "retr_linear_wgrad_group2": ("linear_wgrad", 2)}
 
 
 def _esz(dtype):
@@ -88,6 +93,7 @@ def bytes_of(name, a):
     output written once in its storage type (bf16 operands, fp32 weight gradients / fp32
     outputs where the call says so).  Split-K slabs, re-reads and padding are implementation
     traffic and are NOT counted here -- the rocprofv3 --pmc passes measure those."""
+    name = _ALIAS.get(name, name)
     e = _esz(a[0])
     if name in ("retr_conv2d_fwd", "retr_conv2d_fwd_out"):
         _, _, n, h, w, c, _, _, res, _, co, kh, kw, s, p, d = a[:16]
@@ -148,6 +154,7 @@ def bytes_of(name, a):
 
 def shape_of(name, a):
     """Short shape tag of a call (for the per-shape breakdown)."""
+    name = _ALIAS.get(name, name)
     if name in _GROUPS:
         n, arr = a[_GROUPS[name][1] - 1], a[_GROUPS[name][1]]
         return "group " + " + ".join(f"M{arr[i].M} N{arr[i].N} K{arr[i].K}" for i in range(n))
@@ -183,7 +190,7 @@ TRACKED = ("retr_conv2d_fwd", "retr_conv2d_fwd_out", "retr_conv1x1_fwd_cat",
            "retr_linear_fwd_splitk",
            "retr_linear_dgrad", "retr_linear_dgrad_splitk", "retr_linear_wgrad",
            "retr_linear_fwd_group", "retr_linear_dgrad_group", "retr_linear_wgrad_group",
-           "retr_attention_fwd", "retr_attention_bwd")
+           "retr_linear_wgrad_group2", "retr_attention_fwd", "retr_attention_bwd")
 
 
 FAMILY_SYMBOL = {"linear_fwd": "gemm{,2,2_group}_kernel<0,",

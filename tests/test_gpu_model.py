@@ -228,3 +228,50 @@ def test_fused_layer1_bottlenecks_bitwise_in_model():
     runner.use_fused = True
     assert torch.equal(outs[0][0], outs[1][0])
     assert outs[0][1] == outs[1][1]
+
+
+@pytest.mark.parametrize("hidden", [64, 256])
+def test_fused_ln_dropout_backward_matches_unfused(hidden):
+    """bf16 transformer blocks: the fused backward (each block's LayerNorm backward also writes
+    the previous block's bf16 dropout(dx), and leaves its dgamma/dbeta partial rows to the
+    weight-gradient slab-sum launch) against the unfused launches, residual dropout on.  Every
+    gradient is bitwise equal except the LayerNorm parameters (partials added in another fixed
+    order, rel 1e-5); hidden 256 runs the 4-wide kernel with the in-kernel dropout copy, hidden
+    64 the generic kernel + retr_dropout_apply inside retr_layernorm_bwd2."""
+    from retr_amd import ops
+    cfg = make_config(backbone="ResNet18", hidden=hidden, layers=(2, 2), vocab=1000, max_pos=16,
+                      ffn=2 * hidden, dtype="bf16", dropout=0.1)
+    model, crit = build_model(cfg)
+    model.load_state_dict(synthetic_state_dict(model, seed=3))
+    model.to(DEV).train()
+    images, mask = synthetic_images(2, 64, seed=1, pad_band=True)
+    caps, cap_mask = synthetic_captions(2, 16, 1000, seed=2)
+    s = NestedTensor(images.to(DEV), mask.to(DEV))
+    ctr = ops._seed_state["ctr"]
+    res = []
+    try:
+        for fuse in (True, False):
+            ops.FUSE_LN_BWD = fuse
+            ops._seed_state["ctr"] = ctr
+            ops.DBR_STATS.update(hit=0, miss=0)
+            model.zero_grad(set_to_none=True)
+            out = model(s, caps[:, :-1].to(DEV), cap_mask[:, :-1].to(DEV))
+            loss = crit(out.permute(0, 2, 1), caps[:, 1:].to(DEV))
+            loss.backward()
+            torch.cuda.synchronize()
+            res.append(({n: p.grad.detach().clone() for n, p in model.named_parameters()
+                         if p.grad is not None}, dict(ops.DBR_STATS), loss.item()))
+    finally:
+        ops.FUSE_LN_BWD = True
+    (g1, st1, l1), (g0, st0, l0) = res
+    assert l1 == l0
+    # every block but the first of each stack takes its incoming gradient from the cache
+    assert st1["hit"] == (2 * 2 - 1) + (3 * 2 - 1), st1
+    assert st0["hit"] == 0
+    assert g1.keys() == g0.keys() and len(g1) > 0
+    for n in g1:
+        if ".norm" in n or "norm1" in n or "norm2" in n or "norm3" in n:
+            e = ((g1[n] - g0[n]).double().norm() / (g0[n].double().norm() + 1e-30)).item()
+            assert e < 1e-5, (n, e)
+        else:
+            assert torch.equal(g1[n], g0[n]), n

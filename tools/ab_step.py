@@ -24,13 +24,20 @@ VARIANTS = {
     "side_bb": {("OVERLAP", "backbone"): True},
     "side_tr": {("OVERLAP", "transformer"): True},
     "side_all": {("OVERLAP", "backbone"): True, ("OVERLAP", "transformer"): True},
+    "nofuse_ln": {("ATTR", "FUSE_LN_BWD"): False},
+    "no_lnparams": {("ATTR", "FUSE_LN_PARAMS"): False},
 }
 
 
 def apply(v):
     ops.OVERLAP.update({"backbone": False, "transformer": False})
+    ops.FUSE_LN_BWD = True
+    ops.FUSE_LN_PARAMS = True
     for (table, key), val in VARIANTS[v].items():
-        getattr(ops, table)[key] = val
+        if table == "ATTR":
+            setattr(ops, key, val)
+        else:
+            getattr(ops, table)[key] = val
 
 
 def main():
