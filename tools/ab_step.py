@@ -14,7 +14,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
-from retr_amd import ops  # noqa: E402
+from retr_amd import ops, resnet  # noqa: E402
 from retr_amd.engine import GraphedTrainStep  # noqa: E402
 from retr_amd.models.utils import NestedTensor  # noqa: E402
 from retr_amd.synthetic import synthetic_captions, synthetic_images  # noqa: E402
@@ -36,6 +36,8 @@ def apply(v):
     for (table, key), val in VARIANTS[v].items():
         if table == "ATTR":
             setattr(ops, key, val)
+        elif table == "RESNET":
+            setattr(resnet, key, val)
         else:
             getattr(ops, table)[key] = val
 
