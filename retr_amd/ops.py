@@ -523,9 +523,44 @@ FUSE_LN_PARAMS = True   # dgamma / dbeta partials into the wgrad slab sum (else 
 DBR_STATS = {"hit": 0, "miss": 0}
 
 
+# Gradients of a tensor several blocks read (the decoder's query positions: 12 blocks; the
+# encoder memory and its positional sum: the 6 cross-attention blocks): every contributor adds
+# into ONE buffer in its own kernel (retr_pos_grad adds; the data-gradient GEMM epilogue takes
+# the buffer as addend) and only the last one in backward order returns it -- instead of a
+# zero-filled buffer per block and autograd's pairwise adds.
+_SHARED = {}   # id(tensor) -> [contributors left, buffer or None]
+
+
 def begin_pass():
-    """Forget the previous pass's unused fused dropout-gradient copies."""
+    """Forget the previous pass's unused fused dropout-gradient copies and shared gradients."""
     _DBR.clear()
+    _SHARED.clear()
+
+
+def _share(t):
+    """Forward: one more block will contribute to the gradient of ``t``."""
+    e = _SHARED.get(id(t))
+    if e is None:
+        _SHARED[id(t)] = e = [0, None, t]
+    e[0] += 1
+
+
+def _shared_grad(t, make):
+    """Backward: (buffer, first, last) -- the shared gradient buffer of ``t`` (made by ``make``
+    for its first contributor) and whether this contributor is the first / last one; an
+    unregistered ``t`` gets a buffer of its own (first = last = True)."""
+    e = _SHARED.get(id(t))
+    if e is None or e[0] <= 0:
+        return make(), True, True
+    first = e[1] is None
+    if first:
+        e[1] = make()
+    e[0] -= 1
+    last = e[0] == 0
+    buf = e[1]
+    if last:
+        del _SHARED[id(t)]
+    return buf, first, last
 
 
 def _tag_drop(out, drop_p, seed):
@@ -575,9 +610,11 @@ def _ln_bwd_fused(x, gamma, beta, mean, rstd, dy, dy2, addend, prev, cdtype, pos
     extra = [(ws, 2 * C, n, C, dgamma, 1), (ws[C:], 2 * C, n, C, dbeta, 1)] if n > 0 else []
     dpos = None
     if need_dpos and dy2 is not None:
-        dpos, _ = grad_buffer(pos)
+        dpos, _, last = _shared_grad(pos, lambda: grad_buffer(pos)[0])
         call("retr_pos_grad", dcode(dy2.dtype), ptr(dy2), dy2.stride(0), M, C, int(period),
-             ptr(dpos), _st())
+             ptr(dpos), _st())            # adds into the (zeroed or shared) buffer
+        if not last:
+            dpos = None
     return dx, dgamma, dbeta, dpos, extra
 
 
@@ -620,6 +657,8 @@ class _SelfAttnBlock(torch.autograd.Function):
         ctx.cfg = (B, L, H, causal, drop_attn, drop_res, s_att, s_res, cdtype)
         ctx.prev = getattr(x, "_retr_drop", None)
         _tag_drop(out, drop_res, s_res)
+        if cdtype == torch.bfloat16 and FUSE_LN_BWD and pos is not None and pos.requires_grad:
+            _share(pos)
         if want_probs:
             ctx.mark_non_differentiable(probs)
             return out, probs
@@ -705,6 +744,13 @@ class _CrossAttnBlock(torch.autograd.Function):
         ctx.cfg = (B, Lq, Lk, H, drop_attn, drop_res, s_att, s_res, cdtype)
         ctx.prev = getattr(y, "_retr_drop", None)
         _tag_drop(out, drop_res, s_res)
+        ctx.shared = cdtype == torch.bfloat16 and FUSE_LN_BWD
+        if ctx.shared:
+            if qp is not None and qp.requires_grad:
+                _share(qp)
+            for t in (mem_pos, mem):
+                if t.requires_grad:
+                    _share(t)
         if want_probs:
             ctx.mark_non_differentiable(probs)
             return out, probs
@@ -737,10 +783,21 @@ class _CrossAttnBlock(torch.autograd.Function):
         k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, False, drop_attn,
                         s_att)
         dqpos = torch.empty(Mq, C, dtype=cdtype, device=dev)
-        dmem_pos = torch.empty(Mk, C, dtype=cdtype, device=dev)
-        dmem = torch.empty(Mk, C, dtype=cdtype, device=dev)
-        k_linear_dgrad_group([(dq, wint[:, :C], dqpos), (dk, wint[:, C: 2 * C], dmem_pos),
-                              (dv, wint[:, 2 * C:], dmem)])
+        if ctx.shared:
+            def mk():
+                return torch.empty(Mk, C, dtype=cdtype, device=dev)
+            dmem_pos, f_mp, l_mp = _shared_grad(mem_pos, mk)
+            dmem, f_m, l_m = _shared_grad(mem, mk)
+            # later contributors add the earlier ones' sum in the GEMM epilogue (in place)
+            k_linear_dgrad_group([(dq, wint[:, :C], dqpos),
+                                  (dk, wint[:, C: 2 * C], dmem_pos, None if f_mp else dmem_pos),
+                                  (dv, wint[:, 2 * C:], dmem, None if f_m else dmem)])
+        else:
+            dmem_pos = torch.empty(Mk, C, dtype=cdtype, device=dev)
+            dmem = torch.empty(Mk, C, dtype=cdtype, device=dev)
+            l_mp = l_m = True
+            k_linear_dgrad_group([(dq, wint[:, :C], dqpos), (dk, wint[:, C: 2 * C], dmem_pos),
+                                  (dv, wint[:, 2 * C:], dmem)])
         wg = [(dbr, o, dw_out, db_out, True), (dq, qpos, dw_in[:C], db_in[:C], True),
               (dk, mem_pos, dw_in[C: 2 * C], db_in[C: 2 * C], True),
               (dv, mem, dw_in[2 * C:], db_in[2 * C:], True)]
@@ -754,8 +811,8 @@ class _CrossAttnBlock(torch.autograd.Function):
             k_linear_wgrad_group(wg)
             dy, dlw, dlb, dqp = _ln_bwd(y, ln_w, ln_b, mean, rstd, None, dqpos, dout, qp, period,
                                         ctx.needs_input_grad[3])
-        return (dy, dlw, dlb, dqp, None, None, dmem_pos, dmem, dw_in, db_in, dw_out,
-                db_out) + (None,) * 9
+        return (dy, dlw, dlb, dqp, None, None, dmem_pos if l_mp else None,
+                dmem if l_m else None, dw_in, db_in, dw_out, db_out) + (None,) * 9
 
 
 class _FFNBlock(torch.autograd.Function):

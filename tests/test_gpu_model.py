@@ -236,8 +236,10 @@ def test_fused_ln_dropout_backward_matches_unfused(hidden):
     the previous block's bf16 dropout(dx), and leaves its dgamma/dbeta partial rows to the
     weight-gradient slab-sum launch) against the unfused launches, residual dropout on.  Every
     gradient is bitwise equal except the LayerNorm parameters (partials added in another fixed
-    order, rel 1e-5); hidden 256 runs the 4-wide kernel with the in-kernel dropout copy, hidden
-    64 the generic kernel + retr_dropout_apply inside retr_layernorm_bwd2."""
+    order, rel 1e-5); the memory gradients of the six cross-attention blocks are summed in the
+    data-gradient GEMM epilogues instead of by autograd (bf16 tolerance upstream of the memory);
+    hidden 256 runs the 4-wide kernel with the in-kernel dropout copy, hidden 64 the generic
+    kernel + retr_dropout_apply inside retr_layernorm_bwd2."""
     from retr_amd import ops
     cfg = make_config(backbone="ResNet18", hidden=hidden, layers=(2, 2), vocab=1000, max_pos=16,
                       ffn=2 * hidden, dtype="bf16", dropout=0.1)
@@ -269,9 +271,17 @@ def test_fused_ln_dropout_backward_matches_unfused(hidden):
     assert st1["hit"] == (2 * 2 - 1) + (3 * 2 - 1), st1
     assert st0["hit"] == 0
     assert g1.keys() == g0.keys() and len(g1) > 0
+    def rel(n):
+        return ((g1[n] - g0[n]).double().norm() / (g0[n].double().norm() + 1e-30)).item()
+
     for n in g1:
-        if ".norm" in n or "norm1" in n or "norm2" in n or "norm3" in n:
-            e = ((g1[n] - g0[n]).double().norm() / (g0[n].double().norm() + 1e-30)).item()
-            assert e < 1e-5, (n, e)
-        else:
+        dec = "transformer.decoder" in n or n.startswith("mlp") or "embeddings" in n
+        if dec and (".norm" in n or "position_embeddings" in n):
+            # partials / per-block contributions added in another fixed order
+            assert rel(n) < 1e-5, (n, rel(n))
+        elif dec:
             assert torch.equal(g1[n], g0[n]), n
+        else:
+            # upstream of the memory: the six cross-attention blocks' bf16 memory gradients
+            # are summed in the GEMM epilogues (one bf16 rounding fewer per add)
+            assert rel(n) < 2e-2, (n, rel(n))
