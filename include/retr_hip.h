@@ -388,6 +388,12 @@ int retr_adamw_update(float* param, float* grad, float* exp_avg, float* exp_avg_
                       const float* hyper, double beta1, double beta2, float eps,
                       const float* step, float step_offset, const float* partials, int nparts,
                       float max_norm, void* param_bf16, void* stream);
+/* retr_adamw_update with zero_grad = 1: the gradient arena range is zeroed by the update (the
+ * clipped gradient is not written back) -- GraphedTrainStep's consume mode */
+int retr_adamw_update2(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n,
+                       const float* hyper, double beta1, double beta2, float eps,
+                       const float* step, float step_offset, const float* partials, int nparts,
+                       float max_norm, void* param_bf16, int zero_grad, void* stream);
 
 /* ---- fused incremental-decode step (csrc/decode.hip; eval_utils/decode.py:53-81 in KV-cache
  * form, decoder layer models/ConcatTransformer.py:187-214 + transformer_modules.py:22-97).

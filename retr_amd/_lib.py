@@ -149,6 +149,7 @@ _SIGS = {
     "retr_dec_ffn": [_P, _I, _I, _P, _P, _P, _I, _P, _P],
     "retr_adamw_sumsq": [_P, _L, _P, _I, _P, _P],
     "retr_adamw_update": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P, _P],
+    "retr_adamw_update2": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P, _I, _P],
 }
 _RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
             "retr_layernorm_bwd_workspace": _SZ, "retr_embed_ln_bwd_workspace": _SZ,

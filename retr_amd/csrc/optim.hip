@@ -12,7 +12,9 @@
 //      then one fused pass  p *= 1-lr*wd;  g *= coef;  m = lerp(m, g, 1-b1);
 //      v = b2 v + (1-b2) g^2;  p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps).
 // HBM traffic per element: read p g m v, write p m v (+ g when clipped) = 28-32 bytes,
-// + 2 bytes when the bf16 parameter shadow is written.
+// + 2 bytes when the bf16 parameter shadow is written.  retr_adamw_update2(zero_grad = 1)
+// writes g = 0 instead (the captured training step consumes its gradients: no separate
+// 260 MB zero fill of the arena at the next step).
 #include "common.hpp"
 
 namespace {
@@ -54,7 +56,7 @@ adamw_sumsq_kernel(const float4* g, long n4, float* partials, float* step) {
 __global__ void __launch_bounds__(kThreads)
 adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const float* hyper,
                     double beta1, double beta2, float eps, const float* step, float step_offset,
-                    const float* partials, int nparts, float max_norm, bf16* p16) {
+                    const float* partials, int nparts, float max_norm, bf16* p16, int zero_g) {
   __shared__ float red[16];
   float coef = 1.f;
   if (max_norm > 0.f) {
@@ -89,7 +91,8 @@ adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const f
       ve[e] = vr;
     }
     p[i] = pp; m[i] = mm; v[i] = vv;
-    if (scale) g[i] = gg;
+    if (zero_g) g[i] = float4{0.f, 0.f, 0.f, 0.f};   // consumed: the next step's arena is clean
+    else if (scale) g[i] = gg;
     if (p16) {   // bf16 shadow of the parameters: the GEMM weight operands, no cast launches
       typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
       *(bf16x4*)(p16 + 4 * i) = bf16x4{(bf16)pp.x, (bf16)pp.y, (bf16)pp.z, (bf16)pp.w};
@@ -100,6 +103,11 @@ adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const f
 }  // namespace
 
 extern "C" {
+
+int retr_adamw_update2(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n,
+                       const float* hyper, double beta1, double beta2, float eps,
+                       const float* step, float step_offset, const float* partials, int nparts,
+                       float max_norm, void* param_bf16, int zero_grad, void* stream);
 
 int retr_adamw_sumsq(const float* grad, long n, float* partials, int nparts, float* step,
                      void* stream) {
@@ -114,6 +122,14 @@ int retr_adamw_update(float* param, float* grad, float* exp_avg, float* exp_avg_
                       const float* hyper, double beta1, double beta2, float eps,
                       const float* step, float step_offset, const float* partials, int nparts,
                       float max_norm, void* param_bf16, void* stream) {
+  return retr_adamw_update2(param, grad, exp_avg, exp_avg_sq, n, hyper, beta1, beta2, eps, step,
+                            step_offset, partials, nparts, max_norm, param_bf16, 0, stream);
+}
+
+int retr_adamw_update2(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n,
+                       const float* hyper, double beta1, double beta2, float eps,
+                       const float* step, float step_offset, const float* partials, int nparts,
+                       float max_norm, void* param_bf16, int zero_grad, void* stream) {
   RETR_REQUIRE(n % 4 == 0, "adamw_update: n must be a multiple of 4");
   RETR_REQUIRE((((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15) == 0,
                "adamw_update: 16-byte alignment");
@@ -124,7 +140,7 @@ int retr_adamw_update(float* param, float* grad, float* exp_avg, float* exp_avg_
   hipLaunchKernelGGL(adamw_update_kernel, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream,
                      (float4*)param, (float4*)grad, (float4*)exp_avg, (float4*)exp_avg_sq, n4,
                      hyper, beta1, beta2, eps, step, step_offset, partials, nparts, max_norm,
-                     (bf16*)param_bf16);
+                     (bf16*)param_bf16, zero_grad);
   return retr_check_launch("adamw_update");
 }
 

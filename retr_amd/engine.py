@@ -103,6 +103,9 @@ class GraphedTrainStep:
     def __init__(self, model, criterion, optimizer, max_norm, grad_sync=None, warmup=2):
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
         self.max_norm, self.grad_sync, self.warmup = max_norm, grad_sync, warmup
+        if hasattr(optimizer, "consume_grads"):
+            # FusedAdamW zeroes the gradient arena in its update: no zero fill per replay
+            optimizer.consume_grads = True
         self.graph = None
         self.graph_opt = None
         self.segments = []        # DP: forward/backward segment graphs (segments[0] is graph)

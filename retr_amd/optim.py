@@ -118,6 +118,10 @@ class FusedAdamW(torch.optim.Optimizer):
         # read (ops._WeightCache hands out p._retr_shadow while it is current)
         self.P16 = torch.empty(total, dtype=torch.bfloat16, device=dev) if self._shadow else None
         self.arena = _GradArena(self.G)
+        # consume mode (set by engine.GraphedTrainStep): the update zeroes the stepped gradient
+        # ranges instead of writing the clipped gradients back, so the next step needs no zero
+        # fill of the arena; p.grad then reads zero after step()
+        self.consume_grads = False
         self._step_t = torch.zeros(1, dtype=torch.float32, device=dev)   # device step count
         self._global = 0                                  # host mirror of _step_t
         self._counts = {id(p): 0 for p in plist}          # per-parameter step (torch semantics)
@@ -178,9 +182,10 @@ class FusedAdamW(torch.optim.Optimizer):
                     p.grad = None
                 elif p.grad.data_ptr() != p._retr_grad_view.data_ptr():
                     p.grad.zero_()
-        if torch.cuda.is_current_stream_capturing():
+        if torch.cuda.is_current_stream_capturing() and not self.consume_grads:
             # a captured step must clear G on every replay, whatever the host-side dirty flag
-            # says at capture time (the memset before capture leaves it False)
+            # says at capture time (the memset before capture leaves it False); in consume mode
+            # every replay's update leaves G zero instead
             self.arena.dirty = True
         self.arena.reset()
         if not set_to_none:
@@ -248,16 +253,24 @@ class FusedAdamW(torch.optim.Optimizer):
             if tuple(g["betas"]) != (b1, b2) or g["eps"] != eps:
                 b1, b2 = g["betas"]
                 eps = g["eps"]
-            call("retr_adamw_update", ptr(self.P) + 4 * lo, ptr(self.G) + 4 * lo,
+            call("retr_adamw_update2", ptr(self.P) + 4 * lo, ptr(self.G) + 4 * lo,
                  ptr(self.M) + 4 * lo, ptr(self.V) + 4 * lo, hi - lo, ptr(self._hyper) + 8 * gi,
                  float(b1), float(b2), float(eps), ptr(self._step_t), float(off),
                  ptr(self._partials), nparts, float(max_norm) if clip else 0.0,
-                 ptr(self.P16) + 2 * lo if self.P16 is not None else None, st)
+                 ptr(self.P16) + 2 * lo if self.P16 is not None else None,
+                 int(self.consume_grads), st)
         self._advance_host(active)
         self._last_active = active
-        for p in foreign:          # clipped values back into gradients living elsewhere
-            if clip:
-                p.grad.copy_(p._retr_grad_view)
+        if self.consume_grads:
+            # the update zeroed G over every stepped range; the arena is clean for the next
+            # step unless a handed-out slot belongs to a parameter that was not stepped
+            stepped = {id(p) for p in active}
+            if self.arena.handed <= stepped:
+                self.arena.dirty = False
+        else:
+            for p in foreign:      # clipped values back into gradients living elsewhere
+                if clip:
+                    p.grad.copy_(p._retr_grad_view)
         _bump_versions(self.param_groups)
         self.mark_shadow_fresh(active)     # the update wrote their shadow too
         return loss
