@@ -308,6 +308,24 @@ int retr_attention_bwd(int dtype, const void* q, long ldq, const void* k, long l
                        const unsigned char* kpm, int causal, float drop_p,
                        unsigned long long seed, float* workspace, void* stream);
 size_t retr_attention_bwd_workspace(int B, int H, int Lq);
+/* The same pair with the attention-dropout keep decisions saved by the forward: dmask
+ * (retr_attention_dropout_mask_bytes) receives one bit per score ([B*H][ceil(Lk/32)][Lq]
+ * uint32 words) from retr_attention_fwd_dm when drop_p > 0 on the bf16 head-dim 32/64 kernels,
+ * and retr_attention_bwd_dm reads it instead of regenerating every decision from the hash --
+ * the same bits, so the same results.  Paths that do not use it leave / ignore it. */
+size_t retr_attention_dropout_mask_bytes(int B, int H, int Lq, int Lk);
+int retr_attention_fwd_dm(int dtype, const void* q, long ldq, const void* k, long ldk,
+                          const void* v, long ldv, void* o, long ldo, int B, int H, int Lq,
+                          int Lk, int hd, const unsigned char* kpm, int causal, float drop_p,
+                          unsigned long long seed, float* lse, float* probs, void* dmask,
+                          void* stream);
+int retr_attention_bwd_dm(int dtype, const void* q, long ldq, const void* k, long ldk,
+                          const void* v, long ldv, const void* o, long ldo, const void* dout,
+                          long lddo, const float* lse, void* dq, long lddq, void* dk, long lddk,
+                          void* dv, long lddv, int B, int H, int Lq, int Lk, int hd,
+                          const unsigned char* kpm, int causal, float drop_p,
+                          unsigned long long seed, float* workspace, const void* dmask,
+                          void* stream);
 /* decode step: q [B][.] one query row per caption (or beam); k/v with Lmax rows per kv batch,
  * first Lk valid.  Query row r attends kv batch r / kv_group (kv_group = beams per image for
  * the shared cross-attention memory, else 1); with `anc` (int32 [B][Lmax], beam search) key j

@@ -123,6 +123,11 @@ _SIGS = {
     "retr_attention_bwd": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _P, _L, _P, _L, _P,
                            _L, _I, _I, _I, _I, _I, _P, _I, _F, _U64, _P, _P],
     "retr_attention_bwd_workspace": [_I, _I, _I],
+    "retr_attention_fwd_dm": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _P, _I, _F,
+                              _U64, _P, _P, _P, _P],
+    "retr_attention_bwd_dm": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _P, _L, _P, _P, _L, _P, _L,
+                              _P, _L, _I, _I, _I, _I, _I, _P, _I, _F, _U64, _P, _P, _P],
+    "retr_attention_dropout_mask_bytes": [_I, _I, _I, _I],
     "retr_attention_decode": [_I, _P, _L, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _I, _P, _I,
                               _P, _P],
     "retr_topk_rows": [_I, _P, _L, _I, _I, _I, _P, _P, _P],
@@ -152,6 +157,7 @@ _SIGS = {
     "retr_adamw_update2": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P, _I, _P],
 }
 _RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
+            "retr_attention_dropout_mask_bytes": _SZ,
             "retr_layernorm_bwd_workspace": _SZ, "retr_embed_ln_bwd_workspace": _SZ,
             "retr_linear_wgrad_group_workspace": _SZ, "retr_argmax_workspace": _SZ,
             "retr_set_deterministic": None,

@@ -18,13 +18,13 @@
 int retr_attention_fwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
                         long ldv, void* o, long ldo, int B, int H, int Lq, int Lk, int hd,
                         const unsigned char* kpm, int causal, float p, unsigned long long seed,
-                        float* lse, hipStream_t st);
+                        float* lse, uint32_t* dmask, hipStream_t st);
 int retr_attention_bwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
                         long ldv, const void* o, long ldo, const void* dout, long lddo,
                         const float* lse, void* dq, long lddq, void* dk, long lddk, void* dv,
                         long lddv, int B, int H, int Lq, int Lk, int hd,
                         const unsigned char* kpm, int causal, float p, unsigned long long seed,
-                        float* D, hipStream_t st);
+                        float* D, const uint32_t* dmask, hipStream_t st);
 
 using namespace retr;
 
@@ -588,13 +588,26 @@ int retr_attention_fwd(int dtype, const void* q, long ldq, const void* k, long l
                        const void* v, long ldv, void* o, long ldo, int B, int H, int Lq, int Lk,
                        int hd, const unsigned char* kpm, int causal, float drop_p,
                        unsigned long long seed, float* lse, float* probs, void* stream) {
+  return retr_attention_fwd_dm(dtype, q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, hd, kpm,
+                               causal, drop_p, seed, lse, probs, nullptr, stream);
+}
+
+size_t retr_attention_dropout_mask_bytes(int B, int H, int Lq, int Lk) {
+  return sizeof(uint32_t) * (size_t)B * H * (size_t)((Lk + 31) / 32) * (size_t)Lq;
+}
+
+int retr_attention_fwd_dm(int dtype, const void* q, long ldq, const void* k, long ldk,
+                          const void* v, long ldv, void* o, long ldo, int B, int H, int Lq,
+                          int Lk, int hd, const unsigned char* kpm, int causal, float drop_p,
+                          unsigned long long seed, float* lse, float* probs, void* dmask,
+                          void* stream) {
   RETR_REQUIRE(hd >= 8 && hd <= 64 && hd % 8 == 0, "attention: head dim %d unsupported", hd);
   RETR_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0, "attention: row strides %%8");
   if (B == 0 || Lq == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == RETR_BF16 && (hd == 32 || hd == 64) && ldo % 4 == 0) {
     if (int e = retr_attention_fwd2(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, hd, kpm,
-                                    causal, drop_p, seed, lse, st))
+                                    causal, drop_p, seed, lse, (uint32_t*)dmask, st))
       return e;
     return probs ? launch_probs<bf16>(q, ldq, k, ldk, B, H, Lq, Lk, hd, kpm, causal, lse, probs, st)
                  : 0;
@@ -642,6 +655,18 @@ int retr_attention_bwd(int dtype, const void* q, long ldq, const void* k, long l
                        void* dv, long lddv, int B, int H, int Lq, int Lk, int hd,
                        const unsigned char* kpm, int causal, float drop_p,
                        unsigned long long seed, float* workspace, void* stream) {
+  return retr_attention_bwd_dm(dtype, q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq,
+                               dk, lddk, dv, lddv, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed,
+                               workspace, nullptr, stream);
+}
+
+int retr_attention_bwd_dm(int dtype, const void* q, long ldq, const void* k, long ldk,
+                          const void* v, long ldv, const void* o, long ldo, const void* dout,
+                          long lddo, const float* lse, void* dq, long lddq, void* dk, long lddk,
+                          void* dv, long lddv, int B, int H, int Lq, int Lk, int hd,
+                          const unsigned char* kpm, int causal, float drop_p,
+                          unsigned long long seed, float* workspace, const void* dmask,
+                          void* stream) {
   RETR_REQUIRE(hd >= 8 && hd <= 64 && hd % 8 == 0, "attention: head dim %d unsupported", hd);
   RETR_REQUIRE(ldq % 8 == 0 && ldk % 8 == 0 && ldv % 8 == 0 && lddo % 8 == 0,
                "attention: row strides %%8");
@@ -651,7 +676,7 @@ int retr_attention_bwd(int dtype, const void* q, long ldq, const void* k, long l
       lddv % 4 == 0)
     return retr_attention_bwd2(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk,
                                lddk, dv, lddv, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed,
-                               workspace, st);
+                               workspace, (const uint32_t*)dmask, st);
   if (dtype == RETR_BF16) {
     if (hd <= 32) return bwd_t<bf16, 32>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed, workspace, st);
     return bwd_t<bf16, 64>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed, workspace, st);

@@ -91,6 +91,19 @@ RETR_DEVICE void mask_tile(f32x16 (&S)[2], unsigned long long pmask, bool diag, 
     }
 }
 
+// Dropout keep bits saved by the forward for the backward kernels (retr_attention_fwd_dm /
+// retr_attention_bwd_dm): word (bh, w, q) = bits of keys 32 w .. 32 w + 31 of query row q of
+// (batch, head) bh, laid out [B*H][ceil(Lk/32)][Lq] so that both the forward's stores (lane =
+// query) and the key-on-lane backward's loads (one word per query, 4 queries per 16 bytes) are
+// contiguous.  The bits are the hash decisions themselves: the backward reads them instead of
+// re-hashing every score (~10 VALU per score in the key-on-lane kernel).
+RETR_DEVICE void store_dmask(uint32_t* dmask, uint32_t wbits, int hh, int bh, int Lq, int Lk,
+                             int qi, int w) {
+  const uint32_t full = wbits | (uint32_t)__shfl_xor((int)wbits, 32, 64);
+  const int nw = (Lk + 31) / 32;
+  if (hh == 0 && qi < Lq && w < nw) dmask[((long)bh * nw + w) * Lq + qi] = full;
+}
+
 template <int HD>
 struct Tile {
   static constexpr int KT = 64;              // keys per LDS stage
@@ -137,7 +150,7 @@ template <int HD, int NW>
 __global__ void __launch_bounds__(NW * 64)
 attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
                  bf16* o, long ldo, int H, int Lq, int Lk, int kbr, const unsigned char* kpm,
-                 int causal, float qscale, DropoutParams dp, float* lse) {
+                 int causal, float qscale, DropoutParams dp, float* lse, uint32_t* dmask) {
   using TL = Tile<HD>;
   constexpr int NT = NW * 64, KS = HD / 16, DT = HD / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -229,6 +242,7 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
     bf16x8 pf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
+      uint32_t wbits = 0;                          // keep bits of keys key0 + 32 sub + j
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int kk = key0 + sub * 32 + 8 * g + 4 * hh;   // 4 consecutive keys
@@ -242,10 +256,15 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
           const int e = 4 * g + e4;
           float p = __builtin_amdgcn_exp2f(S[sub][e] - ms);
           l += p;
-          if (drop) p = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? p : 0.f;
+          if (drop) {
+            const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
+            wbits |= (uint32_t)kp << (8 * g + 4 * hh + e4);
+            p = kp ? p : 0.f;
+          }
           pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
         }
       }
+      if (drop && dmask) store_dmask(dmask, wbits, hh, (b * H + h), Lq, Lk, qi, key0 / 32 + sub);
     }
     // O^T += V^T P^T  (A = V^T via transposed LDS reads, B = P in registers)
 #pragma unroll
@@ -287,13 +306,13 @@ template <int HD, int NW>
 int launch_fwd2(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
                 void* o, long ldo, int B, int H, int Lq, int Lk, int kbr,
                 const unsigned char* kpm, int causal, float p, unsigned long long seed,
-                float* lse, hipStream_t st) {
+                float* lse, uint32_t* dmask, hipStream_t st) {
   const float qscale = kLog2e / sqrtf((float)HD);
   const size_t lds = 2 * Tile<HD>::STAGE;
   dim3 grid((Lq + 32 * NW - 1) / (32 * NW), H, B);
   hipLaunchKernelGGL((attn_fwd2_kernel<HD, NW>), grid, dim3(NW * 64), lds, st, (const bf16*)q,
                      ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, H, Lq, Lk, kbr,
-                     kpm, causal, qscale, make_dp(p, seed), lse);
+                     kpm, causal, qscale, make_dp(p, seed), lse, dmask);
   return retr_check_launch("attention_fwd2");
 }
 
@@ -353,13 +372,16 @@ RETR_DEVICE void dma_drain_barrier() {
 template <int HD>
 size_t res_lds_fwd(int ntiles) { return (size_t)2 * ntiles * RL<HD>::TILE + 8 * ntiles; }
 template <int HD>
-size_t res_lds_dkdv(int ntiles) { return (size_t)2 * ntiles * RL<HD>::TILE + 12 * 64 * ntiles; }
+size_t res_lds_dkdv(int ntiles) {   // Q, dO tiles; lse, D, row keys; 4 waves' keep-bit columns
+  return (size_t)2 * ntiles * RL<HD>::TILE + (12 + 4 * 4) * 64 * ntiles;
+}
 
 template <int HD, int NW>
 __global__ void __launch_bounds__(NW * 64)
 attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
                  bf16* o, long ldo, int H, int Lq, int Lk, int kbr, const unsigned char* kpm,
-                 int causal, float qscale, DropoutParams dp, float* lse, int ntiles_max) {
+                 int causal, float qscale, DropoutParams dp, float* lse, int ntiles_max,
+                 uint32_t* dmask) {
   using L = RL<HD>;
   constexpr int KS = HD / 16, DT = HD / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -454,6 +476,7 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
     bf16x8 pf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
+      uint32_t wbits = 0;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int kk = key0 + sub * 32 + 8 * g + 4 * hh;
@@ -467,10 +490,15 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
           const int e = 4 * g + e4;
           float p = __builtin_amdgcn_exp2f(S[sub][e] - ms);
           l += p;
-          if (drop) p = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? p : 0.f;
+          if (drop) {
+            const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
+            wbits |= (uint32_t)kp << (8 * g + 4 * hh + e4);
+            p = kp ? p : 0.f;
+          }
           pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
         }
       }
+      if (drop && dmask) store_dmask(dmask, wbits, hh, (b * H + h), Lq, Lk, qi, key0 / 32 + sub);
     }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
@@ -522,7 +550,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
                     const bf16* o, long ldo, const bf16* dout, long lddo, const float* lse,
                     float* Dout, bf16* dq, long lddq, int H, int Lq, int Lk,
                     const unsigned char* kpm, int causal, float qscale, float scale,
-                    DropoutParams dp, int ntiles_max) {
+                    DropoutParams dp, int ntiles_max, const uint32_t* dmask) {
   using L = RL<HD>;
   constexpr int KS = HD / 16, DT = HD / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -580,6 +608,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
   const bool drop = dp.thresh != 0;
   const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
   const uint32_t rowkey = drop ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
+  const int nwm = (Lk + 31) / 32;
 
   f32x16 G[DT];
 #pragma unroll
@@ -600,6 +629,14 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
     const unsigned long long pml = pmask >> (4 * hh);
     const uint32_t pmlo = (uint32_t)pml, pmhi = (uint32_t)(pml >> 32);
     const int mlim = qi - key0 - 4 * hh;
+    uint32_t wm[2] = {0u, 0u};                     // saved keep bits of the tile's two sub-tiles
+    if (drop && dmask) {
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const int w = min(key0 / 32 + sub, nwm - 1);
+        wm[sub] = dmask[((long)(b * H + h) * nwm + w) * Lq + qc];
+      }
+    }
     bf16x8 sf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
@@ -616,7 +653,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
       for (int g = 0; g < 4; ++g) {
         const int kk = key0 + sub * 32 + 8 * g + 4 * hh;
         uint32_t b01 = 0, b23 = 0;
-        if (drop) {
+        if (drop && !dmask) {
           b01 = attn_pair_bits(rowkey, kk);
           b23 = attn_pair_bits(rowkey, kk + 2);
         }
@@ -626,7 +663,11 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
           const bool msk = anym & key_masked(pmlo, pmhi, kl - 4 * hh, diag, mlim);
           const float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - lq2);
           float dpv = P[e];
-          if (drop) dpv = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? dpv * dp.scale : 0.f;
+          if (drop) {
+            const bool kp = dmask ? ((wm[sub] >> (8 * g + 4 * hh + e4)) & 1u) != 0u
+                                  : attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
+            dpv = kp ? dpv * dp.scale : 0.f;
+          }
           sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - Dq));
         }
       }
@@ -665,7 +706,7 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
                       long ldv, const bf16* dout, long lddo, const float* lse, const float* D,
                       bf16* dk, long lddk, bf16* dv, long lddv, int H, int Lq, int Lk,
                       const unsigned char* kpm, int causal, float kscale, float scale,
-                      DropoutParams dp, int ntiles_max) {
+                      DropoutParams dp, int ntiles_max, const uint32_t* dmask) {
   using L = RL<HD>;
   constexpr int KS = HD / 16, DT = HD / 32, NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -692,6 +733,8 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
   float* exl = (float*)(smem + (size_t)2 * ntiles_max * L::TILE);   // lse * log2e
   float* exd = exl + 64 * ntiles_max;                                 // D
   uint32_t* exk = (uint32_t*)(exd + 64 * ntiles_max);                 // dropout row keys
+  // with saved keep bits: this wave's word column (its 32 keys) for every resident query
+  uint32_t* exw = exk + 64 * ntiles_max + wave * 64 * ntiles_max;
   dma_rows<HD, NW>(Qs, qb + (long)qstart * ldq, ldq, ntiles, Lq - qstart, wave, lane);
   dma_rows<HD, NW>(Ds, db + (long)qstart * lddo, lddo, ntiles, Lq - qstart, wave, lane);
   for (int i = tid; i < ntiles * 64; i += NT) {
@@ -699,7 +742,17 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
     const int qcl = qq < Lq ? qq : Lq - 1;
     exl[i] = lse[sbase + qcl] * kLog2e;
     exd[i] = D[sbase + qcl];
-    exk[i] = drop ? attn_row_key(seed, (uint32_t)((b * H + h) * Lq) + (uint32_t)qq) : 0u;
+    exk[i] = (drop && !dmask) ? attn_row_key(seed, (uint32_t)((b * H + h) * Lq) + (uint32_t)qq)
+                              : 0u;
+  }
+  if (drop && dmask) {
+    const int nwm = (Lk + 31) / 32;
+    const int wc = min((kblk + wave * 32) / 32, nwm - 1);
+    const uint32_t* col = dmask + ((long)(b * H + h) * nwm + wc) * Lq;
+    for (int i = lane; i < ntiles * 64; i += 64) {
+      const int qq = qstart + i;
+      exw[i] = qq < Lq ? col[qq] : 0u;
+    }
   }
 
   bf16x8 kf[KS], vf[KS];
@@ -752,6 +805,8 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
         const int ql = sub * 32 + 8 * g + 4 * hh;
         const f32x4 l4 = *(const f32x4*)(el + ql);
         const f32x4 d4 = *(const f32x4*)(ed + ql);
+        uint4 w4 = {0u, 0u, 0u, 0u};
+        if (drop && dmask) w4 = *(const uint4*)(exw + it * 64 + ql);
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           const int e = 4 * g + e4, qq = qt + ql + e4;
@@ -759,8 +814,10 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
           float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - l4[e4]);
           float dpv = P[e], pmv = p;
           if (drop) {
-            const bool kp = attn_keep(attn_pair_bits(ek[ql + e4], (uint32_t)kj), (uint32_t)kj,
-                                      th16);
+            const uint32_t wv = e4 == 0 ? w4.x : e4 == 1 ? w4.y : e4 == 2 ? w4.z : w4.w;
+            const bool kp = dmask ? ((wv >> r) & 1u) != 0u
+                                  : attn_keep(attn_pair_bits(ek[ql + e4], (uint32_t)kj),
+                                              (uint32_t)kj, th16);
             dpv = kp ? dpv * dp.scale : 0.f;
             pmv = kp ? p * dp.scale : 0.f;
           }
@@ -819,7 +876,8 @@ int attn_res_mode() { return retr_tune_get(RETR_TUNE_ATTN_MODE); }
 template <int HD, int NW>
 int launch_fwd3(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
                 void* o, long ldo, int B, int H, int Lq, int Lk, const unsigned char* kpm,
-                int causal, float p, unsigned long long seed, float* lse, hipStream_t st) {
+                int causal, float p, unsigned long long seed, float* lse, uint32_t* dmask,
+                hipStream_t st) {
   const float qscale = kLog2e / sqrtf((float)HD);
   const int nt = (Lk + 63) / 64;
   const size_t lds = res_lds_fwd<HD>(nt);
@@ -828,7 +886,7 @@ int launch_fwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
   dim3 grid((Lq + 32 * NW - 1) / (32 * NW), H, B);
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, st, (const bf16*)q, ldq, (const bf16*)k,
                      ldk, (const bf16*)v, ldv, (bf16*)o, ldo, H, Lq, Lk, Lk, kpm, causal, qscale,
-                     make_dp(p, seed), lse, nt);
+                     make_dp(p, seed), lse, nt, dmask);
   return retr_check_launch("attention_fwd3");
 }
 
@@ -837,7 +895,8 @@ int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
                 const void* o, long ldo, const void* dout, long lddo, const float* lse,
                 void* dq, long lddq, void* dk, long lddk, void* dv, long lddv, int B, int H,
                 int Lq, int Lk, const unsigned char* kpm, int causal, float p,
-                unsigned long long seed, float* D, int nwq, int nwk, hipStream_t st) {
+                unsigned long long seed, float* D, int nwq, int nwk, const uint32_t* dmask,
+                hipStream_t st) {
   const float scale = 1.f / sqrtf((float)HD);
   const float cs = kLog2e * scale;
   const DropoutParams dp = make_dp(p, seed);
@@ -850,14 +909,14 @@ int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
       hipLaunchKernelGGL(kern, dim3((Lq + 127) / 128, H, B), dim3(256), lds, st, (const bf16*)q,
                          ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
                          (const bf16*)dout, lddo, lse, D, (bf16*)dq, lddq, H, Lq, Lk, kpm, causal,
-                         cs, scale, dp, ntk);
+                         cs, scale, dp, ntk, dmask);
     } else {
       auto kern = attn_bwd_dq3_kernel<HD, 2>;
       allow_lds(kern, lds);
       hipLaunchKernelGGL(kern, dim3((Lq + 63) / 64, H, B), dim3(128), lds, st, (const bf16*)q,
                          ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
                          (const bf16*)dout, lddo, lse, D, (bf16*)dq, lddq, H, Lq, Lk, kpm, causal,
-                         cs, scale, dp, ntk);
+                         cs, scale, dp, ntk, dmask);
     }
     if (int e = retr_check_launch("attention_bwd_dq3")) return e;
   }
@@ -868,14 +927,14 @@ int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
     hipLaunchKernelGGL(kern, dim3((Lk + 127) / 128, H, B), dim3(256), lds, st, (const bf16*)q,
                        ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo, lse,
                        D, (bf16*)dk, lddk, (bf16*)dv, lddv, H, Lq, Lk, kpm, causal, cs, scale, dp,
-                       ntq);
+                       ntq, dmask);
   } else {
     auto kern = attn_bwd_dkdv3_kernel<HD, 2>;
     allow_lds(kern, lds);
     hipLaunchKernelGGL(kern, dim3((Lk + 63) / 64, H, B), dim3(128), lds, st, (const bf16*)q,
                        ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo, lse,
                        D, (bf16*)dk, lddk, (bf16*)dv, lddv, H, Lq, Lk, kpm, causal, cs, scale, dp,
-                       ntq);
+                       ntq, dmask);
   }
   return retr_check_launch("attention_bwd_dkdv3");
 }
@@ -889,7 +948,7 @@ inline int pick_nw(int B, int H, int L) { return (long)B * H * ((L + 127) / 128)
 int retr_attention_fwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
                         long ldv, void* o, long ldo, int B, int H, int Lq, int Lk, int hd,
                         const unsigned char* kpm, int causal, float p, unsigned long long seed,
-                        float* lse, hipStream_t st) {
+                        float* lse, uint32_t* dmask, hipStream_t st) {
   // forward: the streaming kernel (20 KB of LDS, up to 8 blocks per CU) beats the resident
   // one (2 blocks per CU) at every cfg2 shape (tools/attn_micro.py: 400x400 24.8 vs 28.1 us);
   // the resident forward stays selectable (RETR_TUNE_ATTN_MODE = 2) for sweeps
@@ -899,18 +958,18 @@ int retr_attention_fwd2(const void* q, long ldq, const void* k, long ldk, const 
   if (mode == 2 && fits) {
     const int nw = pick_nw(B, H, Lq);
     if (hd == 32)
-      return nw == 4 ? launch_fwd3<32, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, st)
-                     : launch_fwd3<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, st);
-    return nw == 4 ? launch_fwd3<64, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, st)
-                   : launch_fwd3<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, st);
+      return nw == 4 ? launch_fwd3<32, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, dmask, st)
+                     : launch_fwd3<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, dmask, st);
+    return nw == 4 ? launch_fwd3<64, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, dmask, st)
+                   : launch_fwd3<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, dmask, st);
   }
   const bool big = (long)B * H * ((Lq + 63) / 64) >= 1024;
   if (hd == 32) {
-    return big ? launch_fwd2<32, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st)
-               : launch_fwd2<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st);
+    return big ? launch_fwd2<32, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, dmask, st)
+               : launch_fwd2<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, dmask, st);
   }
-  return big ? launch_fwd2<64, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st)
-             : launch_fwd2<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, st);
+  return big ? launch_fwd2<64, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, dmask, st)
+             : launch_fwd2<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p, seed, lse, dmask, st);
 }
 
 // =============================================================================================
@@ -1252,7 +1311,7 @@ int retr_attention_bwd2(const void* q, long ldq, const void* k, long ldk, const 
                         const float* lse, void* dq, long lddq, void* dk, long lddk, void* dv,
                         long lddv, int B, int H, int Lq, int Lk, int hd,
                         const unsigned char* kpm, int causal, float p, unsigned long long seed,
-                        float* D, hipStream_t st) {
+                        float* D, const uint32_t* dmask, hipStream_t st) {
   const int mode = attn_res_mode();
   const int ntk = (Lk + 63) / 64, ntq = (Lq + 63) / 64;
   const bool fits = hd == 32 ? (res_lds_fwd<32>(ntk) <= kResLdsMax && res_lds_dkdv<32>(ntq) <= kResLdsMax)
@@ -1262,9 +1321,10 @@ int retr_attention_bwd2(const void* q, long ldq, const void* k, long ldk, const 
     if (hd == 32)
       return launch_bwd3<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk,
                                 lddk, dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, nwq, nwk,
-                                st);
+                                dmask, st);
     return launch_bwd3<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk,
-                              lddk, dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, nwq, nwk, st);
+                              lddk, dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, nwq, nwk,
+                              dmask, st);
   }
   if (hd == 32)
     return launch_bwd2<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk,

@@ -378,19 +378,32 @@ def k_dropout_apply(x, y, drop_p, seed):
          drop_p, seed, _st())
 
 
-def k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed, lse, probs=None):
-    call("retr_attention_fwd", dcode(q.dtype), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
-         v.stride(0), ptr(o), o.stride(0), B, H, Lq, Lk, hd, ptr(kpm), int(causal), drop_p, seed,
-         ptr(lse), ptr(probs), _st())
+ATTN_DMASK = True   # save the attention-dropout keep bits in the forward for the backward
+
+
+def attn_dmask(B, H, Lq, Lk, drop_p, dtype, hd, dev):
+    """Buffer for the forward's attention-dropout keep bits (retr_attention_fwd_dm), or None
+    when dropout is off or the kernels that use it do not run (bf16, head dim 32 / 64)."""
+    if not (ATTN_DMASK and drop_p > 0 and dtype == torch.bfloat16 and hd in (32, 64)):
+        return None
+    n = _lib.load().retr_attention_dropout_mask_bytes(B, H, Lq, Lk) // 4
+    return torch.empty(max(1, n), dtype=torch.int32, device=dev)
+
+
+def k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, causal, drop_p, seed, lse, probs=None,
+                    dmask=None):
+    call("retr_attention_fwd_dm", dcode(q.dtype), ptr(q), q.stride(0), ptr(k), k.stride(0),
+         ptr(v), v.stride(0), ptr(o), o.stride(0), B, H, Lq, Lk, hd, ptr(kpm), int(causal), drop_p,
+         seed, ptr(lse), ptr(probs), ptr(dmask), _st())
 
 
 def k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, causal, drop_p,
-                    seed):
+                    seed, dmask=None):
     ws = torch.empty(B * H * Lq, dtype=torch.float32, device=q.device)
-    call("retr_attention_bwd", dcode(q.dtype), ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v),
-         v.stride(0), ptr(o), o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(dq), dq.stride(0),
-         ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), B, H, Lq, Lk, hd, ptr(kpm), int(causal),
-         drop_p, seed, ptr(ws), _st())
+    call("retr_attention_bwd_dm", dcode(q.dtype), ptr(q), q.stride(0), ptr(k), k.stride(0),
+         ptr(v), v.stride(0), ptr(o), o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(dq),
+         dq.stride(0), ptr(dk), dk.stride(0), ptr(dv), dv.stride(0), B, H, Lq, Lk, hd, ptr(kpm),
+         int(causal), drop_p, seed, ptr(ws), ptr(dmask), _st())
 
 
 def ln_workspace(M, C, dev):
@@ -647,8 +660,10 @@ class _SelfAttnBlock(torch.autograd.Function):
         lse = torch.empty(B * H * L, dtype=torch.float32, device=dev)
         s_att, s_res = next_seed(), next_seed()
         probs = torch.empty(B, L, L, dtype=torch.float32, device=dev) if want_probs else None
+        dmask = attn_dmask(B, H, L, L, drop_attn, cdtype, hd, dev)
         k_attention_fwd(qk[:, :C], qk[:, C:], v, o, B, H, L, L, hd, kpm, causal, drop_attn,
-                        s_att, lse, probs)
+                        s_att, lse, probs, dmask)
+        ctx.dmask = dmask
         out = torch.empty(M, C, dtype=torch.float32, device=dev)
         k_linear_fwd(o, wout, b_out.detach(), out, res=res, drop_p=drop_res, seed=s_res)
         ctx.save_for_backward(npos, n, qk, v, o, lse, kpm, w_in, w_out, x, ln_w, mean, rstd)
@@ -686,7 +701,8 @@ class _SelfAttnBlock(torch.autograd.Function):
         dqk = torch.empty(M, 2 * C, dtype=cdtype, device=dev)
         dv = torch.empty(M, C, dtype=cdtype, device=dev)
         k_attention_bwd(qk[:, :C], qk[:, C:], v, o, do, lse, dqk[:, :C], dqk[:, C:], dv, B, H,
-                        L, L, hd, kpm, causal, drop_attn, s_att)
+                        L, L, hd, kpm, causal, drop_attn, s_att, ctx.dmask)
+        ctx.dmask = None
         dnpos = torch.empty(M, C, dtype=cdtype, device=dev)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad_group([(dqk, wint[:, : 2 * C], dnpos), (dv, wint[:, 2 * C:], dn)])
@@ -734,7 +750,10 @@ class _CrossAttnBlock(torch.autograd.Function):
         lse = torch.empty(B * H * Lq, dtype=torch.float32, device=dev)
         s_att, s_res = next_seed(), next_seed()
         probs = torch.empty(B, Lq, Lk, dtype=torch.float32, device=dev) if want_probs else None
-        k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, False, drop_attn, s_att, lse, probs)
+        dmask = attn_dmask(B, H, Lq, Lk, drop_attn, cdtype, hd, dev)
+        k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, False, drop_attn, s_att, lse, probs,
+                        dmask)
+        ctx.dmask = dmask
         out = torch.empty(Mq, C, dtype=torch.float32, device=dev)
         k_linear_fwd(o, wout, b_out.detach(), out, res=res, drop_p=drop_res, seed=s_res)
         ctx.save_for_backward(qpos, mem_pos, mem, q, k, v, o, lse, kpm, w_in, w_out, y, ln_w,
@@ -781,7 +800,8 @@ class _CrossAttnBlock(torch.autograd.Function):
         dk = torch.empty(Mk, C, dtype=cdtype, device=dev)
         dv = torch.empty(Mk, C, dtype=cdtype, device=dev)
         k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, False, drop_attn,
-                        s_att)
+                        s_att, ctx.dmask)
+        ctx.dmask = None
         dqpos = torch.empty(Mq, C, dtype=cdtype, device=dev)
         if ctx.shared:
             def mk():

@@ -76,7 +76,8 @@ def flops_of(name, a):
 
 
 # entry points measured as another one (same leading arguments; extras are tiny sums)
-_ALIAS = {"retr_linear_wgrad_group2": "retr_linear_wgrad_group"}
+_ALIAS = {"retr_linear_wgrad_group2": "retr_linear_wgrad_group",
+          "retr_attention_fwd_dm": "retr_attention_fwd", "retr_attention_bwd_dm": "retr_attention_bwd"}
 
 # grouped launches: name -> (family, index of the descriptor array in the call's arguments)
 _GROUPS = {"retr_linear_fwd_group": ("linear_fwd", 3), "retr_linear_dgrad_group": ("linear_dgrad", 5),
@@ -190,7 +191,8 @@ TRACKED = ("retr_conv2d_fwd", "retr_conv2d_fwd_out", "retr_conv1x1_fwd_cat",
            "retr_linear_fwd_splitk",
            "retr_linear_dgrad", "retr_linear_dgrad_splitk", "retr_linear_wgrad",
            "retr_linear_fwd_group", "retr_linear_dgrad_group", "retr_linear_wgrad_group",
-           "retr_linear_wgrad_group2", "retr_attention_fwd", "retr_attention_bwd")
+           "retr_linear_wgrad_group2", "retr_attention_fwd", "retr_attention_bwd",
+           "retr_attention_fwd_dm", "retr_attention_bwd_dm")
 
 
 FAMILY_SYMBOL = {"linear_fwd": "gemm{,2,2_group}_kernel<0,",

@@ -841,3 +841,50 @@ def test_bottleneck_s1_fused_equals_three_launches(N, H, W, ds):
     else:
         r3 = F.conv2d(r2, w3.float().view(256, 64, 1, 1)) + b3.view(1, -1, 1, 1) + xf
     assert rel_err(y1.permute(0, 3, 1, 2), torch.relu(r3)) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,hd,causal,masked,mode", [
+    (16, 8, 400, 400, 32, False, True, 0), (16, 8, 128, 400, 32, False, True, 0),
+    (16, 8, 128, 128, 32, True, False, 0), (2, 8, 130, 200, 64, False, True, 0),
+    (3, 8, 100, 77, 32, False, True, 2), (3, 8, 100, 77, 32, True, True, 1)])
+def test_attention_saved_dropout_bits_equal_rehash(B, H, Lq, Lk, hd, causal, masked, mode):
+    """retr_attention_fwd_dm saves the dropout keep bits, retr_attention_bwd_dm reads them (the
+    resident dq3 / dkdv3 kernels; the streaming backward, mode 1, ignores them): outputs, lse and
+    all three gradients bitwise those of the re-hashing path, and the saved bits are the keep
+    decisions (their density is 1 - p)."""
+    g = torch.Generator(device="cpu").manual_seed(Lq * 5 + Lk)
+    C, p = H * hd, 0.1
+    bf = torch.bfloat16
+    q, k, v, do = (torch.randn(B * L, C, generator=g).to(DEV).to(bf) for L in (Lq, Lk, Lk, Lq))
+    kpm = None
+    if masked:
+        kpm = torch.zeros(B, Lk, dtype=torch.uint8)
+        kpm[:, Lk - Lk // 5:] = 1
+        kpm = kpm.to(DEV)
+    outs = []
+    _lib.load().retr_tune(5, mode)
+    try:
+        for use in (False, True):
+            dm = ops.attn_dmask(B, H, Lq, Lk, p, bf, hd, DEV) if use else None
+            if dm is not None:
+                dm.fill_(-1)
+            o = torch.empty(B * Lq, C, dtype=bf, device=DEV)
+            lse = torch.empty(B * H * Lq, device=DEV)
+            ops.k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, causal, p, 99, lse, None, dm)
+            dq, dk, dv = (torch.empty_like(t) for t in (q, k, v))
+            ops.k_attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B, H, Lq, Lk, hd, kpm, causal, p,
+                                99, dm)
+            torch.cuda.synchronize()
+            outs.append((o, lse, dq, dk, dv))
+    finally:
+        _lib.load().retr_tune(5, 0)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    if causal:   # words of key tiles past a block's diagonal are never written
+        return
+    # keep-bit density over the keys of the first (b, h)
+    nw = (Lk + 31) // 32
+    words = dm.view(B * H, nw, Lq)[0].cpu().numpy().astype(np.uint32)
+    bits = np.unpackbits(words.view(np.uint8).reshape(nw, Lq, 4), axis=2, bitorder="little")
+    bits = bits.reshape(nw, Lq, 32).transpose(1, 0, 2).reshape(Lq, nw * 32)[:, :Lk]
+    assert abs(bits.mean() - (1 - p)) < 0.01, bits.mean()

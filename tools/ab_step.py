@@ -26,6 +26,7 @@ VARIANTS = {
     "side_all": {("OVERLAP", "backbone"): True, ("OVERLAP", "transformer"): True},
     "nofuse_ln": {("ATTR", "FUSE_LN_BWD"): False},
     "no_lnparams": {("ATTR", "FUSE_LN_PARAMS"): False},
+    "no_dmask": {("ATTR", "ATTN_DMASK"): False},
 }
 
 
@@ -33,6 +34,7 @@ def apply(v):
     ops.OVERLAP.update({"backbone": False, "transformer": False})
     ops.FUSE_LN_BWD = True
     ops.FUSE_LN_PARAMS = True
+    ops.ATTN_DMASK = True
     for (table, key), val in VARIANTS[v].items():
         if table == "ATTR":
             setattr(ops, key, val)
