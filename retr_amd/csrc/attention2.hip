@@ -544,7 +544,10 @@ __device__ long long g_attn_t[2][8192][3];
 #define ATTN_T(K, i)
 #endif
 
-template <int HD, int NW>
+// KSP = 2: the key tiles are split between two waves per 32 queries (even / odd tiles), which
+// doubles the waves of a grid that is otherwise ~6 waves per CU at the RE⫶TR sizes; the two
+// partial dQ accumulators are added through LDS at the end (fixed order: even + odd).
+template <int HD, int NW, int KSP = 1>
 __global__ void __launch_bounds__(NW * 64)
 attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
                     const bf16* o, long ldo, const bf16* dout, long lddo, const float* lse,
@@ -558,8 +561,10 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
   const int r = lane & 31, hh = lane >> 5;
   const BlockXYZ bxyz = xcd_block();
   const int b = bxyz.z, h = bxyz.y;
-  const int qblk = bxyz.x * (32 * NW);
-  const int q0 = qblk + wave * 32;
+  constexpr int QW = NW / KSP;                    // query waves
+  const int qw = wave % QW, kh = wave / QW;       // this wave's queries / key-tile parity
+  const int qblk = bxyz.x * (32 * QW);
+  const int q0 = qblk + qw * 32;
   const int qi = q0 + r;
   const int qc = qi < Lq ? qi : Lq - 1;
   const bf16* kb = k + (long)b * Lk * ldk + h * HD;
@@ -568,7 +573,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
   ATTN_T(0, 0)
 
   int kend = Lk;
-  if (causal) kend = min(Lk, qblk + 32 * NW);
+  if (causal) kend = min(Lk, qblk + 32 * QW);
   const int ntiles = (kend + 63) / 64;
   char* Ks = smem;
   char* Vs = smem + (size_t)ntiles_max * L::TILE;
@@ -603,7 +608,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
     }
   }
   const float Dq = dpart + __shfl_xor(dpart, 32, 64);
-  if (hh == 0 && qi < Lq) Dout[srow] = Dq;
+  if (hh == 0 && qi < Lq && kh == 0) Dout[srow] = Dq;
   const float lq2 = lse[srow] * kLog2e;
   const bool drop = dp.thresh != 0;
   const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
@@ -619,7 +624,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
   ATTN_T(0, 1)
 
   const int wtiles = causal ? min(ntiles, (q0 + 32 + 63) / 64) : ntiles;
-  for (int t = 0; t < wtiles; ++t) {
+  for (int t = kh; t < wtiles; t += KSP) {
     const int key0 = t * 64;
     const char* Kl = Ks + t * L::TILE;
     const char* Vl = Vs + t * L::TILE;
@@ -685,6 +690,23 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
     }
   }
   ATTN_T(0, 2)
+  if constexpr (KSP == 2) {
+    // odd-tile partials -> LDS (over the K tiles: every wave is past its loop), even + odd
+    __syncthreads();
+    float* red = (float*)smem + (long)qw * DT * 16 * 64;
+    if (kh == 1) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) red[(dt * 16 + e) * 64 + lane] = G[dt][e];
+    }
+    __syncthreads();
+    if (kh == 1) return;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) G[dt][e] += red[(dt * 16 + e) * 64 + lane];
+  }
   if (qi < Lq) {
     bf16* row = dq + ((long)b * Lq + qi) * lddq + h * HD;
 #pragma unroll
@@ -700,7 +722,9 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
   }
 }
 
-template <int HD, int NW>
+// KSP = 2: the query tiles are split between two waves per 32 keys (even / odd tiles); the
+// dK / dV partials are added through LDS at the end (even + odd).
+template <int HD, int NW, int KSP = 1>
 __global__ void __launch_bounds__(NW * 64)
 attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v,
                       long ldv, const bf16* dout, long lddo, const float* lse, const float* D,
@@ -714,8 +738,10 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
   const int r = lane & 31, hh = lane >> 5;
   const BlockXYZ bxyz = xcd_block();
   const int b = bxyz.z, h = bxyz.y;
-  const int kblk = bxyz.x * (32 * NW);
-  const int kj = kblk + wave * 32 + r;
+  constexpr int KW = NW / KSP;                    // key waves
+  const int kw = wave % KW, qh = wave / KW;       // this wave's keys / query-tile parity
+  const int kblk = bxyz.x * (32 * KW);
+  const int kj = kblk + kw * 32 + r;
   const int kc = kj < Lk ? kj : Lk - 1;
   const bf16* qb = q + (long)b * Lq * ldq + h * HD;
   const bf16* db = dout + (long)b * Lq * lddo + h * HD;
@@ -734,7 +760,7 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
   float* exd = exl + 64 * ntiles_max;                                 // D
   uint32_t* exk = (uint32_t*)(exd + 64 * ntiles_max);                 // dropout row keys
   // with saved keep bits: this wave's word column (its 32 keys) for every resident query
-  uint32_t* exw = exk + 64 * ntiles_max + wave * 64 * ntiles_max;
+  uint32_t* exw = exk + 64 * ntiles_max + kw * 64 * ntiles_max;
   dma_rows<HD, NW>(Qs, qb + (long)qstart * ldq, ldq, ntiles, Lq - qstart, wave, lane);
   dma_rows<HD, NW>(Ds, db + (long)qstart * lddo, lddo, ntiles, Lq - qstart, wave, lane);
   for (int i = tid; i < ntiles * 64; i += NT) {
@@ -745,9 +771,9 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
     exk[i] = (drop && !dmask) ? attn_row_key(seed, (uint32_t)((b * H + h) * Lq) + (uint32_t)qq)
                               : 0u;
   }
-  if (drop && dmask) {
+  if (drop && dmask && qh == 0) {
     const int nwm = (Lk + 31) / 32;
-    const int wc = min((kblk + wave * 32) / 32, nwm - 1);
+    const int wc = min((kblk + kw * 32) / 32, nwm - 1);
     const uint32_t* col = dmask + ((long)(b * H + h) * nwm + wc) * Lq;
     for (int i = lane; i < ntiles * 64; i += 64) {
       const int qq = qstart + i;
@@ -780,8 +806,8 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
   ATTN_T(1, 1)
 
   // a wave's keys see no query below its first key (causal): skip those tiles
-  const int wt0 = causal ? max(0, (kblk + wave * 32 - qstart) / 64) : 0;
-  for (int it = wt0; it < ntiles; ++it) {
+  const int wt0 = causal ? max(0, (kblk + kw * 32 - qstart) / 64) : 0;
+  for (int it = wt0 + ((wt0 & (KSP - 1)) != qh ? 1 : 0); it < ntiles; it += KSP) {
     const int qt = qstart + it * 64;
     const char* Ql = Qs + it * L::TILE;
     const char* Dl = Ds + it * L::TILE;
@@ -841,6 +867,29 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
     }
   }
   ATTN_T(1, 2)
+  if constexpr (KSP == 2) {
+    // odd-tile partials -> LDS (over the Q / dO tiles: every wave is past its loop)
+    __syncthreads();
+    float* red = (float*)smem + (long)kw * 2 * DT * 16 * 64;
+    if (qh == 1) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          red[((2 * dt) * 16 + e) * 64 + lane] = GK[dt][e];
+          red[((2 * dt + 1) * 16 + e) * 64 + lane] = GV[dt][e];
+        }
+    }
+    __syncthreads();
+    if (qh == 1) return;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        GK[dt][e] += red[((2 * dt) * 16 + e) * 64 + lane];
+        GV[dt][e] += red[((2 * dt + 1) * 16 + e) * 64 + lane];
+      }
+  }
   if (kj < Lk) {
     bf16* krow = dk + ((long)b * Lk + kj) * lddk + h * HD;
     bf16* vrow = dv + ((long)b * Lk + kj) * lddv + h * HD;
@@ -901,9 +950,27 @@ int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
   const float cs = kLog2e * scale;
   const DropoutParams dp = make_dp(p, seed);
   const int ntk = (Lk + 63) / 64, ntq = (Lq + 63) / 64;
+  const bool split = retr_tune_get(RETR_TUNE_ATTN_SPLIT) != 1;
   {
-    const size_t lds = res_lds_fwd<HD>(ntk);
-    if (nwq == 4) {
+    // the split kernel's partial-sum exchange (DT x 4 KB per query wave) aliases the K tiles
+    const size_t lds = std::max(res_lds_fwd<HD>(ntk), (size_t)(split ? nwq * (HD / 32) * 4096 : 0));
+    if (split) {   // 2 x nwq waves per block: nwq query waves x 2 key-tile parities
+      if (nwq == 4) {
+        auto kern = attn_bwd_dq3_kernel<HD, 8, 2>;
+        allow_lds(kern, lds);
+        hipLaunchKernelGGL(kern, dim3((Lq + 127) / 128, H, B), dim3(512), lds, st, (const bf16*)q,
+                           ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
+                           (const bf16*)dout, lddo, lse, D, (bf16*)dq, lddq, H, Lq, Lk, kpm,
+                           causal, cs, scale, dp, ntk, dmask);
+      } else {
+        auto kern = attn_bwd_dq3_kernel<HD, 4, 2>;
+        allow_lds(kern, lds);
+        hipLaunchKernelGGL(kern, dim3((Lq + 63) / 64, H, B), dim3(256), lds, st, (const bf16*)q,
+                           ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
+                           (const bf16*)dout, lddo, lse, D, (bf16*)dq, lddq, H, Lq, Lk, kpm,
+                           causal, cs, scale, dp, ntk, dmask);
+      }
+    } else if (nwq == 4) {
       auto kern = attn_bwd_dq3_kernel<HD, 4>;
       allow_lds(kern, lds);
       hipLaunchKernelGGL(kern, dim3((Lq + 127) / 128, H, B), dim3(256), lds, st, (const bf16*)q,
@@ -920,8 +987,29 @@ int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
     }
     if (int e = retr_check_launch("attention_bwd_dq3")) return e;
   }
-  const size_t lds = res_lds_dkdv<HD>(ntq);
-  if (nwk == 4) {
+  // the query-tile split of dkdv pays only on the 2-wave grids (decoder causal 128 x 128:
+  // 21.5 -> 15.8 us); on the 4-wave ones it adds its exchange to short loops (cross 128 x 400:
+  // 31.1 -> 35.1 us, tools/attn_bwd_ab.py, profiles/r3_attn_split.txt)
+  const bool split_kv = split && nwk == 2;
+  const size_t lds = std::max(res_lds_dkdv<HD>(ntq),
+                              (size_t)(split_kv ? nwk * 2 * (HD / 32) * 4096 : 0));
+  if (split_kv) {
+    if (nwk == 4) {
+      auto kern = attn_bwd_dkdv3_kernel<HD, 8, 2>;
+      allow_lds(kern, lds);
+      hipLaunchKernelGGL(kern, dim3((Lk + 127) / 128, H, B), dim3(512), lds, st, (const bf16*)q,
+                         ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo,
+                         lse, D, (bf16*)dk, lddk, (bf16*)dv, lddv, H, Lq, Lk, kpm, causal, cs,
+                         scale, dp, ntq, dmask);
+    } else {
+      auto kern = attn_bwd_dkdv3_kernel<HD, 4, 2>;
+      allow_lds(kern, lds);
+      hipLaunchKernelGGL(kern, dim3((Lk + 63) / 64, H, B), dim3(256), lds, st, (const bf16*)q,
+                         ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo,
+                         lse, D, (bf16*)dk, lddk, (bf16*)dv, lddv, H, Lq, Lk, kpm, causal, cs,
+                         scale, dp, ntq, dmask);
+    }
+  } else if (nwk == 4) {
     auto kern = attn_bwd_dkdv3_kernel<HD, 4>;
     allow_lds(kern, lds);
     hipLaunchKernelGGL(kern, dim3((Lk + 127) / 128, H, B), dim3(256), lds, st, (const bf16*)q,
