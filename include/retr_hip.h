@@ -95,8 +95,9 @@ enum {
                                       >= 2 that many slices (capped by the K-steps) */
   RETR_TUNE_CONV_WGRAD_TILE = 9, /* conv weight-gradient tile (bf16): 1 always 64x64 LDS-DMA,
                                     2 never (0: the built-in shape rule) */
-  RETR_TUNE_ATTN_SPLIT = 10,    /* resident attention backward: 1 = one wave per 32 rows over all
-                                   tiles; 0 (auto) = two waves per 32 rows (even / odd tiles) */
+  RETR_TUNE_ATTN_SPLIT = 10,    /* resident attention backward, two waves per 32 rows (even / odd
+                                   tiles): 1 never, 0 (auto) / 2 dq on every grid and dkdv on
+                                   2-wave grids, 3 both on 2-wave grids only */
   RETR_TUNE_COUNT = 11
 };
 int retr_tune(int knob, int value);

@@ -15,6 +15,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from retr_amd import ops, resnet  # noqa: E402
+from retr_amd._lib import load  # noqa: E402
 from retr_amd.engine import GraphedTrainStep  # noqa: E402
 from retr_amd.models.utils import NestedTensor  # noqa: E402
 from retr_amd.synthetic import synthetic_captions, synthetic_images  # noqa: E402
@@ -27,6 +28,9 @@ VARIANTS = {
     "nofuse_ln": {("ATTR", "FUSE_LN_BWD"): False},
     "no_lnparams": {("ATTR", "FUSE_LN_PARAMS"): False},
     "no_dmask": {("ATTR", "ATTN_DMASK"): False},
+    "split_off": {("TUNE", 10): 1},
+    "split_all": {("TUNE", 10): 2},
+    "no_dmask_split_off": {("ATTR", "ATTN_DMASK"): False, ("TUNE", 10): 1},
 }
 
 
@@ -35,11 +39,14 @@ def apply(v):
     ops.FUSE_LN_BWD = True
     ops.FUSE_LN_PARAMS = True
     ops.ATTN_DMASK = True
+    load().retr_tune(10, 0)
     for (table, key), val in VARIANTS[v].items():
         if table == "ATTR":
             setattr(ops, key, val)
         elif table == "RESNET":
             setattr(resnet, key, val)
+        elif table == "TUNE":
+            load().retr_tune(key, val)
         else:
             getattr(ops, table)[key] = val
 
