@@ -98,7 +98,10 @@ enum {
   RETR_TUNE_ATTN_SPLIT = 10,    /* resident attention backward, two waves per 32 rows (even / odd
                                    tiles): 1 never, 0 (auto) / 2 dq on every grid and dkdv on
                                    2-wave grids, 3 both on 2-wave grids only */
-  RETR_TUNE_COUNT = 11
+  RETR_TUNE_LIN_WGRAD = 11,     /* bf16 linear weight gradient with >= 256 128x128 tiles: 0 auto
+                                   (LDS-DMA 128x128, 4 waves), 1 register-staged 128x128,
+                                   2 LDS-DMA 256x256, 4 LDS-DMA 128x128 8 waves */
+  RETR_TUNE_COUNT = 12
 };
 int retr_tune(int knob, int value);
 

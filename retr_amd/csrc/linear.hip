@@ -220,6 +220,23 @@ int linear_wgrad_t(const void* dy, long lddy, const void* x, long ldx, float* dw
   }
   EpiAccF32 ep{dw, lddw, s > 1, 0, !accumulate && s == 1, db};
   ep.set_vec();
+  if constexpr (sizeof(T) == 2) {
+    // LDS-DMA kernels for the bf16 weight gradients with enough tiles (the vocabulary head's
+    // 30522 x 512: 956 tiles); RETR_TUNE_LIN_WGRAD 1 = the register-staged kernel
+    const int tk = retr_tune_get(RETR_TUNE_LIN_WGRAD);
+    if (big && tk != 1 && (long)cdiv(N, 128) * cdiv(K, 128) * s >= 256) {
+      // no fused row sums in the LDS-DMA kernels: the bias gradient is an ordered column sum
+      if (db) {
+        if (colsum_det<T>(dy, lddy, M, N, db, accumulate, st)) return 1;
+        ep.rowsum = nullptr;
+      }
+      // tools/wgrad_micro.py (profiles/r3_wgrad_micro.txt): vocabulary head 118 us register-
+      // staged -> 99 us on the 4-wave 128x128 LDS-DMA tile (+ the column sum)
+      if (tk == 2) return launch_gemm2<kFamLinearWgrad, 256, 256, 2, 4, 2>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
+      if (tk == 4) return launch_gemm2<kFamLinearWgrad, 128, 128, 4, 2, 2>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
+      return launch_gemm2<kFamLinearWgrad, 128, 128, 2, 2, 2>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
+    }
+  }
   if (big) return launch_gemm<kFamLinearWgrad, T, 128, 128>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
   return launch_gemm<kFamLinearWgrad, T, 64, 64>(la, lb, ep, N, K, M, s, st, "linear_wgrad");
 }
