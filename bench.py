@@ -203,16 +203,22 @@ def decode_bench(args, rank, world, device):
         for name, fn in runs:
             ids = fn()                                  # warm-up (captures the step graphs)
             torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
-            t0 = time.perf_counter()
-            ids = fn()
-            torch.cuda.synchronize()
-            dt = time.perf_counter() - t0
-            if world > 1:
-                t = torch.tensor([dt], device=device)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                dt = t.item()
+            reps = []
+            for _ in range(args.decode_reps):
+                if world > 1:
+                    dist.barrier()
+                t0 = time.perf_counter()
+                ids = fn()
+                torch.cuda.synchronize()
+                dt = time.perf_counter() - t0
+                if world > 1:
+                    t = torch.tensor([dt], device=device)
+                    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                    dt = t.item()
+                reps.append(dt)
+            print(f"decode {name} {dtype}: " + " ".join(f"{r * 1e3:.2f}" for r in reps) + " ms",
+                  file=sys.stderr, flush=True)
+            dt = sorted(reps)[len(reps) // 2]           # median batch time
             out[(name, dtype)] = (dt, int((ids != 0).sum(1).max().item()))
         del model
         torch.cuda.empty_cache()
@@ -404,6 +410,8 @@ def main():
     ap.add_argument("--decode-batch", type=int, default=64)
     ap.add_argument("--beam", type=int, default=5, help="beam width of the decode block (1: off)")
     ap.add_argument("--no-decode", action="store_true")
+    ap.add_argument("--decode-reps", type=int, default=3,
+                    help="timed decode batches per mode (median reported)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="CPU-baseline sample: timed oracle steps (>= 2) until this much time")
