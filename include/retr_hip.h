@@ -213,6 +213,14 @@ int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int
 int retr_bottleneck_s1_fwd(int dtype, const void* x, int N, int H, int W, int Cin,
                            const void* w1, const float* b1, const void* w2, const float* b2,
                            const void* w3, const float* b3, int ds, void* y, void* stream);
+/* Fused frozen stem (retr_amd/csrc/stem.hip; torchvision conv1 + bn1 + relu + maxpool,
+ * models/backbone.py:85-95, frozen by models/backbone.py:58-60): the space-to-depth conv
+ * (x [N][H2][W2][16] from retr_nchw_to_s2d16, w [Co][4][4][16] from retr_stem_s2d_weights, bias
+ * fp32, stride 1, pad 2, output H2 x W2) + bias + ReLU + MaxPool2d(3, 2, 1) in one launch;
+ * y [N][(H2+1)/2][(W2+1)/2][Co] bf16, Co == 64.  The conv output never reaches HBM.  Bitwise
+ * equal to retr_conv2d_fwd_out + retr_maxpool3x3s2. */
+int retr_stem_pool_fwd(int dtype, const void* x, int N, int H2, int W2, const void* w,
+                       const float* bias, void* y, int Co, void* stream);
 /* NCHW fp32 image -> NHWC (channels zero-padded to Cp) */
 int retr_nchw_to_nhwc(int dtype, const float* x, void* y, int N, int C, int H, int W, int Cp,
                       void* stream);

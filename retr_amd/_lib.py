@@ -104,6 +104,7 @@ _SIGS = {
     "retr_conv1x1_fwd_cat": [_I, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _I,
                              _P],
     "retr_maxpool3x3s2": [_I, _P, _P, _I, _I, _I, _I, _I, _I, _P],
+    "retr_stem_pool_fwd": [_I, _P, _I, _I, _I, _P, _P, _P, _I, _P],
     "retr_mask_nearest": [_P, _P, _I, _I, _I, _I, _I, _P],
     "retr_layernorm_fwd": [_I, _P, _L, _P, _P, _F, _I, _I, _P, _L, _P, _P, _I, _P, _P, _P],
     "retr_layernorm_bwd": [_I, _P, _P, _L, _P, _L, _P, _P, _P, _I, _I, _P, _L, _P, _P, _P, _P,

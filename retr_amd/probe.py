@@ -45,6 +45,8 @@ def flops_of(name, a):
         m, cin, ds = a[2] * a[3] * a[4], a[5], a[12]
         k3 = 64 + (cin if ds else 0)
         return "conv_fwd", 2.0 * m * (cin * 64 + 9 * 64 * 64 + k3 * 256)
+    if name == "retr_stem_pool_fwd":           # the conv's own pixels (halo recompute excluded)
+        return "conv_fwd", 2.0 * a[2] * a[3] * a[4] * a[8] * 256
     if name == "retr_conv2d_dgrad":
         _, _, n, h, w, c, _, _, co, kh, kw, s, p, d = a[:14]
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
@@ -111,6 +113,9 @@ def bytes_of(name, a):
         m, cin, ds = a[2] * a[3] * a[4], a[5], a[12]
         k3 = 64 + (cin if ds else 0)
         return e * (m * (cin + 256) + 64 * cin + 9 * 64 * 64 + 256 * k3)
+    if name == "retr_stem_pool_fwd":           # s2d input once, pooled output once, weights
+        n, h2, w2, co = a[2], a[3], a[4], a[8]
+        return e * (n * h2 * w2 * 16 + co * 256 + n * ((h2 + 1) // 2) * ((w2 + 1) // 2) * co)
     if name == "retr_conv2d_dgrad":
         _, _, n, h, w, c, _, _, co, kh, kw, s, p, d, addend, gate = a[:16]
         oh, ow = _conv_out(h, kh, s, p, d), _conv_out(w, kw, s, p, d)
@@ -165,6 +170,8 @@ def shape_of(name, a):
         return f"N{a[5]} {a[6]}x{a[7]} [{a[2]}|{a[4]} s{a[10]}] ->{a[14]} k1 cat"
     if name == "retr_bottleneck_s1_fwd":
         return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} bottleneck ds{a[12]}"
+    if name == "retr_stem_pool_fwd":
+        return f"N{a[2]} {a[3]}x{a[4]}x16 ->{a[8]} k4 stem+maxpool"
     if name == "retr_conv2d_dgrad":
         return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} <-{a[8]} k{a[9]} s{a[11]} d{a[13]}"
     if name == "retr_conv2d_wgrad":
@@ -187,7 +194,7 @@ def shape_of(name, a):
 
 
 TRACKED = ("retr_conv2d_fwd", "retr_conv2d_fwd_out", "retr_conv1x1_fwd_cat",
-           "retr_bottleneck_s1_fwd", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
+           "retr_bottleneck_s1_fwd", "retr_stem_pool_fwd", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
            "retr_linear_fwd_splitk",
            "retr_linear_dgrad", "retr_linear_dgrad_splitk", "retr_linear_wgrad",
            "retr_linear_fwd_group", "retr_linear_dgrad_group", "retr_linear_wgrad_group",
@@ -198,7 +205,7 @@ TRACKED = ("retr_conv2d_fwd", "retr_conv2d_fwd_out", "retr_conv1x1_fwd_cat",
 FAMILY_SYMBOL = {"linear_fwd": "gemm{,2,2_group}_kernel<0,",
                  "linear_dgrad": "gemm{,2,2_group}_kernel<1,",
                  "linear_wgrad": "gemm{,2,2_group}_kernel<2,",
-                 "conv_fwd": "gemm{,2}_kernel<3, + bottleneck_s1_kernel",
+                 "conv_fwd": "gemm{,2}_kernel<3, + bottleneck_s1_kernel + stem_pool_kernel",
                  "conv_dgrad": "gemm{,2}_kernel<4,", "conv_wgrad": "gemm{,2}_kernel<5,",
                  "attention_fwd": "attn_fwd{,2}_kernel",
                  "attention_bwd": "attn_bwd_"}
@@ -213,7 +220,7 @@ def family_of_symbol(name):
     if m:
         return ("linear_fwd", "linear_dgrad", "linear_wgrad", "conv_fwd", "conv_dgrad",
                 "conv_wgrad")[int(m.group(1))]
-    if "bottleneck_s1_kernel" in name:
+    if "bottleneck_s1_kernel" in name or "stem_pool_kernel" in name:
         return "conv_fwd"
     if re.search(r"attn_fwd\d*_kernel", name):
         return "attention_fwd"

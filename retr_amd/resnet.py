@@ -248,10 +248,18 @@ def _stem_s2d(runner, img):
     h2, w2_ = H // 2, W // 2
     x = torch.empty(N, h2, w2_, 16, dtype=runner.cdtype, device=img.device)
     call("retr_nchw_to_s2d16", ptr(img), ptr(x), N, C, H, W, _st())
+    if runner.stem_pool and stem.cout == 64:
+        # conv + bias + ReLU + MaxPool(3, 2, 1) in one launch (csrc/stem.hip): the stem is
+        # frozen (models/backbone.py:58-60), so its conv output is never needed again
+        ph, pw = (h2 - 1) // 2 + 1, (w2_ - 1) // 2 + 1
+        y = torch.empty(N, ph, pw, stem.cout, dtype=runner.cdtype, device=img.device)
+        call("retr_stem_pool_fwd", dcode(runner.cdtype), ptr(x), N, h2, w2_, ptr(w2), ptr(bias),
+             ptr(y), stem.cout, _st())
+        return y, (N, ph, pw, stem.cout), True
     y = torch.empty(N, h2, w2_, stem.cout, dtype=runner.cdtype, device=img.device)
     call("retr_conv2d_fwd_out", dcode(runner.cdtype), ptr(x), N, h2, w2_, 16, ptr(w2), ptr(bias),
          None, ptr(y), stem.cout, 4, 4, 1, 2, 1, h2, w2_, 1, _st())
-    return y, (N, h2, w2_, stem.cout)
+    return y, (N, h2, w2_, stem.cout), False
 
 
 class _Backbone(torch.autograd.Function):
@@ -262,17 +270,21 @@ class _Backbone(torch.autograd.Function):
         PACKS.prepare(runner.specs, cdtype)      # every stale conv packed in one launch
         N, C, H, W = images.shape
         img = images.detach().float().contiguous()
+        pooled = False
         if runner.s2d_stem(C, H, W):
-            s, sh = _stem_s2d(runner, img)
+            s, sh, pooled = _stem_s2d(runner, img)
         else:
             x = torch.empty(N, H, W, stem.cp, dtype=cdtype, device=images.device)
             call("retr_nchw_to_nhwc", dcode(cdtype), ptr(img), ptr(x), N, C, H, W, stem.cp, _st())
             s, sh = _conv_fwd(stem, x, (N, H, W, stem.cp), relu=True)
-        ph, pw = (sh[1] + 2 - 3) // 2 + 1, (sh[2] + 2 - 3) // 2 + 1
-        x = torch.empty(N, ph, pw, sh[3], dtype=cdtype, device=images.device)
-        call("retr_maxpool3x3s2", dcode(cdtype), ptr(s), ptr(x), N, sh[1], sh[2], sh[3], ph, pw,
-             _st())
-        shape = (N, ph, pw, sh[3])
+        if pooled:
+            x, shape = s, sh
+        else:
+            ph, pw = (sh[1] + 2 - 3) // 2 + 1, (sh[2] + 2 - 3) // 2 + 1
+            x = torch.empty(N, ph, pw, sh[3], dtype=cdtype, device=images.device)
+            call("retr_maxpool3x3s2", dcode(cdtype), ptr(s), ptr(x), N, sh[1], sh[2], sh[3], ph,
+                 pw, _st())
+            shape = (N, ph, pw, sh[3])
         del s
         saved = []
         runner.cat_used = []
@@ -378,6 +390,8 @@ class BackboneRunner:
                                     for c in b.convs + ([b.ds] if b.ds is not None else [])]
         self._s2d_w = None
         self.use_s2d = os.environ.get("RETR_S2D_STEM", "1") != "0"
+        # fused stem conv + max-pool on the space-to-depth path (A/B switch)
+        self.stem_pool = os.environ.get("RETR_STEM_POOL", "1") != "0"
         self._cat_w = {}
         self.cat_used = []          # blocks that took the fused tail in the last forward
         self.use_cat = os.environ.get("RETR_CAT_TAIL", "1") != "0"

@@ -739,6 +739,37 @@ def test_stem_space_to_depth(N, H, W):
     assert rel_err(y.permute(0, 3, 1, 2).float().cpu(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H2,W2", [(2, 320, 320), (3, 19, 25), (2, 112, 112), (1, 32, 48),
+                                     (4, 17, 16)])
+def test_stem_pool_fused_equals_conv_then_maxpool(N, H2, W2):
+    """retr_stem_pool_fwd (space-to-depth conv + bias + ReLU + MaxPool(3, 2, 1) in one launch,
+    csrc/stem.hip) == retr_conv2d_fwd_out + retr_maxpool3x3s2 bitwise, at the cfg2 size, ragged
+    pooled tiles (odd sizes, partial 8x16 tiles) and the cfg5 decode size (112 = 224 / 2)."""
+    bf = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(N * 1000 + H2 * 7 + W2)
+    xs = torch.randn(N, H2, W2, 16, generator=g)
+    xs[..., 12:] = 0
+    xs = xs.to(DEV).to(bf)
+    w2 = (torch.randn(64, 4, 4, 16, generator=g) / 16).to(DEV).to(bf)
+    bias = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    y1 = torch.empty(N, H2, W2, 64, dtype=bf, device=DEV)
+    call("retr_conv2d_fwd_out", ops.dcode(bf), ptr(xs), N, H2, W2, 16, ptr(w2), ptr(bias), None,
+         ptr(y1), 64, 4, 4, 1, 2, 1, H2, W2, 1, ops._st())
+    PH, PW = (H2 - 1) // 2 + 1, (W2 - 1) // 2 + 1
+    ref = torch.empty(N, PH, PW, 64, dtype=bf, device=DEV)
+    call("retr_maxpool3x3s2", ops.dcode(bf), ptr(y1), ptr(ref), N, H2, W2, 64, PH, PW, ops._st())
+    y = torch.full((N, PH, PW, 64), float("nan"), dtype=bf, device=DEV)
+    call("retr_stem_pool_fwd", ops.dcode(bf), ptr(xs), N, H2, W2, ptr(w2), ptr(bias), ptr(y), 64,
+         ops._st())
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref), (y.float() - ref.float()).abs().max()
+    # and against fp32 torch (conv over the s2d image, pad 2, cropped to H2 x W2; pool)
+    conv = F.conv2d(xs.float().permute(0, 3, 1, 2).cpu(), w2.float().permute(0, 3, 1, 2).cpu(),
+                    padding=2)[:, :, :H2, :W2]
+    tref = F.max_pool2d(torch.relu(conv + bias.cpu().view(1, -1, 1, 1)), 3, 2, 1)
+    assert rel_err(y.permute(0, 3, 1, 2).float().cpu(), tref) < 1e-2
+
+
 def test_conv_pack_cache_lives_on_the_spec():
     """Packed conv weights are cached on each ConvSpec (they die with the model): a dict keyed by
     id(spec) served a later model -- whose specs reused dead ids and whose tensors reused the

@@ -31,6 +31,7 @@ VARIANTS = {
     "split_off": {("TUNE", 10): 1},
     "split_all": {("TUNE", 10): 2},
     "no_dmask_split_off": {("ATTR", "ATTN_DMASK"): False, ("TUNE", 10): 1},
+    "no_stem_pool": {("ENV", "RETR_STEM_POOL"): "0"},
 }
 
 
@@ -40,8 +41,11 @@ def apply(v):
     ops.FUSE_LN_PARAMS = True
     ops.ATTN_DMASK = True
     load().retr_tune(10, 0)
+    os.environ["RETR_STEM_POOL"] = "1"
     for (table, key), val in VARIANTS[v].items():
-        if table == "ATTR":
+        if table == "ENV":                     # read when the model is built
+            os.environ[key] = val
+        elif table == "ATTR":
             setattr(ops, key, val)
         elif table == "RESNET":
             setattr(resnet, key, val)
