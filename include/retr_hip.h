@@ -89,7 +89,8 @@ enum {
   RETR_TUNE_ATTN_MODE = 5,      /* bf16 attention: 1 streaming K/V tiles, 2 LDS-resident */
   RETR_TUNE_BIG_TILE = 6,       /* large bf16 GEMMs (convs): 1 128x128 S1, 2 128x128 S2,
                                    3 256x256, 4 128x64 S3, 5 reg-staged 64x64, 6 64x64 S2,
-                                   7 128x128 S1 one epilogue band, 8 64x64 S4, 9 64x128 S3 */
+                                   7 128x128 S1 one epilogue band, 8 64x64 S4, 9 64x128 S3,
+                                   10 / 11 / 12 32x64 S4 / S3 / S2 */
   RETR_TUNE_NT_STORE = 7,       /* 1: non-temporal GEMM output stores */
   RETR_TUNE_CONV_WGRAD_SPLITS = 8, /* conv weight-gradient split-K: 1 legacy ceil(512 / tiles),
                                       >= 2 that many slices (capped by the K-steps) */
@@ -101,7 +102,10 @@ enum {
   RETR_TUNE_LIN_WGRAD = 11,     /* bf16 linear weight gradient with >= 256 128x128 tiles: 0 auto
                                    (LDS-DMA 128x128, 4 waves), 1 register-staged 128x128,
                                    2 LDS-DMA 256x256, 4 LDS-DMA 128x128 8 waves */
-  RETR_TUNE_COUNT = 12
+  RETR_TUNE_ATTN_FSPLIT = 12,   /* bf16 streaming attention forward, key split: 0 auto, 1 off,
+                                   2 two parities x 64 queries, 3 four parities x 32 queries,
+                                   4 two parities x 32 queries */
+  RETR_TUNE_COUNT = 13
 };
 int retr_tune(int knob, int value);
 

@@ -146,6 +146,238 @@ struct KVStager {
   }
 };
 
+// One 64-key tile of the streaming forward from K / V images of Tile<HD> layout: S^T = K Q^T,
+// masking, the online-softmax update of (m, l, O) and O^T += V^T drop(P)^T.
+template <int HD>
+RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
+    const char* Kl, const char* Vl, const bf16x8 (&qf)[HD / 16], f32x16 (&O)[HD / 32], float& m,
+    float& l, int key0, unsigned long long pmask, bool diag, int qi, int lane, bool drop,
+    uint32_t rowkey, uint32_t th16, uint32_t* dmask, int bh, int Lq, int Lk) {
+  using TL = Tile<HD>;
+  constexpr int KS = HD / 16, DT = HD / 32;
+  const int r = lane & 31, hh = lane >> 5;
+  // S^T (two 32-key sub-tiles): rows = keys, lane = query
+  f32x16 S[2];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) S[sub][e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 a = *(const bf16x8*)(Kl + (sub * 32 + r) * TL::RB + (16 * s + 8 * hh) * 2);
+      S[sub] = mfma32(a, qf[s], S[sub]);
+    }
+  }
+  if (pmask || diag) mask_tile(S, pmask, diag, qi - key0 - 4 * hh, hh);
+  // online softmax (log2 domain)
+  float mt = -INFINITY;
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) mt = fmaxf(mt, S[sub][e]);
+  mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+  const float mn = fmaxf(m, mt);
+  const float ms = (mn == -INFINITY) ? 0.f : mn;
+  const float alpha = __builtin_amdgcn_exp2f(m - ms);
+  m = mn;
+  if (__any(alpha != 1.f)) {
+    l *= alpha;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) O[dt][e] *= alpha;
+  }
+  bf16x8 pf[4];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    uint32_t wbits = 0;                          // keep bits of keys key0 + 32 sub + j
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int kk = key0 + sub * 32 + 8 * g + 4 * hh;   // 4 consecutive keys
+      uint32_t b01 = 0, b23 = 0;
+      if (drop) {
+        b01 = attn_pair_bits(rowkey, kk);
+        b23 = attn_pair_bits(rowkey, kk + 2);
+      }
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const int e = 4 * g + e4;
+        float p = __builtin_amdgcn_exp2f(S[sub][e] - ms);
+        l += p;
+        if (drop) {
+          const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
+          wbits |= (uint32_t)kp << (8 * g + 4 * hh + e4);
+          p = kp ? p : 0.f;
+        }
+        pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
+      }
+    }
+    if (drop && dmask) store_dmask(dmask, wbits, hh, bh, Lq, Lk, qi, key0 / 32 + sub);
+  }
+  // O^T += V^T P^T  (A = V^T via transposed LDS reads, B = P in registers)
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+    const int qrow = (lane & 15) >> 2;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const char* lo = Vl + (16 * s + 4 * hh + qrow) * TL::RB + c0 * 2;
+      const bf16x8 a = join(tr16(lo), tr16(lo + 8 * TL::RB));
+      O[dt] = mfma32(a, pf[s], O[dt]);
+    }
+  }
+}
+
+// Q fragments (B operand of S^T = K Q^T): lane holds Q[qi][16s + 8hh + j], prescaled
+template <int HD>
+RETR_DEVICE void load_qf(bf16x8 (&qf)[HD / 16], const bf16* q, long ldq, int b, int h, int qi,
+                         int Lq, int hh, float qscale) {
+  const bf16* qr = q + ((long)b * Lq + (qi < Lq ? qi : Lq - 1)) * ldq + h * HD;
+#pragma unroll
+  for (int s = 0; s < HD / 16; ++s) {
+    bf16x8 x = *(const bf16x8*)(qr + 16 * s + 8 * hh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * qscale);
+    qf[s] = x;
+  }
+}
+
+// Normalised output row and log-sum-exp of one lane's query (the lane pair's l partials added).
+template <int HD>
+RETR_DEVICE void fwd_finish(const f32x16 (&O)[HD / 32], float m, float l, bf16* o, long ldo,
+                            int b, int h, int H, int qi, int Lq, int hh, bool drop, float dscale,
+                            float* lse) {
+  l += __shfl_xor(l, 32, 64);
+  if (qi < Lq) {
+    // fully masked row: 0 * inf = NaN (torch's all -inf softmax); kept probabilities were left
+    // unscaled, the dropout scale is applied here once
+    const float inv = (drop ? dscale : 1.f) / l;
+    bf16* orow = o + ((long)b * Lq + qi) * ldo + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+        bf16x4 w;
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) w[e4] = (bf16)(O[dt][4 * g + e4] * inv);
+        *(bf16x4*)(orow + dt * 32 + 8 * g + 4 * hh) = w;
+      }
+    if (hh == 0 && lse) lse[((long)b * H + h) * Lq + qi] = (m + __log2f(l)) * kLn2;
+  }
+}
+
+// Key-split streaming forward: NQ query waves (32 queries each) x KSP key parities per block.
+// Per iteration the block stages KSP consecutive 64-key tiles; parity p's waves run tile
+// KSP * it + p, so every (32-query, parity) wave carries its own online-softmax state over
+// 1 / KSP of the keys -- KSP times the waves of the unsplit kernel on grids that are otherwise
+// ~1.6 waves per SIMD (encoder 400 x 400) or less (cross 128 x 400).  At the end the parities'
+// (m, l, O) go through LDS and parity 0 merges them in parity order (deterministic; the same
+// products as the unsplit kernel, summed in another fixed order).
+template <int HD, int NQ, int KSP>
+__global__ void __launch_bounds__(NQ * KSP * 64)
+attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
+                  bf16* o, long ldo, int H, int Lq, int Lk, int kbr, const unsigned char* kpm,
+                  int causal, float qscale, DropoutParams dp, float* lse, uint32_t* dmask) {
+  using TL = Tile<HD>;
+  constexpr int NW = NQ * KSP, NT = NW * 64, DT = HD / 32;
+  constexpr int SST = KSP * TL::STAGE;              // one ring slot: KSP (K, V) tile pairs
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hh = lane >> 5;
+  const int qw = wave % NQ, par = wave / NQ;
+  const BlockXYZ bxyz = xcd_block();
+  const int b = bxyz.z, h = bxyz.y;
+  const int qblk = bxyz.x * (32 * NQ);
+  const int q0 = qblk + qw * 32;
+  const int qi = q0 + (lane & 31);
+  const bf16* kb = k + (long)b * kbr * ldk + h * HD;
+  const bf16* vb = v + (long)b * kbr * ldv + h * HD;
+
+  bf16x8 qf[HD / 16];
+  load_qf<HD>(qf, q, ldq, b, h, qi, Lq, hh, qscale);
+
+  int kend = Lk;
+  if (causal) kend = min(Lk, qblk + 32 * NQ);
+  const int ntiles = (kend + TL::KT - 1) / TL::KT;
+  const int nit = (ntiles + KSP - 1) / KSP;
+  // a wave's own causal range can end before the block's
+  const int wtiles = causal ? min(ntiles, (q0 + 32 + 63) / 64) : ntiles;
+
+  const bool drop = dp.thresh != 0;
+  const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
+  const uint32_t rowkey = drop ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
+
+  f32x16 O[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) O[dt][e] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  KVStager<HD, NT> stg[KSP];
+#pragma unroll
+  for (int j = 0; j < KSP; ++j) {
+    stg[j].load(kb, ldk, vb, ldv, j * TL::KT, Lk, tid);
+    stg[j].store(smem + j * TL::STAGE, tid);
+  }
+  __syncthreads();
+
+  for (int it = 0; it < nit; ++it) {
+    const char* slot = smem + (it & 1) * SST;
+    if (it + 1 < nit) {
+#pragma unroll
+      for (int j = 0; j < KSP; ++j) stg[j].load(kb, ldk, vb, ldv, ((it + 1) * KSP + j) * TL::KT, Lk, tid);
+    }
+    const int t = it * KSP + par;
+    if (t < wtiles) {
+      const int key0 = t * TL::KT;
+      bool pad = key0 + lane >= Lk;
+      if (kpm && !pad) pad = kpm[(long)b * Lk + key0 + lane] != 0;
+      const unsigned long long pmask = __ballot(pad);
+      const bool diag = causal && (key0 + TL::KT - 1 > q0);
+      const char* Kl = slot + par * TL::STAGE;
+      fwd2_tile<HD>(Kl, Kl + TL::BYTES, qf, O, m, l, key0, pmask, diag, qi, lane, drop, rowkey,
+                    th16, dmask, b * H + h, Lq, Lk);
+    }
+    if (it + 1 < nit) {
+#pragma unroll
+      for (int j = 0; j < KSP; ++j) stg[j].store(smem + ((it + 1) & 1) * SST + j * TL::STAGE, tid);
+    }
+    __syncthreads();
+  }
+
+  // merge: parities 1.. publish (m, l, O) per lane, parity 0 folds them in parity order
+  float* xs = (float*)smem;
+  constexpr int REC = 16 * DT + 2;                  // floats per lane record
+  if (par > 0) {
+    float* rec = xs + (((par - 1) * NQ + qw) * 64 + lane) * REC;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) rec[16 * dt + e] = O[dt][e];
+    rec[16 * DT] = m;
+    rec[16 * DT + 1] = l;
+  }
+  __syncthreads();
+  if (par > 0) return;
+#pragma unroll
+  for (int p = 1; p < KSP; ++p) {
+    const float* rec = xs + (((p - 1) * NQ + qw) * 64 + lane) * REC;
+    const float m1 = rec[16 * DT], l1 = rec[16 * DT + 1];
+    const float mn = fmaxf(m, m1);
+    const float ms = (mn == -INFINITY) ? 0.f : mn;
+    const float a0 = __builtin_amdgcn_exp2f(m - ms), a1 = __builtin_amdgcn_exp2f(m1 - ms);
+    l = l * a0 + l1 * a1;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) O[dt][e] = O[dt][e] * a0 + rec[16 * dt + e] * a1;
+    m = mn;
+  }
+  fwd_finish<HD>(O, m, l, o, ldo, b, h, H, qi, Lq, hh, drop, dp.scale, lse);
+}
+
 template <int HD, int NW>
 __global__ void __launch_bounds__(NW * 64)
 attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
@@ -164,18 +396,8 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
   const bf16* kb = k + (long)b * kbr * ldk + h * HD;
   const bf16* vb = v + (long)b * kbr * ldv + h * HD;
 
-  // Q fragments (B operand of S^T = K Q^T): lane holds Q[qi][16s + 8hh + j], prescaled
   bf16x8 qf[KS];
-  {
-    const bf16* qr = q + ((long)b * Lq + (qi < Lq ? qi : Lq - 1)) * ldq + h * HD;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      bf16x8 x = *(const bf16x8*)(qr + 16 * s + 8 * hh);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * qscale);
-      qf[s] = x;
-    }
-  }
+  load_qf<HD>(qf, q, ldq, b, h, qi, Lq, hh, qscale);
 
   int kend = Lk;
   if (causal) kend = min(Lk, qblk + 32 * NW);
@@ -208,98 +430,13 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
     const unsigned long long pmask = __ballot(pad);
     const bool diag = causal && (key0 + TL::KT - 1 > q0);
 
-    // S^T (two 32-key sub-tiles): rows = keys, lane = query
-    f32x16 S[2];
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) S[sub][e] = 0.f;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const bf16x8 a = *(const bf16x8*)(Kl + (sub * 32 + r) * TL::RB + (16 * s + 8 * hh) * 2);
-        S[sub] = mfma32(a, qf[s], S[sub]);
-      }
-    }
-    if (pmask || diag) mask_tile(S, pmask, diag, qi - key0 - 4 * hh, hh);
-    // online softmax (log2 domain)
-    float mt = -INFINITY;
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) mt = fmaxf(mt, S[sub][e]);
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);
-    const float ms = (mn == -INFINITY) ? 0.f : mn;
-    const float alpha = __builtin_amdgcn_exp2f(m - ms);
-    m = mn;
-    if (__any(alpha != 1.f)) {
-      l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) O[dt][e] *= alpha;
-    }
-    bf16x8 pf[4];
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      uint32_t wbits = 0;                          // keep bits of keys key0 + 32 sub + j
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int kk = key0 + sub * 32 + 8 * g + 4 * hh;   // 4 consecutive keys
-        uint32_t b01 = 0, b23 = 0;
-        if (drop) {
-          b01 = attn_pair_bits(rowkey, kk);
-          b23 = attn_pair_bits(rowkey, kk + 2);
-        }
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-          const int e = 4 * g + e4;
-          float p = __builtin_amdgcn_exp2f(S[sub][e] - ms);
-          l += p;
-          if (drop) {
-            const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
-            wbits |= (uint32_t)kp << (8 * g + 4 * hh + e4);
-            p = kp ? p : 0.f;
-          }
-          pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
-        }
-      }
-      if (drop && dmask) store_dmask(dmask, wbits, hh, (b * H + h), Lq, Lk, qi, key0 / 32 + sub);
-    }
-    // O^T += V^T P^T  (A = V^T via transposed LDS reads, B = P in registers)
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-      const int qrow = (lane & 15) >> 2;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const char* lo = Vl + (16 * s + 4 * hh + qrow) * TL::RB + c0 * 2;
-        const bf16x8 a = join(tr16(lo), tr16(lo + 8 * TL::RB));
-        O[dt] = mfma32(a, pf[s], O[dt]);
-      }
-    }
+    fwd2_tile<HD>(Kl, Vl, qf, O, m, l, key0, pmask, diag, qi, lane, drop, rowkey, th16, dmask,
+                  b * H + h, Lq, Lk);
     if (t + 1 < ntiles) stg.store(smem + ((t + 1) & 1) * TL::STAGE, tid);
     __syncthreads();
   }
 
-  l += __shfl_xor(l, 32, 64);
-  if (qi < Lq) {
-    // fully masked row: 0 * inf = NaN (torch's all -inf softmax); kept probabilities were left
-    // unscaled, the dropout scale is applied here once
-    const float inv = (drop ? dp.scale : 1.f) / l;
-    bf16* orow = o + ((long)b * Lq + qi) * ldo + h * HD;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-        bf16x4 w;
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) w[e4] = (bf16)(O[dt][4 * g + e4] * inv);
-        *(bf16x4*)(orow + dt * 32 + 8 * g + 4 * hh) = w;
-      }
-    if (hh == 0 && lse) lse[((long)b * H + h) * Lq + qi] = (m + __log2f(l)) * kLn2;
-  }
+  fwd_finish<HD>(O, m, l, o, ldo, b, h, H, qi, Lq, hh, drop, dp.scale, lse);
 }
 
 template <int HD, int NW>
@@ -314,6 +451,24 @@ int launch_fwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
                      ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, H, Lq, Lk, kbr,
                      kpm, causal, qscale, make_dp(p, seed), lse, dmask);
   return retr_check_launch("attention_fwd2");
+}
+
+template <int HD, int NQ, int KSP>
+int launch_fwd2s(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+                 void* o, long ldo, int B, int H, int Lq, int Lk, int kbr,
+                 const unsigned char* kpm, int causal, float p, unsigned long long seed,
+                 float* lse, uint32_t* dmask, hipStream_t st) {
+  const float qscale = kLog2e / sqrtf((float)HD);
+  const size_t lds = 2 * KSP * Tile<HD>::STAGE;
+  auto kern = attn_fwd2s_kernel<HD, NQ, KSP>;
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  dim3 grid((Lq + 32 * NQ - 1) / (32 * NQ), H, B);
+  hipLaunchKernelGGL(kern, grid, dim3(NQ * KSP * 64), lds, st, (const bf16*)q, ldq,
+                     (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, H, Lq, Lk, kbr, kpm,
+                     causal, qscale, make_dp(p, seed), lse, dmask);
+  return retr_check_launch("attention_fwd2s");
 }
 
 // =============================================================================================
@@ -1055,6 +1210,32 @@ int retr_attention_fwd2(const void* q, long ldq, const void* k, long ldk, const 
                      : launch_fwd3<32, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, dmask, st);
     return nw == 4 ? launch_fwd3<64, 4>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, dmask, st)
                    : launch_fwd3<64, 2>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, kpm, causal, p, seed, lse, dmask, st);
+  }
+  // key split (attn_fwd2s_kernel): knob 1 off; RETR_TUNE_ATTN_SPLIT = 1 (the unsplit kernels
+  // everywhere) also turns it off, so the resident / streaming bitwise comparisons keep holding
+  int fs = retr_tune_get(RETR_TUNE_ATTN_FSPLIT);
+  if (retr_tune_get(RETR_TUNE_ATTN_SPLIT) == 1) fs = 1;
+  // auto: split only grids of <= 1024 query waves (tools/attn_micro.py fsplit,
+  // profiles/r3_attn_fsplit.txt: cross 128 x 400 18.8 -> 10.7 us at four parities, decoder
+  // causal 128 x 128 7.9 -> 6.4 us at two; the encoder's 1664 query waves run 24.8 us unsplit
+  // vs 30.1 split)
+  if (fs == 0) {
+    const long qwaves = (long)B * H * ((Lq + 31) / 32);
+    fs = qwaves > 1024 || ntk < 2 ? 1 : (ntk >= 4 ? 3 : 2);
+  }
+  if (fs >= 2) {
+#define RETR_FWD2S(HDV, NQ, KSP)                                                                  \
+  launch_fwd2s<HDV, NQ, KSP>(q, ldq, k, ldk, v, ldv, o, ldo, B, H, Lq, Lk, Lk, kpm, causal, p,  \
+                             seed, lse, dmask, st)
+    if (hd == 32) {
+      if (fs == 3) return RETR_FWD2S(32, 1, 4);
+      if (fs == 4) return RETR_FWD2S(32, 1, 2);
+      return RETR_FWD2S(32, 2, 2);
+    }
+    if (fs == 3) return RETR_FWD2S(64, 1, 4);
+    if (fs == 4) return RETR_FWD2S(64, 1, 2);
+    return RETR_FWD2S(64, 2, 2);
+#undef RETR_FWD2S
   }
   const bool big = (long)B * H * ((Lq + 63) / 64) >= 1024;
   if (hd == 32) {

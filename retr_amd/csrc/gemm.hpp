@@ -259,15 +259,19 @@ gemm_kernel(LA la, LB lb, EP ep, int M, int N, int K, int kchunk, int tiles_n) {
 
   if constexpr (EP::kRowSum && !LA::kContig) {
     if (do_rs) {  // block-uniform
-      float* red = (float*)smem;
-      for (int i = tid; i < BM; i += 256) red[i] = 0.f;
-      __syncthreads();
-      const int r0 = (tid % (BM / EPCA)) * EPCA;
+      // thread t holds rows [(t % RG) * EPCA, +EPCA); the 256 / RG threads of one row group
+      // are added in thread order (no LDS atomics: the bias gradient is reproducible bitwise
+      // whenever one block owns a row, i.e. without split-K)
+      constexpr int RG = BM / EPCA, NG = 256 / RG;
+      float* part = (float*)smem;
 #pragma unroll
-      for (int e = 0; e < EPCA; ++e) atomicAdd(red + r0 + e, rs[e]);
+      for (int e = 0; e < EPCA; ++e) part[tid * EPCA + e] = rs[e];
       __syncthreads();
-      for (int i = tid; i < BM; i += 256)
-        if (m0 + i < M) atomicAdd(ep.rowsum + m0 + i, red[i]);
+      for (int i = tid; i < BM; i += 256) {
+        float s = 0.f;
+        for (int g = 0; g < NG; ++g) s += part[((i / EPCA) + g * RG) * EPCA + i % EPCA];
+        if (m0 + i < M) atomicAdd(ep.rowsum + m0 + i, s);
+      }
       __syncthreads();
     }
   }

@@ -503,6 +503,9 @@ int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, in
     case 7: return launch_gemm2<FAM, 128, 128, 2, 2, 1, 1>(la, lb, ep, M, N, K, splits, st, what);
     case 8: return launch_gemm2<FAM, 64, 64, 2, 2, 4>(la, lb, ep, M, N, K, splits, st, what);
     case 9: return launch_gemm2<FAM, 64, 128, 2, 2, 3>(la, lb, ep, M, N, K, splits, st, what);
+    case 10: return launch_gemm2<FAM, 32, 64, 1, 4, 4>(la, lb, ep, M, N, K, splits, st, what);
+    case 11: return launch_gemm2<FAM, 32, 64, 1, 4, 3>(la, lb, ep, M, N, K, splits, st, what);
+    case 12: return launch_gemm2<FAM, 32, 64, 1, 4, 2>(la, lb, ep, M, N, K, splits, st, what);
     default: break;
   }
   // skinny GEMMs over a wide N (the decode step's vocabulary projection, M = 64 caption rows /

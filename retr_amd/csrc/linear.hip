@@ -18,6 +18,9 @@ template <int FAM, typename T, class LA, class LB, class EP>
 int launch_linear(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, hipStream_t st,
                   const char* what) {
   if constexpr (sizeof(T) == 2) {
+    // sweep override (tools/linear_micro.py): every bf16 linear through launch_big's tile
+    if (retr_tune_get(RETR_TUNE_BIG_TILE) != 0)
+      return launch_big<FAM>(la, lb, ep, M, N, K, 1, st, what);
     // short reductions (K <= 256: the FFN expansions) run 15-20 % faster on the 64x64
     // two-stage tile than on 128x128 (tools/linear_micro.py, profiles/r2_linear_tiles.txt)
     if ((long)cdiv(M, 128) * cdiv(N, 128) >= 160 && K >= 128)

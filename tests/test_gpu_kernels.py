@@ -927,3 +927,52 @@ def test_attention_saved_dropout_bits_equal_rehash(B, H, Lq, Lk, hd, causal, mas
     bits = np.unpackbits(words.view(np.uint8).reshape(nw, Lq, 4), axis=2, bitorder="little")
     bits = bits.reshape(nw, Lq, 32).transpose(1, 0, 2).reshape(Lq, nw * 32)[:, :Lk]
     assert abs(bits.mean() - (1 - p)) < 0.01, bits.mean()
+
+
+@pytest.mark.parametrize("B,H,Lq,Lk,hd,causal,masked", [
+    (16, 8, 128, 400, 32, False, True), (16, 8, 128, 128, 32, True, False),
+    (3, 8, 100, 77, 32, False, True), (3, 8, 100, 300, 32, True, True),
+    (2, 8, 130, 200, 64, False, True), (2, 8, 200, 200, 64, True, True)])
+def test_attention_forward_key_split(B, H, Lq, Lk, hd, causal, masked):
+    """The key-split streaming forward (attn_fwd2s_kernel: 2 or 4 key parities per 32 queries,
+    (m, l, O) merged through LDS in parity order) against the unsplit kernel: the dropout keep
+    bits it saves are bitwise the same decisions, outputs and log-sum-exp agree to fp32 / bf16
+    rounding, and each variant is deterministic (two runs bitwise equal)."""
+    g = torch.Generator(device="cpu").manual_seed(Lq * 3 + Lk)
+    C, p = H * hd, 0.1
+    bf = torch.bfloat16
+    q, k, v = (torch.randn(B * L, C, generator=g).to(DEV).to(bf) for L in (Lq, Lk, Lk))
+    kpm = None
+    if masked:
+        kpm = torch.zeros(B, Lk, dtype=torch.uint8)
+        kpm[:, Lk - Lk // 5:] = 1
+        kpm = kpm.to(DEV)
+    outs = {}
+    try:
+        for fs in (1, 2, 3, 4):
+            _lib.load().retr_tune(12, fs)
+            runs = []
+            for _ in range(2):
+                dm = ops.attn_dmask(B, H, Lq, Lk, p, bf, hd, DEV)
+                dm.fill_(0)
+                o = torch.empty(B * Lq, C, dtype=bf, device=DEV)
+                lse = torch.empty(B * H * Lq, device=DEV)
+                ops.k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, causal, p, 5, lse, None, dm)
+                torch.cuda.synchronize()
+                runs.append((o, lse, dm))
+            for a, b in zip(*runs):
+                assert torch.equal(a, b), fs
+            outs[fs] = runs[0]
+    finally:
+        _lib.load().retr_tune(12, 0)
+    o1, l1, d1 = outs[1]
+    for fs in (2, 3, 4):
+        o, lse, dm = outs[fs]
+        if causal:   # a causal wave skips the key tiles past its own diagonal: fewer words
+            w = dm != 0
+            assert torch.equal(dm[w], d1[w]), fs
+        else:
+            assert torch.equal(dm, d1), fs
+        assert (lse - l1).abs().max().item() < 1e-4, fs
+        e = ((o.float() - o1.float()).norm() / o1.float().norm()).item()
+        assert e < 5e-3, (fs, e)

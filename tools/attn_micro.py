@@ -57,6 +57,17 @@ def setup(Lq, Lk, causal, B=16, H=8, hd=32):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "fsplit":   # forward key split (RETR_TUNE_ATTN_FSPLIT)
+        for Lq, Lk, causal in SHAPES:
+            fwd, bwd, fl = setup(Lq, Lk, causal)
+            out = []
+            for fs in (0, 1, 2, 3, 4):
+                load().retr_tune(12, fs)
+                t = timeit(fwd)
+                out.append(f"fs{fs}: {t:6.2f} us {fl / t / 1e6:5.1f} TF/s")
+            load().retr_tune(12, 0)
+            print(f"fwd Lq{Lq:4d} Lk{Lk:4d} causal{causal} | " + " | ".join(out), flush=True)
+        return
     if len(sys.argv) > 1:
         which, Lq, Lk, causal, mode = sys.argv[1], *map(int, sys.argv[2:6])
         load().retr_tune(5, mode)
