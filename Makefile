@@ -20,6 +20,11 @@ $(OBJ_DIR)/%.o: $(SRC_DIR)/%.cpp $(HDRS)
 	@mkdir -p $(OBJ_DIR)
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 
+# MFMA accumulators in VGPRs: the attention kernels' per-tile score accumulators (and the
+# decode FFN's) otherwise round-trip through AGPRs (v_accvgpr_read / write: ~190 of ~1050 VALU
+# per dK/dV tile); the GEMM main loops compile to the same instructions either way
+$(OBJ_DIR)/attention2.o $(OBJ_DIR)/decode.o: CXXFLAGS += -mllvm -amdgpu-mfma-vgpr-form
+
 $(LIB): $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(OBJS) -o $@
 

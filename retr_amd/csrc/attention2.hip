@@ -20,6 +20,8 @@
 //  * dropout: 16-bit keep decisions from one 32-bit integer hash per key pair
 //    (common.hpp attn_keep), regenerated identically by the backward kernels.
 // The log-sum-exp (natural log) of every row is saved for the backward pass.
+#include <type_traits>
+
 #include "common.hpp"
 #include "../../include/retr_hip.h"
 
@@ -148,10 +150,12 @@ struct KVStager {
 
 // One 64-key tile of the streaming forward from K / V images of Tile<HD> layout: S^T = K Q^T,
 // masking, the online-softmax update of (m, l, O) and O^T += V^T drop(P)^T.
-template <int HD>
+// DROP / MASK compile-time (the kernels branch once per tile, wave-uniformly, on whether the
+// tile holds padded or causal-boundary keys): no per-score runtime selects in the common case.
+template <int HD, bool DROP, bool MASK>
 RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
     const char* Kl, const char* Vl, const bf16x8 (&qf)[HD / 16], f32x16 (&O)[HD / 32], float& m,
-    float& l, int key0, unsigned long long pmask, bool diag, int qi, int lane, bool drop,
+    float& l, int key0, unsigned long long pmask, bool diag, int qi, int lane,
     uint32_t rowkey, uint32_t th16, uint32_t* dmask, int bh, int Lq, int Lk) {
   using TL = Tile<HD>;
   constexpr int KS = HD / 16, DT = HD / 32;
@@ -168,7 +172,7 @@ RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
       S[sub] = mfma32(a, qf[s], S[sub]);
     }
   }
-  if (pmask || diag) mask_tile(S, pmask, diag, qi - key0 - 4 * hh, hh);
+  if constexpr (MASK) mask_tile(S, pmask, diag, qi - key0 - 4 * hh, hh);
   // online softmax (log2 domain)
   float mt = -INFINITY;
 #pragma unroll
@@ -195,7 +199,7 @@ RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
     for (int g = 0; g < 4; ++g) {
       const int kk = key0 + sub * 32 + 8 * g + 4 * hh;   // 4 consecutive keys
       uint32_t b01 = 0, b23 = 0;
-      if (drop) {
+      if constexpr (DROP) {
         b01 = attn_pair_bits(rowkey, kk);
         b23 = attn_pair_bits(rowkey, kk + 2);
       }
@@ -204,7 +208,7 @@ RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
         const int e = 4 * g + e4;
         float p = __builtin_amdgcn_exp2f(S[sub][e] - ms);
         l += p;
-        if (drop) {
+        if constexpr (DROP) {
           const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
           wbits |= (uint32_t)kp << (8 * g + 4 * hh + e4);
           p = kp ? p : 0.f;
@@ -212,7 +216,7 @@ RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
         pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
       }
     }
-    if (drop && dmask) store_dmask(dmask, wbits, hh, bh, Lq, Lk, qi, key0 / 32 + sub);
+    if (DROP && dmask) store_dmask(dmask, wbits, hh, bh, Lq, Lk, qi, key0 / 32 + sub);
   }
   // O^T += V^T P^T  (A = V^T via transposed LDS reads, B = P in registers)
 #pragma unroll
@@ -274,7 +278,7 @@ RETR_DEVICE void fwd_finish(const f32x16 (&O)[HD / 32], float m, float l, bf16* 
 // ~1.6 waves per SIMD (encoder 400 x 400) or less (cross 128 x 400).  At the end the parities'
 // (m, l, O) go through LDS and parity 0 merges them in parity order (deterministic; the same
 // products as the unsplit kernel, summed in another fixed order).
-template <int HD, int NQ, int KSP>
+template <int HD, int NQ, int KSP, bool DROP>
 __global__ void __launch_bounds__(NQ * KSP * 64)
 attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
                   bf16* o, long ldo, int H, int Lq, int Lk, int kbr, const unsigned char* kpm,
@@ -304,7 +308,7 @@ attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* 
   // a wave's own causal range can end before the block's
   const int wtiles = causal ? min(ntiles, (q0 + 32 + 63) / 64) : ntiles;
 
-  const bool drop = dp.thresh != 0;
+  constexpr bool drop = DROP;
   const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
   const uint32_t rowkey = drop ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
 
@@ -337,8 +341,12 @@ attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* 
       const unsigned long long pmask = __ballot(pad);
       const bool diag = causal && (key0 + TL::KT - 1 > q0);
       const char* Kl = slot + par * TL::STAGE;
-      fwd2_tile<HD>(Kl, Kl + TL::BYTES, qf, O, m, l, key0, pmask, diag, qi, lane, drop, rowkey,
-                    th16, dmask, b * H + h, Lq, Lk);
+      if (pmask || diag)
+        fwd2_tile<HD, DROP, true>(Kl, Kl + TL::BYTES, qf, O, m, l, key0, pmask, diag, qi, lane,
+                                  rowkey, th16, dmask, b * H + h, Lq, Lk);
+      else
+        fwd2_tile<HD, DROP, false>(Kl, Kl + TL::BYTES, qf, O, m, l, key0, pmask, diag, qi, lane,
+                                   rowkey, th16, dmask, b * H + h, Lq, Lk);
     }
     if (it + 1 < nit) {
 #pragma unroll
@@ -378,7 +386,7 @@ attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* 
   fwd_finish<HD>(O, m, l, o, ldo, b, h, H, qi, Lq, hh, drop, dp.scale, lse);
 }
 
-template <int HD, int NW>
+template <int HD, int NW, bool DROP>
 __global__ void __launch_bounds__(NW * 64)
 attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
                  bf16* o, long ldo, int H, int Lq, int Lk, int kbr, const unsigned char* kpm,
@@ -403,7 +411,7 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
   if (causal) kend = min(Lk, qblk + 32 * NW);
   const int ntiles = (kend + TL::KT - 1) / TL::KT;
 
-  const bool drop = dp.thresh != 0;
+  constexpr bool drop = DROP;
   const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
   const uint32_t rowkey = drop ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
 
@@ -430,8 +438,12 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
     const unsigned long long pmask = __ballot(pad);
     const bool diag = causal && (key0 + TL::KT - 1 > q0);
 
-    fwd2_tile<HD>(Kl, Vl, qf, O, m, l, key0, pmask, diag, qi, lane, drop, rowkey, th16, dmask,
-                  b * H + h, Lq, Lk);
+    if (pmask || diag)
+      fwd2_tile<HD, DROP, true>(Kl, Vl, qf, O, m, l, key0, pmask, diag, qi, lane, rowkey, th16,
+                                dmask, b * H + h, Lq, Lk);
+    else
+      fwd2_tile<HD, DROP, false>(Kl, Vl, qf, O, m, l, key0, pmask, diag, qi, lane, rowkey, th16,
+                                 dmask, b * H + h, Lq, Lk);
     if (t + 1 < ntiles) stg.store(smem + ((t + 1) & 1) * TL::STAGE, tid);
     __syncthreads();
   }
@@ -447,9 +459,11 @@ int launch_fwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
   const float qscale = kLog2e / sqrtf((float)HD);
   const size_t lds = 2 * Tile<HD>::STAGE;
   dim3 grid((Lq + 32 * NW - 1) / (32 * NW), H, B);
-  hipLaunchKernelGGL((attn_fwd2_kernel<HD, NW>), grid, dim3(NW * 64), lds, st, (const bf16*)q,
-                     ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, H, Lq, Lk, kbr,
-                     kpm, causal, qscale, make_dp(p, seed), lse, dmask);
+  const DropoutParams dp = make_dp(p, seed);
+  auto kern = dp.thresh != 0 ? attn_fwd2_kernel<HD, NW, true> : attn_fwd2_kernel<HD, NW, false>;
+  hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, st, (const bf16*)q, ldq, (const bf16*)k, ldk,
+                     (const bf16*)v, ldv, (bf16*)o, ldo, H, Lq, Lk, kbr, kpm, causal, qscale, dp,
+                     lse, dmask);
   return retr_check_launch("attention_fwd2");
 }
 
@@ -460,14 +474,16 @@ int launch_fwd2s(const void* q, long ldq, const void* k, long ldk, const void* v
                  float* lse, uint32_t* dmask, hipStream_t st) {
   const float qscale = kLog2e / sqrtf((float)HD);
   const size_t lds = 2 * KSP * Tile<HD>::STAGE;
-  auto kern = attn_fwd2s_kernel<HD, NQ, KSP>;
+  const DropoutParams dp = make_dp(p, seed);
+  auto kern = dp.thresh != 0 ? attn_fwd2s_kernel<HD, NQ, KSP, true>
+                             : attn_fwd2s_kernel<HD, NQ, KSP, false>;
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
   dim3 grid((Lq + 32 * NQ - 1) / (32 * NQ), H, B);
   hipLaunchKernelGGL(kern, grid, dim3(NQ * KSP * 64), lds, st, (const bf16*)q, ldq,
                      (const bf16*)k, ldk, (const bf16*)v, ldv, (bf16*)o, ldo, H, Lq, Lk, kbr, kpm,
-                     causal, qscale, make_dp(p, seed), lse, dmask);
+                     causal, qscale, dp, lse, dmask);
   return retr_check_launch("attention_fwd2s");
 }
 
@@ -702,7 +718,9 @@ __device__ long long g_attn_t[2][8192][3];
 // KSP = 2: the key tiles are split between two waves per 32 queries (even / odd tiles), which
 // doubles the waves of a grid that is otherwise ~6 waves per CU at the RE⫶TR sizes; the two
 // partial dQ accumulators are added through LDS at the end (fixed order: even + odd).
-template <int HD, int NW, int KSP = 1>
+// DM (dropout source, compile-time so the score loop carries no runtime selects): 0 no dropout,
+// 1 the forward's saved keep bits, 2 re-hashed decisions.
+template <int HD, int NW, int KSP = 1, int DM = 1>
 __global__ void __launch_bounds__(NW * 64)
 attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
                     const bf16* o, long ldo, const bf16* dout, long lddo, const float* lse,
@@ -790,48 +808,56 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
     const uint32_t pmlo = (uint32_t)pml, pmhi = (uint32_t)(pml >> 32);
     const int mlim = qi - key0 - 4 * hh;
     uint32_t wm[2] = {0u, 0u};                     // saved keep bits of the tile's two sub-tiles
-    if (drop && dmask) {
+    if constexpr (DM == 1) {
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         const int w = min(key0 / 32 + sub, nwm - 1);
         wm[sub] = dmask[((long)(b * H + h) * nwm + w) * Lq + qc];
       }
     }
-    bf16x8 sf[4];
+    f32x16 S[2], P[2];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      f32x16 S, P;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) S[e] = 0.f, P[e] = 0.f;
+      for (int e = 0; e < 16; ++e) S[sub][e] = 0.f, P[sub][e] = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const int off = L::off(sub * 32 + r, 2 * s + hh);
-        S = mfma32(*(const bf16x8*)(Kl + off), qf[s], S);
-        P = mfma32(*(const bf16x8*)(Vl + off), dof[s], P);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int kk = key0 + sub * 32 + 8 * g + 4 * hh;
-        uint32_t b01 = 0, b23 = 0;
-        if (drop && !dmask) {
-          b01 = attn_pair_bits(rowkey, kk);
-          b23 = attn_pair_bits(rowkey, kk + 2);
-        }
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-          const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
-          const bool msk = anym & key_masked(pmlo, pmhi, kl - 4 * hh, diag, mlim);
-          const float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - lq2);
-          float dpv = P[e];
-          if (drop) {
-            const bool kp = dmask ? ((wm[sub] >> (8 * g + 4 * hh + e4)) & 1u) != 0u
-                                  : attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
-            dpv = kp ? dpv * dp.scale : 0.f;
-          }
-          sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - Dq));
-        }
+        S[sub] = mfma32(*(const bf16x8*)(Kl + off), qf[s], S[sub]);
+        P[sub] = mfma32(*(const bf16x8*)(Vl + off), dof[s], P[sub]);
       }
     }
+    // dS = P (drop(dP) - D); masking only on tiles that hold padded / causal-boundary keys
+    bf16x8 sf[4];
+    auto scores = [&](auto maskc) {
+      constexpr bool MASK = decltype(maskc)::value;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int kk = key0 + sub * 32 + 8 * g + 4 * hh;
+          uint32_t b01 = 0, b23 = 0;
+          if constexpr (DM == 2) {
+            b01 = attn_pair_bits(rowkey, kk);
+            b23 = attn_pair_bits(rowkey, kk + 2);
+          }
+#pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
+            float p = __builtin_amdgcn_exp2f(S[sub][e] - lq2);
+            if constexpr (MASK) p = key_masked(pmlo, pmhi, kl - 4 * hh, diag, mlim) ? 0.f : p;
+            float dpv = P[sub][e];
+            if constexpr (DM != 0) {
+              const bool kp = DM == 1 ? ((wm[sub] >> (8 * g + 4 * hh + e4)) & 1u) != 0u
+                                      : attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
+              dpv = kp ? dpv * dp.scale : 0.f;
+            }
+            sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - Dq));
+          }
+        }
+    };
+    if (anym) scores(std::true_type{});
+    else scores(std::false_type{});
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
@@ -879,7 +905,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
 
 // KSP = 2: the query tiles are split between two waves per 32 keys (even / odd tiles); the
 // dK / dV partials are added through LDS at the end (even + odd).
-template <int HD, int NW, int KSP = 1>
+template <int HD, int NW, int KSP = 1, int DM = 1>
 __global__ void __launch_bounds__(NW * 64)
 attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v,
                       long ldv, const bf16* dout, long lddo, const float* lse, const float* D,
@@ -961,7 +987,8 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
   ATTN_T(1, 1)
 
   // a wave's keys see no query below its first key (causal): skip those tiles
-  const int wt0 = causal ? max(0, (kblk + kw * 32 - qstart) / 64) : 0;
+  const int kfirst = kblk + kw * 32;
+  const int wt0 = causal ? max(0, (kfirst - qstart) / 64) : 0;
   for (int it = wt0 + ((wt0 & (KSP - 1)) != qh ? 1 : 0); it < ntiles; it += KSP) {
     const int qt = qstart + it * 64;
     const char* Ql = Qs + it * L::TILE;
@@ -969,44 +996,54 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
     const float* el = exl + it * 64;
     const float* ed = exd + it * 64;
     const uint32_t* ek = exk + it * 64;
-    bf16x8 pf[4], sf[4];
+    f32x16 S[2], P[2];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      f32x16 S, P;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) S[e] = 0.f, P[e] = 0.f;
+      for (int e = 0; e < 16; ++e) S[sub][e] = 0.f, P[sub][e] = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const int off = L::off(sub * 32 + r, 2 * s + hh);
-        S = mfma32(*(const bf16x8*)(Ql + off), kf[s], S);
-        P = mfma32(*(const bf16x8*)(Dl + off), vf[s], P);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int ql = sub * 32 + 8 * g + 4 * hh;
-        const f32x4 l4 = *(const f32x4*)(el + ql);
-        const f32x4 d4 = *(const f32x4*)(ed + ql);
-        uint4 w4 = {0u, 0u, 0u, 0u};
-        if (drop && dmask) w4 = *(const uint4*)(exw + it * 64 + ql);
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-          const int e = 4 * g + e4, qq = qt + ql + e4;
-          const bool msk = kmask || qq >= Lq || (causal && kj > qq);
-          float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - l4[e4]);
-          float dpv = P[e], pmv = p;
-          if (drop) {
-            const uint32_t wv = e4 == 0 ? w4.x : e4 == 1 ? w4.y : e4 == 2 ? w4.z : w4.w;
-            const bool kp = dmask ? ((wv >> r) & 1u) != 0u
-                                  : attn_keep(attn_pair_bits(ek[ql + e4], (uint32_t)kj),
-                                              (uint32_t)kj, th16);
-            dpv = kp ? dpv * dp.scale : 0.f;
-            pmv = kp ? p * dp.scale : 0.f;
-          }
-          pf[2 * sub + (e >> 3)][e & 7] = (bf16)pmv;
-          sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - d4[e4]));
-        }
+        S[sub] = mfma32(*(const bf16x8*)(Ql + off), kf[s], S[sub]);
+        P[sub] = mfma32(*(const bf16x8*)(Dl + off), vf[s], P[sub]);
       }
     }
+    // P and dS.  Padded keys (kmask) are left unmasked here -- a lane's accumulators are only
+    // ever its own key's dK / dV columns, written as zeros below -- and the row / causal masks
+    // run only on tiles that hold rows past Lq or cross this wave's diagonal
+    bf16x8 pf[4], sf[4];
+    auto scores = [&](auto maskc) {
+      constexpr bool MASK = decltype(maskc)::value;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int ql = sub * 32 + 8 * g + 4 * hh;
+          const f32x4 l4 = *(const f32x4*)(el + ql);
+          const f32x4 d4 = *(const f32x4*)(ed + ql);
+          uint4 w4 = {0u, 0u, 0u, 0u};
+          if constexpr (DM == 1) w4 = *(const uint4*)(exw + it * 64 + ql);
+#pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4) {
+            const int e = 4 * g + e4, qq = qt + ql + e4;
+            float p = __builtin_amdgcn_exp2f(S[sub][e] - l4[e4]);
+            if constexpr (MASK) p = (qq >= Lq || (causal && kj > qq)) ? 0.f : p;
+            float dpv = P[sub][e], pmv = p;
+            if constexpr (DM != 0) {
+              const uint32_t wv = e4 == 0 ? w4.x : e4 == 1 ? w4.y : e4 == 2 ? w4.z : w4.w;
+              const bool kp = DM == 1 ? ((wv >> r) & 1u) != 0u
+                                      : attn_keep(attn_pair_bits(ek[ql + e4], (uint32_t)kj),
+                                                  (uint32_t)kj, th16);
+              dpv = kp ? dpv * dp.scale : 0.f;
+              pmv = kp ? p * dp.scale : 0.f;
+            }
+            pf[2 * sub + (e >> 3)][e & 7] = (bf16)pmv;
+            sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - d4[e4]));
+          }
+        }
+    };
+    if (qt + 64 > Lq || (causal && qt < kfirst + 32)) scores(std::true_type{});
+    else scores(std::false_type{});
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
@@ -1055,9 +1092,9 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
         typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
         bf16x4 wk, wv;
 #pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-          wk[e4] = (bf16)(GK[dt][4 * g + e4] * scale);
-          wv[e4] = (bf16)GV[dt][4 * g + e4];
+        for (int e4 = 0; e4 < 4; ++e4) {   // a padded key's gradients are zero
+          wk[e4] = kmask ? (bf16)0.f : (bf16)(GK[dt][4 * g + e4] * scale);
+          wv[e4] = kmask ? (bf16)0.f : (bf16)GV[dt][4 * g + e4];
         }
         *(bf16x4*)(krow + dt * 32 + 8 * g + 4 * hh) = wk;
         *(bf16x4*)(vrow + dt * 32 + 8 * g + 4 * hh) = wv;
@@ -1094,8 +1131,8 @@ int launch_fwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
   return retr_check_launch("attention_fwd3");
 }
 
-template <int HD, int NW>
-int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+template <int HD, int NW, int DM>
+int launch_bwd3_t(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
                 const void* o, long ldo, const void* dout, long lddo, const float* lse,
                 void* dq, long lddq, void* dk, long lddk, void* dv, long lddv, int B, int H,
                 int Lq, int Lk, const unsigned char* kpm, int causal, float p,
@@ -1116,14 +1153,14 @@ int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
     const size_t lds = std::max(res_lds_fwd<HD>(ntk), (size_t)(split ? nwq * (HD / 32) * 4096 : 0));
     if (split) {   // 2 x nwq waves per block: nwq query waves x 2 key-tile parities
       if (nwq == 4) {
-        auto kern = attn_bwd_dq3_kernel<HD, 8, 2>;
+        auto kern = attn_bwd_dq3_kernel<HD, 8, 2, DM>;
         allow_lds(kern, lds);
         hipLaunchKernelGGL(kern, dim3((Lq + 127) / 128, H, B), dim3(512), lds, st, (const bf16*)q,
                            ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
                            (const bf16*)dout, lddo, lse, D, (bf16*)dq, lddq, H, Lq, Lk, kpm,
                            causal, cs, scale, dp, ntk, dmask);
       } else {
-        auto kern = attn_bwd_dq3_kernel<HD, 4, 2>;
+        auto kern = attn_bwd_dq3_kernel<HD, 4, 2, DM>;
         allow_lds(kern, lds);
         hipLaunchKernelGGL(kern, dim3((Lq + 63) / 64, H, B), dim3(256), lds, st, (const bf16*)q,
                            ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
@@ -1131,14 +1168,14 @@ int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
                            causal, cs, scale, dp, ntk, dmask);
       }
     } else if (nwq == 4) {
-      auto kern = attn_bwd_dq3_kernel<HD, 4>;
+      auto kern = attn_bwd_dq3_kernel<HD, 4, 1, DM>;
       allow_lds(kern, lds);
       hipLaunchKernelGGL(kern, dim3((Lq + 127) / 128, H, B), dim3(256), lds, st, (const bf16*)q,
                          ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
                          (const bf16*)dout, lddo, lse, D, (bf16*)dq, lddq, H, Lq, Lk, kpm, causal,
                          cs, scale, dp, ntk, dmask);
     } else {
-      auto kern = attn_bwd_dq3_kernel<HD, 2>;
+      auto kern = attn_bwd_dq3_kernel<HD, 2, 1, DM>;
       allow_lds(kern, lds);
       hipLaunchKernelGGL(kern, dim3((Lq + 63) / 64, H, B), dim3(128), lds, st, (const bf16*)q,
                          ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)o, ldo,
@@ -1155,14 +1192,14 @@ int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
                               (size_t)(split_kv ? nwk * 2 * (HD / 32) * 4096 : 0));
   if (split_kv) {
     if (nwk == 4) {
-      auto kern = attn_bwd_dkdv3_kernel<HD, 8, 2>;
+      auto kern = attn_bwd_dkdv3_kernel<HD, 8, 2, DM>;
       allow_lds(kern, lds);
       hipLaunchKernelGGL(kern, dim3((Lk + 127) / 128, H, B), dim3(512), lds, st, (const bf16*)q,
                          ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo,
                          lse, D, (bf16*)dk, lddk, (bf16*)dv, lddv, H, Lq, Lk, kpm, causal, cs,
                          scale, dp, ntq, dmask);
     } else {
-      auto kern = attn_bwd_dkdv3_kernel<HD, 4, 2>;
+      auto kern = attn_bwd_dkdv3_kernel<HD, 4, 2, DM>;
       allow_lds(kern, lds);
       hipLaunchKernelGGL(kern, dim3((Lk + 63) / 64, H, B), dim3(256), lds, st, (const bf16*)q,
                          ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo,
@@ -1170,14 +1207,14 @@ int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
                          scale, dp, ntq, dmask);
     }
   } else if (nwk == 4) {
-    auto kern = attn_bwd_dkdv3_kernel<HD, 4>;
+    auto kern = attn_bwd_dkdv3_kernel<HD, 4, 1, DM>;
     allow_lds(kern, lds);
     hipLaunchKernelGGL(kern, dim3((Lk + 127) / 128, H, B), dim3(256), lds, st, (const bf16*)q,
                        ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo, lse,
                        D, (bf16*)dk, lddk, (bf16*)dv, lddv, H, Lq, Lk, kpm, causal, cs, scale, dp,
                        ntq, dmask);
   } else {
-    auto kern = attn_bwd_dkdv3_kernel<HD, 2>;
+    auto kern = attn_bwd_dkdv3_kernel<HD, 2, 1, DM>;
     allow_lds(kern, lds);
     hipLaunchKernelGGL(kern, dim3((Lk + 63) / 64, H, B), dim3(128), lds, st, (const bf16*)q,
                        ldq, (const bf16*)k, ldk, (const bf16*)v, ldv, (const bf16*)dout, lddo, lse,
@@ -1185,6 +1222,19 @@ int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v,
                        ntq, dmask);
   }
   return retr_check_launch("attention_bwd_dkdv3");
+}
+
+// dropout source of the backward kernels: 0 none, 1 the forward's saved keep bits, 2 re-hash
+template <int HD, int NW>
+int launch_bwd3(const void* q, long ldq, const void* k, long ldk, const void* v, long ldv,
+                const void* o, long ldo, const void* dout, long lddo, const float* lse,
+                void* dq, long lddq, void* dk, long lddk, void* dv, long lddv, int B, int H,
+                int Lq, int Lk, const unsigned char* kpm, int causal, float p,
+                unsigned long long seed, float* D, int nwq, int nwk, const uint32_t* dmask,
+                hipStream_t st) {
+  if (make_dp(p, seed).thresh == 0) return launch_bwd3_t<HD, NW, 0>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, nwq, nwk, dmask, st);
+  if (dmask) return launch_bwd3_t<HD, NW, 1>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, nwq, nwk, dmask, st);
+  return launch_bwd3_t<HD, NW, 2>(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, dq, lddq, dk, lddk, dv, lddv, B, H, Lq, Lk, kpm, causal, p, seed, D, nwq, nwk, dmask, st);
 }
 
 // 4 waves per block when that still gives >= 384 blocks, else 2
