@@ -105,7 +105,10 @@ enum {
   RETR_TUNE_ATTN_FSPLIT = 12,   /* bf16 streaming attention forward, key split: 0 auto, 1 off,
                                    2 two parities x 64 queries, 3 four parities x 32 queries,
                                    4 two parities x 32 queries */
-  RETR_TUNE_COUNT = 13
+  RETR_TUNE_LIN_SMALL = 13,     /* 2: few-tile bf16 linears single-pass on the 32x64 LDS-DMA tile
+                                   (no split-K up to K 2048; rejected: +0.1 ms/step in the graphed
+                                   step, profiles/r3_ab_lin_small.txt); 0 / 1 split-K slabs */
+  RETR_TUNE_COUNT = 14
 };
 int retr_tune(int knob, int value);
 

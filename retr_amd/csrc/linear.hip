@@ -21,13 +21,12 @@ int launch_linear(const LA& la, const LB& lb, const EP& ep, int M, int N, int K,
     // sweep override (tools/linear_micro.py): every bf16 linear through launch_big's tile
     if (retr_tune_get(RETR_TUNE_BIG_TILE) != 0)
       return launch_big<FAM>(la, lb, ep, M, N, K, 1, st, what);
-    // few output tiles: the 32x64 LDS-DMA tile (4 waves side by side over 64 columns, S2 ring)
-    // for long reductions (K >= 1024, single-pass instead of split-K) and for the small
-    // decoder-side projections the register-staged 32x64 kernel took (tools/linear_micro.py
-    // small: M2048 N256 K256 4.3 -> 4.0 us, N512 5.0 -> 4.7 us)
+    // RETR_TUNE_LIN_SMALL = 2 (sweeps; not the default, see retr_linear_splits): few output
+    // tiles on the 32x64 LDS-DMA tile (4 waves side by side over 64 columns, S2 ring)
     {
       const long b128 = (long)cdiv(M, 128) * cdiv(N, 128), b64 = (long)cdiv(M, 64) * cdiv(N, 64);
-      if (b128 < 160 && K >= 128 && (K >= 1024 || b64 < 192))
+      if (b128 < 160 && K >= 128 && (K >= 1024 || b64 < 192) &&
+          retr_tune_get(RETR_TUNE_LIN_SMALL) == 2)
         return launch_gemm2<FAM, 32, 64, 1, 4, 2>(la, lb, ep, M, N, K, 1, st, what);
     }
     // short reductions (K <= 256: the FFN expansions) run 15-20 % faster on the 64x64
@@ -312,14 +311,15 @@ int retr_linear_splits(int dtype, int M, int N, int K) {
   // K-steps per slice, at most 8 slices (bf16; fp32 keeps single-pass GEMMs).
   // tools/splitk_micro.py (profiles/r2_splitk_micro.txt): the vocabulary head's dgrad 276 us
   // single-pass -> 84 us at 8 slices; the FFN shapes gain little beyond 4
-  // K <= 2048 (the d_model-256 FFN down-projections and up-projection data gradients) runs
-  // single-pass on the 32x64 LDS-DMA tile instead (launch_linear): no slab round trip, no
-  // epilogue launch (tools/linear_micro.py splitk, profiles/r3_linear_splitk.txt: M2048 14.7 ->
-  // 11.1 us fwd, 14.4 -> 12.7 us dgrad; M6400 23.5 -> 20.8 / 24.4 -> 21.9 us)
+  // RETR_TUNE_LIN_SMALL = 2: K <= 2048 single-pass on the 32x64 LDS-DMA tile instead
+  // (launch_linear) -- faster in isolation (tools/linear_micro.py splitk,
+  // profiles/r3_linear_splitk.txt: M2048 14.7 -> 11.1 us fwd) but 0.1 ms/step slower in the
+  // graphed step (profiles/r3_ab_lin_small.txt), so not the default
   if (dtype != RETR_BF16 || M <= 0) return 1;
   const long tiles = (long)cdiv(M, 128) * cdiv(N, 128);
   const int ksteps = cdiv(K, 64);
-  if (tiles >= 160 || ksteps <= 32) return 1;
+  if (tiles >= 160 || ksteps < 16) return 1;
+  if (ksteps <= 32 && retr_tune_get(RETR_TUNE_LIN_SMALL) == 2) return 1;
   long s = (512 + tiles - 1) / tiles;
   if (s > ksteps / 8) s = ksteps / 8;
   if (s > 8) s = 8;

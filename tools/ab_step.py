@@ -32,6 +32,8 @@ VARIANTS = {
     "split_all": {("TUNE", 10): 2},
     "no_dmask_split_off": {("ATTR", "ATTN_DMASK"): False, ("TUNE", 10): 1},
     "no_stem_pool": {("ENV", "RETR_STEM_POOL"): "0"},
+    "lin_small": {("TUNE", 13): 2},
+    "fsplit_off": {("TUNE", 12): 1},
 }
 
 
@@ -41,6 +43,9 @@ def apply(v):
     ops.FUSE_LN_PARAMS = True
     ops.ATTN_DMASK = True
     load().retr_tune(10, 0)
+    load().retr_tune(12, 0)
+    load().retr_tune(13, 0)
+    ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
     for (table, key), val in VARIANTS[v].items():
         if table == "ENV":                     # read when the model is built

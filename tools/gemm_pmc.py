@@ -4,7 +4,8 @@ the implicit-GEMM kernel: wave states, LDS traffic / bank conflicts, instruction
     rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY ... -- python tools/gemm_pmc.py fwd3 [tile] [n]
 
 shapes: fwd3 = 3x3 conv 40x40x256 -> 256 (M 25600, N 256, K 2304), fwd1 = 1x1 conv
-80x80x128 -> 512, gemm = the plain GEMM of fwd3's size (retr_linear_fwd).  tile: the
+80x80x128 -> 512, gemm = the plain GEMM of fwd3's size (retr_linear_fwd), ffn = the encoder FFN
+expansion (M 6400, N 2048, K 256, bias + ReLU).  tile: the
 RETR_TUNE_BIG_TILE override (0 = built-in choice).
 """
 import os
@@ -24,15 +25,16 @@ def main():
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 20
     bf = torch.bfloat16
     load().retr_tune(6, tile)
-    if shape == "gemm":
-        M, N, K = 25600, 256, 2304
+    if shape in ("gemm", "ffn"):
+        M, N, K = (25600, 256, 2304) if shape == "gemm" else (6400, 2048, 256)
         x = torch.randn(M, K, device="cuda").to(bf)
         w = (torch.randn(N, K, device="cuda") * 0.05).to(bf)
         b = torch.randn(N, device="cuda")
         y = torch.empty(M, N, device="cuda", dtype=bf)
         fl = 2.0 * M * N * K
+        relu = int(shape == "ffn")
         fn = lambda: call("retr_linear_fwd", BF, ptr(x), K, ptr(w), K, ptr(b), ptr(y), N, 0,  # noqa: E731
-                          M, N, K, 0, None, 0, 0.0, 0, stream())
+                          M, N, K, relu, None, 0, 0.0, 0, stream())
     else:
         Nb, H, C, Co, k, p = (16, 40, 256, 256, 3, 1) if shape == "fwd3" else (16, 80, 128, 512, 1, 0)
         x = torch.randn(Nb * H * H * C, device="cuda").to(bf)
