@@ -90,7 +90,8 @@ enum {
   RETR_TUNE_BIG_TILE = 6,       /* large bf16 GEMMs (convs): 1 128x128 S1, 2 128x128 S2,
                                    3 256x256, 4 128x64 S3, 5 reg-staged 64x64, 6 64x64 S2,
                                    7 128x128 S1 one epilogue band, 8 64x64 S4, 9 64x128 S3,
-                                   10 / 11 / 12 32x64 S4 / S3 / S2 */
+                                   10 / 11 / 12 32x64 S4 / S3 / S2, 13 64x64 S1, 14 64x128 S1,
+                                   15 128x64 S1 */
   RETR_TUNE_NT_STORE = 7,       /* 1: non-temporal GEMM output stores */
   RETR_TUNE_CONV_WGRAD_SPLITS = 8, /* conv weight-gradient split-K: 1 legacy ceil(512 / tiles),
                                       >= 2 that many slices (capped by the K-steps) */
@@ -108,7 +109,9 @@ enum {
   RETR_TUNE_LIN_SMALL = 13,     /* 2: few-tile bf16 linears single-pass on the 32x64 LDS-DMA tile
                                    (no split-K up to K 2048; rejected: +0.1 ms/step in the graphed
                                    step, profiles/r3_ab_lin_small.txt); 0 / 1 split-K slabs */
-  RETR_TUNE_COUNT = 14
+  RETR_TUNE_SHORTK = 14,        /* short-K (K <= 256, N >= 256) bf16 GEMMs on the single-stage
+                                   64x64 LDS-DMA tile: 0 auto (on), 1 off */
+  RETR_TUNE_COUNT = 15
 };
 int retr_tune(int knob, int value);
 

@@ -506,6 +506,9 @@ int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, in
     case 10: return launch_gemm2<FAM, 32, 64, 1, 4, 4>(la, lb, ep, M, N, K, splits, st, what);
     case 11: return launch_gemm2<FAM, 32, 64, 1, 4, 3>(la, lb, ep, M, N, K, splits, st, what);
     case 12: return launch_gemm2<FAM, 32, 64, 1, 4, 2>(la, lb, ep, M, N, K, splits, st, what);
+    case 13: return launch_gemm2<FAM, 64, 64, 2, 2, 1>(la, lb, ep, M, N, K, splits, st, what);
+    case 14: return launch_gemm2<FAM, 64, 128, 2, 2, 1>(la, lb, ep, M, N, K, splits, st, what);
+    case 15: return launch_gemm2<FAM, 128, 64, 2, 2, 1>(la, lb, ep, M, N, K, splits, st, what);
     default: break;
   }
   // skinny GEMMs over a wide N (the decode step's vocabulary projection, M = 64 caption rows /
@@ -516,6 +519,15 @@ int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, in
     return launch_gemm2<FAM, 64, 64, 2, 2, 4>(la, lb, ep, M, N, K, splits, st, what);
   if (M <= 512 && N >= 4096 && K >= 256)
     return launch_gemm2<FAM, 128, 128, 2, 2, 1, 2>(la, lb, ep, M, N, K, splits, st, what);
+  // short reductions over wide outputs (1x1 convs with K <= 256 into >= 256 channels and their
+  // data gradients, the FFN expansions): HBM / latency-bound, so blocks in flight beat ring
+  // depth -- the single-stage 64x64 tile (17 KB of LDS: 8 blocks = 32 waves per CU) over the
+  // 2-stage 64x64 / single-stage 128x128 ones (tools/conv_micro.py r50 with RETR_SWEEP_S1,
+  // profiles/r3_shortk_s1.txt: 80x80x128->512 + residual 50.9 -> 42.7 us, its data gradient
+  // 80x80x512<-128 45.4 -> 36.3 us, 160x160x256<-128 116 -> 103 us; FFN 6400x2048x256
+  // 20.5 -> 19.4 us)
+  if (K <= 256 && N >= 256 && splits == 1 && retr_tune_get(RETR_TUNE_SHORTK) != 1)
+    return launch_gemm2<FAM, 64, 64, 2, 2, 1>(la, lb, ep, M, N, K, splits, st, what);
   // caller's choice of the 64x64 two-stage tile (conv shapes where 4x the blocks win: the
   // 20x20 maps of layer 4 and the 1x1 convolutions to / from 1024 channels at 40x40)
   if (prefer64) return launch_gemm2<FAM, 64, 64, 2, 2, 2>(la, lb, ep, M, N, K, splits, st, what);

@@ -34,6 +34,7 @@ VARIANTS = {
     "no_stem_pool": {("ENV", "RETR_STEM_POOL"): "0"},
     "lin_small": {("TUNE", 13): 2},
     "fsplit_off": {("TUNE", 12): 1},
+    "shortk_off": {("TUNE", 14): 1},
 }
 
 
@@ -45,6 +46,7 @@ def apply(v):
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
+    load().retr_tune(14, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
     for (table, key), val in VARIANTS[v].items():

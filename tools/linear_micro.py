@@ -70,6 +70,8 @@ def main():
     bf = torch.bfloat16
     small = len(sys.argv) > 1 and sys.argv[1] == "small"
     tiles = (0, 2, 4, 5, 6, 8, 9, 10, 11, 12) if small else (0, 1, 2, 3, 4, 6, 8, 9)
+    if os.environ.get("RETR_SWEEP_S1"):
+        tiles = (0, 13, 14, 15)
     for M, N, K, relu, f32 in (SMALL if small else SHAPES):
         x = torch.randn(M, K, device="cuda").to(bf)
         w = (torch.randn(N, K, device="cuda") * 0.05).to(bf)
