@@ -752,6 +752,18 @@ int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* a
         if (sizeof(T) == 2 && g.Co % 64 == 0 && ph.nkh * ph.nkw <= 32) {
           ConvDgradPhaseAU<T> pa{(const T*)dy, g, ph, Mp, Kp};
           DgradPhaseWU<T> pb{(const T*)wt, g, ph, N, Kp};
+          // <= 128 input channels over >= 64k phase pixels (layer2.0's 3x3 stride-2 at cfg2):
+          // the single-stage 64x128 tile, more blocks in flight (tools/conv_micro.py r50,
+          // profiles/r3_shortk_s1.txt: 160x160x128 <- 128 k3s2 120 -> 99 us)
+          if constexpr (sizeof(T) == 2) {
+            if (N <= 128 && Mp >= 65536 && retr_tune_get(RETR_TUNE_BIG_TILE) == 0 &&
+                retr_tune_get(RETR_TUNE_SHORTK) != 1) {
+              if (int e = launch_gemm2<kFamConvDgrad, 64, 128, 2, 2, 1>(pa, pb, pe, Mp, N, Kp, 1,
+                                                                          st, "conv_dgrad_s2"))
+                return e;
+              continue;
+            }
+          }
           if (int e = launch_auto<kFamConvDgrad, T>(pa, pb, pe, Mp, N, Kp, 1, st, "conv_dgrad_s2"))
             return e;
           continue;

@@ -207,7 +207,7 @@ FAMILY_SYMBOL = {"linear_fwd": "gemm{,2,2_group}_kernel<0,",
                  "linear_wgrad": "gemm{,2,2_group}_kernel<2,",
                  "conv_fwd": "gemm{,2}_kernel<3, + bottleneck_s1_kernel + stem_pool_kernel",
                  "conv_dgrad": "gemm{,2}_kernel<4,", "conv_wgrad": "gemm{,2}_kernel<5,",
-                 "attention_fwd": "attn_fwd{,2}_kernel",
+                 "attention_fwd": "attn_fwd{,2,2s}_kernel",
                  "attention_bwd": "attn_bwd_"}
 
 
@@ -222,7 +222,7 @@ def family_of_symbol(name):
                 "conv_wgrad")[int(m.group(1))]
     if "bottleneck_s1_kernel" in name or "stem_pool_kernel" in name:
         return "conv_fwd"
-    if re.search(r"attn_fwd\d*_kernel", name):
+    if re.search(r"attn_fwd\d*s?_kernel", name):
         return "attention_fwd"
     if "attn_bwd_" in name:
         return "attention_bwd"
