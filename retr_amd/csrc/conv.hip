@@ -593,7 +593,9 @@ WgradPlan wgrad_plan(int R, int Ncols, int Mp, bool dense1x1) {
   if (sizeof(T) == 2 && R >= 64 && Ncols >= 64 &&
       (tt == 1 || (tt == 0 && dense1x1 && (R <= 128 || Ncols <= 128 || Mp <= 8192))))
     p.tile = 65;
-  const int bm = (p.tile == 64 || p.tile == 65) ? 64 : 128;
+  // knob 3: the single-stage 64x64 tile (8 blocks per CU) wherever the 64x64 one is chosen
+  if (p.tile == 65 && tt == 3) p.tile = 66;
+  const int bm = (p.tile == 64 || p.tile == 65 || p.tile == 66) ? 64 : 128;
   const int bn = bm;
   const long tiles = (long)cdiv(R, bm) * cdiv(Ncols, bn);
   const int ksteps = cdiv(Mp, BK);
@@ -608,13 +610,13 @@ WgradPlan wgrad_plan(int R, int Ncols, int Mp, bool dense1x1) {
   long s;
   if (tune >= 2) {
     s = tune < smax ? tune : smax;
-  } else if (tune == 1 || (p.tile != 128 && p.tile != 65)) {
+  } else if (tune == 1 || (p.tile != 128 && p.tile != 65 && p.tile != 66)) {
     s = (512 + tiles - 1) / tiles;
     if (s > smax) s = smax;
   } else {
     // (the 64x64 tile: ~4 blocks per CU, a quarter of the slab bytes per tile)
-    const long slots = p.tile == 65 ? 1024 : 512;
-    const double slab_cost = p.tile == 65 ? 0.004 : 0.016;
+    const long slots = p.tile == 66 ? 2048 : p.tile == 65 ? 1024 : 512;
+    const double slab_cost = p.tile == 128 ? 0.016 : 0.004;
     s = 1;
     double best = 1e30;
     for (long c = 1; c <= smax; ++c) {
@@ -646,6 +648,7 @@ int launch_wgrad(const LA& la, const LB& lb, float* ws, long ldws, int R, int Nc
       return launch_gemm2<FAM, 128, 128, 4, 2, 2>(la, lb, ep, R, Ncols, Mp, s, st, what);
     if (p.tile == 128) return launch_gemm2<FAM, 128, 128, 2, 2, 2>(la, lb, ep, R, Ncols, Mp, s, st, what);
     if (p.tile == 65) return launch_gemm2<FAM, 64, 64, 2, 2, 2>(la, lb, ep, R, Ncols, Mp, s, st, what);
+    if (p.tile == 66) return launch_gemm2<FAM, 64, 64, 2, 2, 1>(la, lb, ep, R, Ncols, Mp, s, st, what);
   } else {
     if (p.tile == 129) return launch_gemm<FAM, T, 128, 128>(la, lb, ep, R, Ncols, Mp, s, st, what);
   }

@@ -78,6 +78,7 @@ int launch_group(int n, const LA* la, const LB* lb, const EP* ep, const int* M, 
     return run_group<FAM, 128, 128, 2, 2, 2, 0>(n, la, lb, ep, M, N, K, st, what);
   }
   if (stages == 4) return run_group<FAM, 64, 64, 2, 2, 4, 0>(n, la, lb, ep, M, N, K, st, what);
+  if (stages == 1) return run_group<FAM, 64, 64, 2, 2, 1, 0>(n, la, lb, ep, M, N, K, st, what);
   return run_group<FAM, 64, 64, 2, 2, 2, 0>(n, la, lb, ep, M, N, K, st, what);
 }
 
@@ -391,7 +392,8 @@ int retr_linear_wgrad_group2(int dtype, int n, const retr_linear_wgrad_desc* d, 
       if (p.tile == 128) e = p.stages == 3 ? wgrad_group_gemm<128, 3>(p, d, ws, st)
                                            : wgrad_group_gemm<128, 2>(p, d, ws, st);
       else e = p.stages == 4 ? wgrad_group_gemm<64, 4>(p, d, ws, st)
-                             : wgrad_group_gemm<64, 2>(p, d, ws, st);
+               : p.stages == 1 ? wgrad_group_gemm<64, 1>(p, d, ws, st)
+                               : wgrad_group_gemm<64, 2>(p, d, ws, st);
       if (e) return e;
       for (int j = 0; j < p.n; ++j) {
         const retr_linear_wgrad_desc& q = d[p.src[j]];

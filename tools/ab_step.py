@@ -35,6 +35,9 @@ VARIANTS = {
     "lin_small": {("TUNE", 13): 2},
     "fsplit_off": {("TUNE", 12): 1},
     "shortk_off": {("TUNE", 14): 1},
+    "grp_s1": {("TUNE", 1): 1},
+    "wgrp_s1": {("TUNE", 3): 1},
+    "cwg_s1": {("TUNE", 9): 3},
 }
 
 
@@ -47,6 +50,8 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
+    for k in (1, 3, 9):
+        load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
     for (table, key), val in VARIANTS[v].items():
