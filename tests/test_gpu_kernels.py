@@ -976,3 +976,68 @@ def test_attention_forward_key_split(B, H, Lq, Lk, hd, causal, masked):
         assert (lse - l1).abs().max().item() < 1e-4, fs
         e = ((o.float() - o1.float()).norm() / o1.float().norm()).item()
         assert e < 5e-3, (fs, e)
+
+
+@pytest.mark.parametrize("kind", ["fwd1x1", "dgrad1x1", "dgrad3x3s2", "ffn"])
+def test_shortk_single_stage_tiles_bitwise(kind):
+    """Short-K wide GEMMs on the single-stage 64x64 tile (RETR_TUNE_SHORTK) and the large
+    stride-2 dgrad phases on the single-stage 64x128 tile accumulate the same K-steps in the same
+    order as the tiles they replaced: outputs bitwise equal with the rule on and off, and within
+    bf16 rounding of fp32 torch."""
+    g = torch.Generator(device="cpu").manual_seed(11)
+    bf = torch.bfloat16
+    outs, ref = [], None
+    for off in (1, 0):
+        _lib.load().retr_tune(14, off)
+        try:
+            if kind == "fwd1x1":      # 80x80x128 -> 512 + residual + ReLU (layer2 conv3)
+                Nb, H, C, Co = 2, 80, 128, 512
+                if ref is None:
+                    x = torch.randn(Nb, H, H, C, generator=g).to(DEV).to(bf)
+                    w = (torch.randn(Co, C, generator=g) / math.sqrt(C)).to(DEV).to(bf)
+                    b = torch.randn(Co, generator=g).to(DEV)
+                    res = torch.randn(Nb, H, H, Co, generator=g).to(DEV).to(bf)
+                    ref = torch.relu(x.float() @ w.float().t() + b + res.float())
+                y = torch.empty(Nb, H, H, Co, dtype=bf, device=DEV)
+                call("retr_conv2d_fwd", 1, ptr(x), Nb, H, H, C, ptr(w), ptr(b), ptr(res), ptr(y),
+                     Co, 1, 1, 1, 0, 1, 1, ops._st())
+            elif kind in ("dgrad1x1", "dgrad3x3s2"):
+                # 80x80x512 <- 128 with the residual addend (layer2 conv3's data gradient), or
+                # 160x160x128 <- 128 3x3 stride 2 (layer2.0 conv2: >= 64k pixels per phase)
+                Nb, H, C, Co, k, s_, p_ = ((2, 80, 512, 128, 1, 1, 0) if kind == "dgrad1x1"
+                                           else (11, 160, 128, 128, 3, 2, 1))
+                OH = (H + 2 * p_ - k) // s_ + 1
+                if ref is None:
+                    w = torch.randn(Co, C, k, k, generator=g) / math.sqrt(C * k * k)
+                    wp, wt, _, _, cp, _ = _pack(w.to(DEV), bf)
+                    assert cp == C
+                    weff = wp.float()[..., :C].permute(0, 3, 1, 2).cpu()
+                    gy = torch.randn(Nb, Co, OH, OH, generator=g).to(bf).float()
+                    add = (torch.randn(Nb, H, H, C, generator=g).to(bf) if kind == "dgrad1x1"
+                           else None)
+                    xreq = torch.zeros(Nb, C, H, H, requires_grad=True)
+                    F.conv2d(xreq, weff, stride=s_, padding=p_).backward(gy)
+                    ref = xreq.grad.permute(0, 2, 3, 1).to(DEV)
+                    if add is not None:
+                        ref = ref + add.float().to(DEV)
+                    gn = gy.permute(0, 2, 3, 1).contiguous().to(DEV).to(bf)
+                    add_d = add.to(DEV) if add is not None else None
+                y = torch.empty(Nb, H, H, C, dtype=bf, device=DEV)
+                call("retr_conv2d_dgrad", 1, ptr(gn), Nb, H, H, C, ptr(wt), ptr(y), Co, k, k, s_,
+                     p_, 1, ptr(add_d), None, ops._st())
+            else:                     # encoder FFN expansion 6400 x 2048 x 256, bias + ReLU
+                M, N, K = 6400, 2048, 256
+                if ref is None:
+                    x = torch.randn(M, K, generator=g).to(DEV).to(bf)
+                    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV).to(bf)
+                    b = torch.randn(N, generator=g).to(DEV)
+                    ref = torch.relu(x.float() @ w.float().t() + b)
+                y = torch.empty(M, N, dtype=bf, device=DEV)
+                call("retr_linear_fwd", 1, ptr(x), K, ptr(w), K, ptr(b), ptr(y), N, 0, M, N, K, 1,
+                     None, 0, 0.0, 0, ops._st())
+            torch.cuda.synchronize()
+            outs.append(y)
+        finally:
+            _lib.load().retr_tune(14, 0)
+    assert torch.equal(outs[0], outs[1])
+    assert rel_err(outs[1].float(), ref) < 1e-2
