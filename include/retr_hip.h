@@ -98,8 +98,9 @@ enum {
   RETR_TUNE_CONV_WGRAD_TILE = 9, /* conv weight-gradient tile (bf16): 1 always 64x64 LDS-DMA,
                                     2 never (0: the built-in shape rule) */
   RETR_TUNE_ATTN_SPLIT = 10,    /* resident attention backward, two waves per 32 rows (even / odd
-                                   tiles): 1 never, 0 (auto) / 2 dq on every grid and dkdv on
-                                   2-wave grids, 3 both on 2-wave grids only */
+                                   tiles): 1 never, 2 dq on every grid and dkdv on 2-wave
+                                   grids, 0 (auto) / 3 both on 2-wave grids only, 4 both
+                                   everywhere */
   RETR_TUNE_LIN_WGRAD = 11,     /* bf16 linear weight gradient with >= 256 128x128 tiles: 0 auto
                                    (LDS-DMA 128x128, 4 waves), 1 register-staged 128x128,
                                    2 LDS-DMA 256x256, 4 LDS-DMA 128x128 8 waves */

@@ -1142,11 +1142,13 @@ int launch_bwd3_t(const void* q, long ldq, const void* k, long ldk, const void* 
   const float cs = kLog2e * scale;
   const DropoutParams dp = make_dp(p, seed);
   const int ntk = (Lk + 63) / 64, ntq = (Lq + 63) / 64;
-  // split knob: 1 off; 0 (auto) / 2 dq on every grid, dkdv on the 2-wave grids; 3 both only on
-  // the 2-wave grids (whole-step A/B, profiles/r3_attn_split.txt: auto 11.725 ms, 2-wave only
-  // 11.742, off 11.813)
+  // split knob: 1 off; 2 dq on every grid, dkdv on the 2-wave grids; 0 (auto) / 3 both only on
+  // the 2-wave grids; 4 both everywhere.  With the branch-free score loops the 4-wave encoder
+  // grid no longer gains from the dq split (tools/attn_micro.py bsplit,
+  // profiles/r3_attn_bsplit.txt: encoder 400 x 400 52.9 -> 47.5 us at 3; the pre-rewrite A/B
+  // that chose 2 is profiles/r3_attn_split.txt)
   const int sk = retr_tune_get(RETR_TUNE_ATTN_SPLIT);
-  const bool split = sk == 0 || sk == 2 || (sk == 3 && nwq == 2);
+  const bool split = sk == 2 || sk == 4 || ((sk == 0 || sk == 3) && nwq == 2);
   const bool split2 = sk != 1;          // dkdv: 2-wave grids only (below)
   {
     // the split kernel's partial-sum exchange (DT x 4 KB per query wave) aliases the K tiles
@@ -1187,7 +1189,7 @@ int launch_bwd3_t(const void* q, long ldq, const void* k, long ldk, const void* 
   // the query-tile split of dkdv pays only on the 2-wave grids (decoder causal 128 x 128:
   // 21.5 -> 15.8 us); on the 4-wave ones it adds its exchange to short loops (cross 128 x 400:
   // 31.1 -> 35.1 us, tools/attn_bwd_ab.py, profiles/r3_attn_split.txt)
-  const bool split_kv = split2 && nwk == 2;
+  const bool split_kv = split2 && (nwk == 2 || sk == 4);   // knob 4: on every grid
   const size_t lds = std::max(res_lds_dkdv<HD>(ntq),
                               (size_t)(split_kv ? nwk * 2 * (HD / 32) * 4096 : 0));
   if (split_kv) {

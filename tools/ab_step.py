@@ -30,6 +30,7 @@ VARIANTS = {
     "no_dmask": {("ATTR", "ATTN_DMASK"): False},
     "split_off": {("TUNE", 10): 1},
     "split_all": {("TUNE", 10): 2},
+    "split_dq_all": {("TUNE", 10): 2},
     "no_dmask_split_off": {("ATTR", "ATTN_DMASK"): False, ("TUNE", 10): 1},
     "no_stem_pool": {("ENV", "RETR_STEM_POOL"): "0"},
     "lin_small": {("TUNE", 13): 2},

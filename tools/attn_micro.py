@@ -57,6 +57,17 @@ def setup(Lq, Lk, causal, B=16, H=8, hd=32):
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "bsplit":   # backward split (RETR_TUNE_ATTN_SPLIT)
+        for Lq, Lk, causal in SHAPES:
+            fwd, bwd, fl = setup(Lq, Lk, causal)
+            out = []
+            for sk in (0, 1, 3, 4):
+                load().retr_tune(10, sk)
+                t = timeit(bwd)
+                out.append(f"split{sk}: {t:6.2f} us {2.5 * fl / t / 1e6:5.1f} TF/s")
+            load().retr_tune(10, 0)
+            print(f"bwd Lq{Lq:4d} Lk{Lk:4d} causal{causal} | " + " | ".join(out), flush=True)
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "fsplit":   # forward key split (RETR_TUNE_ATTN_FSPLIT)
         for Lq, Lk, causal in SHAPES:
             fwd, bwd, fl = setup(Lq, Lk, causal)
