@@ -112,7 +112,9 @@ enum {
                                    step, profiles/r3_ab_lin_small.txt); 0 / 1 split-K slabs */
   RETR_TUNE_SHORTK = 14,        /* short-K (K <= 256, N >= 256) bf16 GEMMs on the single-stage
                                    64x64 LDS-DMA tile: 0 auto (on), 1 off */
-  RETR_TUNE_COUNT = 15
+  RETR_TUNE_ADAMW_NT = 15,      /* AdamW update streams: 0 (auto) / 1 non-temporal loads and
+                                   stores, 2 plain */
+  RETR_TUNE_COUNT = 16
 };
 int retr_tune(int knob, int value);
 

@@ -16,8 +16,19 @@
 // writes g = 0 instead (the captured training step consumes its gradients: no separate
 // 260 MB zero fill of the arena at the next step).
 #include "common.hpp"
+#include "../../include/retr_hip.h"
 
 namespace {
+
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+typedef __attribute__((ext_vector_type(4))) float f32v4;
+RETR_DEVICE float4 nt_load(const float4* p) {
+  const f32v4 x = __builtin_nontemporal_load((const f32v4*)p);
+  return float4{x[0], x[1], x[2], x[3]};
+}
+RETR_DEVICE void nt_store(const float4& v, float4* p) {
+  __builtin_nontemporal_store(f32v4{v.x, v.y, v.z, v.w}, (f32v4*)p);
+}
 
 constexpr int kThreads = 256;
 
@@ -53,6 +64,9 @@ adamw_sumsq_kernel(const float4* g, long n4, float* partials, float* step) {
   }
 }
 
+// NT: non-temporal loads and stores (every byte is touched once per step, and none of the
+// outputs is read again before the next step's forward / backward)
+template <bool NT>
 __global__ void __launch_bounds__(kThreads)
 adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const float* hyper,
                     double beta1, double beta2, float eps, const float* step, float step_offset,
@@ -76,7 +90,15 @@ adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const f
   const float omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2), b2f = (float)beta2;
   const bool scale = !(coef >= 1.f);   // also for a NaN coefficient
   for (long i = (long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long)gridDim.x * kThreads) {
-    float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+    float4 pp, gg, mm, vv;
+    if constexpr (NT) {
+      pp = nt_load(p + i);
+      gg = nt_load(g + i);
+      mm = nt_load(m + i);
+      vv = nt_load(v + i);
+    } else {
+      pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+    }
     float* pe = &pp.x; float* ge = &gg.x; float* me = &mm.x; float* ve = &vv.x;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -90,12 +112,23 @@ adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const f
       me[e] = mr;
       ve[e] = vr;
     }
-    p[i] = pp; m[i] = mm; v[i] = vv;
-    if (zero_g) g[i] = float4{0.f, 0.f, 0.f, 0.f};   // consumed: the next step's arena is clean
-    else if (scale) g[i] = gg;
-    if (p16) {   // bf16 shadow of the parameters: the GEMM weight operands, no cast launches
-      typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-      *(bf16x4*)(p16 + 4 * i) = bf16x4{(bf16)pp.x, (bf16)pp.y, (bf16)pp.z, (bf16)pp.w};
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    if constexpr (NT) {
+      nt_store(pp, p + i);
+      nt_store(mm, m + i);
+      nt_store(vv, v + i);
+      if (zero_g) nt_store(float4{0.f, 0.f, 0.f, 0.f}, g + i);
+      else if (scale) nt_store(gg, g + i);
+      if (p16) {
+        const bf16x4 w = bf16x4{(bf16)pp.x, (bf16)pp.y, (bf16)pp.z, (bf16)pp.w};
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x2, w), (u32x2*)(p16 + 4 * i));
+      }
+    } else {
+      p[i] = pp; m[i] = mm; v[i] = vv;
+      if (zero_g) g[i] = float4{0.f, 0.f, 0.f, 0.f};   // consumed: the next step's arena is clean
+      else if (scale) g[i] = gg;
+      if (p16)   // bf16 shadow of the parameters: the GEMM weight operands, no cast launches
+        *(bf16x4*)(p16 + 4 * i) = bf16x4{(bf16)pp.x, (bf16)pp.y, (bf16)pp.z, (bf16)pp.w};
     }
   }
 }
@@ -137,7 +170,11 @@ int retr_adamw_update2(float* param, float* grad, float* exp_avg, float* exp_avg
   if (n == 0) return 0;
   long n4 = n / 4;
   int blocks = (int)std::min<long>(2048, (n4 + kThreads - 1) / kThreads);
-  hipLaunchKernelGGL(adamw_update_kernel, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream,
+  // non-temporal streams by default (same-process A/B, profiles/r3_ab_adamw_nt.txt: graphed
+  // step 11.190 -> 11.121 ms); knob 2 = plain loads / stores
+  auto kern = retr_tune_get(RETR_TUNE_ADAMW_NT) == 2 ? adamw_update_kernel<false>
+                                                     : adamw_update_kernel<true>;
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream,
                      (float4*)param, (float4*)grad, (float4*)exp_avg, (float4*)exp_avg_sq, n4,
                      hyper, beta1, beta2, eps, step, step_offset, partials, nparts, max_norm,
                      (bf16*)param_bf16, zero_grad);

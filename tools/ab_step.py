@@ -39,6 +39,8 @@ VARIANTS = {
     "grp_s1": {("TUNE", 1): 1},
     "wgrp_s1": {("TUNE", 3): 1},
     "cwg_s1": {("TUNE", 9): 3},
+    "adamw_nt": {("TUNE", 15): 1},
+    "adamw_plain": {("TUNE", 15): 2},
 }
 
 
@@ -51,7 +53,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 3, 9):
+    for k in (1, 3, 9, 15):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
