@@ -41,6 +41,7 @@ VARIANTS = {
     "cwg_s1": {("TUNE", 9): 3},
     "adamw_nt": {("TUNE", 15): 1},
     "adamw_plain": {("TUNE", 15): 2},
+    "gemm_nt": {("TUNE", 7): 1},
 }
 
 
@@ -53,7 +54,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 3, 9, 15):
+    for k in (1, 3, 7, 9, 15):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
