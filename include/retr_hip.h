@@ -368,6 +368,16 @@ int retr_ce_fwd(int dtype, const void* logits, long ld, int M, int V, const long
 int retr_ce_bwd(int dtype, const void* logits, long ld, int M, int V, const long long* targets,
                 const float* lse, const float* dloss, float inv_count, void* dlogits, long lddl,
                 void* stream);
+/* Training form of the pair above (bf16 logits, ld % 8 == 0, lddl % 8 == 0): one pass over the
+   logits writes lse, the per-row losses, the mean and dlogits = (softmax - onehot) * inv_count
+   as for dloss = 1 (what loss.backward() passes); retr_ce_bwd_rescale then rewrites dlogits with
+   retr_ce_bwd's arithmetic only when *dloss != 1. */
+int retr_ce_fwd_bwd(int dtype, const void* logits, long ld, int M, int V,
+                    const long long* targets, float* lse, float* loss_rows, float* loss,
+                    float inv_count, void* dlogits, long lddl, void* stream);
+int retr_ce_bwd_rescale(int dtype, const void* logits, long ld, int M, int V,
+                        const long long* targets, const float* lse, const float* dloss,
+                        float inv_count, void* dlogits, long lddl, void* stream);
 int retr_argmax_rows(int dtype, const void* x, long ld, int M, int V, long long* out,
                      void* stream);
 /* the same first-index argmax for few long rows (decode logits): 16 segments per row in

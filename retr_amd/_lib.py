@@ -137,6 +137,8 @@ _SIGS = {
     "retr_greedy_update": [_P, _I, _I, _I, ctypes.c_longlong, _P, _P, _P, _P, _P],
     "retr_ce_fwd": [_I, _P, _L, _I, _I, _P, _P, _P, _P, _P],
     "retr_ce_bwd": [_I, _P, _L, _I, _I, _P, _P, _P, _F, _P, _L, _P],
+    "retr_ce_fwd_bwd": [_I, _P, _L, _I, _I, _P, _P, _P, _P, _F, _P, _L, _P],
+    "retr_ce_bwd_rescale": [_I, _P, _L, _I, _I, _P, _P, _P, _F, _P, _L, _P],
     "retr_argmax_rows": [_I, _P, _L, _I, _I, _P, _P],
     "retr_argmax_workspace": [_I],
     "retr_argmax_rows_ws": [_I, _P, _L, _I, _I, _P, _P, _P],

@@ -75,6 +75,93 @@ ce_bwd_kernel(const T* x, long ld, int V, const long long* tgt, const float* lse
   }
 }
 
+// One pass over a bf16 logit row for the training step: the row's 16-byte chunks stay in
+// registers (NCH per thread), so the logits are read once for lse, the row loss and
+// dlogits = (exp(x - lse) - onehot) * g, g = 1 * inv_count -- ce_bwd_kernel's arithmetic for
+// dloss = 1.  Columns in [V, lddx) are written as 0.
+template <int NCH>
+__global__ void __launch_bounds__(256)
+ce_fused_kernel(const bf16* x, long ld, int V, const long long* tgt, float* lse,
+                float* loss_rows, float inv_count, bf16* dx, long lddx) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const bf16* xr = x + (long)row * ld;
+  const int nch = (V + 7) / 8;                  // chunks holding real columns
+  bf16x8 c[NCH];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int j = tid + 256 * i;
+    if (j < nch) c[i] = *(const bf16x8*)(xr + 8 * j);
+  }
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int j = tid + 256 * i;
+    if (j < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (8 * j + e < V) m = fmaxf(m, (float)c[i][e]);
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (lane == 0) red[w] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int j = tid + 256 * i;
+    if (j < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (8 * j + e < V) s += __expf((float)c[i][e] - m);
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  const float l = m + logf(red[0] + red[1] + red[2] + red[3]);
+  const long long t = tgt[row];
+  if (tid == 0) {
+    lse[row] = l;
+    loss_rows[row] = l - to_f(xr[t]);
+  }
+  bf16* dr = dx + (long)row * lddx;
+  const int ndch = (int)(lddx / 8);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int j = tid + 256 * i;
+    if (j >= ndch) continue;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int col = 8 * j + e;
+      float d = 0.f;
+      if (j < nch && col < V) d = (__expf((float)c[i][e] - l) - (col == t ? 1.f : 0.f)) * inv_count;
+      o[e] = (bf16)d;
+    }
+    *(bf16x8*)(dr + 8 * j) = o;
+  }
+}
+
+// ce_bwd_kernel for a dlogits buffer the fused forward already wrote for dloss = 1: every block
+// returns at once when dloss is 1, else recomputes the gradient with the given dloss
+template <typename T, typename TD>
+__global__ void __launch_bounds__(256)
+ce_bwd_rescale_kernel(const T* x, long ld, int V, const long long* tgt, const float* lse,
+                      const float* dloss, float inv_count, TD* dx, long lddx) {
+  if (dloss[0] == 1.f) return;
+  const int row = blockIdx.x;
+  const T* xr = x + (long)row * ld;
+  TD* dr = dx + (long)row * lddx;
+  const float l = lse[row], g = dloss[0] * inv_count;
+  const long long t = tgt[row];
+  for (int j = threadIdx.x; j < lddx; j += 256) {
+    float d = 0.f;
+    if (j < V) d = (__expf(to_f(xr[j]) - l) - (j == t ? 1.f : 0.f)) * g;
+    dr[j] = from_f<TD>(d);
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 argmax_kernel(const T* x, long ld, int V, long long* out) {
@@ -241,6 +328,37 @@ int retr_ce_bwd(int dtype, const void* logits, long ld, int M, int V, const long
                        (const float*)logits, ld, V, targets, lse, dloss, inv_count,
                        (float*)dlogits, lddl);
   return retr_check_launch("ce_bwd");
+}
+
+int retr_ce_fwd_bwd(int dtype, const void* logits, long ld, int M, int V,
+                    const long long* targets, float* lse, float* loss_rows, float* loss,
+                    float inv_count, void* dlogits, long lddl, void* stream) {
+  if (M == 0) return 0;
+  RETR_REQUIRE(dtype == RETR_BF16 && ld % 8 == 0 && lddl % 8 == 0 && lddl >= V && ld >= V &&
+                   (((uintptr_t)logits | (uintptr_t)dlogits) & 15) == 0,
+               "ce_fwd_bwd: bf16, 8-aligned rows");
+  constexpr int kNch = 16;                       // 16 x 8 x 256 = 32768 columns per row
+  RETR_REQUIRE(lddl <= 8L * 256 * kNch, "ce_fwd_bwd: row of %ld columns too long", lddl);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ce_fused_kernel<kNch>, dim3(M), dim3(256), 0, st, (const bf16*)logits, ld, V,
+                     targets, lse, loss_rows, inv_count, (bf16*)dlogits, lddl);
+  if (retr_check_launch("ce_fwd_bwd")) return 1;
+  if (loss) {
+    hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(256), 0, st, loss_rows, M, loss);
+    return retr_check_launch("ce_mean");
+  }
+  return 0;
+}
+
+int retr_ce_bwd_rescale(int dtype, const void* logits, long ld, int M, int V,
+                        const long long* targets, const float* lse, const float* dloss,
+                        float inv_count, void* dlogits, long lddl, void* stream) {
+  if (M == 0) return 0;
+  RETR_REQUIRE(dtype == RETR_BF16, "ce_bwd_rescale: bf16 only");
+  hipLaunchKernelGGL((ce_bwd_rescale_kernel<bf16, bf16>), dim3(M), dim3(256), 0,
+                     (hipStream_t)stream, (const bf16*)logits, ld, V, targets, lse, dloss,
+                     inv_count, (bf16*)dlogits, lddl);
+  return retr_check_launch("ce_bwd_rescale");
 }
 
 int retr_argmax_rows(int dtype, const void* x, long ld, int M, int V, long long* out,

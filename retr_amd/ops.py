@@ -1090,6 +1090,9 @@ def mlp_head(mlp, hs, B, T, cdtype):
 # cross entropy (engine.py:71: criterion(outputs.permute(0, 2, 1), caps[:, 1:]))
 # ---------------------------------------------------------------------------------------------
 
+FUSED_CE = True   # bf16 training: loss and dlogits from one pass (tests / A/B switch it off)
+
+
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, target):
@@ -1107,8 +1110,18 @@ class _CrossEntropy(torch.autograd.Function):
         lse = torch.empty(M, dtype=torch.float32, device=dev)
         rows = torch.empty(M, dtype=torch.float32, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
-        call("retr_ce_fwd", dcode(base.dtype), ptr(base), ld, M, V, ptr(tgt), ptr(lse), ptr(rows),
-             ptr(loss), _st())
+        Vp = _round_up(V, 64)
+        ctx.dl = None
+        if (ctx.needs_input_grad[0] and base.dtype == torch.bfloat16 and ld % 8 == 0
+                and Vp <= 32768 and FUSED_CE):
+            # training: the gradient for dloss = 1 comes out of the same pass over the logits
+            # (retr_ce_fwd_bwd); backward only rewrites it if dloss != 1
+            ctx.dl = torch.empty(M, Vp, dtype=base.dtype, device=dev)
+            call("retr_ce_fwd_bwd", dcode(base.dtype), ptr(base), ld, M, V, ptr(tgt), ptr(lse),
+                 ptr(rows), ptr(loss), 1.0 / M, ptr(ctx.dl), Vp, _st())
+        else:
+            call("retr_ce_fwd", dcode(base.dtype), ptr(base), ld, M, V, ptr(tgt), ptr(lse),
+                 ptr(rows), ptr(loss), _st())
         ctx.save_for_backward(base, tgt, lse)
         ctx.cfg = (B, V, T, ld)
         return loss
@@ -1119,10 +1132,16 @@ class _CrossEntropy(torch.autograd.Function):
         B, V, T, ld = ctx.cfg
         M = B * T
         Vp = _round_up(V, 64)
-        dl = torch.empty(M, Vp, dtype=base.dtype, device=base.device)
         dloss = dloss.reshape(1).float().contiguous()
-        call("retr_ce_bwd", dcode(base.dtype), ptr(base), ld, M, V, ptr(tgt), ptr(lse),
-             ptr(dloss), 1.0 / M, ptr(dl), Vp, _st())
+        dl = ctx.dl
+        ctx.dl = None
+        if dl is not None:
+            call("retr_ce_bwd_rescale", dcode(base.dtype), ptr(base), ld, M, V, ptr(tgt),
+                 ptr(lse), ptr(dloss), 1.0 / M, ptr(dl), Vp, _st())
+        else:
+            dl = torch.empty(M, Vp, dtype=base.dtype, device=base.device)
+            call("retr_ce_bwd", dcode(base.dtype), ptr(base), ld, M, V, ptr(tgt), ptr(lse),
+                 ptr(dloss), 1.0 / M, ptr(dl), Vp, _st())
         return dl[:, :V].view(B, T, V).permute(0, 2, 1), None
 
 

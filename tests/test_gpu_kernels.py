@@ -1041,3 +1041,33 @@ def test_shortk_single_stage_tiles_bitwise(kind):
             _lib.load().retr_tune(14, 0)
     assert torch.equal(outs[0], outs[1])
     assert rel_err(outs[1].float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("scale", [1.0, 2.0])
+def test_fused_cross_entropy_matches_two_pass(scale):
+    """Training-mode CrossEntropyLoss (bf16 logits): retr_ce_fwd_bwd writes lse, the loss and
+    dlogits for dloss = 1 in one pass over the logits, retr_ce_bwd_rescale recomputes the
+    gradient only for dloss != 1 -- against the two-pass kernels and fp32 torch."""
+    from retr_amd.models.caption import CrossEntropyLoss
+    g = torch.Generator(device="cpu").manual_seed(5)
+    B, T, V, Vp = 4, 33, 30522, 30528
+    store = (torch.randn(B, T, Vp, generator=g) * 3).to(DEV).to(torch.bfloat16)
+    tgt = torch.randint(0, V, (B, T), generator=g).to(DEV)
+    res = []
+    try:
+        for fused in (False, True):
+            ops.FUSED_CE = fused
+            x = store.clone().requires_grad_(True)
+            loss = CrossEntropyLoss()(x[..., :V].permute(0, 2, 1), tgt)
+            (loss * scale).backward()
+            torch.cuda.synchronize()
+            res.append((loss.detach().clone(), x.grad.detach().clone()))
+    finally:
+        ops.FUSED_CE = True
+    (l0, g0), (l1, g1) = res
+    ref = F.cross_entropy(store[..., :V].float().permute(0, 2, 1), tgt)
+    assert abs(l1.item() - ref.item()) < 1e-4 * abs(ref.item())
+    assert abs(l1.item() - l0.item()) < 1e-5 * abs(l0.item())
+    assert torch.equal(g1[..., V:], torch.zeros_like(g1[..., V:]))
+    e = ((g1.float() - g0.float()).norm() / g0.float().norm()).item()
+    assert e < 1e-2, e

@@ -42,6 +42,7 @@ VARIANTS = {
     "adamw_nt": {("TUNE", 15): 1},
     "adamw_plain": {("TUNE", 15): 2},
     "gemm_nt": {("TUNE", 7): 1},
+    "ce_unfused": {("ATTR", "FUSED_CE"): False},
 }
 
 
@@ -50,6 +51,7 @@ def apply(v):
     ops.FUSE_LN_BWD = True
     ops.FUSE_LN_PARAMS = True
     ops.ATTN_DMASK = True
+    ops.FUSED_CE = True
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
