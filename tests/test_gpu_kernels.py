@@ -921,12 +921,15 @@ def test_attention_saved_dropout_bits_equal_rehash(B, H, Lq, Lk, hd, causal, mas
         assert torch.equal(a, b)
     if causal:   # words of key tiles past a block's diagonal are never written
         return
-    # keep-bit density over the keys of the first (b, h)
+    # keep-bit density over every (b, h): the effective seed includes the process's device step
+    # seed, so one (b, h) of a small shape (7700 bits, sigma 0.0034) could land outside the bound
     nw = (Lk + 31) // 32
-    words = dm.view(B * H, nw, Lq)[0].cpu().numpy().astype(np.uint32)
-    bits = np.unpackbits(words.view(np.uint8).reshape(nw, Lq, 4), axis=2, bitorder="little")
-    bits = bits.reshape(nw, Lq, 32).transpose(1, 0, 2).reshape(Lq, nw * 32)[:, :Lk]
-    assert abs(bits.mean() - (1 - p)) < 0.01, bits.mean()
+    words = dm.view(B * H, nw, Lq).cpu().numpy().astype(np.uint32)
+    bits = np.unpackbits(words.view(np.uint8).reshape(B * H, nw, Lq, 4), axis=3,
+                         bitorder="little")
+    bits = bits.reshape(B * H, nw, Lq, 32).transpose(0, 2, 1, 3).reshape(B * H, Lq, nw * 32)
+    bits = bits[:, :, :Lk]
+    assert abs(bits.mean() - (1 - p)) < 0.005, bits.mean()
 
 
 @pytest.mark.parametrize("B,H,Lq,Lk,hd,causal,masked", [
@@ -1071,3 +1074,23 @@ def test_fused_cross_entropy_matches_two_pass(scale):
     assert torch.equal(g1[..., V:], torch.zeros_like(g1[..., V:]))
     e = ((g1.float() - g0.float()).norm() / g0.float().norm()).item()
     assert e < 1e-2, e
+
+
+@pytest.mark.parametrize("dt,M,C,period", [(torch.bfloat16, 2048, 256, 128),
+                                           (torch.float32, 6400, 256, 400),
+                                           (torch.bfloat16, 100, 12, 7)])
+def test_pos_grad_rows_in_order(dt, M, C, period):
+    """retr_pos_grad (dpos[p] += sum of rows p, p + period, ... in row order; the 8-column
+    vector kernel for C % 8 == 0, the scalar one otherwise) equals the in-order fp32 sum."""
+    g = torch.Generator(device="cpu").manual_seed(M + C)
+    d = torch.randn(M, C, generator=g).to(dt)
+    init = torch.randn(period, C, generator=g)
+    dpos = init.clone().to(DEV)
+    call("retr_pos_grad", ops.dcode(dt), ptr(d.to(DEV)), C, M, C, period, ptr(dpos), ops._st())
+    torch.cuda.synchronize()
+    df = d.float().numpy()
+    s = np.zeros((period, C), dtype=np.float32)
+    for m in range(M):
+        s[m % period] += df[m]
+    ref = init.numpy() + s
+    assert np.array_equal(dpos.cpu().numpy(), ref)
