@@ -186,6 +186,16 @@ typedef struct {
   int Co, Ci, KH, KW, Cp, pad;
 } retr_conv_pack_desc;
 int retr_conv_pack_group(int dtype, int n, const retr_conv_pack_desc* d, void* stream);
+/* bf16 [W3eff | Wdseff] (rows x (ka + kb), ka, kb % 8 == 0) and b3 + bds of the fused bottleneck
+   tails (retr_conv1x1_fwd_cat operands), up to 8 per launch */
+typedef struct {
+  const void *a, *b;
+  void* dst;
+  const float *bias_a, *bias_b;
+  float* bias_dst;
+  int rows, ka, kb;
+} retr_cat_rows_desc;
+int retr_cat_rows_group(int n, const retr_cat_rows_desc* d, void* stream);
 int retr_conv2d_fwd(int dtype, const void* x, int Nb, int H, int W, int C, const void* w,
                     const float* bias, const void* residual, void* y, int Co, int KH, int KW,
                     int stride, int pad, int dil, int relu, void* stream);

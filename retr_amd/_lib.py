@@ -54,6 +54,12 @@ class ConvPackDesc(ctypes.Structure):
                 ("pad", _I)]
 
 
+class CatRowsDesc(ctypes.Structure):
+    """retr_cat_rows_desc"""
+    _fields_ = [("a", _P), ("b", _P), ("dst", _P), ("bias_a", _P), ("bias_b", _P),
+                ("bias_dst", _P), ("rows", _I), ("ka", _I), ("kb", _I)]
+
+
 class SlabSumDesc(ctypes.Structure):
     """retr_slab_sum_desc"""
     _fields_ = [("parts", _P), ("stride", _L), ("nparts", _I), ("cols", _I), ("dst", _P),
@@ -89,6 +95,7 @@ _SIGS = {
     "retr_linear_wgrad_group2": [_I, _I, _PWD, _P, _I, ctypes.POINTER(SlabSumDesc), _P],
     "retr_conv_pack": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "retr_conv_pack_group": [_I, _I, ctypes.POINTER(ConvPackDesc), _P],
+    "retr_cat_rows_group": [_I, ctypes.POINTER(CatRowsDesc), _P],
     "retr_conv2d_fwd": [_I, _P, _I, _I, _I, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "retr_conv2d_dgrad": [_I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "retr_conv2d_wgrad": [_I, _P, _P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P],

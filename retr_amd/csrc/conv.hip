@@ -1206,6 +1206,52 @@ int pack_all(int n, const retr_conv_pack_desc* d, hipStream_t st) {
 
 extern "C" {
 
+// [W3eff | Wdseff] rows and b3 + bds of every fused bottleneck tail in one launch (one thread
+// per 16-byte chunk of a destination row; each problem owns a block range)
+struct CatGroup {
+  retr_cat_rows_desc d[8];
+  int blk0[9];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) cat_rows_group_kernel(CatGroup g) {
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < 8; ++i)
+    if (i < g.n && (int)blockIdx.x >= g.blk0[i]) p = i;
+  const retr_cat_rows_desc& d = g.d[p];
+  const long i = (long)(blockIdx.x - g.blk0[p]) * 256 + threadIdx.x;
+  const int ca = d.ka / 8, cb = d.kb / 8, c = ca + cb;
+  if (i < (long)d.rows * c) {
+    const int r = (int)(i / c), j = (int)(i % c);
+    const u32x4 v = j < ca ? ((const u32x4*)d.a)[(long)r * ca + j]
+                           : ((const u32x4*)d.b)[(long)r * cb + (j - ca)];
+    ((u32x4*)d.dst)[i] = v;
+  }
+  if (i < d.rows) d.bias_dst[i] = d.bias_a[i] + d.bias_b[i];
+}
+
+int retr_cat_rows_group(int n, const retr_cat_rows_desc* d, void* stream) {
+  RETR_REQUIRE(n >= 0 && n <= 8, "cat_rows_group: n=%d (0..8)", n);
+  if (n == 0) return 0;
+  CatGroup g{};
+  g.n = n;
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    RETR_REQUIRE(d[i].ka % 8 == 0 && d[i].kb % 8 == 0 && d[i].rows > 0,
+                 "cat_rows_group[%d]: ka=%d kb=%d rows=%d", i, d[i].ka, d[i].kb, d[i].rows);
+    RETR_REQUIRE((((uintptr_t)d[i].a | (uintptr_t)d[i].b | (uintptr_t)d[i].dst) & 15) == 0,
+                 "cat_rows_group[%d]: 16-byte alignment", i);
+    g.d[i] = d[i];
+    g.blk0[i] = blocks;
+    const long chunks = (long)d[i].rows * ((d[i].ka + d[i].kb) / 8);
+    blocks += (int)cdiv(chunks > d[i].rows ? chunks : (long)d[i].rows, 256L);
+  }
+  g.blk0[n] = blocks;
+  hipLaunchKernelGGL(cat_rows_group_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, g);
+  return retr_check_launch("cat_rows_group");
+}
+
 int retr_conv_pack_group(int dtype, int n, const retr_conv_pack_desc* d, void* stream) {
   RETR_REQUIRE(n >= 0 && n <= 256, "conv_pack_group: n=%d (0..256)", n);
   hipStream_t st = (hipStream_t)stream;

@@ -146,8 +146,11 @@ class _WeightCache:
         if ent is not None and key in ent and ent[key][0] == ver:
             return ent[key][1]
         src = p.detach().contiguous()
-        out = torch.zeros((rows,) + tuple(p.shape[1:]), dtype=dtype, device=p.device) \
-            if rows != p.shape[0] else torch.empty(p.shape, dtype=dtype, device=p.device)
+        if ent is not None and key in ent:
+            out = ent[key][1]   # same shape: re-cast in place (padding rows stay zero, no fill)
+        else:
+            out = torch.zeros((rows,) + tuple(p.shape[1:]), dtype=dtype, device=p.device) \
+                if rows != p.shape[0] else torch.empty(p.shape, dtype=dtype, device=p.device)
         call("retr_cast", dcode(dtype), ptr(src), ptr(out), src.numel(), _st())
         if ent is None:
             ent = {}
@@ -206,12 +209,20 @@ class _TView:
 
 
 def _pad_vec(v, n):
+    """fp32 copy of ``v`` zero-padded to ``n`` (the vocabulary head's bias): the padded buffer
+    lives on the parameter and is refreshed in place (one copy, no fill) when ``v`` changes."""
     if v is None:
         return None
     if v.shape[0] == n:
         return v.detach().contiguous()
-    out = torch.zeros(n, dtype=torch.float32, device=v.device)
-    out[: v.shape[0]] = v.detach()
+    ver = (v._version, v.data_ptr(), n)
+    ent = getattr(v, "_retr_padvec", None)
+    if ent is not None and ent[0] == ver:
+        return ent[1]
+    out = ent[1] if ent is not None and ent[1].shape[0] == n else \
+        torch.zeros(n, dtype=torch.float32, device=v.device)
+    out[: v.shape[0]].copy_(v.detach())
+    v._retr_padvec = (ver, out)
     return out
 
 

@@ -207,10 +207,43 @@ def _cat_weights(runner, blk, dtype):
     wpd, _, bd, _ = PACKS.get(ds, dtype)
     ent = runner._cat_w.get(blk.name)
     if ent is None or ent[0] is not wp3 or ent[1] is not wpd:
-        wcat = torch.cat([wp3.view(c3.cout, -1), wpd.view(ds.cout, -1)], 1).contiguous()
-        ent = (wp3, wpd, wcat, b3 + bd)
-        runner._cat_w[blk.name] = ent
+        _prepare_cats(runner, dtype, [blk])
+        ent = runner._cat_w[blk.name]
     return ent[2], ent[3]
+
+
+def _prepare_cats(runner, dtype, blocks=None):
+    """Refresh the [W3eff | Wdseff] / b3 + bds operands of every stale fused-tail block in one
+    retr_cat_rows_group launch (bf16; after PACKS.prepare repacked the weights of the step)."""
+    if dtype != torch.bfloat16 or not runner.use_cat:
+        return
+    todo = []
+    for blk in (blocks if blocks is not None else runner.blocks):
+        if blk.ds is None or blk.kind != "bottleneck":
+            continue
+        c3, ds = blk.convs[2], blk.ds
+        wp3, _, b3, _ = PACKS.get(c3, dtype)
+        wpd, _, bd, _ = PACKS.get(ds, dtype)
+        ent = runner._cat_w.get(blk.name)
+        if ent is not None and ent[0] is wp3 and ent[1] is wpd:
+            continue
+        ka, kb = wp3[0].numel(), wpd[0].numel()
+        if ent is not None and ent[2].shape == (c3.cout, ka + kb):
+            wcat, bcat = ent[2], ent[3]            # same shapes: refresh in place
+        else:
+            wcat = torch.empty(c3.cout, ka + kb, dtype=dtype, device=wp3.device)
+            bcat = torch.empty(c3.cout, dtype=torch.float32, device=wp3.device)
+        todo.append((blk, wp3, wpd, b3, bd, wcat, bcat, ka, kb))
+    for i in range(0, len(todo), 8):
+        chunk = todo[i:i + 8]
+        arr = (_lib.CatRowsDesc * len(chunk))()
+        for j, (blk, wp3, wpd, b3, bd, wcat, bcat, ka, kb) in enumerate(chunk):
+            d = arr[j]
+            d.a, d.b, d.dst = ptr(wp3), ptr(wpd), ptr(wcat)
+            d.bias_a, d.bias_b, d.bias_dst = ptr(b3), ptr(bd), ptr(bcat)
+            d.rows, d.ka, d.kb = wcat.shape[0], ka, kb
+            runner._cat_w[blk.name] = (wp3, wpd, wcat, bcat)
+        call("retr_cat_rows_group", len(chunk), arr, _st())
 
 
 def _bottleneck_fused(runner, blk, x, xshape):
@@ -268,6 +301,7 @@ class _Backbone(torch.autograd.Function):
         stem, blocks, cdtype = runner.stem, runner.blocks, runner.cdtype
         _lib.require_device(images)
         PACKS.prepare(runner.specs, cdtype)      # every stale conv packed in one launch
+        _prepare_cats(runner, cdtype)            # and every fused tail's [W3 | Wds] in one more
         N, C, H, W = images.shape
         img = images.detach().float().contiguous()
         pooled = False
