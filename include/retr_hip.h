@@ -114,7 +114,9 @@ enum {
                                    64x64 LDS-DMA tile: 0 auto (on), 1 off */
   RETR_TUNE_ADAMW_NT = 15,      /* AdamW update streams: 0 (auto) / 1 non-temporal loads and
                                    stores, 2 plain */
-  RETR_TUNE_COUNT = 16
+  RETR_TUNE_WGRAD_B32 = 16,     /* 1: 3x3 / strided conv weight gradients on the 64-bit-cursor
+                                   ConvWgradB loader instead of ConvWgradB32 */
+  RETR_TUNE_COUNT = 17
 };
 int retr_tune(int knob, int value);
 

@@ -310,6 +310,75 @@ struct ConvWgradB {  // B(row = kh,kw,ci ; k = pixel n,oh,ow) = X[n, oh*s-p+kh d
   }
 };
 
+// ConvWgradB with 32-bit element offsets (inputs under 2^31 elements) and at most one output-row
+// and one image wrap per K-step (OH * OW >= BK): the cursor advance is four 32-bit adds and two
+// conditional ones, the chunk test and address one compare chain and one 64-bit add -- the
+// 64-bit cursor arithmetic, its selects and the image-wrap loop of ConvWgradB were most of the
+// weight-gradient loop's vector instructions (82 per K-step beside 16 MFMAs).
+template <typename T>
+struct ConvWgradB32 {  // B(row = kh,kw,ci ; k = pixel n,oh,ow) = X[n, oh*s-p+kh d, ow*s-p+kw d, ci]
+  static constexpr bool kContig = false;
+  const T* x;
+  Geom g;
+  int rows, M;
+  int adv_q, adv_r;          // one K-step = adv_q output rows + adv_r columns
+  int d_step, d_row, d_img;  // element-offset deltas: a K-step, an output-row wrap, an image wrap
+  struct Ctx { int khd, kwd, off; bool ok; };
+  struct KCur { int m, oh, ow, base; };
+  RETR_DEVICE Ctx row_ctx(int r) const {
+    Ctx c;
+    c.ok = r < rows;
+    const int rr = c.ok ? r : 0;
+    const int khw = rr / g.C;
+    const int ci = rr - khw * g.C;
+    const int kh = khw / g.KW, kw = khw - kh * g.KW;
+    c.khd = kh * g.d - g.p;
+    c.kwd = kw * g.d - g.p;
+    c.off = (c.khd * g.W + c.kwd) * g.C + ci;
+    return c;
+  }
+  RETR_DEVICE KCur kcur(int m) const {
+    KCur k;
+    k.m = m;
+    const int hw = g.OH * g.OW;
+    const int n = m / hw;
+    const int rem = m - n * hw;
+    k.oh = rem / g.OW;
+    k.ow = rem - k.oh * g.OW;
+    k.base = ((n * g.H + k.oh * g.s) * g.W + k.ow * g.s) * g.C;
+    return k;
+  }
+  RETR_DEVICE void advance(KCur& k, int d) const {
+    if (d != Elem<T>::BK) {   // generic step (not used by the GEMM cores)
+      k = kcur(k.m + d);
+      return;
+    }
+    k.m += d;
+    k.ow += adv_r;
+    k.oh += adv_q;
+    k.base += d_step;
+    if (k.ow >= g.OW) {
+      k.ow -= g.OW;
+      k.oh += 1;
+      k.base += d_row;
+    }
+    if (k.oh >= g.OH) {
+      k.oh -= g.OH;
+      k.base += d_img;
+    }
+  }
+  RETR_DEVICE bool ok(const Ctx& c, const KCur& k) const {
+    const int ih = k.oh * g.s + c.khd, iw = k.ow * g.s + c.kwd;
+    return c.ok & (k.m < M) & ((unsigned)ih < (unsigned)g.H) & ((unsigned)iw < (unsigned)g.W);
+  }
+  RETR_DEVICE const void* addr(const Ctx& c, const KCur& k) const {
+    return ok(c, k) ? (const void*)(x + (unsigned)(k.base + c.off)) : nullptr;
+  }
+  RETR_DEVICE const void* addr_or(const Ctx& c, const KCur& k, const void* fb) const {
+    return ok(c, k) ? (const void*)(x + (unsigned)(k.base + c.off)) : fb;
+  }
+};
+
 // ---- stride-2 data gradient by output phase ------------------------------------------------
 // For stride 2 (dilation 1) only taps kh == (ih + p) mod 2 reach an input row ih, so the
 // dgrad of each of the four (ih, iw) parity classes is a dense implicit GEMM over its own tap
@@ -796,7 +865,20 @@ int conv_wgrad_t(const void* dy, const void* x, Geom g, float* ws, hipStream_t s
     return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st, "conv_wgrad_1x1",
                                           true);
   }
-  ConvWgradB<T> lb{(const T*)x, g, Ncols, Mp, Elem<T>::BK / g.OW, Elem<T>::BK % g.OW};
+  constexpr int BK = Elem<T>::BK;
+  if constexpr (sizeof(T) == 2) {
+    if ((long)g.Nb * g.H * g.W * g.C < (1L << 31) && g.OH * g.OW >= BK &&
+        retr_tune_get(RETR_TUNE_WGRAD_B32) != 1) {
+      const int q = BK / g.OW, r = BK % g.OW;
+      ConvWgradB32<T> lb{(const T*)x, g, Ncols, Mp, q, r,
+                         (q * g.s * g.W + r * g.s) * g.C,
+                         g.s * g.W * g.C - g.OW * g.s * g.C,
+                         (g.H - g.OH * g.s) * g.W * g.C};
+      return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st,
+                                            "conv_wgrad", false);
+    }
+  }
+  ConvWgradB<T> lb{(const T*)x, g, Ncols, Mp, BK / g.OW, BK % g.OW};
   return launch_wgrad<kFamConvWgrad, T>(la, lb, ws, (long)Ncols, R, Ncols, Mp, st, "conv_wgrad", false);
 }
 

@@ -243,6 +243,35 @@ def _check_conv(dtype, tol, cfg):
     assert rel_err(grad, wreq.grad) < tol
 
 
+@pytest.mark.parametrize("cfg", CONVS[2:] + BIG_CONVS[:2] + BIG_CONVS[3:5] + BIG_CONVS[6:8])
+def test_conv_wgrad_b32_loader_bitwise(cfg):
+    """The 32-bit-offset weight-gradient loader (ConvWgradB32) visits the same pixels in the same
+    K order as the 64-bit one: identical split-K slabs (RETR_TUNE_WGRAD_B32 = 1 selects the
+    64-bit loader)."""
+    N, Ci, H, Co, k, s, p, d = cfg
+    bf = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(sum(cfg) + 7)
+    cp = max(8, (Ci + 7) // 8 * 8)
+    OH = (H + 2 * p - d * (k - 1) - 1) // s + 1
+    xn = torch.zeros(N, H, H, cp, dtype=bf, device=DEV)
+    xn[..., :Ci] = torch.randn(N, H, H, Ci, generator=g).to(DEV).to(bf)
+    gn = torch.randn(N, OH, OH, Co, generator=g).to(DEV).to(bf)
+    lib = _lib.load()
+    splits = lib.retr_conv2d_wgrad_splits(ops.dcode(bf), N, H, H, cp, Co, k, k, s, p, d)
+    out = []
+    try:
+        for knob in (0, 1):
+            lib.retr_tune(16, knob)
+            ws = torch.full((splits, Co, k * k * cp), float("nan"), device=DEV)
+            call("retr_conv2d_wgrad", ops.dcode(bf), ptr(gn), ptr(xn), N, H, H, cp, ptr(ws), Co,
+                 k, k, s, p, d, ops._st())
+            out.append(ws)
+    finally:
+        lib.retr_tune(16, 0)
+    assert not torch.isnan(out[0]).any()
+    assert torch.equal(out[0], out[1])
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("M,C", [(37, 64), (512, 256), (130, 512), (6400, 256), (4100, 512)])
 def test_layernorm(dtype, tol, M, C):

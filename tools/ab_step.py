@@ -43,6 +43,7 @@ VARIANTS = {
     "adamw_plain": {("TUNE", 15): 2},
     "gemm_nt": {("TUNE", 7): 1},
     "ce_unfused": {("ATTR", "FUSED_CE"): False},
+    "wgrad_b64": {("TUNE", 16): 1},
 }
 
 
@@ -56,7 +57,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 3, 7, 9, 15):
+    for k in (1, 3, 7, 9, 15, 16):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"

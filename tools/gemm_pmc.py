@@ -35,6 +35,15 @@ def main():
         relu = int(shape == "ffn")
         fn = lambda: call("retr_linear_fwd", BF, ptr(x), K, ptr(w), K, ptr(b), ptr(y), N, 0,  # noqa: E731
                           M, N, K, relu, None, 0, 0.0, 0, stream())
+    elif shape == "dg1":   # 1x1 data gradient 80x80x512 <- 128 with the residual addend
+        Nb, H, C, Co = 16, 80, 512, 128
+        dy = torch.randn(Nb * H * H * Co, device="cuda").to(bf)
+        w = (torch.randn(Co * C, device="cuda") * 0.05).to(bf)
+        add = torch.randn(Nb * H * H * C, device="cuda").to(bf)
+        dx = torch.empty(Nb * H * H * C, dtype=bf, device="cuda")
+        fl = 2.0 * Nb * H * H * Co * C
+        fn = lambda: call("retr_conv2d_dgrad", BF, ptr(dy), Nb, H, H, C, ptr(w), ptr(dx), Co,  # noqa: E731
+                          1, 1, 1, 0, 1, ptr(add), None, stream())
     else:
         Nb, H, C, Co, k, p = (16, 40, 256, 256, 3, 1) if shape == "fwd3" else (16, 80, 128, 512, 1, 0)
         x = torch.randn(Nb * H * H * C, device="cuda").to(bf)
@@ -42,7 +51,8 @@ def main():
         b = torch.randn(Co, device="cuda")
         y = torch.empty(Nb * H * H * Co, dtype=bf, device="cuda")
         fl = 2.0 * Nb * H * H * Co * k * k * C
-        fn = lambda: call("retr_conv2d_fwd", BF, ptr(x), Nb, H, H, C, ptr(w), ptr(b), None,  # noqa: E731
+        res = torch.randn(Nb * H * H * Co, device="cuda").to(bf) if shape == "fwd1" else None
+        fn = lambda: call("retr_conv2d_fwd", BF, ptr(x), Nb, H, H, C, ptr(w), ptr(b), ptr(res),  # noqa: E731
                           ptr(y), Co, k, k, 1, p, 1, 1, stream())
     for _ in range(3):
         fn()
