@@ -140,7 +140,8 @@ WPlan wgrad_plan(int n, const retr_linear_wgrad_desc* d) {
   for (int i = 0; i < n; ++i)
     if (d[i].M > 0) t128 += (long)cdiv(d[i].N, 128) * cdiv(d[i].K, 128);
   // 128x128 tiles only for token-heavy groups (the encoder FFN: 64 tiles x 6400 tokens);
-  // 64x64 with 512-1024-token slices elsewhere (tools/group_micro.py sweep)
+  // 64x64 with 512-1024-token slices elsewhere (tools/group_micro.py sweep; a 120k threshold,
+  // which moves the decoder FFN to 128x128, did not reproduce in-step: r3_ab_wgrad_tile.txt)
   long tok128 = 0;
   for (int i = 0; i < n; ++i)
     if (d[i].M > 0) tok128 += (long)cdiv(d[i].N, 128) * cdiv(d[i].K, 128) * d[i].M;
@@ -148,6 +149,7 @@ WPlan wgrad_plan(int n, const retr_linear_wgrad_desc* d) {
   (void)t128;
   const int tt = retr_tune_get(RETR_TUNE_WGRAD_TILE);
   if (tt == 64 || tt == 128) p.tile = tt;
+  if (tt > 128) p.tile = tok128 >= tt ? 128 : 64;   // A/B: another threshold
   p.stages = retr_tune_get(RETR_TUNE_WGRAD_STAGES);
   if (p.stages == 0) p.stages = 2;
   // one K-slice length (in tokens) for the whole group: about two blocks per CU over the

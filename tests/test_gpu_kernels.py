@@ -75,6 +75,7 @@ GROUPS = {
     "enc_attn": [(6400, 512, 256), (6400, 256, 256), (6400, 256, 256)],
     "dec_cross": [(2048, 256, 256), (6400, 256, 256), (6400, 256, 256), (2048, 256, 256)],
     "ffn": [(6400, 2048, 256), (6400, 256, 2048)],
+    "dec_ffn": [(2048, 2048, 256), (2048, 256, 2048)],
     "small_ragged": [(100, 64, 64), (37, 136, 72), (513, 264, 128)],
 }
 

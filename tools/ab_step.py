@@ -44,6 +44,15 @@ VARIANTS = {
     "gemm_nt": {("TUNE", 7): 1},
     "ce_unfused": {("ATTR", "FUSED_CE"): False},
     "wgrad_b64": {("TUNE", 16): 1},
+    "grp_s4": {("TUNE", 1): 4},
+    "wgrp_s4": {("TUNE", 3): 4},
+    "wkc256": {("TUNE", 4): 256},
+    "wkc1024": {("TUNE", 4): 1024},
+    "wtile128": {("TUNE", 2): 128},
+    "wthr50k": {("TUNE", 2): 50000},
+    "wthr100k": {("TUNE", 2): 100000},
+    "wthr120k": {("TUNE", 2): 120000},
+    "wthr400k": {("TUNE", 2): 400000},
 }
 
 
@@ -57,7 +66,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 3, 7, 9, 15, 16):
+    for k in (1, 2, 3, 4, 7, 9, 15, 16):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
