@@ -1011,20 +1011,23 @@ def test_attention_forward_key_split(B, H, Lq, Lk, hd, causal, masked):
         assert e < 5e-3, (fs, e)
 
 
-@pytest.mark.parametrize("kind", ["fwd1x1", "dgrad1x1", "dgrad3x3s2", "ffn"])
+@pytest.mark.parametrize("kind", ["fwd1x1", "dgrad1x1", "dgrad3x3s2", "ffn", "fwd1x1_k512",
+                                  "dgrad1x1_k512"])
 def test_shortk_single_stage_tiles_bitwise(kind):
     """Short-K wide GEMMs on the single-stage 64x64 tile (RETR_TUNE_SHORTK) and the large
     stride-2 dgrad phases on the single-stage 64x128 tile accumulate the same K-steps in the same
     order as the tiles they replaced: outputs bitwise equal with the rule on and off, and within
-    bf16 rounding of fp32 torch."""
+    bf16 rounding of fp32 torch.  (The *_k512 layer-4 shapes stay on their tiles either way:
+    parity coverage for the 512-deep 1x1 convs.)"""
     g = torch.Generator(device="cpu").manual_seed(11)
     bf = torch.bfloat16
     outs, ref = [], None
     for off in (1, 0):
         _lib.load().retr_tune(14, off)
         try:
-            if kind == "fwd1x1":      # 80x80x128 -> 512 + residual + ReLU (layer2 conv3)
-                Nb, H, C, Co = 2, 80, 128, 512
+            if kind.startswith("fwd1x1"):   # 80x80x128 -> 512 + residual + ReLU (layer2 conv3)
+                # or 20x20x512 -> 2048 (layer4 conv3, <= 8192 pixels)
+                Nb, H, C, Co = (2, 80, 128, 512) if kind == "fwd1x1" else (4, 20, 512, 2048)
                 if ref is None:
                     x = torch.randn(Nb, H, H, C, generator=g).to(DEV).to(bf)
                     w = (torch.randn(Co, C, generator=g) / math.sqrt(C)).to(DEV).to(bf)
@@ -1034,11 +1037,13 @@ def test_shortk_single_stage_tiles_bitwise(kind):
                 y = torch.empty(Nb, H, H, Co, dtype=bf, device=DEV)
                 call("retr_conv2d_fwd", 1, ptr(x), Nb, H, H, C, ptr(w), ptr(b), ptr(res), ptr(y),
                      Co, 1, 1, 1, 0, 1, 1, ops._st())
-            elif kind in ("dgrad1x1", "dgrad3x3s2"):
+            elif kind in ("dgrad1x1", "dgrad3x3s2", "dgrad1x1_k512"):
                 # 80x80x512 <- 128 with the residual addend (layer2 conv3's data gradient), or
                 # 160x160x128 <- 128 3x3 stride 2 (layer2.0 conv2: >= 64k pixels per phase)
-                Nb, H, C, Co, k, s_, p_ = ((2, 80, 512, 128, 1, 1, 0) if kind == "dgrad1x1"
-                                           else (11, 160, 128, 128, 3, 2, 1))
+                # or 20x20x2048 <- 512 (layer4 conv1's, K 512)
+                Nb, H, C, Co, k, s_, p_ = {"dgrad1x1": (2, 80, 512, 128, 1, 1, 0),
+                                           "dgrad1x1_k512": (4, 20, 2048, 512, 1, 1, 0),
+                                           "dgrad3x3s2": (11, 160, 128, 128, 3, 2, 1)}[kind]
                 OH = (H + 2 * p_ - k) // s_ + 1
                 if ref is None:
                     w = torch.randn(Co, C, k, k, generator=g) / math.sqrt(C * k * k)
@@ -1046,8 +1051,8 @@ def test_shortk_single_stage_tiles_bitwise(kind):
                     assert cp == C
                     weff = wp.float()[..., :C].permute(0, 3, 1, 2).cpu()
                     gy = torch.randn(Nb, Co, OH, OH, generator=g).to(bf).float()
-                    add = (torch.randn(Nb, H, H, C, generator=g).to(bf) if kind == "dgrad1x1"
-                           else None)
+                    add = (torch.randn(Nb, H, H, C, generator=g).to(bf)
+                           if kind.startswith("dgrad1x1") else None)
                     xreq = torch.zeros(Nb, C, H, H, requires_grad=True)
                     F.conv2d(xreq, weff, stride=s_, padding=p_).backward(gy)
                     ref = xreq.grad.permute(0, 2, 3, 1).to(DEV)

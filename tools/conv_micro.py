@@ -119,6 +119,8 @@ def main():
         stem()
         return
     shapes = SHAPES
+    if os.environ.get("RETR_VARIANTS"):   # e.g. RETR_VARIANTS=0,6,8,13 (RETR_TUNE_BIG_TILE values)
+        VARIANTS = [(int(t), 0) for t in os.environ["RETR_VARIANTS"].split(",")]
     if only == "r50":
         shapes = r50_shapes()
         VARIANTS = [(0, 0), (13, 0), (14, 0)] if os.environ.get("RETR_SWEEP_S1") else [(0, 0), (4, 0), (6, 0)]
