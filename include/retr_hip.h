@@ -437,6 +437,9 @@ int retr_cast(int dtype, const float* x, void* y, long n, void* stream);
 /* dpos[p][c] += sum_{m: m % period == p} d[m][c] */
 int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
                   void* stream);
+/* retr_pos_grad with dpos overwritten (dpos = the sums): no zero fill before a fresh gradient */
+int retr_pos_grad_set(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
+                      void* stream);
 
 /* ---- fused clip_grad_norm_ + AdamW over flat fp32 arenas --------------------------------
  * Replaces engine.py:80-83 (torch.nn.utils.clip_grad_norm_ + optimizer.step()) with the

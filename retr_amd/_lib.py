@@ -154,6 +154,7 @@ _SIGS = {
     "retr_add_pos_fwd": [_I, _P, _L, _I, _I, _P, _I, _P, _P, _L, _P],
     "retr_sum2": [_I, _P, _P, _L, _P, _P],
     "retr_pos_grad": [_I, _P, _L, _I, _I, _I, _P, _P],
+    "retr_pos_grad_set": [_I, _P, _L, _I, _I, _I, _P, _P],
     "retr_dec_gemm": [_P, _P, _I, _I, _P, _P, _I, _P, _L, _I, _P, _L, _I, _P, _L, _I, _I, _I, _P],
     "retr_dec_rows": [_P, _P, _I, _P, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P],
     "retr_dec_embed_rows": [_P, _I, _I, _P, _P, _P, _P, _F, _P, _P, _P, _F, _P, _P, _P],

@@ -210,20 +210,23 @@ __global__ void cast_kernel(const float* x, T* y, long n) {
 }
 
 template <typename T>
-__global__ void pos_grad_kernel(const T* d, long ld, int M, int C, int period, float* dpos) {
+__global__ void pos_grad_kernel(const T* d, long ld, int M, int C, int period, float* dpos,
+                                int acc) {
   long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
   if (i >= (long)period * C) return;
   int c = i % C, p = (int)(i / C);
   float s = 0.f;
   for (int m = p; m < M; m += period) s += to_f(d[(long)m * ld + c]);
-  dpos[(long)p * C + c] += s;
+  float* o = dpos + (long)p * C + c;
+  *o = (acc ? *o : 0.f) + s;
 }
 
 // 8 consecutive columns per thread with 16-byte loads, and the rows of one position loaded 8
 // at a time before they are added (in row order, as pos_grad_kernel: bitwise the same sums) --
 // the scalar loop kept one dependent 2-byte load per row in flight (7 us per call at cfg2)
 template <typename T>
-__global__ void pos_grad8_kernel(const T* d, long ld, int M, int C, int period, float* dpos) {
+__global__ void pos_grad8_kernel(const T* d, long ld, int M, int C, int period, float* dpos,
+                                 int acc) {
   const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const int c8 = C / 8;
   if (i >= (long)period * c8) return;
@@ -246,8 +249,8 @@ __global__ void pos_grad8_kernel(const T* d, long ld, int M, int C, int period, 
     for (int e = 0; e < 8; ++e) s[e] += v[e];
   }
   float* o = dpos + (long)p * C + c;
-  float cur[8];
-  retr::load8<float>(o, cur);
+  float cur[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // (0 + s: the zero-filled sums)
+  if (acc) retr::load8<float>(o, cur);
 #pragma unroll
   for (int e = 0; e < 8; ++e) cur[e] += s[e];
   retr::store8<float>(o, cur);
@@ -343,8 +346,8 @@ int retr_cast(int dtype, const float* x, void* y, long n, void* stream) {
   return retr_check_launch("cast");
 }
 
-int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
-                  void* stream) {
+static int pos_grad(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
+                    int acc, void* stream) {
   long total = (long)period * C;
   if (total == 0 || M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
@@ -353,16 +356,26 @@ int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, f
       ((uintptr_t)dpos & 15) == 0) {
     const unsigned blocks = (unsigned)((total / 8 + 255) / 256);
     if (dtype == RETR_BF16)
-      hipLaunchKernelGGL(pos_grad8_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)d, ld, M, C, period, dpos);
+      hipLaunchKernelGGL(pos_grad8_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)d, ld, M, C, period, dpos, acc);
     else
-      hipLaunchKernelGGL(pos_grad8_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)d, ld, M, C, period, dpos);
+      hipLaunchKernelGGL(pos_grad8_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)d, ld, M, C, period, dpos, acc);
     return retr_check_launch("pos_grad8");
   }
   if (dtype == RETR_BF16)
-    hipLaunchKernelGGL(pos_grad_kernel<bf16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const bf16*)d, ld, M, C, period, dpos);
+    hipLaunchKernelGGL(pos_grad_kernel<bf16>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const bf16*)d, ld, M, C, period, dpos, acc);
   else
-    hipLaunchKernelGGL(pos_grad_kernel<float>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const float*)d, ld, M, C, period, dpos);
+    hipLaunchKernelGGL(pos_grad_kernel<float>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const float*)d, ld, M, C, period, dpos, acc);
   return retr_check_launch("pos_grad");
+}
+
+int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
+                  void* stream) {
+  return pos_grad(dtype, d, ld, M, C, period, dpos, 1, stream);
+}
+
+int retr_pos_grad_set(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
+                      void* stream) {
+  return pos_grad(dtype, d, ld, M, C, period, dpos, 0, stream);
 }
 
 }  // extern "C"

@@ -27,6 +27,11 @@ class MLP(nn.Module):
         h = [hidden_dim] * (num_layers - 1)
         self.layers = nn.ModuleList(nn.Linear(n, k) for n, k in zip([input_dim] + h,
                                                                      h + [output_dim]))
+        # ops.mlp_head runs the last layer over output rows padded to a multiple of 64: with
+        # FusedAdamW the parameter slots reserve those rows (always zero), so the padded bf16
+        # weight and fp32 bias are views of the optimizer's arenas (no per-step copies)
+        last = self.layers[-1]
+        last.weight._retr_pad_rows = last.bias._retr_pad_rows = (output_dim + 63) // 64 * 64
 
 
 class Caption(nn.Module):

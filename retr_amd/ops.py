@@ -131,7 +131,11 @@ class _WeightCache:
         if dtype == torch.float32 and rows == p.shape[0] and p.is_contiguous():
             return p.detach()
         sh = getattr(p, "_retr_shadow", None)
-        if sh is not None and dtype == torch.bfloat16 and rows == p.shape[0]:
+        if rows != p.shape[0]:   # FusedAdamW's slot reserves the padding rows (models/caption.py)
+            pad = getattr(p, "_retr_pad_shadow", None)
+            if sh is None or pad is None or pad.shape[0] != rows:
+                sh = None
+        if sh is not None and dtype == torch.bfloat16:
             # FusedAdamW's bf16 parameter shadow (written by its update kernel): cast into it
             # only when the parameter changed some other way
             ver = (p._version, p.data_ptr())
@@ -139,7 +143,7 @@ class _WeightCache:
                 src = p.detach().contiguous()
                 call("retr_cast", dcode(dtype), ptr(src), ptr(sh), src.numel(), _st())
                 p._retr_shadow_ver = ver
-            return sh
+            return sh if rows == p.shape[0] else p._retr_pad_shadow
         key = (dtype, rows)
         ent = getattr(p, self.ATTR, None)   # cache lives on the parameter object itself
         ver = (p._version, p.data_ptr())
@@ -215,6 +219,9 @@ def _pad_vec(v, n):
         return None
     if v.shape[0] == n:
         return v.detach().contiguous()
+    pad = getattr(v, "_retr_pad_data", None)   # FusedAdamW slot with the zero padding rows
+    if pad is not None and pad.shape[0] == n and pad.data_ptr() == v.data_ptr():
+        return pad
     ver = (v._version, v.data_ptr(), n)
     ent = getattr(v, "_retr_padvec", None)
     if ent is not None and ent[0] == ver:
@@ -1203,8 +1210,9 @@ class _AddPos(torch.autograd.Function):
         call("retr_sum2", dcode(ref.dtype), ptr(dy), ptr(dy2), M * C, ptr(dx), _st())
         dpos = None
         if ctx.needs_input_grad[1] and dy2 is not None:
-            dpos = torch.zeros(pshape, dtype=torch.float32, device=dev)
-            call("retr_pos_grad", dcode(dy2.dtype), ptr(dy2), C, M, C, period, ptr(dpos), _st())
+            dpos = torch.empty(pshape, dtype=torch.float32, device=dev)
+            call("retr_pos_grad_set", dcode(dy2.dtype), ptr(dy2), C, M, C, period, ptr(dpos),
+                 _st())
         return dx, dpos, None, None
 
 
@@ -1253,8 +1261,8 @@ class _LearnedPos(torch.autograd.Function):
             call("retr_dropout_apply", F32, ptr(d), C, ptr(dd), C, B * S, C, float(drop_p), seed,
                  _st())
             d = dd
-        dtab = torch.zeros(S, C, dtype=torch.float32, device=dev)
-        call("retr_pos_grad", F32, ptr(d), C, B * S, C, S, ptr(dtab), _st())
+        dtab = torch.empty(S, C, dtype=torch.float32, device=dev)
+        call("retr_pos_grad_set", F32, ptr(d), C, B * S, C, S, ptr(dtab), _st())
         dw, _ = grad_buffer(weight)
         dgamma, _ = grad_buffer(gamma)
         dbeta, _ = grad_buffer(ctx.beta)

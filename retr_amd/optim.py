@@ -107,7 +107,7 @@ class FusedAdamW(torch.optim.Optimizer):
             lo = off
             for p in g["params"]:
                 self._slots[id(p)] = (off, p.numel())
-                off += _round(p.numel())
+                off += _round(max(p.numel(), self._padded_numel(p)))
             self._groups.append((lo, off))
         total = max(off, _ALIGN)
         self.P = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -139,10 +139,23 @@ class FusedAdamW(torch.optim.Optimizer):
                 p._retr_arena = self.arena
                 if self.P16 is not None:
                     p._retr_shadow = self.P16[o:o + n].view_as(p)
+                pn = self._padded_numel(p)
+                if pn > n:   # rows past the parameter: never written, so always zero
+                    shape = (p._retr_pad_rows,) + tuple(p.shape[1:])
+                    p._retr_pad_data = self.P[o:o + pn].view(shape)
+                    if self.P16 is not None:
+                        p._retr_pad_shadow = self.P16[o:o + pn].view(shape)
                 self.state[p] = {"exp_avg": self.M[o:o + n].view_as(p),
                                  "exp_avg_sq": self.V[o:o + n].view_as(p)}
         self.sync_hyper()
         self.sync_shadow()
+
+    @staticmethod
+    def _padded_numel(p):
+        """Elements of ``p`` zero-padded to ``p._retr_pad_rows`` rows (models/caption.py MLP):
+        the slot reserves them so padded views of P / P16 need no copies."""
+        rows = getattr(p, "_retr_pad_rows", 0)
+        return rows * (p.numel() // p.shape[0]) if rows > p.shape[0] else 0
 
     def sync_shadow(self):
         """Re-cast the whole bf16 shadow from P (after P was written outside step())."""

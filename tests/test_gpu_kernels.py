@@ -1116,7 +1116,8 @@ def test_fused_cross_entropy_matches_two_pass(scale):
                                            (torch.bfloat16, 100, 12, 7)])
 def test_pos_grad_rows_in_order(dt, M, C, period):
     """retr_pos_grad (dpos[p] += sum of rows p, p + period, ... in row order; the 8-column
-    vector kernel for C % 8 == 0, the scalar one otherwise) equals the in-order fp32 sum."""
+    vector kernel for C % 8 == 0, the scalar one otherwise) equals the in-order fp32 sum, and
+    retr_pos_grad_set writes that sum."""
     g = torch.Generator(device="cpu").manual_seed(M + C)
     d = torch.randn(M, C, generator=g).to(dt)
     init = torch.randn(period, C, generator=g)
@@ -1129,3 +1130,9 @@ def test_pos_grad_rows_in_order(dt, M, C, period):
         s[m % period] += df[m]
     ref = init.numpy() + s
     assert np.array_equal(dpos.cpu().numpy(), ref)
+    # overwrite mode (retr_pos_grad_set): the old contents (NaN here) are never read
+    dset = torch.full((period, C), float("nan"), device=DEV)
+    call("retr_pos_grad_set", ops.dcode(dt), ptr(d.to(DEV)), C, M, C, period, ptr(dset),
+         ops._st())
+    torch.cuda.synchronize()
+    assert np.array_equal(dset.cpu().numpy(), np.float32(0) + s)
