@@ -165,7 +165,13 @@ def train_bench(args, rank, world, device):
                 d[f] += v[f]
         for d in fam.values():
             probe_mod.finish(d)
-    return dt, loss_v, fam, max(1, args.probe_steps)
+    sched = None
+    if graph_step is not None and graph_step.schedule is not None:
+        # the segment / bucket schedule every rank agreed on before the first replay
+        sched = {"segments": len(graph_step.segments),
+                 "buckets": len(graph_step.schedule["bucket_numel"]),
+                 "checked_across_ranks": world}
+    return dt, loss_v, fam, max(1, args.probe_steps), sched
 
 
 def decode_step_bytes(cfg, B, S, T, esize):
@@ -439,7 +445,7 @@ def main():
     device = torch.device("cuda", local)
     torch.manual_seed(42 + rank)
 
-    dt, loss, fam, psteps = train_bench(args, rank, world, device)
+    dt, loss, fam, psteps, sched = train_bench(args, rank, world, device)
     imgs = world * args.batch * args.steps
     value = imgs / dt
     roof = _roofline(fam, psteps)
@@ -513,6 +519,9 @@ def main():
                           "parallelism": f"dp{world}"},
                "loss": round(loss, 4), "roofline": roof, "cpu_baseline": cpu,
                "launch": launch,
+               "dist": {"world_size_seen": dist.get_world_size() if dist.is_initialized() else 1,
+                        "backend": dist.get_backend() if dist.is_initialized() else None,
+                        "dp_schedule": sched},
                "optimizer": "torch.optim.AdamW" if args.torch_adamw else "FusedAdamW",
                "decode": decode, "kernel_families": families}
         print(json.dumps(out), flush=True)

@@ -10,9 +10,13 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libretr_hip.so")
-# A/B measurements only (tools/*_micro.py): time a baseline build of the same C-ABI
+# A/B measurements only (tools/*_micro.py, tools/ab_step.py): time a baseline build of the same
+# C-ABI.  Never silent: a stray setting would swap every kernel of the process.
 if os.environ.get("RETR_AB_LIB"):
     LIB_PATH = os.environ["RETR_AB_LIB"]
+    import sys as _sys
+    print(f"retr_amd: RETR_AB_LIB is set -- loading kernels from {LIB_PATH} instead of the "
+          f"in-tree libretr_hip.so (A/B tooling only)", file=_sys.stderr)
 
 F32, BF16 = 0, 1
 

@@ -141,6 +141,10 @@ class GradSync:
             elif self.on_ready is not None:
                 self.on_ready(bi)
 
+    def check_schedule(self, after):
+        """``check_schedule`` over this GradSync's buckets and group (see there)."""
+        return check_schedule(after, self.flat, self.group)
+
     def synchronize(self):
         """Wait for every bucket (launching the ones not launched yet: deferred mode, or
         parameters that received no gradient, whose slots hold zeros) and leave the averaged
@@ -173,6 +177,37 @@ class GradSync:
                     p.grad.copy_(g)
         self.foreign.clear()
         self.reset()
+
+
+def schedule_signature(after, flat):
+    """What every rank must agree on before replaying a segmented DP step: the buckets whose
+    all-reduce follows each segment (``GraphedTrainStep.after``) and every bucket's element
+    count.  Plain ints only, so the signature compares exactly across processes."""
+    return {"after": [[int(b) for b in a] for a in after],
+            "bucket_numel": [int(f.numel()) for f in flat]}
+
+
+def check_schedule(after, flat, group=None):
+    """Pre-flight for the segmented, hipGraph-replayed DP step (engine.GraphedTrainStep).
+
+    Each rank derives its segment cuts from its OWN autograd hook order at capture time.  If two
+    ranks ever cut differently (different bucket order, a bucket completing in another segment,
+    different bucket sizes), their replays would enqueue mismatched RCCL all-reduces and hang
+    or average the wrong bytes.  All-gather every rank's ``schedule_signature`` and raise on
+    any difference -- once, after capture, before the first replay.  Returns the signature."""
+    mine = schedule_signature(after, flat)
+    world = dist.get_world_size(group)
+    if world == 1:
+        return mine
+    got = [None] * world
+    dist.all_gather_object(got, mine, group=group)
+    bad = [r for r, sig in enumerate(got) if sig != got[0]]
+    if bad:
+        rows = "; ".join(f"rank {r}: after={got[r]['after']} "
+                         f"buckets={got[r]['bucket_numel']}" for r in [0] + bad)
+        raise RuntimeError("GradSync: ranks disagree on the segmented all-reduce schedule "
+                           f"(ranks {bad} differ from rank 0): {rows}")
+    return mine
 
 
 def broadcast_parameters(module, src=0, group=None):

@@ -51,8 +51,9 @@ def forward_backward(model, criterion, samples, caps, cap_masks, optimizer):
     """engine.py:70-79: forward, CE loss, zero_grad, backward (no host sync)."""
     from . import ops
     ops.bump_seed()
-    outputs = model(*samples, caps[:, :-1], cap_masks[:, :-1])
-    loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
+    with ops.train_step_scope():
+        outputs = model(*samples, caps[:, :-1], cap_masks[:, :-1])
+        loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
     optimizer.zero_grad()
     loss.backward()
     return loss
@@ -103,14 +104,12 @@ class GraphedTrainStep:
     def __init__(self, model, criterion, optimizer, max_norm, grad_sync=None, warmup=2):
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
         self.max_norm, self.grad_sync, self.warmup = max_norm, grad_sync, warmup
-        if hasattr(optimizer, "consume_grads"):
-            # FusedAdamW zeroes the gradient arena in its update: no zero fill per replay
-            optimizer.consume_grads = True
         self.graph = None
         self.graph_opt = None
         self.segments = []        # DP: forward/backward segment graphs (segments[0] is graph)
         self.after = []           # DP: buckets whose all-reduce follows segment k
         self.order = []           # DP: enqueue order of the last replay
+        self.schedule = None      # DP: the cross-rank-checked schedule (ddp.check_schedule)
         self.static = None
         self.loss = None
         self._active = None
@@ -177,6 +176,9 @@ class GraphedTrainStep:
         finally:
             gs.on_ready = None
         torch.cuda.current_stream().wait_stream(cs)
+        # every rank must have cut at the same buckets, or the replays would issue mismatched
+        # collectives: all-gather the schedules and raise on a difference (ddp.check_schedule)
+        self.schedule = gs.check_schedule(self.after)
         try:
             gs.synchronize()                 # eager: p.grad -> bucket views for the last graph
             self.graph_opt = torch.cuda.CUDAGraph()
@@ -240,6 +242,14 @@ class GraphedTrainStep:
                         v.copy_(old[k])
         self._bump()
 
+    def _clean_arena(self):
+        """The captured step expects a zero gradient arena (its own update leaves it so): an
+        eager step run since the last replay without consume mode left gradients in it."""
+        a = getattr(self.optimizer, "arena", None)
+        if a is not None and a.dirty:
+            a.G.zero_()
+            a.dirty = False
+
     def _bump(self):
         inc = torch.autograd.graph.increment_version
         for p in self._params():
@@ -257,18 +267,32 @@ class GraphedTrainStep:
             for dst, src in zip(self.static, (nt.tensors, nt.mask, caps, cap_masks)):
                 dst.copy_(src, non_blocking=True)
         if self.graph is None:
-            snap = self._snapshot()
-            side = torch.cuda.Stream()
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                for _ in range(self.warmup):
-                    self._step().detach()
-            torch.cuda.current_stream().wait_stream(side)
-            torch.cuda.synchronize()
-            self.optimizer.zero_grad(set_to_none=True)
-            self._capture()
-            self._active = list(getattr(self.optimizer, "_last_active", []))
-            self._restore(snap)
+            opt = self.optimizer
+            consume0 = getattr(opt, "consume_grads", None)
+            if consume0 is not None:
+                # FusedAdamW consume mode (its update zeroes the gradient arena: no zero fill
+                # per replay) only for the steps this object runs -- warm-up and capture; the
+                # captured update keeps it on every replay, eager steps outside keep the
+                # optimizer's own setting (p.grad holds the clipped gradient after step())
+                opt.consume_grads = True
+            try:
+                snap = self._snapshot()
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    for _ in range(self.warmup):
+                        self._step().detach()
+                torch.cuda.current_stream().wait_stream(side)
+                torch.cuda.synchronize()
+                opt.zero_grad(set_to_none=True)
+                self._capture()
+                self._active = list(getattr(opt, "_last_active", []))
+                self._restore(snap)
+            finally:
+                if consume0 is not None:
+                    opt.consume_grads = consume0
+        else:
+            self._clean_arena()
         if hasattr(self.optimizer, "sync_hyper"):
             self.optimizer.sync_hyper()      # lr schedule changes reach the captured kernels
         if self.graph_opt is None:
@@ -292,6 +316,7 @@ class GraphedTrainStep:
 
 def train_one_epoch(model, criterion, data_loader, optimizer, device, epoch, max_norm,
                     grad_sync=None):
+    from . import ops
     model.train()
     criterion.train()
     epoch_loss = 0.0
@@ -304,8 +329,9 @@ def train_one_epoch(model, criterion, data_loader, optimizer, device, epoch, max
                                           device)
             caps = caps.to(device)
             cap_masks = cap_masks.to(device)
-            outputs = model(*samples, caps[:, :-1], cap_masks[:, :-1])
-            loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
+            with ops.train_step_scope():
+                outputs = model(*samples, caps[:, :-1], cap_masks[:, :-1])
+                loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
             loss_value = loss.item()
             epoch_loss += loss_value
             finite = math.isfinite(loss_value)

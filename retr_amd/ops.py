@@ -1109,6 +1109,24 @@ def mlp_head(mlp, hs, B, T, cdtype):
 # ---------------------------------------------------------------------------------------------
 
 FUSED_CE = True   # bf16 training: loss and dlogits from one pass (tests / A/B switch it off)
+_TRAIN_STEP = 0   # > 0 inside train_step_scope(): a backward pass is about to follow
+
+
+class train_step_scope:
+    """Marks a forward whose loss will be back-propagated right away (engine.forward_backward,
+    engine.train_one_epoch).  Only there does the cross-entropy compute dlogits in its forward
+    pass (retr_ce_fwd_bwd): a loss computed with grad enabled for logging, or a step that fails
+    before backward, then costs no extra [M, Vp] buffer or HBM pass."""
+
+    def __enter__(self):
+        global _TRAIN_STEP
+        _TRAIN_STEP += 1
+        return self
+
+    def __exit__(self, *exc):
+        global _TRAIN_STEP
+        _TRAIN_STEP -= 1
+        return False
 
 
 class _CrossEntropy(torch.autograd.Function):
@@ -1131,7 +1149,7 @@ class _CrossEntropy(torch.autograd.Function):
         Vp = _round_up(V, 64)
         ctx.dl = None
         if (ctx.needs_input_grad[0] and base.dtype == torch.bfloat16 and ld % 8 == 0
-                and Vp <= 32768 and FUSED_CE):
+                and Vp <= 32768 and FUSED_CE and _TRAIN_STEP > 0):
             # training: the gradient for dloss = 1 comes out of the same pass over the logits
             # (retr_ce_fwd_bwd); backward only rewrites it if dloss != 1
             ctx.dl = torch.empty(M, Vp, dtype=base.dtype, device=dev)

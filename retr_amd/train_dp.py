@@ -25,6 +25,15 @@ import torch.distributed as dist
 from torch.utils.data import BatchSampler, DataLoader, DistributedSampler
 
 
+def dist_timeout():
+    """Collective timeout of the process group: ``RETR_DIST_TIMEOUT_S`` seconds, default one
+    hour.  The validation pass runs on rank 0 alone while every other rank waits in the
+    broadcast of its loss (``_from_rank0``), so the timeout must exceed one full ``evaluate()``
+    over the validation set -- NCCL's 10-minute default does not on a large set."""
+    import datetime
+    return datetime.timedelta(seconds=float(os.environ.get("RETR_DIST_TIMEOUT_S", "3600")))
+
+
 def init_distributed():
     """Process group from the torchrun environment (RANK/WORLD_SIZE/MASTER_*), RCCL when a GPU
     is visible.  Returns (rank, world_size, local_rank); (0, 1, 0) without torchrun."""
@@ -33,7 +42,7 @@ def init_distributed():
         backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, timeout=dist_timeout())
     if not dist.is_initialized():
         return 0, 1, 0
     return dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", 0))

@@ -180,3 +180,34 @@ def test_validation_loss_is_reference_evaluate_on_rank0():
     assert [r[1] for r in res] == [True, False]
     for rank, _, v, ref in res:
         assert v == ref, (rank, v, ref)
+
+
+def _schedule_worker(rank, world, port, q, mismatch):
+    _init(rank, world, port)
+    from retr_amd.ddp import check_schedule
+    flat = [torch.zeros(64), torch.zeros(32), torch.zeros(16)]
+    after = [[0], [], [1, 2]]
+    if mismatch == "order" and rank == 1:
+        after = [[0], [2], [1]]          # bucket 2 completed in another segment on rank 1
+    if mismatch == "size" and rank == 1:
+        flat[1] = torch.zeros(48)        # a bucket cut at other bounds
+    try:
+        sig = check_schedule(after, flat)
+        q.put((rank, "ok", sig["after"]))
+    except RuntimeError as e:
+        q.put((rank, "raised", str(e)))
+    dist.destroy_process_group()
+
+
+def test_segmented_schedule_agreement_checked_across_ranks():
+    """GraphedTrainStep pre-flight (ddp.check_schedule): every rank all-gathers its segment cut
+    schedule + bucket sizes after capture; equal schedules pass, a rank whose hooks cut at
+    another bucket or whose bucket bounds differ makes EVERY rank raise (no rank replays into
+    a mismatched collective)."""
+    ok = _spawn(_schedule_worker, None)
+    assert [r[1] for r in ok] == ["ok", "ok"], ok
+    assert ok[0][2] == [[0], [], [1, 2]]
+    for mismatch in ("order", "size"):
+        res = _spawn(_schedule_worker, mismatch)
+        assert [r[1] for r in res] == ["raised", "raised"], (mismatch, res)
+        assert "disagree" in res[0][2] and "rank 1" in res[0][2]

@@ -285,3 +285,74 @@ def test_fused_ln_dropout_backward_matches_unfused(hidden):
             # upstream of the memory: the six cross-attention blocks' bf16 memory gradients
             # are summed in the GEMM epilogues (one bf16 rounding fewer per add)
             assert rel(n) < 2e-2, (n, rel(n))
+
+
+@pytest.mark.parametrize("extra_use", [False, True])
+def test_shared_memory_gradient_is_sum_of_block_contributions(extra_use):
+    """The bf16 decoder sums the six cross-attention blocks' memory gradients (dmem, dmem_pos)
+    in ONE shared buffer inside the data-gradient GEMM epilogues (ops._shared_grad: the first
+    contributor writes it, later ones add the running sum as the epilogue addend, the last
+    returns it).  Checked directly against the fp32 sum of the per-block contributions that
+    the unfused path returns one by one: every element within a few bf16 roundings of the sum,
+    the norm within 1e-2 -- a dropped, doubled or misplaced contributor is off by ~1/6 of the
+    sum.  ``extra_use``: the memory also feeds a plain autograd op, so autograd accumulates
+    the shared buffer with a foreign gradient."""
+    from retr_amd import ops
+    cfg = make_config(backbone="ResNet18", hidden=64, layers=(1, 6), vocab=1000, max_pos=16,
+                      ffn=128, dtype="bf16", dropout=0.0)
+    model, _ = build_model(cfg)
+    model.load_state_dict(synthetic_state_dict(model, seed=5))
+    model.to(DEV).train()
+    tr = model.transformer
+    B, S, T, C = 2, 24, 16, 64
+    g = torch.Generator().manual_seed(7)
+    mem0 = torch.randn(B * S, C, generator=g)
+    memp0 = mem0 + 0.1 * torch.randn(B * S, C, generator=g)
+    mem0, memp0 = mem0.to(DEV, torch.bfloat16), memp0.to(DEV, torch.bfloat16)
+    kpm = torch.zeros(B, S, dtype=torch.uint8, device=DEV)
+    kpm[1, S - 5:] = 1
+    caps, cap_mask = synthetic_captions(B, T, 1000, seed=3)
+    tgt, tm = caps[:, :-1].to(DEV), cap_mask[:, :-1].to(DEV)
+    w_hs = torch.randn(B * T, C, generator=g).to(DEV)
+    w_x = torch.randn(B * S, C, generator=g).to(DEV)
+    contrib = []
+    orig = ops._CrossAttnBlock.backward
+
+    def recording(ctx, *grads):
+        r = orig(ctx, *grads)
+        contrib.append((r[6].float().clone(), r[7].float().clone()))
+        return r
+
+    res = {}
+    try:
+        for fuse in (False, True):
+            ops.FUSE_LN_BWD = fuse
+            ops._CrossAttnBlock.backward = staticmethod(recording) if not fuse else orig
+            mem = mem0.clone().requires_grad_(True)
+            memp = memp0.clone().requires_grad_(True)
+            ops.begin_pass()
+            hs, _, _ = tr.decode(mem, memp, B, S, kpm, tgt, tm, torch.bfloat16)
+            loss = (hs.float() * w_hs).sum()
+            if extra_use:
+                loss = loss + (mem.float() * w_x).sum()
+            loss.backward()
+            torch.cuda.synchronize()
+            res[fuse] = (memp.grad.float().clone(), mem.grad.float().clone())
+    finally:
+        ops.FUSE_LN_BWD = True
+        ops._CrossAttnBlock.backward = orig
+    assert len(contrib) == 6
+    extra = w_x.to(torch.bfloat16).float() if extra_use else torch.zeros_like(w_x)
+    for i, what in enumerate(("dmem_pos", "dmem")):
+        parts = [c[i] for c in contrib]
+        s = torch.stack(parts).sum(0) + (extra if i == 1 else 0)
+        mag = torch.stack([p.abs() for p in parts]).sum(0) + (extra.abs() if i == 1 else 0)
+        for fuse in (True, False):
+            got = res[fuse][i]
+            assert torch.isfinite(got).all()
+            # <= 7 adds, each rounding the running sum to bf16 (2^-9 relative): 2^-6 of the
+            # element's absolute-sum is a 2x margin
+            bad = ((got - s).abs() > 2.0 ** -6 * mag + 1e-6).sum().item()
+            assert bad == 0, (what, fuse, bad, (got - s).abs().max().item())
+            e = ((got - s).norm() / s.norm()).item()
+            assert e < 1e-2, (what, fuse, e)

@@ -189,6 +189,35 @@ def test_graphed_step_with_fused_adamw_matches_eager():
         assert _rel(a.detach(), b.detach()) < 5e-5, n
 
 
+def test_graphed_and_eager_steps_mix_on_one_fused_adamw():
+    """Consume mode (the captured update zeroes the gradient arena) belongs to GraphedTrainStep
+    only: an eager train_step on the same optimizer between replays still leaves the clipped
+    gradients in p.grad (torch semantics), and the next replay starts from a clean arena --
+    same result as the same sequence of steps run eagerly."""
+    from retr_amd.engine import GraphedTrainStep, train_step
+    cfg, m1, crit = _micro_model()
+    _, m2, _ = _micro_model()
+    o1 = FusedAdamW(_groups(m1, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    o2 = FusedAdamW(_groups(m2, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    samples, caps, cm = _batch(cfg)
+    m1.train()
+    m2.train()
+    graphed = GraphedTrainStep(m1, crit, o1, 0.1, warmup=2)
+    assert o1.consume_grads is False
+    graphed(samples, caps, cm)
+    assert o1.consume_grads is False           # restored after warm-up + capture
+    train_step(m1, crit, samples, caps, cm, o1, 0.1)
+    g_eager = {n: p.grad.detach().clone() for n, p in m1.named_parameters()
+               if p.grad is not None}
+    assert g_eager and any(g.abs().max().item() > 0 for g in g_eager.values())
+    lg = graphed(samples, caps, cm).item()
+    for _ in range(3):
+        le = train_step(m2, crit, samples, caps, cm, o2, 0.1).item()
+    assert abs(lg - le) <= 1e-5 * abs(le), (lg, le)
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert _rel(a.detach(), b.detach()) < 5e-5, n
+
+
 def _micro_bf16(lr):
     from bench import build
     cfg = make_config(dtype="bf16")

@@ -6,10 +6,14 @@
         --source "<what was run>" [--by-kernel 25]
 
 Per dispatch (rocprofv3 sums each counter over its hardware instances):
-  * mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024): the fraction of
-    SIMD-cycles the matrix pipes were busy -- rocprof's own MfmaUtil
-    (counter_defs.yaml: sum(MFMA_BUSY) / (max(GRBM_GUI_ACTIVE) x SIMD_NUM)); GRBM_GUI_ACTIVE
-    is summed over the 8 XCDs (MI355X_MICROARCH.md "DVFS give-back"), 256 CUs x 4 SIMDs;
+  * mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (cycles x 1024 SIMDs), cycles per dispatch =
+    min(GRBM_GUI_ACTIVE / 8, duration x 2.4 GHz): rocprof's own MfmaUtil
+    (counter_defs.yaml: sum(MFMA_BUSY) / (max(GRBM_GUI_ACTIVE) x SIMD_NUM); GRBM_GUI_ACTIVE
+    is summed over the 8 XCDs, MI355X_MICROARCH.md "DVFS give-back"), except that on short
+    dispatches GRBM_GUI_ACTIVE spans more than the dispatch (its quotient by the duration
+    reads above the 2.4 GHz maximum clock): there the dispatch's own duration at the maximum
+    clock is the denominator (a lower bound on the busy fraction).  ``mfma_busy_grbm`` keeps
+    the uncorrected figure and ``clock_ghz`` the raw GRBM quotient;
   * mfma_flop = SQ_VALU_MFMA_BUSY_CYCLES x 1024: the FLOPs the busy cycles correspond to for
     bf16 (a 32x32x16 bf16 MFMA = 32 busy cycles = 32768 FLOP; MI355X_MICROARCH.md), to compare
     with the algorithmic FLOPs (padding and recomputation show as a surplus);
@@ -27,6 +31,9 @@ from retr_amd.probe import family_of_symbol  # noqa: E402
 
 SIMDS = 1024
 XCDS = 8
+
+
+MAX_CLOCK_GHZ = 2.4
 
 
 def read(path):
@@ -56,7 +63,10 @@ def summarise(groups):
     for key, (n, c, ns) in groups.items():
         busy, grbm = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0), c.get("GRBM_GUI_ACTIVE", 0.0)
         valu, mfma = c.get("SQ_INSTS_VALU", 0.0), c.get("SQ_INSTS_MFMA", 0.0)
-        e = {"dispatches": n, "mfma_busy": round(busy / (grbm / XCDS * SIMDS), 4) if grbm else None,
+        cyc = c.get("_cycles", 0.0)
+        e = {"dispatches": n, "mfma_busy": round(busy / (cyc * SIMDS), 4) if cyc else None,
+             "mfma_busy_grbm": round(busy / (grbm / XCDS * SIMDS), 4) if grbm else None,
+             "clock_corrected_dispatches": int(c.get("_clamped", 0)),
              "mfma_flop_per_dispatch": round(busy * 1024 / n),
              "valu_per_mfma": round(valu / mfma, 2) if mfma else None,
              "insts_per_dispatch": {k: round(v / n) for k, v in sorted(c.items())
@@ -76,6 +86,13 @@ def main():
     fam = defaultdict(lambda: [0, defaultdict(float), 0])
     ker = defaultdict(lambda: [0, defaultdict(float), 0])
     for name, c, ns in rows.values():
+        # per-dispatch cycle denominator: GRBM_GUI_ACTIVE / 8, clamped to the dispatch's own
+        # duration at the maximum clock when GRBM spans more than the dispatch
+        g8 = c.get("GRBM_GUI_ACTIVE", 0.0) / XCDS
+        cap = ns * MAX_CLOCK_GHZ if ns else g8
+        c = dict(c)
+        c["_cycles"] = min(g8, cap) if ns else g8
+        c["_clamped"] = 1.0 if (ns and g8 > cap) else 0.0
         f = family_of_symbol(name) or "(other)"
         for g, k in ((fam, f), (ker, short(name))):
             g[k][0] += 1
@@ -85,9 +102,10 @@ def main():
     fams = summarise(fam)
     top = sorted(ker.items(), key=lambda kv: -kv[1][2])[:nk]
     kers = summarise(dict(top))
-    res = {"source": src, "formula": "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE "
-           "/ 8 XCDs x 1024 SIMDs) (rocprof MfmaUtil); mfma_flop = busy cycles x 1024 (bf16); "
-           "valu_per_mfma = SQ_INSTS_VALU / SQ_INSTS_MFMA", "families": fams, "kernels": kers}
+    res = {"source": src, "formula": "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (min(GRBM_GUI_ACTIVE "
+           "/ 8 XCDs, duration x 2.4 GHz) x 1024 SIMDs) per dispatch (rocprof MfmaUtil, clamped "
+           "where GRBM spans more than the dispatch); mfma_busy_grbm = the unclamped figure; "
+           "mfma_flop = busy cycles x 1024 (bf16); valu_per_mfma = SQ_INSTS_VALU / SQ_INSTS_MFMA", "families": fams, "kernels": kers}
     if out:
         with open(out, "w") as f:
             json.dump(res, f, indent=1)

@@ -3,9 +3,12 @@
 
     python tools/rocprof_families.py <run_results.db | *_kernel_trace.csv> [--steps N]
 
-With ``--steps N`` totals are also divided by N (the number of training steps in the trace)
-so they compare directly with bench.py's ``kernel_families`` (ms per step) and its
-``roofline.avg_launch_us``.
+Totals are also divided by the number of training steps in the trace so they compare directly
+with bench.py's ``kernel_families`` (ms per step) and its ``roofline.avg_launch_us``.  That
+count is read from the trace itself: the fused stem (``stem_pool_kernel``) runs exactly once
+per training step (warm-up, captured and probe steps alike; decode runs its own stem
+launches only when the trace holds decode, so pass ``--steps N`` explicitly there).
+``--steps N`` overrides; the header line says which count was used and where it came from.
 """
 import os
 import sys
@@ -18,8 +21,16 @@ from tools.prof_summary import from_csv, from_db  # noqa: E402
 
 def main():
     path = sys.argv[1]
-    steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 1
     rows = from_db(path) if path.endswith(".db") else from_csv(path)
+    if "--steps" in sys.argv:
+        steps = int(sys.argv[sys.argv.index("--steps") + 1])
+        src = "--steps"
+    else:
+        steps = sum(1 for name, _, _ in rows if "stem_pool_kernel" in name)
+        src = "stem_pool_kernel launches in the trace (one per training step)"
+        if steps == 0:
+            steps, src = 1, "no stem_pool_kernel in the trace: totals per trace"
+    print(f"# steps in trace: {steps} ({src})")
     agg = defaultdict(lambda: [0, 0.0])
     other = [0, 0.0]
     for name, us, _ in rows:
