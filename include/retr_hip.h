@@ -116,7 +116,10 @@ enum {
                                    stores, 2 plain */
   RETR_TUNE_WGRAD_B32 = 16,     /* 1: 3x3 / strided conv weight gradients on the 64-bit-cursor
                                    ConvWgradB loader instead of ConvWgradB32 */
-  RETR_TUNE_COUNT = 17
+  RETR_TUNE_WGRAD_FUSED = 17,   /* grouped bf16 linear weight gradients: 0 slabs + a separate
+                                   slab_sum_group launch (default), 1 split-K reduced by each
+                                   tile's last-arriving block inside the GEMM launch */
+  RETR_TUNE_COUNT = 18
 };
 int retr_tune(int knob, int value);
 

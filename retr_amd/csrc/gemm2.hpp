@@ -509,6 +509,11 @@ int launch_big(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, in
     case 13: return launch_gemm2<FAM, 64, 64, 2, 2, 1>(la, lb, ep, M, N, K, splits, st, what);
     case 14: return launch_gemm2<FAM, 64, 128, 2, 2, 1>(la, lb, ep, M, N, K, splits, st, what);
     case 15: return launch_gemm2<FAM, 128, 64, 2, 2, 1>(la, lb, ep, M, N, K, splits, st, what);
+    // 8 waves of 64x64 (one block per CU): half the LDS fragment bytes per MFMA of the 32x64
+    // wave tile, 1.33x fewer loader chunks per MFMA than 2 x 128x128
+    case 16: return launch_gemm2<FAM, 256, 128, 4, 2, 2>(la, lb, ep, M, N, K, splits, st, what);
+    case 17: return launch_gemm2<FAM, 128, 256, 2, 4, 2>(la, lb, ep, M, N, K, splits, st, what);
+    case 18: return launch_gemm2<FAM, 256, 128, 4, 2, 3>(la, lb, ep, M, N, K, splits, st, what);
     default: break;
   }
   // skinny GEMMs over a wide N (the decode step's vocabulary projection, M = 64 caption rows /

@@ -299,6 +299,267 @@ int wgrad_group_gemm(const WPlan& p, const retr_linear_wgrad_desc* d, float* ws,
   return g.launch(st, "linear_wgrad_group");
 }
 
+// ---- weight gradients with the split-K reduction inside the GEMM launch -----------------------
+// (RETR_TUNE_WGRAD_FUSED = 1; measured slower than slabs + slab_sum_group, kept for A/B.)
+// Every (tile, K-slice) block writes its fp32 slab with write-through stores (EpiSlab); the block that
+// arrives LAST at its tile's ticket (agent-scope release / acquire, cdna_hip_programming.md §5
+// "Projection GEMM at M = 256" item 2 and §6 Guideline 16) adds all slices' slabs in SLICE
+// order -- whoever arrives last, the sum is the same, and the same as slab_sum_group's -- and
+// writes (or accumulates into) dW / db.  The slabs are re-read while L2 / Infinity-Cache
+// resident, no second launch.  Blocks past the GEMM blocks sum the extra partial rows
+// (LayerNorm dgamma / dbeta from retr_layernorm_bwd2) in the same launch.
+struct EpiSlab {
+  float* ws;              // slab of slice 0 (row-major [rows][cols])
+  long ld;                // = cols
+  long split_stride;      // floats between consecutive slices' slabs
+  int split = 0;          // set per block
+  float* dst;             // dW ([rows][lddw]) or db
+  long lddw;
+  int rows, cols, splits, accumulate, vec;
+  int* tickets;           // one counter per output tile (zero between launches)
+  static constexpr bool kRowSum = false;
+  // write-through (sc1) stores: the slab reaches memory without an L2 write-back, so the
+  // publish needs no release fence (Guideline 16 R1: plain stores + agent release made every
+  // block flush its XCD's dirty L2 -- +19 us per launch, measured)
+  RETR_DEVICE __amdgpu_buffer_rsrc_t rsrc() const {
+    return __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
+  }
+  RETR_DEVICE unsigned off(int m, int n) const {
+    return (unsigned)(((long)split * split_stride + (long)m * ld + n) * 4);
+  }
+  RETR_DEVICE void apply(int m, int n, float v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc(), off(m, n), 0,
+                                          16);
+  }
+  RETR_DEVICE void apply8(int m, int n, float (&v)[8]) const {
+    if (vec) {
+      const auto r = rsrc();
+      const unsigned o = off(m, n);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{__builtin_bit_cast(unsigned, v[0]),
+                                                   __builtin_bit_cast(unsigned, v[1]),
+                                                   __builtin_bit_cast(unsigned, v[2]),
+                                                   __builtin_bit_cast(unsigned, v[3])},
+                                             r, o, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{__builtin_bit_cast(unsigned, v[4]),
+                                                   __builtin_bit_cast(unsigned, v[5]),
+                                                   __builtin_bit_cast(unsigned, v[6]),
+                                                   __builtin_bit_cast(unsigned, v[7])},
+                                             r, o + 16, 0, 16);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) apply(m, n + e, v[e]);
+    }
+  }
+  RETR_DEVICE void empty_split(int, int) const {}
+  RETR_DEVICE bool lane_contiguous() const { return false; }
+};
+
+constexpr int kTickets = 1 << 18;
+static __device__ int g_wgrad_tickets[kTickets];   // zero at load; every last arriver re-zeroes
+
+struct RowParJob {          // dst[c] (=|+=) sum_s parts[s * stride + c], 64 columns per block
+  const float* parts;
+  float* dst;
+  long stride;
+  int nparts, cols, accumulate, blk0;
+};
+
+struct WgradSide {
+  RowParJob job[kMaxExtra];
+  int njobs, gemm_blocks;
+};
+
+// dst rows [m0, m0 + BM) x cols [n0, n0 + BN) of problem ep: sum of the slabs in slice order
+template <int BM, int BN, int NT>
+RETR_DEVICE void slab_tile_sum(const EpiSlab& ep, int m0, int n0) {
+  const int tid = threadIdx.x;
+  const int r1 = min(ep.rows, m0 + BM), c1 = min(ep.cols, n0 + BN);
+  if (ep.vec) {
+    constexpr int Q = BN / 4;
+    for (int q = tid; q < BM * Q; q += NT) {
+      const int r = m0 + q / Q, c = n0 + 4 * (q % Q);
+      if (r >= r1 || c >= c1) continue;
+      const float* src = ep.ws + (long)r * ep.ld + c;
+      f32x4 v = *(const f32x4*)src;
+      int s = 1;
+      for (; s + 3 < ep.splits; s += 4) {
+        f32x4 t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t[u] = *(const f32x4*)(src + (long)(s + u) * ep.split_stride);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v = v + t[u];
+      }
+      for (; s < ep.splits; ++s) v = v + *(const f32x4*)(src + (long)s * ep.split_stride);
+      float* o = ep.dst + (long)r * ep.lddw + c;
+      if (ep.accumulate) {
+        const f32x4 a = *(const f32x4*)o;
+        v = a + v;
+      }
+      *(f32x4*)o = v;
+    }
+    return;
+  }
+  for (int q = tid; q < BM * BN; q += NT) {
+    const int r = m0 + q / BN, c = n0 + q % BN;
+    if (r >= r1 || c >= c1) continue;
+    const float* src = ep.ws + (long)r * ep.ld + c;
+    float v = src[0];
+    for (int s = 1; s < ep.splits; ++s) v += src[(long)s * ep.split_stride];
+    float* o = ep.dst + (long)r * ep.lddw + c;
+    *o = ep.accumulate ? *o + v : v;
+  }
+}
+
+template <int BM, int S>
+__global__ void __launch_bounds__(256)
+wgrad_fused_kernel(GGroup<DenseT<bf16>, DenseT<bf16>, EpiSlab, 2 * kMaxWgrad> g, WgradSide side) {
+  constexpr int NT = 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  if (bid >= side.gemm_blocks) {
+    // partial-row sums: four waves take every fourth partial row, 8 loads in flight, summed in
+    // wave order (slab_sum_group's rowpar arithmetic)
+    int j = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxExtra; ++i)
+      if (i < side.njobs && bid - side.gemm_blocks >= side.job[i].blk0) j = i;
+    const RowParJob& d = side.job[j];
+    float* red = (float*)smem;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = (bid - side.gemm_blocks - d.blk0) * 64 + lane;
+    float v = 0.f;
+    if (c < d.cols) {
+      const float* src = d.parts + c;
+      int s = w;
+      for (; s + 28 < d.nparts; s += 32) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = src[(long)(s + 4 * u) * d.stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += t[u];
+      }
+      for (; s < d.nparts; s += 4) v += src[(long)s * d.stride];
+    }
+    red[w * 64 + lane] = v;
+    __syncthreads();
+    if (w == 0 && c < d.cols) {
+      const float t = ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+      d.dst[c] = d.accumulate ? d.dst[c] + t : t;
+    }
+    return;
+  }
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < 2 * kMaxWgrad; ++i)
+    if (i < g.n && bid >= g.p[i].blk0) p = i;
+  const auto& d = g.p[p];
+  const int local = bid - d.blk0;
+  if (local >= d.nblk) return;
+  const int split = local / d.tiles, tile = local - split * d.tiles;
+  EpiSlab ep = d.ep;
+  ep.split = split;
+  gemm2_tile<kFamLinearWgrad, BM, BM, 2, 2, S, 0>(d.la, d.lb, ep, d.M, d.N, d.K, d.kchunk,
+                                                  d.tiles_n, tile, split);
+  // publish this slice's slab (every storing wave drains its write-through stores, then the
+  // barrier), draw the tile's ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = (int*)smem;
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(ep.tickets + tile, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == ep.splits - 1;
+    if (last) {
+      // re-arm the counter for the next launch (a memory-side atomic, like the adds)
+      __hip_atomic_exchange(ep.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  const int m0 = (tile / d.tiles_n) * BM, n0 = (tile % d.tiles_n) * BM;
+  slab_tile_sum<BM, BM, NT>(ep, m0, n0);
+}
+
+int g_ticket_cursor = 0;
+
+int* take_tickets(int n) {
+  static int* base = nullptr;
+  if (!base) {
+    void* a = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_wgrad_tickets)) != hipSuccess) return nullptr;
+    base = (int*)a;
+  }
+  if (n > kTickets) return nullptr;
+  if (g_ticket_cursor + n > kTickets) g_ticket_cursor = 0;
+  int* p = base + g_ticket_cursor;
+  g_ticket_cursor += (n + 63) / 64 * 64;
+  return p;
+}
+
+template <int BM, int S>
+int wgrad_fused_launch(const WPlan& p, const retr_linear_wgrad_desc* d, float* ws, int nx,
+                       const retr_slab_sum_desc* x, hipStream_t st) {
+  using L = DenseT<bf16>;
+  Group2<kFamLinearWgrad, BM, BM, 2, 2, S, 0, L, L, EpiSlab, 2 * kMaxWgrad> g;
+  const bf16* ones = ones_ptr();
+  RETR_REQUIRE(ones != nullptr, "linear_wgrad_group: ones vector unavailable");
+  for (int j = 0; j < p.n; ++j) {
+    const retr_linear_wgrad_desc& q = d[p.src[j]];
+    L la{(const bf16*)q.dy, q.lddy, q.N, q.M};
+    const int cols = p.bias[j] ? 1 : q.K;
+    L lb = p.bias[j] ? L{ones, 0, 1, q.M} : L{(const bf16*)q.x, q.ldx, q.K, q.M};
+    EpiSlab ep{};
+    ep.ws = ws + p.ws_off[j];
+    ep.ld = cols;
+    ep.split_stride = (long)q.N * cols;
+    ep.dst = p.bias[j] ? q.db : q.dw;
+    ep.lddw = p.bias[j] ? 1 : q.lddw;
+    ep.rows = q.N;
+    ep.cols = cols;
+    ep.splits = p.splits[j];
+    ep.accumulate = q.accumulate;
+    ep.vec = cols % 8 == 0 && ((uintptr_t)ep.ws & 15) == 0 && ep.lddw % 4 == 0 &&
+             ((uintptr_t)ep.dst & 15) == 0 && ep.split_stride % 4 == 0;
+    if (g.add(la, lb, ep, q.N, cols, q.M, p.splits[j])) return 1;
+    auto& pr = g.g.p[g.g.n - 1];
+    pr.ep.tickets = take_tickets(pr.tiles);
+    RETR_REQUIRE(pr.ep.tickets != nullptr, "linear_wgrad_group: ticket array unavailable");
+  }
+  WgradSide side{};
+  side.gemm_blocks = g.blocks;
+  int extra = 0;
+  for (int i = 0; i < nx; ++i) {
+    const retr_slab_sum_desc& q = x[i];
+    if (!q.dst || q.nparts <= 0 || q.cols <= 0) continue;
+    RowParJob& r = side.job[side.njobs++];
+    r.parts = q.parts;
+    r.dst = q.dst;
+    r.stride = q.stride;
+    r.nparts = q.nparts;
+    r.cols = q.cols;
+    r.accumulate = q.accumulate;
+    r.blk0 = extra;
+    extra += (int)cdiv(q.cols, 64);
+  }
+  const int blocks = g.blocks + extra;
+  if (blocks == 0) return 0;
+  constexpr size_t lds = gemm2_lds_bytes<BM, BM, S, 0>();
+  auto kern = wgrad_fused_kernel<BM, S>;
+  if constexpr (lds > 65536) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds, st, g.g, side);
+  return retr_check_launch("linear_wgrad_fused");
+}
+
 }  // namespace
 
 extern "C" {
@@ -387,6 +648,19 @@ int retr_linear_wgrad_group2(int dtype, int n, const retr_linear_wgrad_desc* d, 
                        d[i].lddy % 8 == 0 && d[i].ldx % 8 == 0 && d[i].lddy >= (d[i].N + 7) / 8 * 8,
                    "linear_wgrad_group[%d]: bad shape M=%d N=%d K=%d", i, d[i].M, d[i].N, d[i].K);
     const WPlan p = wgrad_plan(n, d);
+    if (retr_tune_get(RETR_TUNE_WGRAD_FUSED) == 1) {
+      // split-K reduction by each tile's last-arriving block, partial rows as side blocks: one
+      // launch, no slab_sum_group -- bitwise equal, but 0.31 ms per step SLOWER in the graphed
+      // cfg2 step (profiles/r4_ab_wgrad_lastarriver.txt: the last arriver's serial read of
+      // 8-16 slabs is the launch's tail), so not the default
+      RETR_REQUIRE(p.n == 0 || workspace != nullptr, "linear_wgrad_group: workspace required");
+      float* ws = (float*)workspace;
+      if (p.tile == 128) return p.stages == 3 ? wgrad_fused_launch<128, 3>(p, d, ws, nx, x, st)
+                                              : wgrad_fused_launch<128, 2>(p, d, ws, nx, x, st);
+      return p.stages == 4 ? wgrad_fused_launch<64, 4>(p, d, ws, nx, x, st)
+           : p.stages == 1 ? wgrad_fused_launch<64, 1>(p, d, ws, nx, x, st)
+                           : wgrad_fused_launch<64, 2>(p, d, ws, nx, x, st);
+    }
     if (p.n > 0) {
       RETR_REQUIRE(workspace != nullptr, "linear_wgrad_group: workspace required");
       float* ws = (float*)workspace;

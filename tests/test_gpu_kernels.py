@@ -1136,3 +1136,59 @@ def test_pos_grad_rows_in_order(dt, M, C, period):
          ops._st())
     torch.cuda.synchronize()
     assert np.array_equal(dset.cpu().numpy(), np.float32(0) + s)
+
+
+@pytest.mark.parametrize("case", ["ffn6400", "attn2048", "ragged"])
+def test_wgrad_group_last_arriver_equals_slab_sum(case):
+    """Grouped bf16 weight + bias gradients with the split-K reduction done by each output
+    tile's last-arriving block inside the GEMM launch (RETR_TUNE_WGRAD_FUSED 1) against slabs +
+    the separate slab_sum_group launch (knob 0, the default): bitwise equal (both add the slices in
+    slice order), with the LayerNorm-style partial rows summed by the same launch's side
+    blocks; repeated launches (tickets re-armed by the last arriver) stay bitwise identical."""
+    from retr_amd import _lib
+    shapes = {"ffn6400": [(6400, 256, 2048), (6400, 2048, 256)],
+              "attn2048": [(2048, 256, 256), (2048, 512, 256), (6400, 256, 256),
+                           (6400, 256, 256)],
+              "ragged": [(1000, 200, 136), (777, 72, 64)]}[case]
+    g = torch.Generator(device="cpu").manual_seed(len(case))
+    items = []
+    for i, (M, N, K) in enumerate(shapes):
+        dy = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+        x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+        items.append([dy, x, M, N, K, i % 2 == 0])
+    nparts, C = 37, 256
+    parts = torch.randn(nparts * 2 * C, generator=g).to(DEV)
+    outs = []
+    try:
+        for knob in (0, 1, 1, 1):
+            _lib.load().retr_tune(17, knob)
+            for acc in (False, True):
+                run = []
+                for dy, x, M, N, K, has_b in items:
+                    dw = torch.randn(N, K, generator=torch.Generator().manual_seed(N + K)).to(DEV)
+                    db = torch.randn(N, generator=torch.Generator().manual_seed(N)).to(DEV) \
+                        if has_b else None
+                    run.append((dy, x, dw, db, acc))
+                gam = torch.randn(C, generator=torch.Generator().manual_seed(1)).to(DEV)
+                bet = torch.randn(C, generator=torch.Generator().manual_seed(2)).to(DEV)
+                extra = [(parts, 2 * C, nparts, C, gam, acc),
+                         (parts[C:], 2 * C, nparts, C, bet, acc)]
+                ops.k_linear_wgrad_group(run, extra)
+                torch.cuda.synchronize()
+                outs.append([t.clone() for it in run for t in it[2:4] if t is not None] +
+                            [gam.clone(), bet.clone()])
+    finally:
+        _lib.load().retr_tune(17, 0)
+    n = 2
+    for k in range(1, 4):
+        for a in range(n):
+            ref, got = outs[a], outs[k * n + a]
+            for r, t in zip(ref, got):
+                assert torch.equal(r, t), (case, k, a)
+    # and against fp32 torch (overwrite mode: dW = dY^T X, db = colsum dY; the LN rows)
+    dy, x = items[0][0], items[0][1]
+    assert rel_err(outs[2][0], dy.float().t() @ x.float()) < 1e-2
+    assert rel_err(outs[2][1], dy.float().sum(0)) < 1e-2
+    p2 = parts.view(nparts, 2, C)
+    assert rel_err(outs[2][-2], p2[:, 0].sum(0)) < 1e-5
+    assert rel_err(outs[2][-1], p2[:, 1].sum(0)) < 1e-5

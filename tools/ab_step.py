@@ -53,6 +53,9 @@ VARIANTS = {
     "wthr100k": {("TUNE", 2): 100000},
     "wthr120k": {("TUNE", 2): 120000},
     "wthr400k": {("TUNE", 2): 400000},
+    "wgrad_fused": {("TUNE", 17): 1},
+    "wkc2048": {("TUNE", 4): 2048},
+    "wkc3200": {("TUNE", 4): 3200},
 }
 
 
@@ -66,7 +69,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 2, 3, 4, 7, 9, 15, 16):
+    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"

@@ -37,6 +37,12 @@ def main():
                                      ptr(y), N, 0, M, N, K, 0, None, 0, 0.0, 0, ptr(ws), s,
                                      stream()))
             line += f" | retr split{s} {ts:7.1f} us {2 * M * N * K / ts / 1e6:5.0f} TF"
+        for v in [int(t) for t in os.environ.get("RETR_VARIANTS", "").split(",") if t]:
+            load().retr_tune(6, v)           # RETR_TUNE_BIG_TILE: launch_big tile override
+            tv = timeit(lambda: call("retr_linear_fwd", 1, ptr(x), K, ptr(w), K, None, ptr(y),
+                                     N, 0, M, N, K, 0, None, 0, 0.0, 0, stream()))
+            load().retr_tune(6, 0)
+            line += f" | t{v} {tv:7.1f} us {2 * M * N * K / tv / 1e6:5.0f} TF"
         print(line, flush=True)
 
 

@@ -123,7 +123,9 @@ def main():
         VARIANTS = [(int(t), 0) for t in os.environ["RETR_VARIANTS"].split(",")]
     if only == "r50":
         shapes = r50_shapes()
-        VARIANTS = [(0, 0), (13, 0), (14, 0)] if os.environ.get("RETR_SWEEP_S1") else [(0, 0), (4, 0), (6, 0)]
+        if not os.environ.get("RETR_VARIANTS"):
+            VARIANTS = ([(0, 0), (13, 0), (14, 0)] if os.environ.get("RETR_SWEEP_S1")
+                        else [(0, 0), (4, 0), (6, 0)])
     if only == "wtile":   # every cfg2 weight-gradient conv, 128x128 vs 64x64 tile
         shapes = sorted({("wgrad",) + t[1:9] + (0,) for t in r50_shapes() if t[0] == "dgrad"},
                         key=lambda t: (-t[2], t[4], t[5]))
