@@ -177,6 +177,23 @@ typedef struct {
 int retr_linear_wgrad_group2(int dtype, int n, const retr_linear_wgrad_desc* d, void* workspace,
                              int nx, const retr_slab_sum_desc* x, void* stream);
 
+/* ---- fused feed-forward block (models/transformer_modules.py:6-11,77-97 feed_forward inside
+ * FFResidual; replaces the linear_fwd (ReLU) + linear_fwd_splitk pair of the forward and the
+ * linear_dgrad (ReLU gate) + linear_dgrad_splitk pair of the backward at d_model 256, bf16):
+ *   retr_ffn_fwd       h = relu(n W1^T + b1) -> h [M][F] bf16;  y = res + drop(h W2^T + b2) fp32
+ *   retr_ffn_bwd_data  dh = [h > 0] (dbr W2) -> dh [M][F] bf16;  dn = dh W1 -> dn [M][C] bf16
+ * W1 [F][C], W2 [C][F] row-major bf16 (the backward reads them transposed in LDS).  ws: fp32
+ * [splits][M][C] slabs; splits from retr_ffn_splits(M, C, F) (0 = shape not supported: C must
+ * be 256, F a multiple of 64). */
+int retr_ffn_splits(int M, int C, int F);
+int retr_ffn_fwd(const void* n, long ldn, const void* w1, const float* b1, const void* w2,
+                 const float* b2, void* h, long ldh, const float* residual, long ldr, float* y,
+                 long ldy, int M, int C, int F, float drop_p, unsigned long long seed, float* ws,
+                 int splits, void* stream);
+int retr_ffn_bwd_data(const void* dbr, long lddbr, const void* w2, const void* h, long ldh,
+                      const void* w1, void* dh, long lddh, void* dn, long lddn, int M, int C,
+                      int F, float* ws, int splits, void* stream);
+
 /* ---- ResNet convolutions (torchvision conv stack via models/backbone.py:65-69, FrozenBN
  * models/backbone.py:41-51 folded into the weights) --------------------------------------- */
 int retr_conv_pack(int dtype, const float* w, const float* bn_w, const float* bn_b,

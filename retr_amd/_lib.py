@@ -86,6 +86,10 @@ _SIGS = {
                           _P],
     "retr_transpose_cast": [_I, _P, _P, _I, _I, _I, _P],
     "retr_linear_splits": [_I, _I, _I, _I],
+    "retr_ffn_splits": [_I, _I, _I],
+    "retr_ffn_fwd": [_P, _L, _P, _P, _P, _P, _P, _L, _P, _L, _P, _L, _I, _I, _I, _F, _U64, _P,
+                     _I, _P],
+    "retr_ffn_bwd_data": [_P, _L, _P, _P, _L, _P, _P, _L, _P, _L, _I, _I, _I, _P, _I, _P],
     "retr_linear_fwd_splitk": [_I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _I, _P, _L, _F,
                                _U64, _P, _I, _P],
     "retr_linear_dgrad_splitk": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _L, _P, _L,

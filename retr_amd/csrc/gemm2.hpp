@@ -78,7 +78,10 @@ struct GStager {
   static constexpr int CPR = ROWS / 8;          // 16-byte slots per k-row of the k-major image
   static constexpr int NCH = ROWS * 8 / NT;     // chunks per thread per tile
   static_assert(NCH >= 1 && (ROWS * 8) % NT == 0, "tile too small for the block");
-  static_assert(L::kContig || ((8 * NT / ROWS) % 16 == 0 && NT % CPR == 0),
+  // (uniform-K loaders keep one row context per chunk, so each chunk may take its own swizzle
+  // column; the per-chunk-cursor form needs one column for all of a thread's k rows)
+  static_assert(L::kContig || (NT % CPR == 0 &&
+                               (uniform_k<L>::value || (8 * NT / ROWS) % 16 == 0)),
                 "k-major image: thread's k rows must share one swizzle phase");
   static constexpr bool kU = uniform_k<L>::value;
   typename L::Ctx ctx[(L::kContig || kU) ? NCH : 1];
@@ -100,14 +103,19 @@ struct GStager {
     } else {
       // linear slot (k = tid/CPR + (NT/CPR) i, slot tid%CPR) holds row-chunk slot ^ (f(k)/2)
       const int k0 = tid / CPR, slot = tid % CPR;
-      int f;
-      if constexpr (ROWS >= 128) f = 4 * ((k0 & 3) | (((k0 >> 3) & 1) << 2));
-      else f = 4 * (((k0 >> 1) & 1) | (((k0 >> 3) & 1) << 1));
-      const int c = slot ^ (f >> 1);
+      auto phase = [](int k) {
+        if constexpr (ROWS >= 128) return 4 * ((k & 3) | (((k >> 3) & 1) << 2));
+        else return 4 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+      };
+      const int c = slot ^ (phase(k0) >> 1);
       if constexpr (uniform_k<L>::value) {
-        // one row context per k row of the thread (its k offset baked in), one block cursor
+        // one row context per k row of the thread (its k offset and swizzle column baked in),
+        // one block cursor
 #pragma unroll
-        for (int i = 0; i < NCH; ++i) ctx[i] = l.row_ctx_c(row0 + c * EPC, k0 + (NT / CPR) * i);
+        for (int i = 0; i < NCH; ++i) {
+          const int k = k0 + (NT / CPR) * i;
+          ctx[i] = l.row_ctx_c(row0 + (slot ^ (phase(k) >> 1)) * EPC, k);
+        }
         kc[0] = l.kcur(kb);
       } else {
         ctx[0] = l.row_ctx(row0 + c * EPC);

@@ -853,6 +853,25 @@ class _CrossAttnBlock(torch.autograd.Function):
                 dmem if l_m else None, dw_in, db_in, dw_out, db_out) + (None,) * 9
 
 
+# bf16 FFN blocks at d_model 256 as one fused launch per direction (csrc/ffn.hip: the hidden
+# activation chunk goes from the first GEMM's accumulators into the second GEMM's LDS operand;
+# same bits as the two-launch path).  Off by default: measured slower than linear_fwd +
+# linear_fwd_splitk (profiles/r4_ffn_fused.txt: one 4-wave block per CU, 10 % MFMA busy)
+FUSE_FFN = False
+_FFN_SPLITS = {}
+
+
+def _ffn_splits(M, C, F, cdtype):
+    """F-split of the fused FFN kernels, 0 where the shape / dtype runs the unfused path."""
+    if cdtype != torch.bfloat16 or not FUSE_FFN:
+        return 0
+    key = (M, C, F)
+    s = _FFN_SPLITS.get(key)
+    if s is None:
+        s = _FFN_SPLITS[key] = int(_lib.load().retr_ffn_splits(M, C, F))
+    return s
+
+
 class _FFNBlock(torch.autograd.Function):
     """x_new = x + drop(W2 relu(W1 LN(x) + b1) + b2)  — FFResidual(feed_forward)
     (models/transformer_modules.py:6-11, 77-97) with its pre-norm inside the Function."""
@@ -867,10 +886,20 @@ class _FFNBlock(torch.autograd.Function):
         dev = n.device
         w1c, w2c = WEIGHTS.get(w1, cdtype), WEIGHTS.get(w2, cdtype)
         h = torch.empty(M, F, dtype=cdtype, device=dev)
-        k_linear_fwd(n, w1c, b1.detach(), h, relu=1)
         out = torch.empty(M, C, dtype=torch.float32, device=dev)
-        seed = next_seed()
-        k_linear_fwd(h, w2c, b2.detach(), out, res=res, drop_p=drop_res, seed=seed)
+        splits = _ffn_splits(M, C, F, cdtype)
+        if splits:
+            seed = next_seed()
+            ws = torch.empty(splits, M, C, dtype=torch.float32, device=dev)
+            b1d, b2d = b1.detach().contiguous(), b2.detach().contiguous()
+            call("retr_ffn_fwd", ptr(n), n.stride(0), ptr(w1c), ptr(b1d), ptr(w2c), ptr(b2d),
+                 ptr(h), h.stride(0), ptr(res), res.stride(0), ptr(out), out.stride(0), M, C, F,
+                 drop_res, seed, ptr(ws), splits, _st())
+        else:
+            k_linear_fwd(n, w1c, b1.detach(), h, relu=1)
+            seed = next_seed()
+            k_linear_fwd(h, w2c, b2.detach(), out, res=res, drop_p=drop_res, seed=seed)
+        ctx.splits = splits
         ctx.save_for_backward(n, h, w1, w2, x, ln_w, mean, rstd)
         ctx.gparams = (w1, b1, w2, b2)
         ctx.ln_b = ln_b
@@ -895,9 +924,17 @@ class _FFNBlock(torch.autograd.Function):
             k_dropout_apply(dout, dbr, drop_res, seed)
         (dw1, _), (db1, _), (dw2, _), (db2, _) = map(grad_buffer, ctx.gparams)
         dh = torch.empty(M, F, dtype=cdtype, device=dev)
-        k_linear_dgrad(dbr, w2t, dh, gate=h)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
-        k_linear_dgrad(dh, w1t, dn)
+        if ctx.splits:
+            # one fused launch: dh = [h > 0] dbr W2 (written for the weight gradients), dn = dh W1
+            w1c, w2c = WEIGHTS.get(w1, cdtype), WEIGHTS.get(w2, cdtype)
+            ws = torch.empty(ctx.splits, M, C, dtype=torch.float32, device=dev)
+            call("retr_ffn_bwd_data", ptr(dbr), dbr.stride(0), ptr(w2c), ptr(h), h.stride(0),
+                 ptr(w1c), ptr(dh), dh.stride(0), ptr(dn), dn.stride(0), M, C, F, ptr(ws),
+                 ctx.splits, _st())
+        else:
+            k_linear_dgrad(dbr, w2t, dh, gate=h)
+            k_linear_dgrad(dh, w1t, dn)
         wg = [(dbr, h, dw2, db2, True), (dh, n, dw1, db1, True)]
         if fused:
             dx, dlw, dlb, _, extra = _ln_bwd_fused(x, ln_w, ctx.ln_b, mean, rstd, dn, None, dout,

@@ -1192,3 +1192,51 @@ def test_wgrad_group_last_arriver_equals_slab_sum(case):
     p2 = parts.view(nparts, 2, C)
     assert rel_err(outs[2][-2], p2[:, 0].sum(0)) < 1e-5
     assert rel_err(outs[2][-1], p2[:, 1].sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("M", [6400, 2048, 1000])
+def test_fused_ffn_equals_two_launch_path(M):
+    """The fused FFN kernels (csrc/ffn.hip: retr_ffn_fwd / retr_ffn_bwd_data, the hidden chunk
+    passed from the first GEMM's accumulators to the second GEMM's LDS operand) against the
+    unfused launches (linear_fwd ReLU + linear_fwd_splitk, linear_dgrad gate + linear_dgrad_splitk)
+    for a bf16 FFResidual block at d_model 256, F 2048, residual dropout 0.1: output, saved
+    hidden activation and every gradient bitwise equal (same products, same order, the same
+    F-split); and within bf16 rounding of an fp32 torch restatement
+    (models/transformer_modules.py:6-11,77-97)."""
+    from retr_amd.models.transformer_modules import FFResidual, feed_forward
+    torch.manual_seed(M)
+    mod = FFResidual(feed_forward(256, 2048), 256, dropout=0.1).to(DEV)
+    with torch.no_grad():
+        for p in mod.parameters():
+            p.add_(torch.randn_like(p) * 0.02)
+    x0 = torch.randn(M, 256, device=DEV)
+    w_out = torch.randn(M, 256, device=DEV)
+    res = []
+    try:
+        for fused in (False, True):
+            ops.FUSE_FFN = fused
+            ops._seed_state["ctr"] = 777
+            mod.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            y = ops.ffn_block(mod, x, True, torch.bfloat16)
+            (y * w_out).sum().backward()
+            torch.cuda.synchronize()
+            res.append((y.detach().clone(), x.grad.clone(),
+                        {n: p.grad.clone() for n, p in mod.named_parameters()}))
+    finally:
+        ops.FUSE_FFN = False
+    (y0, dx0, g0), (y1, dx1, g1) = res
+    assert torch.equal(y0, y1)
+    assert torch.equal(dx0, dx1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
+    # fp32 restatement without dropout (eval) for scale
+    ops.FUSE_FFN = True
+    try:
+        ye = ops.ffn_block(mod, x0, False, torch.bfloat16).float()
+    finally:
+        ops.FUSE_FFN = False
+    ln = torch.nn.functional.layer_norm(x0, (256,), mod.norm.weight, mod.norm.bias, 1e-5)
+    l1, l2 = mod.sublayer[0], mod.sublayer[2]
+    ref = x0 + l2(torch.relu(l1(ln)))
+    assert rel_err(ye - x0, ref - x0) < 2e-2

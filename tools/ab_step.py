@@ -54,6 +54,7 @@ VARIANTS = {
     "wthr120k": {("TUNE", 2): 120000},
     "wthr400k": {("TUNE", 2): 400000},
     "wgrad_fused": {("TUNE", 17): 1},
+    "ffn_fused": {("ATTR", "FUSE_FFN"): True},
     "wkc2048": {("TUNE", 4): 2048},
     "wkc3200": {("TUNE", 4): 3200},
 }
@@ -65,6 +66,7 @@ def apply(v):
     ops.FUSE_LN_PARAMS = True
     ops.ATTN_DMASK = True
     ops.FUSED_CE = True
+    ops.FUSE_FFN = False
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
