@@ -61,7 +61,10 @@ def main():
             rows.append([(t[i] - t[0]) * 10 for i in range(11)])
         print(f"== {name} (ns since first instruction of wave 0, block 0; last 3 reps)")
         for i, n in enumerate(NAMES):
-            print(f"  {n:14s} " + " ".join(f"{r[i]:7d}" for r in rows[-3:]))
+            # the cross-attention case has no next-layer q projection: its last three stamps are
+            # never written (stale values from the previous case read negative)
+            print(f"  {n:14s} " + " ".join(f"{r[i]:7d}" if r[i] >= 0 else "    n/a"
+                                           for r in rows[-3:]))
 
 
 if __name__ == "__main__":

@@ -6,10 +6,35 @@ step), takes one step window (default: the 7th) and prints (a) per-kernel totals
 
     python tools/prof_step.py gpurun_out/prof/run_results.db [--step N]
 """
+import os
 import re
 import sqlite3
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from retr_amd.probe import family_of_symbol  # noqa: E402
+
+# kernels outside the roofline families, by name fragment (first match wins)
+CATEGORIES = [("slab_sum_group", "linear wgrad slab sums"),
+              ("slab_epilogue", "split-K slab epilogues"),
+              ("wgrad_unpack", "conv wgrad slab sums + OIHW"),
+              ("adamw", "clip + AdamW"), ("ln_", "LayerNorm"), ("embed", "embeddings"),
+              ("ce_", "cross-entropy"), ("pos_grad", "position gradients"),
+              ("conv_pack", "conv weight packing"), ("cat_rows", "conv weight packing"),
+              ("dropout", "dropout"), ("phase_fill", "dgrad phase fill"),
+              ("nchw_to", "input layout"), ("mask", "masks"), ("seed", "dropout seed"),
+              ("fill", "fills / copies"), ("copy", "fills / copies"), ("cast", "casts")]
+
+
+def category(name):
+    f = family_of_symbol(name)
+    if f:
+        return f
+    for frag, cat in CATEGORIES:
+        if frag in name:
+            return cat
+    return "other"
 
 
 def main():
@@ -25,6 +50,14 @@ def main():
     span = (w[-1][2] - w[0][1]) / 1e6
     busy = sum(r[2] - r[1] for r in w) / 1e6
     print(f"step window {step}: {len(w)} dispatches, span {span:.3f} ms, kernel busy {busy:.3f} ms")
+    cat = defaultdict(lambda: [0, 0.0])
+    for r in w:
+        c = category(r[0])
+        cat[c][0] += 1
+        cat[c][1] += (r[2] - r[1]) / 1e3
+    print(f"\n{'category':32s} {'calls':>5} {'ms':>7} {'share':>6}")
+    for c, (n, us) in sorted(cat.items(), key=lambda kv: -kv[1][1]):
+        print(f"{c:32s} {n:5d} {us / 1e3:7.3f} {us / 1e3 / busy:6.1%}")
     agg = defaultdict(lambda: [0, 0.0])
     for r in w:
         k = re.sub(r"^_ZN\d*", "", r[0])[:110]
@@ -35,9 +68,9 @@ def main():
         print(f"{n:5d} {us:9.1f}  {k}")
     g = defaultdict(lambda: [0, 0.0])
     for r in w:
-        if "gemm_kernel" not in r[0]:
+        if "gemm" not in r[0]:
             continue
-        key = (r[0][20:120], r[3] // r[6], r[4], r[5])
+        key = (re.sub(r"^_ZN\d*", "", r[0])[:100], r[3] // r[6], r[4], r[5])
         g[key][0] += 1
         g[key][1] += (r[2] - r[1]) / 1e3
     print(f"\nGEMM launches by instantiation and grid (blocks x splits):")
