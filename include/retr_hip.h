@@ -176,6 +176,18 @@ typedef struct {
 } retr_slab_sum_desc;
 int retr_linear_wgrad_group2(int dtype, int n, const retr_linear_wgrad_desc* d, void* workspace,
                              int nx, const retr_slab_sum_desc* x, void* stream);
+/* Deferred weight-gradient batch (bf16): the weight gradients of many blocks -- e.g. every
+ * projection of a whole transformer backward, models/transformer_modules.py:22-97 via
+ * torch/nn/functional.py:5785-5850 -- in ONE launch, one K-slice per tile (no fp32 slabs, no
+ * slab-sum launch); db[N] (=|+=) colsum dy rides along in the first column tile; the nx extra
+ * partial-row sums (LayerNorm dgamma / dbeta) are summed by extra blocks of the same launch.
+ * Every output element is one fp32 chain over all M tokens in order, whatever the batch.
+ * table: device memory of retr_linear_wgrad_batch_table_bytes(n, nx) bytes (16-byte aligned),
+ * written in stream order by this call; keep it alive until the launch has run. */
+size_t retr_linear_wgrad_batch_table_bytes(int n, int nx);
+int retr_linear_wgrad_batch(int n, const retr_linear_wgrad_desc* d, int nx,
+                            const retr_slab_sum_desc* x, void* table, size_t table_bytes,
+                            void* stream);
 
 /* ---- fused feed-forward block (models/transformer_modules.py:6-11,77-97 feed_forward inside
  * FFResidual; replaces the linear_fwd (ReLU) + linear_fwd_splitk pair of the forward and the

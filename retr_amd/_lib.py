@@ -101,6 +101,8 @@ _SIGS = {
     "retr_linear_wgrad_group_workspace": [_I, _PWD],
     "retr_linear_wgrad_group": [_I, _I, _PWD, _P, _P],
     "retr_linear_wgrad_group2": [_I, _I, _PWD, _P, _I, ctypes.POINTER(SlabSumDesc), _P],
+    "retr_linear_wgrad_batch_table_bytes": [_I, _I],
+    "retr_linear_wgrad_batch": [_I, _PWD, _I, ctypes.POINTER(SlabSumDesc), _P, _SZ, _P],
     "retr_conv_pack": [_I, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P],
     "retr_conv_pack_group": [_I, _I, ctypes.POINTER(ConvPackDesc), _P],
     "retr_cat_rows_group": [_I, ctypes.POINTER(CatRowsDesc), _P],
@@ -178,7 +180,7 @@ _SIGS = {
 _RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
             "retr_attention_dropout_mask_bytes": _SZ,
             "retr_layernorm_bwd_workspace": _SZ, "retr_embed_ln_bwd_workspace": _SZ,
-            "retr_linear_wgrad_group_workspace": _SZ, "retr_argmax_workspace": _SZ,
+            "retr_linear_wgrad_group_workspace": _SZ, "retr_linear_wgrad_batch_table_bytes": _SZ, "retr_argmax_workspace": _SZ,
             "retr_set_deterministic": None,
             "retr_set_seed_base": None}
 

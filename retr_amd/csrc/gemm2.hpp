@@ -170,6 +170,17 @@ RETR_DEVICE int xcd_remap(int bid, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
+// Epilogues with kOnesBias = true also want the row sums of A over the tile's K range (the
+// bias gradient colsum(dY) of a weight-gradient GEMM): the waves of the first column tile
+// (wn == 0, when ep.bias_here(tile column)) run one more MFMA per A fragment against a
+// constant all-ones B fragment and hand the sums to ep.bias_apply(row, sum) -- no ones-vector
+// GEMM problem, no extra operand traffic.
+template <class E, class = void>
+struct has_ones_bias : std::false_type {};
+template <class E>
+struct has_ones_bias<E, std::void_t<decltype(E::kOnesBias)>>
+    : std::integral_constant<bool, E::kOnesBias> {};
+
 // One BM x BN output tile (index `tile` in row-major tile order), K range
 // [split * kchunk, (split + 1) * kchunk).
 template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB, class LA, class LB, class EP>
@@ -183,6 +194,7 @@ RETR_DEVICE __attribute__((always_inline)) void gemm2_tile(const LA& la, const L
   constexpr int WTM = BM / WM, WTN = BN / WN;   // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int kStage = (BM + BN) * kBKBytes;
+  constexpr bool kBias = has_ones_bias<EP>::value;
   using SA = GStager<BM, NT, LA>;
   using SB = GStager<BN, NT, LB>;
   constexpr int LPT = SA::NCH + SB::NCH;        // DMA instructions per wave per tile
@@ -195,6 +207,8 @@ RETR_DEVICE __attribute__((always_inline)) void gemm2_tile(const LA& la, const L
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+  bool bias_wave = false;
+  if constexpr (kBias) bias_wave = wn == 0 && ep.bias_here(tile % tiles_n);
   const int kb = split * kchunk;
   const int ke = min(K, kb + kchunk);
   if (kb >= ke && K > 0) {
@@ -213,6 +227,11 @@ RETR_DEVICE __attribute__((always_inline)) void gemm2_tile(const LA& la, const L
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[kBias ? TM : 1];
+#pragma unroll
+  for (int i = 0; i < (kBias ? TM : 1); ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr unsigned kOne2 = 0x3F803F80u;       // two bf16 1.0
+  const u32x4 ones{kOne2, kOne2, kOne2, kOne2};
 
 #pragma unroll
   for (int s = 0; s < S - 1; ++s) {
@@ -253,8 +272,28 @@ RETR_DEVICE __attribute__((always_inline)) void gemm2_tile(const LA& la, const L
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) mfma_step<T>(acc[i][j], af[i], bfr[j]);
+      if constexpr (kBias) {
+        if (bias_wave) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) mfma_step<T>(accb[i], af[i], ones);
+        }
+      }
     }
   }
+  if constexpr (kBias) {
+    // D = A * ones: every column of the 16x16 block holds the row sums; lanes 0/16/32/48 own
+    // column 0 of rows 4 (lane / 16) + e
+    if (bias_wave && (lane & 15) == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wm * WTM + 16 * i + 4 * (lane >> 4) + e;
+          if (m < M) ep.bias_apply(m, accb[i][e]);
+        }
+    }
+  }
+  (void)ones;
   __syncthreads();
 
   // ---- epilogue through LDS (see gemm.hpp), in EP_PASSES row bands when the fp32 tile does

@@ -12,6 +12,9 @@
 // fp32 slabs written with plain stores; the bias gradient is one more GEMM problem against a
 // ones vector (dY^T 1); a second launch adds every problem's slabs in slice order into dW / db.
 // Deterministic by construction, no float atomics.
+#include <cstring>
+#include <vector>
+
 #include "gemm2.hpp"
 #include "epilogues.hpp"
 #include "../../include/retr_hip.h"
@@ -560,6 +563,143 @@ int wgrad_fused_launch(const WPlan& p, const retr_linear_wgrad_desc* d, float* w
   return retr_check_launch("linear_wgrad_fused");
 }
 
+// ---- deferred weight-gradient batch (retr_linear_wgrad_batch) -------------------------------
+// The weight gradients of many blocks (a whole transformer backward) in ONE launch, one K-slice
+// per tile: with ~1000 128x128 tiles there is no reason to split the token reduction, so there
+// are no fp32 slabs and no slab-sum launch.  The bias gradients ride along as one extra MFMA
+// per A fragment against an all-ones fragment in the first column tile (gemm2.hpp
+// has_ones_bias); the LayerNorm dgamma / dbeta partial rows are summed by extra blocks.  The
+// problem table lives in device memory (written by table_put_kernel launches in stream order),
+// so the problem count is not bounded by the kernel-argument size.  Each output element is one
+// fp32 MFMA chain over all tokens in order: the bits do not depend on how problems are batched.
+struct EpiWB : EpiAccF32 {
+  float* db;
+  int bias_on;
+  static constexpr bool kOnesBias = true;
+  RETR_DEVICE bool bias_here(int tile_col) const { return bias_on && tile_col == 0; }
+  RETR_DEVICE void bias_apply(int m, float v) const { db[m] = overwrite ? v : db[m] + v; }
+};
+
+struct WBProb {               // dW[N][K] (=|+=) dY[M][N]^T X[M][K], db[N] (=|+=) colsum dY
+  const bf16* dy;
+  const bf16* x;
+  float* dw;
+  float* db;                  // or null
+  int lddy, ldx, lddw, M, N, K, blk0, flags;   // flags: accumulate | vec << 1 | tiles_n << 2
+};
+struct WBRow {                // dst[c] (=|+=) sum_s parts[s * stride + c]
+  const float* parts;
+  float* dst;
+  int stride, nparts, cols, accumulate, blk0, pad;
+};
+struct WBHead {
+  int nprob, nrow, gemm_blocks, total;
+};
+static_assert(sizeof(WBProb) == 64 && sizeof(WBRow) == 40 && sizeof(WBHead) == 16, "table");
+
+constexpr int kWBChunk = 4;   // consecutive logical blocks per XCD turn
+
+size_t wb_table_bytes(int n, int nx) {
+  return sizeof(WBHead) + (size_t)n * sizeof(WBProb) + (size_t)nx * sizeof(WBRow);
+}
+
+template <int BM, int S>
+__global__ void __launch_bounds__(256) wgrad_batch_kernel(const char* __restrict__ table) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const WBHead h = *(const WBHead*)table;
+  const WBProb* P = (const WBProb*)(table + sizeof(WBHead));
+  const WBRow* R = (const WBRow*)(table + sizeof(WBHead) + (size_t)h.nprob * sizeof(WBProb));
+  // hardware block b runs on XCD b % 8: logical blocks go out in kWBChunk runs, the XCDs taking
+  // turns, so the longest problems (sorted first) spread over every XCD while a run of
+  // neighbouring tiles (shared operand panels) stays in one L2
+  const int hw = blockIdx.x, x = hw & 7, q = hw >> 3;
+  const int L = (q / kWBChunk) * (8 * kWBChunk) + x * kWBChunk + q % kWBChunk;
+  if (L >= h.total) return;
+  if (L >= h.gemm_blocks) {
+    const int rb = L - h.gemm_blocks;
+    int j = 0;
+    for (int i = 1; i < h.nrow; ++i)
+      if (rb >= R[i].blk0) j = i;
+    const WBRow d = R[j];
+    float* red = (float*)smem;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = (rb - d.blk0) * 64 + lane;
+    float v = 0.f;
+    if (c < d.cols) {
+      const float* src = d.parts + c;
+      int s = w;
+      for (; s + 28 < d.nparts; s += 32) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = src[(long)(s + 4 * u) * d.stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += t[u];
+      }
+      for (; s < d.nparts; s += 4) v += src[(long)s * d.stride];
+    }
+    red[w * 64 + lane] = v;
+    __syncthreads();
+    if (w == 0 && c < d.cols) {
+      const float t = ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+      d.dst[c] = d.accumulate ? d.dst[c] + t : t;
+    }
+    return;
+  }
+  int lo = 0, hi = h.nprob - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (P[mid].blk0 <= L) lo = mid;
+    else hi = mid - 1;
+  }
+  const WBProb d = P[lo];
+  const int tiles_n = d.flags >> 2;
+  const int tile = L - d.blk0;
+  using Ld = DenseT<bf16>;
+  // dW[n][k] = sum_m dY[m][n] X[m][k]: A(n, m) = dY[m][n], B(k, m) = X[m][k]
+  const Ld la{d.dy, d.lddy, d.N, d.M};
+  const Ld lb{d.x, d.ldx, d.K, d.M};
+  EpiWB ep{};
+  ep.out = d.dw;
+  ep.ldo = d.lddw;
+  ep.atomic = 0;
+  ep.vec = (d.flags >> 1) & 1;
+  ep.overwrite = !(d.flags & 1);
+  ep.rowsum = nullptr;
+  ep.split_stride = 0;
+  ep.split = 0;
+  ep.db = d.db;
+  ep.bias_on = d.db != nullptr;
+  const int kchunk = (d.M + 63) / 64 * 64;
+  gemm2_tile<kFamLinearWgrad, BM, BM, 2, 2, S, 0>(la, lb, ep, d.N, d.K, d.M, kchunk, tiles_n,
+                                                  tile, 0);
+}
+
+struct PutChunk {
+  unsigned w[640];            // 2.5 KiB of the table per launch (kernel-argument payload)
+  int off, n;                 // word offset, words
+};
+
+__global__ void __launch_bounds__(256) table_put_kernel(PutChunk c, unsigned* dst) {
+  for (int i = threadIdx.x; i < c.n; i += 256) dst[c.off + i] = c.w[i];
+}
+
+template <int BM, int S>
+int wgrad_batch_launch(const char* table, int total, hipStream_t st) {
+  constexpr size_t lds = gemm2_lds_bytes<BM, BM, S, 0>();
+  auto kern = wgrad_batch_kernel<BM, S>;
+  if constexpr (lds > 65536) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      attr_set = true;
+    }
+  }
+  const int grid = cdiv(total, 8 * kWBChunk) * 8 * kWBChunk;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, table);
+  return retr_check_launch("linear_wgrad_batch");
+}
+
 }  // namespace
 
 extern "C" {
@@ -714,6 +854,111 @@ int retr_linear_wgrad_group2(int dtype, int n, const retr_linear_wgrad_desc* d, 
   if (blocks == 0) return 0;
   hipLaunchKernelGGL(slab_sum_group_kernel, dim3(blocks), dim3(256), 0, st, sg);
   return retr_check_launch("linear_wgrad_group sum");
+}
+
+size_t retr_linear_wgrad_batch_table_bytes(int n, int nx) {
+  if (n < 0 || nx < 0) return 0;
+  return wb_table_bytes(n, nx);
+}
+
+int retr_linear_wgrad_batch(int n, const retr_linear_wgrad_desc* d, int nx,
+                            const retr_slab_sum_desc* x, void* table, size_t table_bytes,
+                            void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RETR_REQUIRE(n >= 0 && nx >= 0 && (n == 0 || d) && (nx == 0 || x),
+               "linear_wgrad_batch: n=%d nx=%d", n, nx);
+  RETR_REQUIRE(table != nullptr && table_bytes >= wb_table_bytes(n, nx) &&
+                   ((uintptr_t)table & 15) == 0,
+               "linear_wgrad_batch: table of %zu bytes at %p (need %zu, 16-byte aligned)",
+               table_bytes, table, wb_table_bytes(n, nx));
+  for (int i = 0; i < n; ++i)
+    RETR_REQUIRE(d[i].M >= 0 && d[i].N > 0 && d[i].K > 0 && d[i].K % 8 == 0 &&
+                     d[i].lddy % 8 == 0 && d[i].ldx % 8 == 0 && d[i].lddy >= d[i].N &&
+                     d[i].ldx >= d[i].K && d[i].lddw >= d[i].K && d[i].lddy < (1L << 31) &&
+                     d[i].ldx < (1L << 31) && d[i].lddw < (1L << 31),
+                 "linear_wgrad_batch[%d]: bad shape M=%d N=%d K=%d", i, d[i].M, d[i].N, d[i].K);
+  // tile: 128x128 once the batch has enough of them to fill the chip (2 blocks per CU)
+  long t128 = 0;
+  for (int i = 0; i < n; ++i)
+    if (d[i].M > 0) t128 += (long)cdiv(d[i].N, 128) * cdiv(d[i].K, 128);
+  int bm = t128 >= 384 ? 128 : 64;
+  const int tt = retr_tune_get(RETR_TUNE_WGRAD_TILE);
+  if (tt == 64 || tt == 128) bm = tt;
+  // longest reductions first (the hardware hands out blocks in order; the short ones fill
+  // the tail), stable within equal lengths
+  int order[1024];
+  RETR_REQUIRE(n <= 1024, "linear_wgrad_batch: n=%d (max 1024)", n);
+  int np = 0;
+  for (int i = 0; i < n; ++i)
+    if (d[i].M > 0) order[np++] = i;
+  for (int i = 1; i < np; ++i) {
+    const int v = order[i];
+    int j = i - 1;
+    while (j >= 0 && d[order[j]].M < d[v].M) {
+      order[j + 1] = order[j];
+      --j;
+    }
+    order[j + 1] = v;
+  }
+  std::vector<char> buf(wb_table_bytes(np, nx) + 16, 0);
+  WBHead* h = (WBHead*)buf.data();
+  WBProb* P = (WBProb*)(buf.data() + sizeof(WBHead));
+  int blocks = 0;
+  for (int j = 0; j < np; ++j) {
+    const retr_linear_wgrad_desc& q = d[order[j]];
+    WBProb& p = P[j];
+    p.dy = (const bf16*)q.dy;
+    p.x = (const bf16*)q.x;
+    p.dw = q.dw;
+    p.db = q.db;
+    p.lddy = (int)q.lddy;
+    p.ldx = (int)q.ldx;
+    p.lddw = (int)q.lddw;
+    p.M = q.M;
+    p.N = q.N;
+    p.K = q.K;
+    p.blk0 = blocks;
+    const int tiles_n = cdiv(q.K, bm);
+    const int vec = vec8_ok<float>(q.dw, q.lddw) ? 1 : 0;
+    p.flags = (q.accumulate ? 1 : 0) | vec << 1 | tiles_n << 2;
+    blocks += cdiv(q.N, bm) * tiles_n;
+  }
+  WBRow* R = (WBRow*)(buf.data() + sizeof(WBHead) + (size_t)np * sizeof(WBProb));
+  int nr = 0, rblocks = 0;
+  for (int i = 0; i < nx; ++i) {
+    const retr_slab_sum_desc& q = x[i];
+    if (!q.dst || q.nparts <= 0 || q.cols <= 0) continue;
+    RETR_REQUIRE(q.stride < (1L << 31), "linear_wgrad_batch: extra stride %ld", q.stride);
+    WBRow& r = R[nr++];
+    r.parts = q.parts;
+    r.dst = q.dst;
+    r.stride = (int)q.stride;
+    r.nparts = q.nparts;
+    r.cols = q.cols;
+    r.accumulate = q.accumulate;
+    r.blk0 = rblocks;
+    rblocks += cdiv(q.cols, 64);
+  }
+  h->nprob = np;
+  h->nrow = nr;
+  h->gemm_blocks = blocks;
+  h->total = blocks + rblocks;
+  if (h->total == 0) return 0;
+  // the table into device memory, in stream order before the GEMM launch
+  const size_t used = wb_table_bytes(np, nr);
+  const int words = (int)((used + 3) / 4);
+  const unsigned* src = (const unsigned*)buf.data();
+  for (int off = 0; off < words; off += 640) {
+    PutChunk c;
+    c.off = off;
+    c.n = words - off < 640 ? words - off : 640;
+    memcpy(c.w, src + off, (size_t)c.n * 4);
+    hipLaunchKernelGGL(table_put_kernel, dim3(1), dim3(256), 0, st, c, (unsigned*)table);
+    if (int e = retr_check_launch("linear_wgrad_batch table")) return e;
+  }
+  const char* tb = (const char*)table;
+  return bm == 128 ? wgrad_batch_launch<128, 2>(tb, h->total, st)
+                   : wgrad_batch_launch<64, 2>(tb, h->total, st);
 }
 
 }  // extern "C"

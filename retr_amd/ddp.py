@@ -126,16 +126,21 @@ class GradSync:
 
     def _on_grad(self, p):
         bi, off = self.where[p]
+        from . import ops
         if self.arena is not None:
             view = p._retr_grad_view
             if p.grad.data_ptr() != view.data_ptr():     # produced outside the arena
+                ops.flush_wgrad()
                 view.copy_(p.grad)
                 self.foreign.add(p)
                 self._mark_dirty()
         else:
+            ops.flush_wgrad()
             self.flat[bi][off:off + p.numel()].copy_(p.grad.reshape(-1))
         self.pending[bi] -= 1
         if self.pending[bi] == 0:
+            # the bucket's gradients may still sit in the deferred weight-gradient queue
+            ops.flush_wgrad()
             if not self.defer:
                 self._launch(bi)
             elif self.on_ready is not None:

@@ -56,6 +56,7 @@ def forward_backward(model, criterion, samples, caps, cap_masks, optimizer):
         loss = criterion(outputs.permute(0, 2, 1), caps[:, 1:])
     optimizer.zero_grad()
     loss.backward()
+    ops.flush_wgrad()            # no-op: backward's final callback already ran the queue
     return loss
 
 

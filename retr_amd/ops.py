@@ -380,6 +380,111 @@ def k_linear_wgrad_group(items, extra=()):
          _st())
 
 
+# Deferred weight gradients (bf16 transformer blocks).  A block's backward needs only the DATA
+# gradient to go on; its weight / bias gradients (and its LayerNorm dgamma / dbeta partial-row
+# sums) are queued and run later as ONE retr_linear_wgrad_batch launch over every queued
+# problem: with a whole transformer's projections in one grid (~1000 128x128 tiles) the token
+# reduction is not split, so no fp32 slabs and no slab-sum launches (the per-block group path
+# splits each block's 80-100 tiles 8-16 ways to fill the chip).  The queue is flushed
+#   * at the end of the backward pass (autograd final callback, armed by the first enqueue),
+#   * by ddp.GradSync before a gradient bucket is all-reduced (or copied out),
+#   * explicitly (flush_wgrad(); engine.forward_backward calls it after backward()).
+# Only gradients handed out by FusedAdamW's arena are deferred: autograd adopts those views as
+# p.grad without reading them (an accumulating p.grad would read the buffer at once).  Every
+# output element is one fp32 chain over all tokens in order, so the bits do not depend on where
+# the flushes fall (segmented DP capture == single graph).
+WGRAD_DEFER = True
+_WQ = []            # [(descs, extras, keepalive, dst ranges)]
+_WQ_STATE = {"armed": False, "ranges": []}
+WGRAD_STATS = {"flushes": 0, "problems": 0}
+
+
+def _wq_dst_ranges(wg, extra):
+    out = []
+    for dy, x, dw, db, _ in wg:
+        out.append((dw.data_ptr(), dw.data_ptr() + dw.shape[0] * dw.stride(0) * 4))
+        if db is not None:
+            out.append((db.data_ptr(), db.data_ptr() + db.numel() * 4))
+    for (_, _, _, cols, dst, _) in extra:
+        out.append((dst.data_ptr(), dst.data_ptr() + cols * 4))
+    return out
+
+
+def _wgrad(wg, extra, arena_ok):
+    """Weight gradients of one block: queued (see WGRAD_DEFER) or one grouped launch now."""
+    if not (WGRAD_DEFER and arena_ok and wg and wg[0][0].dtype == torch.bfloat16):
+        k_linear_wgrad_group(wg, extra) if extra else k_linear_wgrad_group(wg)
+        return
+    rng = _wq_dst_ranges(wg, extra)
+    # two queued problems accumulating into one buffer would race inside the batch launch
+    if any(a < d and c < b for a, b in rng for c, d in _WQ_STATE["ranges"]):
+        flush_wgrad()
+    descs = []
+    keep = []
+    for dy, x, dw, db, acc in wg:
+        descs.append((ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(dw), dw.stride(0), ptr(db),
+                      dy.shape[0], dw.shape[0], x.shape[1], int(acc)))
+        keep += [dy, x]
+    xs = []
+    for (parts, stride, nparts, cols, dst, acc) in extra:
+        xs.append((ptr(parts), stride, nparts, cols, ptr(dst), int(acc)))
+        keep.append(parts)
+    _WQ.append((descs, xs, keep))
+    _WQ_STATE["ranges"] += rng
+    if not _WQ_STATE["armed"]:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(flush_wgrad)
+            _WQ_STATE["armed"] = True
+        except RuntimeError:        # not inside a backward pass: nothing would flush later
+            flush_wgrad()
+
+
+def flush_wgrad():
+    """Run every queued weight gradient (one launch); no-op when the queue is empty."""
+    _WQ_STATE["armed"] = False
+    if not _WQ:
+        return
+    descs = [d for q in _WQ for d in q[0]]
+    xs = [x for q in _WQ for x in q[1]]
+    keep = [t for q in _WQ for t in q[2]]
+    _WQ.clear()
+    _WQ_STATE["ranges"] = []
+    _wgrad_batch_launch(descs, xs, keep[0].device)
+    WGRAD_STATS["flushes"] += 1
+    WGRAD_STATS["problems"] += len(descs)
+    del keep
+
+
+def _wgrad_batch_launch(descs, xs, dev):
+    n, nx = len(descs), len(xs)
+    arr = (_lib.LinearWgradDesc * max(1, n))()
+    for i, (dy, lddy, x, ldx, dw, lddw, db, M, N, K, acc) in enumerate(descs):
+        d = arr[i]
+        d.dy, d.lddy, d.x, d.ldx, d.dw, d.lddw, d.db = dy, lddy, x, ldx, dw, lddw, db
+        d.M, d.N, d.K, d.accumulate = M, N, K, acc
+    xa = (_lib.SlabSumDesc * max(1, nx))()
+    for i, (parts, stride, nparts, cols, dst, acc) in enumerate(xs):
+        xa[i].parts, xa[i].stride, xa[i].nparts = parts, stride, nparts
+        xa[i].cols, xa[i].dst, xa[i].accumulate = cols, dst, acc
+    nbytes = int(_lib.load().retr_linear_wgrad_batch_table_bytes(n, nx))
+    table = torch.empty((nbytes + 15) // 16 * 16, dtype=torch.uint8, device=dev)
+    call("retr_linear_wgrad_batch", n, arr, nx, xa, ptr(table), table.numel(), _st())
+
+
+def k_linear_wgrad_batch(items, extra=()):
+    """One retr_linear_wgrad_batch launch now: items of (dy, x, dw, db, accumulate) as in
+    k_linear_wgrad_group, any number of them; ``extra`` partial-row sums likewise."""
+    descs = [(ptr(dy), dy.stride(0), ptr(x), x.stride(0), ptr(dw), dw.stride(0), ptr(db),
+              dy.shape[0], dw.shape[0], x.shape[1], int(acc)) for dy, x, dw, db, acc in items]
+    xs = [(ptr(parts), stride, nparts, cols, ptr(dst), int(acc))
+          for (parts, stride, nparts, cols, dst, acc) in extra]
+    _wgrad_batch_launch(descs, xs, items[0][0].device)
+
+
+def wgrad_pending():
+    return len(_WQ)
+
+
 def _empty(*shape, dev):
     return torch.empty(shape, dtype=torch.float32, device=dev)
 
@@ -563,9 +668,11 @@ _SHARED = {}   # id(tensor) -> [contributors left, buffer or None]
 
 
 def begin_pass():
-    """Forget the previous pass's unused fused dropout-gradient copies and shared gradients."""
+    """Forget the previous pass's unused fused dropout-gradient copies and shared gradients
+    (and run any weight gradient still queued: a backward that never reached its end)."""
     _DBR.clear()
     _SHARED.clear()
+    flush_wgrad()
 
 
 def _share(t):
@@ -617,8 +724,9 @@ def _take_dbr(dout, drop_p, seed, cdtype):
 
 def _ln_bwd_fused(x, gamma, beta, mean, rstd, dy, dy2, addend, prev, cdtype, pos=None, period=1,
                   need_dpos=False):
-    """_ln_bwd for the bf16 blocks: returns (dx, dgamma, dbeta, dpos, extra) where ``extra``
-    are the dgamma / dbeta partial-row sums for k_linear_wgrad_group; with ``prev`` = (drop_p,
+    """_ln_bwd for the bf16 blocks: returns (dx, dgamma, dbeta, dpos, extra, arena) where
+    ``extra`` are the dgamma / dbeta partial-row sums for the block's weight-gradient launch and
+    ``arena`` says both parameter gradients are FusedAdamW arena views; with ``prev`` = (drop_p,
     seed) of the block that produced x, also caches bf16 dropout(dx) for that block."""
     import ctypes
     M, C = x.shape
@@ -626,8 +734,8 @@ def _ln_bwd_fused(x, gamma, beta, mean, rstd, dy, dy2, addend, prev, cdtype, pos
     if dy is not None and dy2 is not None and dy.dtype != dy2.dtype:
         dy2 = dy2.to(dy.dtype)
     dx = torch.empty(M, C, dtype=torch.float32, device=x.device)
-    dgamma, _ = grad_buffer(gamma)
-    dbeta, _ = grad_buffer(beta)
+    dgamma, ag = grad_buffer(gamma)
+    dbeta, ab = grad_buffer(beta)
     ws = ln_workspace(M, C, x.device)
     dxd = torch.empty(M, C, dtype=cdtype, device=x.device) if prev is not None else None
     nparts = ctypes.c_int(0)
@@ -646,7 +754,7 @@ def _ln_bwd_fused(x, gamma, beta, mean, rstd, dy, dy2, addend, prev, cdtype, pos
              ptr(dpos), _st())            # adds into the (zeroed or shared) buffer
         if not last:
             dpos = None
-    return dx, dgamma, dbeta, dpos, extra
+    return dx, dgamma, dbeta, dpos, extra, ag and ab
 
 
 # ---------------------------------------------------------------------------------------------
@@ -713,7 +821,8 @@ class _SelfAttnBlock(torch.autograd.Function):
         else:
             dbr = torch.empty(M, C, dtype=cdtype, device=dev)
             k_dropout_apply(dout, dbr, drop_res, s_res)
-        (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
+        (dw_in, a0), (db_in, a1), (dw_out, a2), (db_out, a3) = map(grad_buffer, ctx.gparams)
+        arena = a0 and a1 and a2 and a3
         do = torch.empty(M, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
         dqk = torch.empty(M, 2 * C, dtype=cdtype, device=dev)
@@ -730,10 +839,10 @@ class _SelfAttnBlock(torch.autograd.Function):
         wg = [(dbr, o, dw_out, db_out, True), (dqk, npos, dw_in[: 2 * C], db_in[: 2 * C], True),
               (dv, n, dw_in[2 * C:], db_in[2 * C:], True)]
         if fused:
-            dx, dlw, dlb, dpos, extra = _ln_bwd_fused(x, ln_w, ln_b, mean, rstd, dn, dnpos, dout,
-                                                      ctx.prev, cdtype, pos, period,
-                                                      ctx.needs_input_grad[3])
-            k_linear_wgrad_group(wg, extra)
+            dx, dlw, dlb, dpos, extra, la = _ln_bwd_fused(x, ln_w, ln_b, mean, rstd, dn, dnpos,
+                                                          dout, ctx.prev, cdtype, pos, period,
+                                                          ctx.needs_input_grad[3])
+            _wgrad(wg, extra, arena and la)
         else:
             k_linear_wgrad_group(wg)
             dx, dlw, dlb, dpos = _ln_bwd(x, ln_w, ln_b, mean, rstd, dn, dnpos, dout, pos, period,
@@ -811,7 +920,8 @@ class _CrossAttnBlock(torch.autograd.Function):
         else:
             dbr = torch.empty(Mq, C, dtype=cdtype, device=dev)
             k_dropout_apply(dout, dbr, drop_res, s_res)
-        (dw_in, _), (db_in, _), (dw_out, _), (db_out, _) = map(grad_buffer, ctx.gparams)
+        (dw_in, a0), (db_in, a1), (dw_out, a2), (db_out, a3) = map(grad_buffer, ctx.gparams)
+        arena = a0 and a1 and a2 and a3
         do = torch.empty(Mq, C, dtype=cdtype, device=dev)
         k_linear_dgrad(dbr, woutt, do)
         dq = torch.empty(Mq, C, dtype=cdtype, device=dev)
@@ -841,10 +951,10 @@ class _CrossAttnBlock(torch.autograd.Function):
               (dv, mem, dw_in[2 * C:], db_in[2 * C:], True)]
         _, ln_b, qp, period = ctx.ln
         if fused:
-            dy, dlw, dlb, dqp, extra = _ln_bwd_fused(y, ln_w, ln_b, mean, rstd, None, dqpos, dout,
-                                                     ctx.prev, cdtype, qp, period,
-                                                     ctx.needs_input_grad[3])
-            k_linear_wgrad_group(wg, extra)
+            dy, dlw, dlb, dqp, extra, la = _ln_bwd_fused(y, ln_w, ln_b, mean, rstd, None, dqpos,
+                                                         dout, ctx.prev, cdtype, qp, period,
+                                                         ctx.needs_input_grad[3])
+            _wgrad(wg, extra, arena and la)
         else:
             k_linear_wgrad_group(wg)
             dy, dlw, dlb, dqp = _ln_bwd(y, ln_w, ln_b, mean, rstd, None, dqpos, dout, qp, period,
@@ -922,7 +1032,8 @@ class _FFNBlock(torch.autograd.Function):
         else:
             dbr = torch.empty(M, C, dtype=cdtype, device=dev)
             k_dropout_apply(dout, dbr, drop_res, seed)
-        (dw1, _), (db1, _), (dw2, _), (db2, _) = map(grad_buffer, ctx.gparams)
+        (dw1, a0), (db1, a1), (dw2, a2), (db2, a3) = map(grad_buffer, ctx.gparams)
+        arena = a0 and a1 and a2 and a3
         dh = torch.empty(M, F, dtype=cdtype, device=dev)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
         if ctx.splits:
@@ -937,9 +1048,9 @@ class _FFNBlock(torch.autograd.Function):
             k_linear_dgrad(dh, w1t, dn)
         wg = [(dbr, h, dw2, db2, True), (dh, n, dw1, db1, True)]
         if fused:
-            dx, dlw, dlb, _, extra = _ln_bwd_fused(x, ln_w, ctx.ln_b, mean, rstd, dn, None, dout,
-                                                   ctx.prev, cdtype)
-            k_linear_wgrad_group(wg, extra)
+            dx, dlw, dlb, _, extra, la = _ln_bwd_fused(x, ln_w, ctx.ln_b, mean, rstd, dn, None,
+                                                       dout, ctx.prev, cdtype)
+            _wgrad(wg, extra, arena and la)
         else:
             k_linear_wgrad_group(wg)
             dx, dlw, dlb, _ = _ln_bwd(x, ln_w, ctx.ln_b, mean, rstd, dn, None, dout)

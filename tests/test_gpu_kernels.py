@@ -593,7 +593,7 @@ def test_attention_resident_equals_streaming(B, H, Lq, Lk, hd, causal, masked, p
             outs.append((o, lse, dq, dk, dv))
         finally:
             _lib.load().retr_tune(5, 0)
-            _lib.load().retr_tune(10, 0)
+            _lib.load().retr_tune(2, 0)
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
     # the default split backward (two waves per 32 rows, even + odd tile partials added at the
@@ -1240,3 +1240,81 @@ def test_fused_ffn_equals_two_launch_path(M):
     l1, l2 = mod.sublayer[0], mod.sublayer[2]
     ref = x0 + l2(torch.relu(l1(ln)))
     assert rel_err(ye - x0, ref - x0) < 2e-2
+
+
+@pytest.mark.parametrize("tile", [0, 64, 128])
+def test_wgrad_batch_matches_fp32_and_is_batching_invariant(tile):
+    """retr_linear_wgrad_batch (the deferred weight gradients of whole transformer passes): every
+    problem's dW = dY^T X and db = colsum dY (bias folded into the first column tile as an
+    all-ones MFMA) against fp32 torch on the same bf16 operands, in overwrite and accumulate
+    mode, plus LayerNorm-style partial-row sums in the same launch; and the bits do not depend
+    on how the problems are batched (one launch of all vs three launches of subsets in another
+    order) or on the tile (RETR_TUNE_WGRAD_TILE 64 / 128 / auto)."""
+    from retr_amd import _lib
+    # encoder block shapes (6400 tokens), decoder (2048), cross-attention K/V over the memory,
+    # a ragged one (tokens and rows off every tile multiple)
+    shapes = [(6400, 512, 256), (6400, 256, 256), (6400, 256, 256), (6400, 2048, 256),
+              (6400, 256, 2048), (2048, 512, 256), (2048, 256, 256), (2048, 256, 256),
+              (6400, 256, 256), (6400, 256, 256), (2048, 2048, 256), (2048, 256, 2048),
+              (1000, 200, 136), (77, 72, 64)]
+    g = torch.Generator(device="cpu").manual_seed(11)
+    ops_ = []
+    for i, (M, N, K) in enumerate(shapes):
+        dy = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+        x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+        ops_.append((dy, x, i % 3 != 1))
+    nparts, C = 53, 256
+    parts = torch.randn(nparts * 2 * C, generator=g).to(DEV)
+
+    def fresh(acc):
+        run = []
+        for k, (dy, x, has_b) in enumerate(ops_):
+            N, K = dy.shape[1], x.shape[1]
+            dw = torch.randn(N, K, generator=torch.Generator().manual_seed(k)).to(DEV)
+            db = torch.randn(N, generator=torch.Generator().manual_seed(100 + k)).to(DEV) \
+                if has_b else None
+            run.append((dy, x, dw, db, acc))
+        gam = torch.randn(C, generator=torch.Generator().manual_seed(1)).to(DEV)
+        bet = torch.randn(C, generator=torch.Generator().manual_seed(2)).to(DEV)
+        extra = [(parts, 2 * C, nparts, C, gam, acc), (parts[C:], 2 * C, nparts, C, bet, acc)]
+        return run, extra
+
+    def outs(run, extra):
+        return [t.clone() for it in run for t in it[2:4] if t is not None] + \
+               [e[4].clone() for e in extra]
+
+    try:
+        _lib.load().retr_tune(2, tile)          # RETR_TUNE_WGRAD_TILE
+        res = {}
+        for acc in (False, True):
+            run, extra = fresh(acc)
+            init = outs(run, extra)
+            ops.k_linear_wgrad_batch(run, extra)
+            torch.cuda.synchronize()
+            got = outs(run, extra)
+            res[acc] = got
+            # fp32 references
+            k = 0
+            for dy, x, has_b in ops_:
+                refw = dy.float().t() @ x.float()
+                base = init[k] if acc else 0
+                assert rel_err(got[k] - base, refw) < 2e-5, ("dw", dy.shape, x.shape, acc)
+                k += 1
+                if has_b:
+                    base = init[k] if acc else 0
+                    assert rel_err(got[k] - base, dy.float().sum(0)) < 2e-5, ("db", dy.shape)
+                    k += 1
+            p2 = parts.view(nparts, 2, C)
+            for j in range(2):
+                base = init[k + j] if acc else 0
+                assert rel_err(got[k + j] - base, p2[:, j].sum(0)) < 1e-5
+        # batching invariance: the same problems as three launches, reversed order
+        run, extra = fresh(True)
+        ops.k_linear_wgrad_batch(run[9:][::-1], extra)
+        ops.k_linear_wgrad_batch(run[4:9])
+        ops.k_linear_wgrad_batch(run[:4][::-1])
+        torch.cuda.synchronize()
+        for a, b in zip(res[True], outs(run, extra)):
+            assert torch.equal(a, b)
+    finally:
+        _lib.load().retr_tune(2, 0)

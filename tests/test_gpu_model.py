@@ -356,3 +356,49 @@ def test_shared_memory_gradient_is_sum_of_block_contributions(extra_use):
             assert bad == 0, (what, fuse, bad, (got - s).abs().max().item())
             e = ((got - s).norm() / s.norm()).item()
             assert e < 1e-2, (what, fuse, e)
+
+
+def test_deferred_weight_gradients_match_per_block_launches():
+    """bf16 training with FusedAdamW's gradient arena: the transformer blocks' weight / bias /
+    LayerNorm-parameter gradients are queued and run as ONE retr_linear_wgrad_batch launch at
+    the end of backward (ops.WGRAD_DEFER, flushed by autograd's final callback -- no explicit
+    flush here) instead of one grouped split-K launch + slab sum per block.  Against the
+    per-block path (which at these token counts does not split the reduction either): every
+    gradient bitwise equal, one flush per backward and nothing left queued.  (Split-K vs the
+    unsplit batch at the full token counts: tests/test_gpu_kernels.py::test_wgrad_batch_*.)"""
+    from retr_amd import ops
+    from retr_amd.optim import FusedAdamW
+    cfg = make_config(backbone="ResNet18", hidden=256, layers=(2, 2), vocab=1000, max_pos=16,
+                      ffn=512, dtype="bf16", dropout=0.1)
+    model, crit = build_model(cfg)
+    model.load_state_dict(synthetic_state_dict(model, seed=4))
+    model.to(DEV).train()
+    opt = FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+    images, mask = synthetic_images(2, 64, seed=1, pad_band=True)
+    caps, cap_mask = synthetic_captions(2, 16, 1000, seed=2)
+    s = NestedTensor(images.to(DEV), mask.to(DEV))
+    ctr = ops._seed_state["ctr"]
+    res = []
+    try:
+        for defer in (True, False):
+            ops.WGRAD_DEFER = defer
+            ops._seed_state["ctr"] = ctr
+            f0 = ops.WGRAD_STATS["flushes"]
+            opt.zero_grad(set_to_none=True)
+            out = model(s, caps[:, :-1].to(DEV), cap_mask[:, :-1].to(DEV))
+            loss = crit(out.permute(0, 2, 1), caps[:, 1:].to(DEV))
+            loss.backward()
+            assert ops.wgrad_pending() == 0
+            torch.cuda.synchronize()
+            res.append(({n: p.grad.detach().clone() for n, p in model.named_parameters()
+                         if p.grad is not None}, ops.WGRAD_STATS["flushes"] - f0, loss.item()))
+    finally:
+        ops.WGRAD_DEFER = True
+    (g1, nf1, l1), (g0, nf0, l0) = res
+    assert l1 == l0
+    assert nf1 == 1 and nf0 == 0, (nf1, nf0)
+    assert g1.keys() == g0.keys() and len(g1) > 0
+    # at these token counts (< 512 per block) the per-block path does not split the reduction
+    # either, so both are the same single fp32 chain per element: bitwise equal everywhere
+    for n in g1:
+        assert torch.equal(g1[n], g0[n]), n

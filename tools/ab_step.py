@@ -57,6 +57,9 @@ VARIANTS = {
     "ffn_fused": {("ATTR", "FUSE_FFN"): True},
     "wkc2048": {("TUNE", 4): 2048},
     "wkc3200": {("TUNE", 4): 3200},
+    "wdefer_off": {("ATTR", "WGRAD_DEFER"): False},
+    "wb64": {("TUNE", 2): 64},
+    "wb128": {("TUNE", 2): 128},
 }
 
 
@@ -67,6 +70,7 @@ def apply(v):
     ops.ATTN_DMASK = True
     ops.FUSED_CE = True
     ops.FUSE_FFN = False
+    ops.WGRAD_DEFER = True
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
