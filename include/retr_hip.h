@@ -257,6 +257,23 @@ int retr_conv2d_wgrad(int dtype, const void* dy, const void* x, int Nb, int H, i
                       void* stream);
 int retr_conv2d_wgrad_splits(int dtype, int Nb, int H, int W, int C, int Co, int KH, int KW,
                              int stride, int pad, int dil);
+/* Grouped bf16 weight gradients of many convolutions -- the whole backbone backward of
+ * models/backbone.py:65,69,86-91 (torchvision Bottleneck convs) -- in two launches (dense 1x1
+ * stride-1 convs; 3x3 / strided convs), one K-slice length for the whole group instead of each
+ * conv's own split count.  Usage: fill the geometry, call _plan (sets kind: 0 dense 1x1, 1 3x3 /
+ * strided, -1 not groupable -> retr_conv2d_wgrad; and splits), allocate ws[splits][Co][KH*KW*C]
+ * fp32 per problem, call retr_conv2d_wgrad_group, then retr_conv_wgrad_unpack(..., splits) per
+ * problem.  table: retr_conv2d_wgrad_group_table_bytes(n) + 512 bytes of device memory. */
+typedef struct {
+  const void* dy; const void* x;    /* dY [Nb*OH*OW][Co], X [Nb][H][W][C] (bf16, NHWC) */
+  float* ws;                        /* [splits][Co][KH*KW*C] fp32 slabs */
+  int Nb, H, W, C, Co, KH, KW, stride, pad, dil;
+  int splits, kind;                 /* set by retr_conv2d_wgrad_group_plan */
+} retr_conv_wgrad_desc;
+size_t retr_conv2d_wgrad_group_table_bytes(int n);
+int retr_conv2d_wgrad_group_plan(int dtype, int n, retr_conv_wgrad_desc* d);
+int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, void* table,
+                            size_t table_bytes, void* stream);
 /* grad[Co][Ci][KH][KW] (=|+=) scale[co] * sum_s ws[s] (slices added in order: deterministic) */
 int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,
                            int Cp, int KH, int KW, int accumulate, int splits, void* stream);

@@ -50,6 +50,13 @@ class LinearWgradDesc(ctypes.Structure):
                 ("db", _P), ("M", _I), ("N", _I), ("K", _I), ("accumulate", _I)]
 
 
+class ConvWgradDesc(ctypes.Structure):
+    """retr_conv_wgrad_desc"""
+    _fields_ = [("dy", _P), ("x", _P), ("ws", _P), ("Nb", _I), ("H", _I), ("W", _I), ("C", _I),
+                ("Co", _I), ("KH", _I), ("KW", _I), ("stride", _I), ("pad", _I), ("dil", _I),
+                ("splits", _I), ("kind", _I)]
+
+
 class ConvPackDesc(ctypes.Structure):
     """retr_conv_pack_desc"""
     _fields_ = [("w", _P), ("bn_w", _P), ("bn_b", _P), ("bn_rm", _P), ("bn_rv", _P),
@@ -110,6 +117,9 @@ _SIGS = {
     "retr_conv2d_dgrad": [_I, _P, _I, _I, _I, _I, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "retr_conv2d_wgrad": [_I, _P, _P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P],
     "retr_conv_wgrad_unpack": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "retr_conv2d_wgrad_group_table_bytes": [_I],
+    "retr_conv2d_wgrad_group_plan": [_I, _I, ctypes.POINTER(ConvWgradDesc)],
+    "retr_conv2d_wgrad_group": [_I, _I, ctypes.POINTER(ConvWgradDesc), _P, _SZ, _P],
     "retr_conv2d_wgrad_splits": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
     "retr_nchw_to_nhwc": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "retr_nchw_to_s2d16": [_P, _P, _I, _I, _I, _I, _P],
@@ -180,7 +190,7 @@ _SIGS = {
 _RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
             "retr_attention_dropout_mask_bytes": _SZ,
             "retr_layernorm_bwd_workspace": _SZ, "retr_embed_ln_bwd_workspace": _SZ,
-            "retr_linear_wgrad_group_workspace": _SZ, "retr_linear_wgrad_batch_table_bytes": _SZ, "retr_argmax_workspace": _SZ,
+            "retr_linear_wgrad_group_workspace": _SZ, "retr_linear_wgrad_batch_table_bytes": _SZ, "retr_conv2d_wgrad_group_table_bytes": _SZ, "retr_argmax_workspace": _SZ,
             "retr_set_deterministic": None,
             "retr_set_seed_base": None}
 

@@ -6,6 +6,10 @@
 //             with ih = oh*s - p + kh*d  (stride handled by a divisibility test)
 //   wgrad   : dWeff[co, (kh,kw,ci)] = sum_pixels G[pix,co] X[pix @ (kh,kw), ci]   (split-K)
 //             then dW = dWeff * bn_scale, scattered to the OIHW parameter layout.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
 #include "gemm2.hpp"
 #include "epilogues.hpp"
 #include "../../include/retr_hip.h"
@@ -1140,6 +1144,83 @@ Geom make_geom(int Nb, int H, int W, int C, int Co, int KH, int KW, int s, int p
   return g;
 }
 
+
+// ---- grouped weight gradients of many convolutions (retr_conv2d_wgrad_group) -----------------
+// The weight gradients of a whole backbone backward in two launches (dense 1x1 stride-1 convs;
+// 3x3 / strided convs on the ConvWgradB32 loader) instead of one split-K GEMM + one slab-sum
+// unpack per conv.  One K-slice length for the whole group (about two blocks per slot over all
+// problems' tiles) replaces each conv's own slice count, which had to fill the chip from 9-144
+// tiles alone: layer 3 / 4 3x3 convs drop from 14 / 3 slices to 2 / 1, the slab bytes written and
+// re-read by the unpacks fall ~5x.  Problems live in a device table (put by table_put launches in
+// stream order); logical blocks go to the XCDs in runs of kCWChunk, the XCDs taking turns, with
+// the longest blocks first.
+struct CWProb {
+  const bf16* dy;
+  const bf16* x;
+  float* ws;
+  Geom g;
+  int splits, kchunk, tiles_n, tiles, blk0, vec;
+};
+struct CWHead {
+  int nprob, total, pad0, pad1;
+};
+static_assert(sizeof(CWProb) == 96 && sizeof(CWHead) == 16, "conv wgrad table");
+constexpr int kCWChunk = 4;
+
+template <int KIND>
+__global__ void __launch_bounds__(KIND ? 512 : 256) conv_wgrad_group_kernel(const char* __restrict__ table) {
+  const CWHead h = *(const CWHead*)table;
+  const CWProb* P = (const CWProb*)(table + sizeof(CWHead));
+  const int hw = blockIdx.x, xc = hw & 7, q = hw >> 3;
+  const int L = (q / kCWChunk) * (8 * kCWChunk) + xc * kCWChunk + q % kCWChunk;
+  if (L >= h.total) return;
+  int lo = 0, hi = h.nprob - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (P[mid].blk0 <= L) lo = mid;
+    else hi = mid - 1;
+  }
+  const CWProb d = P[lo];
+  const Geom& g = d.g;
+  const int local = L - d.blk0;
+  const int split = local / d.tiles, tile = local - split * d.tiles;
+  const int Mp = g.Nb * g.OH * g.OW, R = g.Co, Ncols = g.KH * g.KW * g.C;
+  const DenseT<bf16> la{d.dy, (long)g.Co, R, Mp};
+  EpiAccF32 ep{d.ws, (long)Ncols, 0, d.vec, 1, nullptr};
+  ep.split_stride = (long)R * Ncols;
+  ep.split = split;
+  if constexpr (KIND == 0) {
+    const DenseT<bf16> lb{d.x, (long)g.C, Ncols, Mp};
+    gemm2_tile<kFamConvWgrad, 128, 128, 2, 2, 2, 0>(la, lb, ep, R, Ncols, Mp, d.kchunk, d.tiles_n,
+                                                    tile, split);
+  } else {
+    constexpr int BK = 64;
+    const int qq = BK / g.OW, rr = BK % g.OW;
+    const ConvWgradB32<bf16> lb{d.x, g, Ncols, Mp, qq, rr, (qq * g.s * g.W + rr * g.s) * g.C,
+                                g.s * g.W * g.C - g.OW * g.s * g.C, (g.H - g.OH * g.s) * g.W * g.C};
+    gemm2_tile<kFamConvWgrad, 128, 128, 4, 2, 2, 0>(la, lb, ep, R, Ncols, Mp, d.kchunk, d.tiles_n,
+                                                    tile, split);
+  }
+}
+
+struct CWPut {
+  unsigned w[640];
+  int off, n;
+};
+
+__global__ void __launch_bounds__(256) cw_table_put_kernel(CWPut c, unsigned* dst) {
+  for (int i = threadIdx.x; i < c.n; i += 256) dst[c.off + i] = c.w[i];
+}
+
+// 0: dense 1x1 stride-1, 1: ConvWgradB32 (3x3 / strided), -1: not groupable
+int cw_kind(const Geom& g) {
+  if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) return 0;
+  if ((long)g.Nb * g.H * g.W * g.C < (1L << 31) && g.OH * g.OW >= 64 && g.C % 8 == 0 &&
+      g.Co % 8 == 0)
+    return 1;
+  return -1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1347,6 +1428,130 @@ int retr_conv2d_wgrad_splits(int dtype, int Nb, int H, int W, int C, int Co, int
   const bool d1 = g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0;
   return dtype == RETR_BF16 ? wgrad_plan<bf16>(g.Co, Ncols, Mp, d1).splits
                             : wgrad_plan<float>(g.Co, Ncols, Mp, d1).splits;
+}
+
+size_t retr_conv2d_wgrad_group_table_bytes(int n) {
+  return n < 0 ? 0 : sizeof(CWHead) + (size_t)n * sizeof(CWProb);
+}
+
+int retr_conv2d_wgrad_group_plan(int dtype, int n, retr_conv_wgrad_desc* d) {
+  RETR_REQUIRE(n >= 0 && (n == 0 || d), "conv2d_wgrad_group_plan: n=%d", n);
+  // one K-slice length per kind: ~2 blocks per slot (512 slots: two 64 KB-LDS blocks per CU)
+  // over all of the kind's tiles
+  long work[2] = {0, 0};
+  for (int i = 0; i < n; ++i) {
+    retr_conv_wgrad_desc& q = d[i];
+    const Geom g = make_geom(q.Nb, q.H, q.W, q.C, q.Co, q.KH, q.KW, q.stride, q.pad, q.dil);
+    q.kind = dtype == RETR_BF16 ? cw_kind(g) : -1;
+    q.splits = 0;
+    if (q.kind < 0) continue;
+    const long tiles = (long)cdiv(g.Co, 128) * cdiv(g.KH * g.KW * g.C, 128);
+    work[q.kind] += tiles * cdiv(g.Nb * g.OH * g.OW, 64);
+  }
+  for (int i = 0; i < n; ++i) {
+    retr_conv_wgrad_desc& q = d[i];
+    if (q.kind < 0) continue;
+    const Geom g = make_geom(q.Nb, q.H, q.W, q.C, q.Co, q.KH, q.KW, q.stride, q.pad, q.dil);
+    const int ksteps = cdiv(g.Nb * g.OH * g.OW, 64);
+    long chunk = (work[q.kind] + 1023) / 1024;
+    if (retr_tune_get(RETR_TUNE_CONV_WGRAD_SPLITS) >= 2) chunk = retr_tune_get(RETR_TUNE_CONV_WGRAD_SPLITS);
+    if (chunk < 8) chunk = 8;
+    long s = (ksteps + chunk - 1) / chunk;
+    if (s > 128) s = 128;
+    if (s < 1) s = 1;
+    const int kchunk = cdiv(ksteps, (int)s) * 64;   // whole K-steps; no empty slices
+    q.splits = cdiv(g.Nb * g.OH * g.OW, kchunk);
+  }
+  return 0;
+}
+
+int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, void* table,
+                            size_t table_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RETR_REQUIRE(dtype == RETR_BF16, "conv2d_wgrad_group: bf16 only");
+  RETR_REQUIRE(n >= 0 && (n == 0 || d) && n <= 4096, "conv2d_wgrad_group: n=%d", n);
+  RETR_REQUIRE(table && table_bytes >= retr_conv2d_wgrad_group_table_bytes(n) &&
+                   ((uintptr_t)table & 15) == 0,
+               "conv2d_wgrad_group: table of %zu bytes (need %zu, 16-byte aligned)", table_bytes,
+               retr_conv2d_wgrad_group_table_bytes(n));
+  for (int kind = 0; kind < 2; ++kind) {
+    // this kind's problems, longest blocks first (stable)
+    std::vector<int> ord;
+    for (int i = 0; i < n; ++i)
+      if (d[i].kind == kind) {
+        RETR_REQUIRE(d[i].splits >= 1 && d[i].ws && d[i].dy && d[i].x,
+                     "conv2d_wgrad_group[%d]: unplanned problem", i);
+        ord.push_back(i);
+      }
+    if (ord.empty()) continue;
+    auto blk_len = [&](int i) {
+      const Geom g = make_geom(d[i].Nb, d[i].H, d[i].W, d[i].C, d[i].Co, d[i].KH, d[i].KW,
+                               d[i].stride, d[i].pad, d[i].dil);
+      return cdiv(g.Nb * g.OH * g.OW, d[i].splits);
+    };
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return blk_len(a) > blk_len(b); });
+    std::vector<char> buf(sizeof(CWHead) + ord.size() * sizeof(CWProb) + 16, 0);
+    CWHead* h = (CWHead*)buf.data();
+    CWProb* P = (CWProb*)(buf.data() + sizeof(CWHead));
+    int blocks = 0;
+    for (size_t j = 0; j < ord.size(); ++j) {
+      const retr_conv_wgrad_desc& q = d[ord[j]];
+      const Geom g = make_geom(q.Nb, q.H, q.W, q.C, q.Co, q.KH, q.KW, q.stride, q.pad, q.dil);
+      RETR_REQUIRE(cw_kind(g) == kind, "conv2d_wgrad_group[%d]: kind %d does not fit", ord[j], kind);
+      CWProb& p = P[j];
+      p.dy = (const bf16*)q.dy;
+      p.x = (const bf16*)q.x;
+      p.ws = q.ws;
+      p.g = g;
+      const int Mp = g.Nb * g.OH * g.OW, Ncols = g.KH * g.KW * g.C;
+      p.kchunk = cdiv(cdiv(Mp, 64), q.splits) * 64;
+      p.splits = cdiv(Mp, p.kchunk);
+      RETR_REQUIRE(p.splits == q.splits, "conv2d_wgrad_group[%d]: splits %d != plan %d", ord[j],
+                   p.splits, q.splits);
+      p.tiles_n = cdiv(Ncols, 128);
+      p.tiles = cdiv(g.Co, 128) * p.tiles_n;
+      p.blk0 = blocks;
+      p.vec = vec8_ok<float>(q.ws, (long)Ncols) ? 1 : 0;
+      blocks += p.tiles * p.splits;
+    }
+    h->nprob = (int)ord.size();
+    h->total = blocks;
+    const int words = (int)((sizeof(CWHead) + ord.size() * sizeof(CWProb) + 3) / 4);
+    const unsigned* src = (const unsigned*)buf.data();
+    for (int off = 0; off < words; off += 640) {
+      CWPut c;
+      c.off = off;
+      c.n = words - off < 640 ? words - off : 640;
+      memcpy(c.w, src + off, (size_t)c.n * 4);
+      hipLaunchKernelGGL(cw_table_put_kernel, dim3(1), dim3(256), 0, st, c, (unsigned*)table);
+      if (int e = retr_check_launch("conv2d_wgrad_group table")) return e;
+    }
+    const int grid = cdiv(blocks, 8 * kCWChunk) * 8 * kCWChunk;
+    constexpr size_t lds = gemm2_lds_bytes<128, 128, 2, 0>();
+    if (kind == 0) {
+      auto kern = conv_wgrad_group_kernel<0>;
+      static bool attr0 = false;
+      if (lds > 65536 && !attr0) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr0 = true;
+      }
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, (const char*)table);
+    } else {
+      auto kern = conv_wgrad_group_kernel<1>;
+      static bool attr1 = false;
+      if (lds > 65536 && !attr1) {
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr1 = true;
+      }
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, (const char*)table);
+    }
+    if (int e = retr_check_launch(kind == 0 ? "conv2d_wgrad_group 1x1" : "conv2d_wgrad_group")) return e;
+    // the next kind's table must not overwrite this one before the launch has read it: use
+    // the second half of the caller's table for kind 1
+    table = (char*)table + (((sizeof(CWHead) + ord.size() * sizeof(CWProb)) + 255) / 256 * 256);
+    table_bytes -= ((sizeof(CWHead) + ord.size() * sizeof(CWProb)) + 255) / 256 * 256;
+  }
+  return 0;
 }
 
 int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,

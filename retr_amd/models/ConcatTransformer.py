@@ -158,6 +158,7 @@ class ConcatTransformer(nn.Module):
         """Hot path.  Returns (hs [B*T, C] compute dtype, att dict or {})."""
         from .. import ops
         ops.begin_pass()
+        src_rows = ops.wgrad_fence(src_rows)
         kpm_src = src_mask.reshape(B, S).contiguous().view(torch.uint8)
         mem, mem_pos, att_e = self.encode(src_rows, B, S, kpm_src, cdtype, return_attention)
         hs, att_s, att_x = self.decode(mem, mem_pos, B, S, kpm_src, tgt, tgt_mask, cdtype,

@@ -439,20 +439,73 @@ def _wgrad(wg, extra, arena_ok):
             flush_wgrad()
 
 
-def flush_wgrad():
-    """Run every queued weight gradient (one launch); no-op when the queue is empty."""
-    _WQ_STATE["armed"] = False
-    if not _WQ:
-        return
-    descs = [d for q in _WQ for d in q[0]]
-    xs = [x for q in _WQ for x in q[1]]
-    keep = [t for q in _WQ for t in q[2]]
-    _WQ.clear()
-    _WQ_STATE["ranges"] = []
-    _wgrad_batch_launch(descs, xs, keep[0].device)
-    WGRAD_STATS["flushes"] += 1
-    WGRAD_STATS["problems"] += len(descs)
-    del keep
+# The fence's flush on a side stream, overlapping the backbone backward: measured 0.3 ms/step
+# SLOWER in the graphed cfg2 step (profiles/r4_ab_wgrad_defer.txt), so off by default
+WGRAD_SIDE = False
+_SIDE = {"stream": None, "pending": False}
+
+
+def _side_stream(dev):
+    st = _SIDE["stream"]
+    if st is None or st.device != dev:
+        st = _SIDE["stream"] = torch.cuda.Stream(device=dev)
+    return st
+
+
+def join_side():
+    """Make the current stream wait for a weight-gradient batch running on the side stream."""
+    if _SIDE["pending"]:
+        torch.cuda.current_stream(_SIDE["stream"].device).wait_stream(_SIDE["stream"])
+        _SIDE["pending"] = False
+
+
+def flush_wgrad(side=False):
+    """Run every queued weight gradient (one launch) and, unless ``side``, wait for any batch
+    still running on the side stream.  ``side``: launch on the side stream (forked from the
+    current one), so the batch overlaps the kernels that follow until the next join."""
+    if not side:
+        _WQ_STATE["armed"] = False
+    if _WQ:
+        descs = [d for q in _WQ for d in q[0]]
+        xs = [x for q in _WQ for x in q[1]]
+        keep = [t for q in _WQ for t in q[2]]
+        _WQ.clear()
+        _WQ_STATE["ranges"] = []
+        dev = keep[0].device
+        if side:
+            st = _side_stream(dev)
+            st.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(st):
+                for t in keep:
+                    t.record_stream(st)
+                _wgrad_batch_launch(descs, xs, dev)
+            _SIDE["pending"] = True
+        else:
+            _wgrad_batch_launch(descs, xs, dev)
+        WGRAD_STATS["flushes"] += 1
+        WGRAD_STATS["problems"] += len(descs)
+        del keep
+    if not side:
+        join_side()
+
+
+class _WgradFence(torch.autograd.Function):
+    """Identity on the transformer's input rows: its backward runs once every transformer block
+    has queued its weight gradients, and starts their batch (on the side stream with
+    WGRAD_SIDE) while the backbone backward proceeds."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        flush_wgrad(side=WGRAD_SIDE)
+        return g
+
+
+def wgrad_fence(x):
+    return _WgradFence.apply(x) if x.requires_grad and torch.is_grad_enabled() else x
 
 
 def _wgrad_batch_launch(descs, xs, dev):

@@ -71,6 +71,15 @@ def flops_of(name, a):
     if name == "retr_linear_wgrad_batch":
         n, arr = a[0], a[1]
         return "linear_wgrad", sum(2.0 * arr[i].M * arr[i].N * arr[i].K for i in range(n))
+    if name == "retr_conv2d_wgrad_group":
+        n, arr = a[1], a[2]
+        fl = 0.0
+        for d in (arr[i] for i in range(n)):
+            if d.kind >= 0:
+                oh = _conv_out(d.H, d.KH, d.stride, d.pad, d.dil)
+                ow = _conv_out(d.W, d.KW, d.stride, d.pad, d.dil)
+                fl += 2.0 * d.Nb * oh * ow * d.Co * d.KH * d.KW * d.C
+        return "conv_wgrad", fl
     if name == "retr_attention_fwd":
         b, h, lq, lk, hd, causal = a[9], a[10], a[11], a[12], a[13], a[15]
         return "attention_fwd", 4.0 * b * h * lq * lk * hd * (0.5 if causal else 1.0)
@@ -100,6 +109,16 @@ def bytes_of(name, a):
     outputs where the call says so).  Split-K slabs, re-reads and padding are implementation
     traffic and are NOT counted here -- the rocprofv3 --pmc passes measure those."""
     name = _ALIAS.get(name, name)
+    if name == "retr_conv2d_wgrad_group":      # bf16 dY and X once, fp32 slab-free dW once
+        n, arr = a[1], a[2]
+        by = 0
+        for d in (arr[i] for i in range(n)):
+            if d.kind >= 0:
+                oh = _conv_out(d.H, d.KH, d.stride, d.pad, d.dil)
+                ow = _conv_out(d.W, d.KW, d.stride, d.pad, d.dil)
+                by += 2 * (d.Nb * oh * ow * d.Co + d.Nb * d.H * d.W * d.C) \
+                    + 4 * d.Co * d.KH * d.KW * d.C
+        return by
     if name == "retr_linear_wgrad_batch":      # bf16 operands, fp32 dW / db
         cnt, arr = a[0], a[1]
         return sum(2 * (d.M * d.N + d.M * d.K) + 4 * (d.N * d.K + (d.N if d.db else 0))
@@ -173,6 +192,8 @@ def shape_of(name, a):
         return "group " + " + ".join(f"M{arr[i].M} N{arr[i].N} K{arr[i].K}" for i in range(n))
     if name == "retr_linear_wgrad_batch":
         return f"batch of {a[0]} (+{a[2]} partial-row sums)"
+    if name == "retr_conv2d_wgrad_group":
+        return f"group of {a[1]} conv weight gradients"
     if name in ("retr_conv2d_fwd", "retr_conv2d_fwd_out"):
         return f"N{a[2]} {a[3]}x{a[4]}x{a[5]} ->{a[10]} k{a[11]} s{a[13]} d{a[15]}"
     if name == "retr_conv1x1_fwd_cat":
@@ -207,7 +228,8 @@ TRACKED = ("retr_conv2d_fwd", "retr_conv2d_fwd_out", "retr_conv1x1_fwd_cat",
            "retr_linear_fwd_splitk",
            "retr_linear_dgrad", "retr_linear_dgrad_splitk", "retr_linear_wgrad",
            "retr_linear_fwd_group", "retr_linear_dgrad_group", "retr_linear_wgrad_group",
-           "retr_linear_wgrad_group2", "retr_linear_wgrad_batch", "retr_attention_fwd",
+           "retr_linear_wgrad_group2", "retr_linear_wgrad_batch", "retr_conv2d_wgrad_group",
+           "retr_attention_fwd",
            "retr_attention_bwd",
            "retr_attention_fwd_dm", "retr_attention_bwd_dm")
 
@@ -216,7 +238,8 @@ FAMILY_SYMBOL = {"linear_fwd": "gemm{,2,2_group}_kernel<0,",
                  "linear_dgrad": "gemm{,2,2_group}_kernel<1,",
                  "linear_wgrad": "gemm{,2,2_group}_kernel<2, + wgrad_batch_kernel",
                  "conv_fwd": "gemm{,2}_kernel<3, + bottleneck_s1_kernel + stem_pool_kernel",
-                 "conv_dgrad": "gemm{,2}_kernel<4,", "conv_wgrad": "gemm{,2}_kernel<5,",
+                 "conv_dgrad": "gemm{,2}_kernel<4,",
+                 "conv_wgrad": "gemm{,2}_kernel<5, + conv_wgrad_group_kernel",
                  "attention_fwd": "attn_fwd{,2,2s}_kernel",
                  "attention_bwd": "attn_bwd_"}
 
@@ -232,6 +255,8 @@ def family_of_symbol(name):
                 "conv_wgrad")[int(m.group(1))]
     if "wgrad_batch_kernel" in name:
         return "linear_wgrad"
+    if "conv_wgrad_group_kernel" in name:
+        return "conv_wgrad"
     if "bottleneck_s1_kernel" in name or "stem_pool_kernel" in name:
         return "conv_fwd"
     if re.search(r"attn_fwd\d*s?_kernel", name):

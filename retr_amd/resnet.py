@@ -187,6 +187,55 @@ def _conv_wgrad(spec, g, x, in_shape):
     return grad
 
 
+# The bf16 backbone backward queues every conv weight gradient and runs them as one grouped
+# launch per loader kind at the end (retr_conv2d_wgrad_group): one K-slice length over all
+# convs instead of each conv's own split-K plan (which had to fill 256 CUs from 9-144 tiles),
+# ~5x fewer fp32 slab bytes written and re-read by the unpacks.
+CONV_WGRAD_GROUP = True
+CONV_WGRAD_STATS = {"grouped": 0, "single": 0}
+
+
+def _conv_wgrad_group(items, grads):
+    """items: (spec, G, x, in_shape) of every conv weight gradient of one backward."""
+    n = len(items)
+    arr = (_lib.ConvWgradDesc * n)()
+    for i, (spec, G, x, shape) in enumerate(items):
+        nb, h, w, c = shape
+        d = arr[i]
+        d.dy, d.x = ptr(G), ptr(x)
+        d.Nb, d.H, d.W, d.C, d.Co = nb, h, w, c, spec.cout
+        d.KH = d.KW = spec.k
+        d.stride, d.pad, d.dil = spec.s, spec.p, spec.d
+    G0 = items[0][1]
+    call("retr_conv2d_wgrad_group_plan", dcode(G0.dtype), n, arr)
+    slabs = []
+    for i, (spec, G, x, shape) in enumerate(items):
+        if arr[i].kind < 0:
+            grads[spec.conv.weight] = _conv_wgrad(spec, G, x, shape)
+            CONV_WGRAD_STATS["single"] += 1
+            slabs.append(None)
+            continue
+        c = shape[3]
+        ws = torch.empty(arr[i].splits, spec.cout, spec.k * spec.k * c, dtype=torch.float32,
+                         device=G.device)
+        arr[i].ws = ptr(ws)
+        slabs.append(ws)
+    if any(t is not None for t in slabs):
+        nbytes = int(_lib.load().retr_conv2d_wgrad_group_table_bytes(n)) + 512
+        table = torch.empty(nbytes, dtype=torch.uint8, device=G0.device)
+        call("retr_conv2d_wgrad_group", dcode(G0.dtype), n, arr, ptr(table), nbytes, _st())
+    for i, (spec, G, x, shape) in enumerate(items):
+        ws = slabs[i]
+        if ws is None:
+            continue
+        _, _, _, scale = PACKS.get(spec, G.dtype)
+        grad, _ = grad_buffer(spec.conv.weight)     # sole writer: overwrite mode below
+        call("retr_conv_wgrad_unpack", ptr(ws), ptr(scale), ptr(grad), spec.cout, spec.cin,
+             shape[3], spec.k, spec.k, 0, arr[i].splits, _st())
+        grads[spec.conv.weight] = grad
+        CONV_WGRAD_STATS["grouped"] += 1
+
+
 def _conv_tail_cat(runner, blk, h2, s2, x, xshape):
     """relu(conv3(h2) + downsample(x)) as one 1x1 conv over the channel concatenation
     (BackboneRunner.cat_tail); weights [W3eff | Wdseff] and bias b3 + bds cached per pack."""
@@ -369,8 +418,13 @@ class _Backbone(torch.autograd.Function):
         saved = ctx.saved_acts
         ov = _Overlap(OVERLAP["backbone"])
         keep = []
+        group = CONV_WGRAD_GROUP and g.dtype == torch.bfloat16 and not OVERLAP["backbone"]
+        pending = []
 
         def wgrad(spec, G, x, shape):
+            if group:
+                pending.append((spec, G, x, shape))
+                return
             keep.extend((G, x))
             with ov.side():
                 grads[spec.conv.weight] = _conv_wgrad(spec, G, x, shape)
@@ -400,6 +454,9 @@ class _Backbone(torch.autograd.Function):
                     g = _conv_dgrad(c1, G1, ishape, addend=G3, gate=inp)
             else:
                 g = None
+        if pending:
+            _conv_wgrad_group(pending, grads)
+            del pending
         ov.join()
         del keep
         out = [None, None]

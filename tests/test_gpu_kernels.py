@@ -1318,3 +1318,59 @@ def test_wgrad_batch_matches_fp32_and_is_batching_invariant(tile):
             assert torch.equal(a, b)
     finally:
         _lib.load().retr_tune(2, 0)
+
+
+def test_conv_wgrad_group_matches_fp32_and_single_path():
+    """retr_conv2d_wgrad_group (the bf16 backbone's weight gradients, one grouped launch per
+    loader kind with one K-slice length for all convs) + retr_conv_wgrad_unpack against fp32
+    torch's conv2d weight gradient on the same bf16 operands (3x3 stride 1 / 2, dilated 3x3, 1x1
+    stride 1 / 2, a ragged map), and against the per-conv retr_conv2d_wgrad path (same products,
+    other slice boundaries: fp32 reassociation only)."""
+    from torch.nn.grad import conv2d_weight
+    from retr_amd import _lib
+    # (Nb, H, W, C, Co, k, s, p, d)
+    geos = [(4, 40, 40, 64, 64, 3, 1, 1, 1), (4, 40, 40, 64, 128, 3, 2, 1, 1),
+            (2, 20, 20, 128, 64, 3, 1, 2, 2), (4, 40, 40, 128, 256, 1, 1, 0, 1),
+            (4, 40, 40, 256, 128, 1, 1, 0, 1), (4, 40, 40, 64, 128, 1, 2, 0, 1),
+            (3, 26, 18, 64, 64, 3, 1, 1, 1), (8, 80, 80, 64, 64, 1, 1, 0, 1)]
+    g = torch.Generator().manual_seed(5)
+    items = []
+    for nb, h, w, c, co, k, s, p, d in geos:
+        oh = (h + 2 * p - d * (k - 1) - 1) // s + 1
+        ow = (w + 2 * p - d * (k - 1) - 1) // s + 1
+        x = torch.randn(nb, h, w, c, generator=g).to(DEV, torch.bfloat16)
+        dy = torch.randn(nb, oh, ow, co, generator=g).to(DEV, torch.bfloat16)
+        items.append((x, dy, (nb, h, w, c, co, k, s, p, d)))
+    n = len(items)
+    arr = (_lib.ConvWgradDesc * n)()
+    for i, (x, dy, (nb, h, w, c, co, k, s, p, d)) in enumerate(items):
+        a = arr[i]
+        a.dy, a.x = ptr(dy), ptr(x)
+        a.Nb, a.H, a.W, a.C, a.Co, a.KH, a.KW, a.stride, a.pad, a.dil = nb, h, w, c, co, k, k, s, p, d
+    call("retr_conv2d_wgrad_group_plan", 1, n, arr)
+    assert all(arr[i].kind in (0, 1) for i in range(n))
+    assert [arr[i].kind for i in range(n)] == [1, 1, 1, 0, 0, 1, 1, 0]
+    slabs = []
+    for i, (x, dy, (nb, h, w, c, co, k, s, p, d)) in enumerate(items):
+        ws = torch.full((arr[i].splits, co, k * k * c), float("nan"), device=DEV)
+        arr[i].ws = ptr(ws)
+        slabs.append(ws)
+    nbytes = int(_lib.load().retr_conv2d_wgrad_group_table_bytes(n)) + 512
+    table = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
+    call("retr_conv2d_wgrad_group", 1, n, arr, ptr(table), nbytes, ops._st())
+    for i, (x, dy, (nb, h, w, c, co, k, s, p, d)) in enumerate(items):
+        got = torch.empty(co, c, k, k, device=DEV)
+        call("retr_conv_wgrad_unpack", ptr(slabs[i]), None, ptr(got), co, c, c, k, k, 0,
+             arr[i].splits, ops._st())
+        ref = conv2d_weight(x.permute(0, 3, 1, 2).float(), (co, c, k, k),
+                            dy.permute(0, 3, 1, 2).float(), stride=s, padding=p, dilation=d)
+        assert rel_err(got, ref) < 1e-5, (geos[i], rel_err(got, ref))
+        # the per-conv path (its own split plan)
+        sp = int(_lib.load().retr_conv2d_wgrad_splits(1, nb, h, w, c, co, k, k, s, p, d))
+        ws1 = torch.empty(sp, co, k * k * c, device=DEV)
+        call("retr_conv2d_wgrad", 1, ptr(dy), ptr(x), nb, h, w, c, ptr(ws1), co, k, k, s, p, d,
+             ops._st())
+        one = torch.empty(co, c, k, k, device=DEV)
+        call("retr_conv_wgrad_unpack", ptr(ws1), None, ptr(one), co, c, c, k, k, 0, sp, ops._st())
+        assert rel_err(got, one) < 1e-6, (geos[i], rel_err(got, one))
+    torch.cuda.synchronize()

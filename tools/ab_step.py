@@ -60,6 +60,8 @@ VARIANTS = {
     "wdefer_off": {("ATTR", "WGRAD_DEFER"): False},
     "wb64": {("TUNE", 2): 64},
     "wb128": {("TUNE", 2): 128},
+    "wside_on": {("ATTR", "WGRAD_SIDE"): True},
+    "cwg_off": {("RESNET", "CONV_WGRAD_GROUP"): False},
 }
 
 
@@ -71,6 +73,8 @@ def apply(v):
     ops.FUSED_CE = True
     ops.FUSE_FFN = False
     ops.WGRAD_DEFER = True
+    ops.WGRAD_SIDE = False
+    resnet.CONV_WGRAD_GROUP = True
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)

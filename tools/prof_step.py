@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from retr_amd.probe import family_of_symbol  # noqa: E402
 
 # kernels outside the roofline families, by name fragment (first match wins)
-CATEGORIES = [("slab_sum_group", "linear wgrad slab sums"), ("table_put", "wgrad batch table"),
+CATEGORIES = [("slab_sum_group", "linear wgrad slab sums"), ("table_put", "wgrad batch tables"),
               ("slab_epilogue", "split-K slab epilogues"),
               ("wgrad_unpack", "conv wgrad slab sums + OIHW"),
               ("adamw", "clip + AdamW"), ("ln_", "LayerNorm"), ("embed", "embeddings"),
