@@ -119,7 +119,10 @@ enum {
   RETR_TUNE_WGRAD_FUSED = 17,   /* grouped bf16 linear weight gradients: 0 slabs + a separate
                                    slab_sum_group launch (default), 1 split-K reduced by each
                                    tile's last-arriving block inside the GEMM launch */
-  RETR_TUNE_COUNT = 18
+  RETR_TUNE_SPLITK_FUSED = 18,  /* split-K forward / data-gradient linears: 0 slabs + a separate
+                                   slab-epilogue launch, 1 slice sum + epilogue by each tile's
+                                   last-arriving block (csrc/splitk_fused.hpp) */
+  RETR_TUNE_COUNT = 19
 };
 int retr_tune(int knob, int value);
 
@@ -274,6 +277,18 @@ size_t retr_conv2d_wgrad_group_table_bytes(int n);
 int retr_conv2d_wgrad_group_plan(int dtype, int n, retr_conv_wgrad_desc* d);
 int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, void* table,
                             size_t table_bytes, void* stream);
+/* Every grouped conv's slab sum + OIHW re-layout (+ scale) in one launch:
+ * grad[Co][Ci][KH][KW] (=|+=) scale[co] * sum_s ws[s][co][kh][kw][ci] (slices summed by four
+ * waves in a fixed order).  table: retr_conv_wgrad_unpack_group_table_bytes(n) bytes of device
+ * memory (16-byte aligned), written in stream order by the call. */
+typedef struct {
+  const float* ws; const float* scale;   /* scale [Co] or NULL */
+  float* grad;
+  int Co, Ci, Cp, KH, KW, splits, accumulate, pad;
+} retr_conv_unpack_desc;
+size_t retr_conv_wgrad_unpack_group_table_bytes(int n);
+int retr_conv_wgrad_unpack_group(int n, const retr_conv_unpack_desc* d, void* table,
+                                 size_t table_bytes, void* stream);
 /* grad[Co][Ci][KH][KW] (=|+=) scale[co] * sum_s ws[s] (slices added in order: deterministic) */
 int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,
                            int Cp, int KH, int KW, int accumulate, int splits, void* stream);

@@ -57,6 +57,12 @@ class ConvWgradDesc(ctypes.Structure):
                 ("splits", _I), ("kind", _I)]
 
 
+class ConvUnpackDesc(ctypes.Structure):
+    """retr_conv_unpack_desc"""
+    _fields_ = [("ws", _P), ("scale", _P), ("grad", _P), ("Co", _I), ("Ci", _I), ("Cp", _I),
+                ("KH", _I), ("KW", _I), ("splits", _I), ("accumulate", _I), ("pad", _I)]
+
+
 class ConvPackDesc(ctypes.Structure):
     """retr_conv_pack_desc"""
     _fields_ = [("w", _P), ("bn_w", _P), ("bn_b", _P), ("bn_rm", _P), ("bn_rv", _P),
@@ -120,6 +126,8 @@ _SIGS = {
     "retr_conv2d_wgrad_group_table_bytes": [_I],
     "retr_conv2d_wgrad_group_plan": [_I, _I, ctypes.POINTER(ConvWgradDesc)],
     "retr_conv2d_wgrad_group": [_I, _I, ctypes.POINTER(ConvWgradDesc), _P, _SZ, _P],
+    "retr_conv_wgrad_unpack_group_table_bytes": [_I],
+    "retr_conv_wgrad_unpack_group": [_I, ctypes.POINTER(ConvUnpackDesc), _P, _SZ, _P],
     "retr_conv2d_wgrad_splits": [_I, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I],
     "retr_nchw_to_nhwc": [_I, _P, _P, _I, _I, _I, _I, _I, _P],
     "retr_nchw_to_s2d16": [_P, _P, _I, _I, _I, _I, _P],
@@ -190,7 +198,7 @@ _SIGS = {
 _RESTYPE = {"retr_last_error": ctypes.c_char_p, "retr_attention_bwd_workspace": _SZ,
             "retr_attention_dropout_mask_bytes": _SZ,
             "retr_layernorm_bwd_workspace": _SZ, "retr_embed_ln_bwd_workspace": _SZ,
-            "retr_linear_wgrad_group_workspace": _SZ, "retr_linear_wgrad_batch_table_bytes": _SZ, "retr_conv2d_wgrad_group_table_bytes": _SZ, "retr_argmax_workspace": _SZ,
+            "retr_linear_wgrad_group_workspace": _SZ, "retr_linear_wgrad_batch_table_bytes": _SZ, "retr_conv2d_wgrad_group_table_bytes": _SZ, "retr_conv_wgrad_unpack_group_table_bytes": _SZ, "retr_argmax_workspace": _SZ,
             "retr_set_deterministic": None,
             "retr_set_seed_base": None}
 

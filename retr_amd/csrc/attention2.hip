@@ -32,6 +32,18 @@ typedef __attribute__((ext_vector_type(4))) short s16x4;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
+typedef __attribute__((ext_vector_type(2))) float f2v;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
+
+// four scores -> elements 4 half .. 4 half + 3 of a bf16x8 MFMA fragment held as u32x4: two
+// v_cvt_pk_bf16_f32 (a per-element (bf16) conversion compiles to one cvt per score + a v_perm
+// per pair)
+RETR_DEVICE void put4(u32x4& w, int half, const float (&v)[4]) {
+  const f2v lo = {v[0], v[1]}, hi = {v[2], v[3]};
+  w[2 * half] = __builtin_bit_cast(uint32_t, __builtin_convertvector(lo, bf16x2v));
+  w[2 * half + 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(hi, bf16x2v));
+}
+
 RETR_DEVICE f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -191,7 +203,9 @@ RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
 #pragma unroll
       for (int e = 0; e < 16; ++e) O[dt][e] *= alpha;
   }
-  bf16x8 pf[4];
+  // P as bf16 pairs (one v_cvt_pk_bf16_f32 per two scores; per-element conversions compiled
+  // to one cvt per score plus a v_perm per pair)
+  u32x4 pw[4];
 #pragma unroll
   for (int sub = 0; sub < 2; ++sub) {
     uint32_t wbits = 0;                          // keep bits of keys key0 + 32 sub + j
@@ -203,6 +217,7 @@ RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
         b01 = attn_pair_bits(rowkey, kk);
         b23 = attn_pair_bits(rowkey, kk + 2);
       }
+      float pv[4];
 #pragma unroll
       for (int e4 = 0; e4 < 4; ++e4) {
         const int e = 4 * g + e4;
@@ -213,11 +228,21 @@ RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
           wbits |= (uint32_t)kp << (8 * g + 4 * hh + e4);
           p = kp ? p : 0.f;
         }
-        pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
+        pv[e4] = p;
+      }
+      // scores e = 4 g .. 4 g + 3 are elements 4 (g & 1) .. + 3 of pf[2 sub + (g >> 1)]
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const f2v v = {pv[2 * h2], pv[2 * h2 + 1]};
+        pw[2 * sub + (g >> 1)][2 * (g & 1) + h2] =
+            __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
       }
     }
     if (DROP && dmask) store_dmask(dmask, wbits, hh, bh, Lq, Lk, qi, key0 / 32 + sub);
   }
+  bf16x8 pf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) pf[s] = __builtin_bit_cast(bf16x8, pw[s]);
   // O^T += V^T P^T  (A = V^T via transposed LDS reads, B = P in registers)
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
@@ -644,7 +669,7 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
 #pragma unroll
         for (int e = 0; e < 16; ++e) O[dt][e] *= alpha;
     }
-    bf16x8 pf[4];
+    u32x4 pw[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       uint32_t wbits = 0;
@@ -656,6 +681,7 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
           b01 = attn_pair_bits(rowkey, kk);
           b23 = attn_pair_bits(rowkey, kk + 2);
         }
+        float pv[4];
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           const int e = 4 * g + e4;
@@ -666,11 +692,15 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
             wbits |= (uint32_t)kp << (8 * g + 4 * hh + e4);
             p = kp ? p : 0.f;
           }
-          pf[2 * sub + (e >> 3)][e & 7] = (bf16)p;
+          pv[e4] = p;
         }
+        put4(pw[2 * sub + (g >> 1)], g & 1, pv);
       }
       if (drop && dmask) store_dmask(dmask, wbits, hh, (b * H + h), Lq, Lk, qi, key0 / 32 + sub);
     }
+    bf16x8 pf[4];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) pf[q4] = __builtin_bit_cast(bf16x8, pw[q4]);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
@@ -828,7 +858,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
       }
     }
     // dS = P (drop(dP) - D); masking only on tiles that hold padded / causal-boundary keys
-    bf16x8 sf[4];
+    u32x4 sw[4];
     auto scores = [&](auto maskc) {
       constexpr bool MASK = decltype(maskc)::value;
 #pragma unroll
@@ -841,6 +871,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
             b01 = attn_pair_bits(rowkey, kk);
             b23 = attn_pair_bits(rowkey, kk + 2);
           }
+          float sv[4];
 #pragma unroll
           for (int e4 = 0; e4 < 4; ++e4) {
             const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
@@ -852,12 +883,16 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
                                       : attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
               dpv = kp ? dpv * dp.scale : 0.f;
             }
-            sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - Dq));
+            sv[e4] = p * (dpv - Dq);
           }
+          put4(sw[2 * sub + (g >> 1)], g & 1, sv);
         }
     };
     if (anym) scores(std::true_type{});
     else scores(std::false_type{});
+    bf16x8 sf[4];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) sf[q4] = __builtin_bit_cast(bf16x8, sw[q4]);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
@@ -1011,7 +1046,7 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
     // P and dS.  Padded keys (kmask) are left unmasked here -- a lane's accumulators are only
     // ever its own key's dK / dV columns, written as zeros below -- and the row / causal masks
     // run only on tiles that hold rows past Lq or cross this wave's diagonal
-    bf16x8 pf[4], sf[4];
+    u32x4 pw[4], sw[4];
     auto scores = [&](auto maskc) {
       constexpr bool MASK = decltype(maskc)::value;
 #pragma unroll
@@ -1023,6 +1058,7 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
           const f32x4 d4 = *(const f32x4*)(ed + ql);
           uint4 w4 = {0u, 0u, 0u, 0u};
           if constexpr (DM == 1) w4 = *(const uint4*)(exw + it * 64 + ql);
+          float pv[4], sv[4];
 #pragma unroll
           for (int e4 = 0; e4 < 4; ++e4) {
             const int e = 4 * g + e4, qq = qt + ql + e4;
@@ -1037,13 +1073,21 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
               dpv = kp ? dpv * dp.scale : 0.f;
               pmv = kp ? p * dp.scale : 0.f;
             }
-            pf[2 * sub + (e >> 3)][e & 7] = (bf16)pmv;
-            sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - d4[e4]));
+            pv[e4] = pmv;
+            sv[e4] = p * (dpv - d4[e4]);
           }
+          put4(pw[2 * sub + (g >> 1)], g & 1, pv);
+          put4(sw[2 * sub + (g >> 1)], g & 1, sv);
         }
     };
     if (qt + 64 > Lq || (causal && qt < kfirst + 32)) scores(std::true_type{});
     else scores(std::false_type{});
+    bf16x8 pf[4], sf[4];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      pf[q4] = __builtin_bit_cast(bf16x8, pw[q4]);
+      sf[q4] = __builtin_bit_cast(bf16x8, sw[q4]);
+    }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int c0 = dt * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
@@ -1414,7 +1458,7 @@ attn_bwd_dq2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
     const unsigned long long pml = pmask >> (4 * hh);
     const uint32_t pmlo = (uint32_t)pml, pmhi = (uint32_t)(pml >> 32);
     const int mlim = qi - key0 - 4 * hh;
-    bf16x8 sf[4];
+    u32x4 sw[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       f32x16 S, P;
@@ -1434,6 +1478,7 @@ attn_bwd_dq2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
           b01 = attn_pair_bits(rowkey, kk);
           b23 = attn_pair_bits(rowkey, kk + 2);
         }
+        float sv[4];
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
@@ -1441,10 +1486,14 @@ attn_bwd_dq2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
           const float p = msk ? 0.f : __builtin_amdgcn_exp2f(S[e] - lq2);
           float dpv = P[e];
           if (drop) dpv = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16) ? dpv * dp.scale : 0.f;
-          sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - Dq));
+          sv[e4] = p * (dpv - Dq);
         }
+        put4(sw[2 * sub + (g >> 1)], g & 1, sv);
       }
     }
+    bf16x8 sf[4];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) sf[q4] = __builtin_bit_cast(bf16x8, sw[q4]);
     // dQ^T += K^T dS^T
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
@@ -1534,7 +1583,7 @@ attn_bwd_dkdv2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
     if (qt + TL::KT < Lq)
       stg.load(qb, ldq, db, lddo, qt + TL::KT, Lq, lse, D, sbase, seed, drop,
                (uint32_t)((b * H + h) * Lq), tid);
-    bf16x8 pf[4], sf[4];
+    u32x4 pw[4], sw[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       f32x16 S, P;
@@ -1551,6 +1600,7 @@ attn_bwd_dkdv2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
         const int ql = sub * 32 + 8 * g + 4 * hh;               // 4 consecutive queries
         const f32x4 l4 = *(const f32x4*)(ex + ql);
         const f32x4 d4 = *(const f32x4*)(ex + 64 + ql);
+        float pv[4], sv[4];
 #pragma unroll
         for (int e4 = 0; e4 < 4; ++e4) {
           const int e = 4 * g + e4, qq = qt + ql + e4;
@@ -1563,10 +1613,18 @@ attn_bwd_dkdv2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
             dpv = kp ? dpv * dp.scale : 0.f;
             pm = kp ? p * dp.scale : 0.f;
           }
-          pf[2 * sub + (e >> 3)][e & 7] = (bf16)pm;
-          sf[2 * sub + (e >> 3)][e & 7] = (bf16)(p * (dpv - d4[e4]));
+          pv[e4] = pm;
+          sv[e4] = p * (dpv - d4[e4]);
         }
+        put4(pw[2 * sub + (g >> 1)], g & 1, pv);
+        put4(sw[2 * sub + (g >> 1)], g & 1, sv);
       }
+    }
+    bf16x8 pf[4], sf[4];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      pf[q4] = __builtin_bit_cast(bf16x8, pw[q4]);
+      sf[q4] = __builtin_bit_cast(bf16x8, sw[q4]);
     }
     // dV^T += dO^T drop(P);  dK^T += Q^T dS  (A operands by transposed reads of the tiles)
 #pragma unroll

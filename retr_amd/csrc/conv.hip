@@ -1212,6 +1212,67 @@ __global__ void __launch_bounds__(256) cw_table_put_kernel(CWPut c, unsigned* ds
   for (int i = threadIdx.x; i < c.n; i += 256) dst[c.off + i] = c.w[i];
 }
 
+// Every grouped conv's slab sum + OIHW re-layout (+ FrozenBN scale) in ONE launch: 64 chunks of 4
+// input channels per block, the 4 waves take every fourth slice (8 loads in flight) and wave 0
+// adds the 4 partial sums in wave order (wgrad_unpack4w_kernel's arithmetic) -- instead of one
+// unpack launch per conv.
+struct UPJob {
+  const float* ws;
+  const float* scale;
+  float* grad;
+  int Co, Ci, Cp, KHW, splits, accumulate, blk0, pad;
+};
+static_assert(sizeof(UPJob) == 56, "unpack table");
+
+__global__ void __launch_bounds__(256) wgrad_unpack_group_kernel(const char* __restrict__ table) {
+  __shared__ f32x4 red[4][64];
+  const CWHead h = *(const CWHead*)table;
+  const UPJob* J = (const UPJob*)(table + sizeof(CWHead));
+  const int bid = blockIdx.x;
+  if (bid >= h.total) return;
+  int lo = 0, hi = h.nprob - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (J[mid].blk0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const UPJob d = J[lo];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c4 = d.Ci / 4;
+  const long total = (long)d.Co * d.KHW * c4;
+  const long slab = (long)d.Co * d.KHW * d.Cp;
+  const long i = (long)(bid - d.blk0) * 64 + lane;
+  int ci = 0, tap = 0, co = 0;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (i < total) {
+    ci = (int)(i % c4) * 4;
+    const long t = i / c4;
+    tap = (int)(t % d.KHW);
+    co = (int)(t / d.KHW);
+    const float* src = d.ws + ((long)co * d.KHW + tap) * d.Cp + ci;
+    int s = w;
+    for (; s + 28 < d.splits; s += 32) {
+      f32x4 u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = *(const f32x4*)(src + (long)(s + 4 * k) * slab);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v += u[k];
+    }
+    for (; s < d.splits; s += 4) v += *(const f32x4*)(src + (long)s * slab);
+  }
+  red[w][lane] = v;
+  __syncthreads();
+  if (w != 0 || i >= total) return;
+  v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  const float sc = d.scale ? d.scale[co] : 1.f;
+  float* dst = d.grad + ((long)co * d.Ci + ci) * d.KHW + tap;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float x = v[e] * sc;
+    dst[(long)e * d.KHW] = d.accumulate ? dst[(long)e * d.KHW] + x : x;
+  }
+}
+
 // 0: dense 1x1 stride-1, 1: ConvWgradB32 (3x3 / strided), -1: not groupable
 int cw_kind(const Geom& g) {
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) return 0;
@@ -1552,6 +1613,59 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
     table_bytes -= ((sizeof(CWHead) + ord.size() * sizeof(CWProb)) + 255) / 256 * 256;
   }
   return 0;
+}
+
+size_t retr_conv_wgrad_unpack_group_table_bytes(int n) {
+  return n < 0 ? 0 : sizeof(CWHead) + (size_t)n * sizeof(UPJob);
+}
+
+int retr_conv_wgrad_unpack_group(int n, const retr_conv_unpack_desc* d, void* table,
+                                 size_t table_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RETR_REQUIRE(n >= 0 && (n == 0 || d), "conv_wgrad_unpack_group: n=%d", n);
+  RETR_REQUIRE(table && table_bytes >= retr_conv_wgrad_unpack_group_table_bytes(n) &&
+                   ((uintptr_t)table & 15) == 0,
+               "conv_wgrad_unpack_group: table of %zu bytes (need %zu, 16-byte aligned)",
+               table_bytes, retr_conv_wgrad_unpack_group_table_bytes(n));
+  if (n == 0) return 0;
+  std::vector<char> buf(retr_conv_wgrad_unpack_group_table_bytes(n) + 16, 0);
+  CWHead* h = (CWHead*)buf.data();
+  UPJob* J = (UPJob*)(buf.data() + sizeof(CWHead));
+  int blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const retr_conv_unpack_desc& q = d[i];
+    RETR_REQUIRE(q.ws && q.grad && q.Ci % 4 == 0 && q.Cp % 4 == 0 && q.Cp >= q.Ci &&
+                     q.splits >= 1 && ((uintptr_t)q.ws & 15) == 0,
+                 "conv_wgrad_unpack_group[%d]: Co=%d Ci=%d Cp=%d splits=%d", i, q.Co, q.Ci,
+                 q.Cp, q.splits);
+    UPJob& j = J[i];
+    j.ws = q.ws;
+    j.scale = q.scale;
+    j.grad = q.grad;
+    j.Co = q.Co;
+    j.Ci = q.Ci;
+    j.Cp = q.Cp;
+    j.KHW = q.KH * q.KW;
+    j.splits = q.splits;
+    j.accumulate = q.accumulate;
+    j.blk0 = blocks;
+    blocks += (int)cdiv((long)q.Co * j.KHW * (q.Ci / 4), 64);
+  }
+  h->nprob = n;
+  h->total = blocks;
+  const int words = (int)((retr_conv_wgrad_unpack_group_table_bytes(n) + 3) / 4);
+  const unsigned* src = (const unsigned*)buf.data();
+  for (int off = 0; off < words; off += 640) {
+    CWPut c;
+    c.off = off;
+    c.n = words - off < 640 ? words - off : 640;
+    memcpy(c.w, src + off, (size_t)c.n * 4);
+    hipLaunchKernelGGL(cw_table_put_kernel, dim3(1), dim3(256), 0, st, c, (unsigned*)table);
+    if (int e = retr_check_launch("conv_wgrad_unpack_group table")) return e;
+  }
+  hipLaunchKernelGGL(wgrad_unpack_group_kernel, dim3(blocks), dim3(256), 0, st,
+                     (const char*)table);
+  return retr_check_launch("conv_wgrad_unpack_group");
 }
 
 int retr_conv_wgrad_unpack(const float* ws, const float* scale, float* grad, int Co, int Ci,

@@ -4,10 +4,29 @@
 //   wgrad   : dW += dY^T X                 (fp32, split-K + atomics)
 //   bias    : db += colsum(dY)
 #include "gemm2.hpp"
+#include "splitk_fused.hpp"
 #include "epilogues.hpp"
 #include "../../include/retr_hip.h"
 
 using namespace retr;
+
+namespace retr {
+static __device__ int g_splitk_tickets[1 << 16];   // zero at load; every last arriver re-zeroes
+static int g_splitk_cursor = 0;
+int* splitk_tickets(int n) {
+  static int* base = nullptr;
+  if (!base) {
+    void* a = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_splitk_tickets)) != hipSuccess) return nullptr;
+    base = (int*)a;
+  }
+  if (n > (1 << 16)) return nullptr;
+  if (g_splitk_cursor + n > (1 << 16)) g_splitk_cursor = 0;
+  int* p = base + g_splitk_cursor;
+  g_splitk_cursor += (n + 63) / 64 * 64;
+  return p;
+}
+}  // namespace retr
 
 namespace {
 
@@ -118,11 +137,25 @@ int norm_splits_k(int K, int BK, int splits) {
   return cdiv(K, cdiv(ksteps, splits) * BK);
 }
 
+
 template <typename T, class LA, class LB, class EP>
 int splitk_run(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, float* ws,
                int splits, int fam_dgrad, hipStream_t st, const char* what) {
   constexpr int BK = Elem<T>::BK;
   splits = norm_splits_k(K, BK, splits);
+  if constexpr (sizeof(T) == 2) {
+    // slice reduction + epilogue by each tile's last-arriving block (splitk_fused.hpp)
+    if (retr_tune_get(RETR_TUNE_SPLITK_FUSED) == 1 && N % 8 == 0 && splits > 1) {
+      const long t128 = (long)cdiv(M, 128) * cdiv(N, 128) * splits;
+      if (t128 >= 160)
+        return fam_dgrad
+                   ? launch_splitk_fused<kFamLinearDgrad, 128, 128, 4, 2, 2>(la, lb, ep, ws, M, N, K, splits, st, what)
+                   : launch_splitk_fused<kFamLinearFwd, 128, 128, 4, 2, 2>(la, lb, ep, ws, M, N, K, splits, st, what);
+      return fam_dgrad
+                 ? launch_splitk_fused<kFamLinearDgrad, 64, 64, 2, 2, 2>(la, lb, ep, ws, M, N, K, splits, st, what)
+                 : launch_splitk_fused<kFamLinearFwd, 64, 64, 2, 2, 2>(la, lb, ep, ws, M, N, K, splits, st, what);
+    }
+  }
   EpiAccF32 acc{ws, (long)N, 0, 0, 1, nullptr};
   acc.split_stride = (long)M * N;
   acc.set_vec();

@@ -224,16 +224,29 @@ def _conv_wgrad_group(items, grads):
         nbytes = int(_lib.load().retr_conv2d_wgrad_group_table_bytes(n)) + 512
         table = torch.empty(nbytes, dtype=torch.uint8, device=G0.device)
         call("retr_conv2d_wgrad_group", dcode(G0.dtype), n, arr, ptr(table), nbytes, _st())
-    for i, (spec, G, x, shape) in enumerate(items):
-        ws = slabs[i]
-        if ws is None:
-            continue
+    jobs = [i for i in range(n) if slabs[i] is not None]
+    if not jobs:
+        return
+    ua = (_lib.ConvUnpackDesc * len(jobs))()
+    for j, i in enumerate(jobs):
+        spec, G, x, shape = items[i]
         _, _, _, scale = PACKS.get(spec, G.dtype)
-        grad, _ = grad_buffer(spec.conv.weight)     # sole writer: overwrite mode below
-        call("retr_conv_wgrad_unpack", ptr(ws), ptr(scale), ptr(grad), spec.cout, spec.cin,
-             shape[3], spec.k, spec.k, 0, arr[i].splits, _st())
+        grad, _ = grad_buffer(spec.conv.weight)     # sole writer: overwrite mode
+        u = ua[j]
+        u.ws, u.scale, u.grad = ptr(slabs[i]), ptr(scale), ptr(grad)
+        u.Co, u.Ci, u.Cp, u.KH, u.KW = spec.cout, spec.cin, shape[3], spec.k, spec.k
+        u.splits, u.accumulate = arr[i].splits, 0
         grads[spec.conv.weight] = grad
         CONV_WGRAD_STATS["grouped"] += 1
+    if all(ua[j].Ci % 4 == 0 for j in range(len(jobs))):
+        nb = int(_lib.load().retr_conv_wgrad_unpack_group_table_bytes(len(jobs)))
+        utab = torch.empty((nb + 15) // 16 * 16, dtype=torch.uint8, device=G0.device)
+        call("retr_conv_wgrad_unpack_group", len(jobs), ua, ptr(utab), utab.numel(), _st())
+        return
+    for j in range(len(jobs)):                   # channel counts off the 4-wide chunks
+        u = ua[j]
+        call("retr_conv_wgrad_unpack", u.ws, u.scale, u.grad, u.Co, u.Ci, u.Cp, u.KH, u.KW, 0,
+             u.splits, _st())
 
 
 def _conv_tail_cat(runner, blk, h2, s2, x, xshape):

@@ -1373,4 +1373,60 @@ def test_conv_wgrad_group_matches_fp32_and_single_path():
         one = torch.empty(co, c, k, k, device=DEV)
         call("retr_conv_wgrad_unpack", ptr(ws1), None, ptr(one), co, c, c, k, k, 0, sp, ops._st())
         assert rel_err(got, one) < 1e-6, (geos[i], rel_err(got, one))
+    # every problem's slab sum + OIHW re-layout (+ a per-channel scale) in one grouped launch
+    ua = (_lib.ConvUnpackDesc * n)()
+    outs, scales = [], []
+    for i, (x, dy, (nb, h, w, c, co, k, s, p, d)) in enumerate(items):
+        sc = torch.rand(co, generator=g).to(DEV) + 0.5
+        o = torch.full((co, c, k, k), float("nan"), device=DEV)
+        u = ua[i]
+        u.ws, u.scale, u.grad = ptr(slabs[i]), ptr(sc), ptr(o)
+        u.Co, u.Ci, u.Cp, u.KH, u.KW, u.splits, u.accumulate = co, c, c, k, k, arr[i].splits, 0
+        outs.append(o)
+        scales.append(sc)
+    nb2 = int(_lib.load().retr_conv_wgrad_unpack_group_table_bytes(n))
+    utab = torch.empty((nb2 + 15) // 16 * 16, dtype=torch.uint8, device=DEV)
+    call("retr_conv_wgrad_unpack_group", n, ua, ptr(utab), utab.numel(), ops._st())
+    for i, (x, dy, (nb, h, w, c, co, k, s, p, d)) in enumerate(items):
+        one = torch.empty(co, c, k, k, device=DEV)
+        call("retr_conv_wgrad_unpack", ptr(slabs[i]), ptr(scales[i]), ptr(one), co, c, c, k, k,
+             0, arr[i].splits, ops._st())
+        assert rel_err(outs[i], one) < 1e-6, (geos[i], rel_err(outs[i], one))
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("M,N,K", [(6400, 256, 2048), (2048, 256, 2048), (1000, 264, 1800)])
+def test_splitk_fused_equals_slab_epilogue(M, N, K):
+    """Split-K linears with the slice sum + epilogue done by each tile's last-arriving block
+    (RETR_TUNE_SPLITK_FUSED 1, csrc/splitk_fused.hpp) against the slabs + separate
+    slab-epilogue launch (knob 0): bitwise equal (both add the slices in slice order), forward
+    with bias + residual + dropout (fp32 out) and data gradient with addend + ReLU gate (bf16
+    out); repeated launches (tickets re-armed) stay bitwise identical."""
+    bf = torch.bfloat16
+    assert _lib.load().retr_linear_splits(1, M, N, K) > 1
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    x = torch.randn(M, K, generator=g).to(DEV).to(bf)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV).to(bf)
+    b = torch.randn(N, generator=g).to(DEV)
+    res = torch.randn(M, N, generator=g).to(DEV)
+    dy = torch.randn(M, K, generator=g).to(DEV).to(bf)
+    add = torch.randn(M, N, generator=g).to(DEV).to(bf)
+    gate = torch.randn(M, N, generator=g).to(DEV).to(bf)
+    wt = ops._TView(w.t().contiguous())
+    outs = []
+    try:
+        for knob in (0, 1, 1, 1):
+            _lib.load().retr_tune(18, knob)
+            y = torch.full((M, N), float("nan"), device=DEV)
+            ops.k_linear_fwd(x, w, b, y, res=res, drop_p=0.1, seed=91)
+            dx = torch.full((M, N), float("nan"), dtype=bf, device=DEV)
+            ops.k_linear_dgrad(dy, wt, dx, addend=add, gate=gate)
+            torch.cuda.synchronize()
+            outs.append((y, dx))
+    finally:
+        _lib.load().retr_tune(18, 0)
+    for y, dx in outs[1:]:
+        assert torch.equal(y, outs[0][0])
+        assert torch.equal(dx, outs[0][1])
+    ref = x.float() @ w.float().t() + b
+    assert rel_err(outs[1][0], ref + res) < 0.5   # dropout applied: only a sanity bound

@@ -62,6 +62,7 @@ VARIANTS = {
     "wb128": {("TUNE", 2): 128},
     "wside_on": {("ATTR", "WGRAD_SIDE"): True},
     "cwg_off": {("RESNET", "CONV_WGRAD_GROUP"): False},
+    "skf": {("TUNE", 18): 1},
 }
 
 
@@ -79,7 +80,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17):
+    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
