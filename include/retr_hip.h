@@ -122,7 +122,9 @@ enum {
   RETR_TUNE_SPLITK_FUSED = 18,  /* split-K forward / data-gradient linears: 0 slabs + a separate
                                    slab-epilogue launch, 1 slice sum + epilogue by each tile's
                                    last-arriving block (csrc/splitk_fused.hpp) */
-  RETR_TUNE_COUNT = 19
+  RETR_TUNE_WB_CHUNK = 19,      /* logical blocks per XCD turn in retr_linear_wgrad_batch (0: 4) */
+  RETR_TUNE_CW_CHUNK = 20,      /* logical blocks per XCD turn in retr_conv2d_wgrad_group (0: 4) */
+  RETR_TUNE_COUNT = 21
 };
 int retr_tune(int knob, int value);
 

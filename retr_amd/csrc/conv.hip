@@ -1168,11 +1168,12 @@ static_assert(sizeof(CWProb) == 96 && sizeof(CWHead) == 16, "conv wgrad table");
 constexpr int kCWChunk = 4;
 
 template <int KIND>
-__global__ void __launch_bounds__(KIND ? 512 : 256) conv_wgrad_group_kernel(const char* __restrict__ table) {
+__global__ void __launch_bounds__(KIND ? 512 : 256) conv_wgrad_group_kernel(const char* __restrict__ table,
+                                                                            int chunk) {
   const CWHead h = *(const CWHead*)table;
   const CWProb* P = (const CWProb*)(table + sizeof(CWHead));
   const int hw = blockIdx.x, xc = hw & 7, q = hw >> 3;
-  const int L = (q / kCWChunk) * (8 * kCWChunk) + xc * kCWChunk + q % kCWChunk;
+  const int L = (q / chunk) * (8 * chunk) + xc * chunk + q % chunk;
   if (L >= h.total) return;
   int lo = 0, hi = h.nprob - 1;
   while (lo < hi) {
@@ -1587,7 +1588,9 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
       hipLaunchKernelGGL(cw_table_put_kernel, dim3(1), dim3(256), 0, st, c, (unsigned*)table);
       if (int e = retr_check_launch("conv2d_wgrad_group table")) return e;
     }
-    const int grid = cdiv(blocks, 8 * kCWChunk) * 8 * kCWChunk;
+    int chunk = retr_tune_get(RETR_TUNE_CW_CHUNK);
+    if (chunk <= 0) chunk = kCWChunk;
+    const int grid = cdiv(blocks, 8 * chunk) * 8 * chunk;
     constexpr size_t lds = gemm2_lds_bytes<128, 128, 2, 0>();
     if (kind == 0) {
       auto kern = conv_wgrad_group_kernel<0>;
@@ -1596,7 +1599,7 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr0 = true;
       }
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, (const char*)table);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, (const char*)table, chunk);
     } else {
       auto kern = conv_wgrad_group_kernel<1>;
       static bool attr1 = false;
@@ -1604,7 +1607,7 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         attr1 = true;
       }
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, (const char*)table);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, (const char*)table, chunk);
     }
     if (int e = retr_check_launch(kind == 0 ? "conv2d_wgrad_group 1x1" : "conv2d_wgrad_group")) return e;
     // the next kind's table must not overwrite this one before the launch has read it: use

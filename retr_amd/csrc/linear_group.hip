@@ -604,7 +604,8 @@ size_t wb_table_bytes(int n, int nx) {
 }
 
 template <int BM, int S>
-__global__ void __launch_bounds__(256) wgrad_batch_kernel(const char* __restrict__ table) {
+__global__ void __launch_bounds__(256) wgrad_batch_kernel(const char* __restrict__ table,
+                                                          int chunk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const WBHead h = *(const WBHead*)table;
   const WBProb* P = (const WBProb*)(table + sizeof(WBHead));
@@ -613,7 +614,7 @@ __global__ void __launch_bounds__(256) wgrad_batch_kernel(const char* __restrict
   // turns, so the longest problems (sorted first) spread over every XCD while a run of
   // neighbouring tiles (shared operand panels) stays in one L2
   const int hw = blockIdx.x, x = hw & 7, q = hw >> 3;
-  const int L = (q / kWBChunk) * (8 * kWBChunk) + x * kWBChunk + q % kWBChunk;
+  const int L = (q / chunk) * (8 * chunk) + x * chunk + q % chunk;
   if (L >= h.total) return;
   if (L >= h.gemm_blocks) {
     const int rb = L - h.gemm_blocks;
@@ -695,8 +696,10 @@ int wgrad_batch_launch(const char* table, int total, hipStream_t st) {
       attr_set = true;
     }
   }
-  const int grid = cdiv(total, 8 * kWBChunk) * 8 * kWBChunk;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, table);
+  int chunk = retr_tune_get(RETR_TUNE_WB_CHUNK);
+  if (chunk <= 0) chunk = kWBChunk;
+  const int grid = cdiv(total, 8 * chunk) * 8 * chunk;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, table, chunk);
   return retr_check_launch("linear_wgrad_batch");
 }
 

@@ -63,6 +63,11 @@ VARIANTS = {
     "wside_on": {("ATTR", "WGRAD_SIDE"): True},
     "cwg_off": {("RESNET", "CONV_WGRAD_GROUP"): False},
     "skf": {("TUNE", 18): 1},
+    "wbc16": {("TUNE", 19): 16},
+    "wbc64": {("TUNE", 19): 64},
+    "cwc16": {("TUNE", 20): 16},
+    "cwc64": {("TUNE", 20): 64},
+    "c16": {("TUNE", 19): 16, ("TUNE", 20): 16},
 }
 
 
@@ -80,7 +85,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18):
+    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"

@@ -21,7 +21,7 @@ from tools.prof_summary import from_csv, from_db  # noqa: E402
 
 def main():
     path = sys.argv[1]
-    rows = from_db(path) if path.endswith(".db") else from_csv(path)
+    rows = list(from_db(path) if path.endswith(".db") else from_csv(path))   # read twice below
     if "--steps" in sys.argv:
         steps = int(sys.argv[sys.argv.index("--steps") + 1])
         src = "--steps"
