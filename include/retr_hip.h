@@ -124,7 +124,11 @@ enum {
                                    last-arriving block (csrc/splitk_fused.hpp) */
   RETR_TUNE_WB_CHUNK = 19,      /* logical blocks per XCD turn in retr_linear_wgrad_batch (0: 4) */
   RETR_TUNE_CW_CHUNK = 20,      /* logical blocks per XCD turn in retr_conv2d_wgrad_group (0: 4) */
-  RETR_TUNE_COUNT = 21
+  RETR_TUNE_CONV3X3 = 21,       /* bf16 3x3 stride-1 convs (fwd / dgrad): 0 the direct kernel with
+                                   the input halo in LDS on maps >= 32 wide (csrc/conv3x3.hip),
+                                   1 the implicit GEMM, 2 the direct kernel on every map >= 16 */
+  RETR_TUNE_C3_TILE = 22,       /* direct 3x3 kernel tile variant (sweeps; 0 auto) */
+  RETR_TUNE_COUNT = 23
 };
 int retr_tune(int knob, int value);
 

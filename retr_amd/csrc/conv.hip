@@ -16,6 +16,15 @@
 
 using namespace retr;
 
+namespace retr {
+bool conv3x3_direct_ok(int H, int W, int CI, int CO);
+int conv3x3_fwd_direct(const bf16* x, const bf16* w, const float* bias, bf16* y, int relu, int Nb,
+                       int H, int W, int CI, int CO, hipStream_t st);
+int conv3x3_dgrad_direct(const bf16* dy, const bf16* wt, bf16* dx, const bf16* addend,
+                         const bf16* gate, int Nb, int H, int W, int CI_out, int CO_in,
+                         hipStream_t st);
+}  // namespace retr
+
 namespace {
 
 struct Geom {
@@ -740,6 +749,13 @@ int conv_fwd_t(const void* x, Geom g, const void* w, const float* bias, const vo
     return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd_1x1", true,
                                        res != nullptr && K <= 64);
   }
+  // 3x3 stride-1 pad-1: the direct kernel, input halo resident in LDS (conv3x3.hip)
+  if constexpr (sizeof(T) == 2) {
+    if (g.KH == 3 && g.KW == 3 && g.s == 1 && g.p == 1 && g.d == 1 && !res && relu &&
+        conv3x3_direct_ok(g.H, g.W, g.C, g.Co))
+      return conv3x3_fwd_direct((const bf16*)x, (const bf16*)w, bias, (bf16*)y, relu, g.Nb, g.H,
+                                g.W, g.C, g.Co, st);
+  }
   // (1x1 strided convs keep ConvFwdA: a single tap gains nothing and measured slower)
   if (sizeof(T) == 2 && g.C % 64 == 0 && g.KH * g.KW > 1 && g.KH * g.KW <= 32) {
     ConvFwdAU<T> la{(const T*)x, g, M, K};
@@ -850,6 +866,13 @@ int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* a
           return e;
       }
     return 0;
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (g.KH == 3 && g.KW == 3 && g.s == 1 && g.p == 1 && g.d == 1 &&
+        conv3x3_direct_ok(g.H, g.W, g.Co, g.C))
+      return conv3x3_dgrad_direct((const bf16*)dy, (const bf16*)wt, (bf16*)dx,
+                                  (const bf16*)addend, (const bf16*)gate, g.Nb, g.H, g.W, g.Co,
+                                  g.C, st);
   }
   if (sizeof(T) == 2 && g.s == 1 && g.Co % 64 == 0 && g.KH * g.KW <= 32) {
     ConvDgradAU<T> la{(const T*)dy, g, M, K};

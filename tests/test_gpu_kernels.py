@@ -1430,3 +1430,49 @@ def test_splitk_fused_equals_slab_epilogue(M, N, K):
         assert torch.equal(dx, outs[0][1])
     ref = x.float() @ w.float().t() + b
     assert rel_err(outs[1][0], ref + res) < 0.5   # dropout applied: only a sanity bound
+
+
+@pytest.mark.parametrize("nb,H,W,C,Co", [(16, 80, 80, 128, 128), (8, 40, 40, 256, 256),
+                                         (4, 20, 20, 512, 512), (2, 26, 18, 64, 128),
+                                         (3, 40, 40, 128, 256)])
+def test_conv3x3_direct_matches_implicit_gemm_and_fp32(nb, H, W, C, Co):
+    """The direct 3x3 stride-1 kernel (csrc/conv3x3.hip: input halo resident in LDS, one halo
+    load per 64-channel chunk for all nine taps) against the implicit GEMM (RETR_TUNE_CONV3X3
+    1) and fp32 torch on the same bf16 operands: forward (bias + ReLU, bf16 out) and data
+    gradient (ReLU gate); ragged maps (26 x 18) and both tile shapes (16- and 20-pixel rows)."""
+    import torch.nn.functional as F
+    from torch.nn.grad import conv2d_input
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(H * W + C)
+    x = torch.randn(nb, H, W, C, generator=g).to(DEV, bf)
+    w = (torch.randn(Co, C, 3, 3, generator=g) / math.sqrt(9 * C)).to(DEV)
+    b = torch.randn(Co, generator=g).to(DEV)
+    wf = w.permute(0, 2, 3, 1).contiguous().to(bf)          # [Co][3][3][C] forward pack
+    wt = w.permute(1, 2, 3, 0).contiguous().to(bf)          # [C][3][3][Co] dgrad pack
+    dy = torch.randn(nb, H, W, Co, generator=g).to(DEV, bf)
+    gate = torch.randn(nb, H, W, C, generator=g).to(DEV, bf)
+    res = {}
+    try:
+        for knob in (2, 1):                     # 2: the direct kernel on every map (>= 16 wide)
+            _lib.load().retr_tune(21, knob)
+            y = torch.full((nb, H, W, Co), float("nan"), dtype=bf, device=DEV)
+            call("retr_conv2d_fwd", 1, ptr(x), nb, H, W, C, ptr(wf), ptr(b), None, ptr(y), Co,
+                 3, 3, 1, 1, 1, 1, ops._st())
+            dx = torch.full((nb, H, W, C), float("nan"), dtype=bf, device=DEV)
+            call("retr_conv2d_dgrad", 1, ptr(dy), nb, H, W, C, ptr(wt), ptr(dx), Co, 3, 3, 1, 1,
+                 1, None, ptr(gate), ops._st())
+            torch.cuda.synchronize()
+            res[knob] = (y.float(), dx.float())
+    finally:
+        _lib.load().retr_tune(21, 0)
+    xr = x.float().permute(0, 3, 1, 2)
+    wr = wf.float().permute(0, 3, 1, 2)
+    yref = torch.relu(F.conv2d(xr, wr, b, padding=1)).permute(0, 2, 3, 1)
+    dxr = conv2d_input(xr.shape, wr, dy.float().permute(0, 3, 1, 2), padding=1)
+    dxr = (dxr.permute(0, 2, 3, 1) * (gate.float() > 0))
+    for knob in (2, 1):
+        assert rel_err(res[knob][0], yref) < 1e-2, (knob, rel_err(res[knob][0], yref))
+        assert rel_err(res[knob][1], dxr) < 1e-2, (knob, rel_err(res[knob][1], dxr))
+    # same products in another fixed order: within bf16 rounding of the implicit GEMM
+    assert rel_err(res[2][0], res[1][0]) < 5e-3
+    assert rel_err(res[2][1], res[1][1]) < 5e-3
