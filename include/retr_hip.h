@@ -128,7 +128,14 @@ enum {
                                    the input halo in LDS on maps >= 32 wide (csrc/conv3x3.hip),
                                    1 the implicit GEMM, 2 the direct kernel on every map >= 16 */
   RETR_TUNE_C3_TILE = 22,       /* direct 3x3 kernel tile variant (sweeps; 0 auto) */
-  RETR_TUNE_COUNT = 23
+  RETR_TUNE_PANEL = 23,         /* bf16 linears with K <= 256 into N >= 1024 (FFN expansions and
+                                   their gated data gradients): 0 the 64x64 gemm2 tile, 1 the
+                                   resident-A panel kernel (csrc/panel.hpp; measured 0.39 ms/step
+                                   slower, profiles/r4_ab_panel_rejected.txt) */
+  RETR_TUNE_PANEL_GROUPS = 24,  /* column-tile runs per row panel (0: ~512 blocks) */
+  RETR_TUNE_PANEL_CONV = 25,    /* 1: also the 1x1 stride-1 convs with K <= 256 into >= 1024
+                                   channels on the panel kernel (A/B) */
+  RETR_TUNE_COUNT = 26
 };
 int retr_tune(int knob, int value);
 

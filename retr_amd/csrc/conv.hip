@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "gemm2.hpp"
+#include "panel.hpp"
 #include "epilogues.hpp"
 #include "../../include/retr_hip.h"
 
@@ -746,6 +747,12 @@ int conv_fwd_t(const void* x, Geom g, const void* w, const float* bias, const vo
   ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseK<T> la{(const T*)x, (long)g.C, M, K};
+    // short reductions into >= 1024 channels: the resident-A panel kernel (panel.hpp)
+    if constexpr (sizeof(T) == 2) {
+      if (K <= 256 && K % 64 == 0 && N >= 1024 && retr_tune_get(RETR_TUNE_PANEL) == 1 &&
+          retr_tune_get(RETR_TUNE_PANEL_CONV) == 1)
+        return launch_panel<kFamConvFwd>(la, lb, ep, M, N, K, st, "conv_fwd_1x1");
+    }
     return launch_auto<kFamConvFwd, T>(la, lb, ep, M, N, K, 1, st, "conv_fwd_1x1", true,
                                        res != nullptr && K <= 64);
   }
@@ -802,6 +809,11 @@ int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* a
   ep.set_vec();
   if (g.KH == 1 && g.KW == 1 && g.s == 1 && g.p == 0) {
     DenseK<T> la{(const T*)dy, (long)g.Co, M, K};
+    if constexpr (sizeof(T) == 2) {
+      if (K <= 256 && K % 64 == 0 && N >= 1024 && retr_tune_get(RETR_TUNE_PANEL) == 1 &&
+          retr_tune_get(RETR_TUNE_PANEL_CONV) == 1)
+        return launch_panel<kFamConvDgrad>(la, lb, ep, M, N, K, st, "conv_dgrad_1x1");
+    }
     return launch_auto<kFamConvDgrad, T>(la, lb, ep, M, N, K, 1, st, "conv_dgrad_1x1", true);
   }
   if (g.s == 2 && g.d == 1) {

@@ -5,6 +5,7 @@
 //   bias    : db += colsum(dY)
 #include "gemm2.hpp"
 #include "splitk_fused.hpp"
+#include "panel.hpp"
 #include "epilogues.hpp"
 #include "../../include/retr_hip.h"
 
@@ -48,6 +49,11 @@ int launch_linear(const LA& la, const LB& lb, const EP& ep, int M, int N, int K,
           retr_tune_get(RETR_TUNE_LIN_SMALL) == 2)
         return launch_gemm2<FAM, 32, 64, 1, 4, 2>(la, lb, ep, M, N, K, 1, st, what);
     }
+    // short reductions into wide outputs (the FFN expansions and their gated data gradients):
+    // the A panel resident in LDS, B streamed over a run of column tiles (panel.hpp) -- opt-in
+    // only: measured slower than the 64x64 tile's wider grid (profiles/r4_ab_panel_rejected.txt)
+    if (K <= 256 && K % 64 == 0 && N >= 1024 && M >= 64 && retr_tune_get(RETR_TUNE_PANEL) == 1)
+      return launch_panel<FAM>(la, lb, ep, M, N, K, st, what);
     // short reductions (K <= 256: the FFN expansions) run 15-20 % faster on the 64x64
     // two-stage tile than on 128x128 (tools/linear_micro.py, profiles/r2_linear_tiles.txt)
     if ((long)cdiv(M, 128) * cdiv(N, 128) >= 160 && K >= 128)

@@ -108,7 +108,9 @@ panel_kernel(LA la, LB lb, EP ep, int M, int N, int K, int npb, int ngroups) {
         for (int e = 0; e < 4; ++e)
           ct[(wm * WTM + 16 * i + 4 * (lane >> 4) + e) * CS + wn * WTN + 16 * j + (lane & 15)] =
               acc[i][j][e];
-    __syncthreads();
+    // LDS-only barriers: __syncthreads() would also drain the B stages in flight (vmcnt(0))
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
     constexpr int CH = BN / 8;
     for (int r = tid; r < BM * CH; r += NT) {
       const int rr = r / CH, c = (r % CH) * 8;
@@ -123,7 +125,8 @@ panel_kernel(LA la, LB lb, EP ep, int M, int N, int K, int npb, int ngroups) {
         for (int e = 0; e < 8 && n + e < N; ++e) ep.apply(m, n + e, v[e]);
       }
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();                                   // staging area free for the next tile
   }
 }
 

@@ -1476,3 +1476,41 @@ def test_conv3x3_direct_matches_implicit_gemm_and_fp32(nb, H, W, C, Co):
     # same products in another fixed order: within bf16 rounding of the implicit GEMM
     assert rel_err(res[2][0], res[1][0]) < 5e-3
     assert rel_err(res[2][1], res[1][1]) < 5e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(6400, 2048, 256), (2048, 2048, 256), (1000, 1800, 192),
+                                   (640, 1024, 128)])
+def test_panel_gemm_equals_tile_gemm(M, N, K):
+    """Short-reduction wide-output linears on the resident-A panel kernel (csrc/panel.hpp,
+    RETR_TUNE_PANEL 1, opt-in) against the 64x64 gemm2 tile (knob 0, the default): bitwise equal (same MFMA chain
+    per output), forward with bias + ReLU (bf16 out) and the ReLU-gated data gradient with the
+    weight both as W^T (K-contiguous) and as W read transposed; ragged M and N; vs fp32 torch."""
+    bf = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV).to(bf)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV).to(bf)
+    b = torch.randn(N, generator=g).to(DEV)
+    dy = torch.randn(M, K, generator=g).to(DEV).to(bf)            # dX[M][N] = dY[M][K] W2[K][N]
+    w2 = (torch.randn(K, N, generator=g) / math.sqrt(K)).to(DEV).to(bf)
+    gate = torch.randn(M, N, generator=g).to(DEV).to(bf)
+    outs = {}
+    try:
+        for knob in (0, 1):
+            _lib.load().retr_tune(23, knob)
+            y = torch.full((M, N), float("nan"), dtype=bf, device=DEV)
+            ops.k_linear_fwd(x, w, b, y, relu=1)
+            d1 = torch.full((M, N), float("nan"), dtype=bf, device=DEV)
+            ops.k_linear_dgrad(dy, w2.t().contiguous(), d1, gate=gate)       # W^T stored [N][K]
+            d2 = torch.full((M, N), float("nan"), dtype=bf, device=DEV)
+            ops.k_linear_dgrad(dy, ops._TView(w2), d2, gate=gate)            # W [K][N] transposed
+            torch.cuda.synchronize()
+            outs[knob] = (y, d1, d2)
+    finally:
+        _lib.load().retr_tune(23, 0)
+    for a, c in zip(outs[1], outs[0]):
+        assert torch.equal(a, c)
+    ref = torch.relu(x.float() @ w.float().t() + b)
+    assert rel_err(outs[1][0].float(), ref) < 1e-2
+    dref = (dy.float() @ w2.float()) * (gate.float() > 0)
+    assert rel_err(outs[1][1].float(), dref) < 1e-2
+    assert torch.equal(outs[1][1], outs[1][2])

@@ -69,6 +69,10 @@ VARIANTS = {
     "cwc64": {("TUNE", 20): 64},
     "c16": {("TUNE", 19): 16, ("TUNE", 20): 16},
     "c3_off": {("TUNE", 21): 1},
+    "panel_on": {("TUNE", 23): 1},
+    "pg4": {("TUNE", 23): 1, ("TUNE", 24): 4},
+    "pg16": {("TUNE", 23): 1, ("TUNE", 24): 16},
+    "pconv": {("TUNE", 23): 1, ("TUNE", 25): 1},
 }
 
 
@@ -86,7 +90,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21):
+    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
