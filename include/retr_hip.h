@@ -135,7 +135,11 @@ enum {
   RETR_TUNE_PANEL_GROUPS = 24,  /* column-tile runs per row panel (0: ~512 blocks) */
   RETR_TUNE_PANEL_CONV = 25,    /* 1: also the 1x1 stride-1 convs with K <= 256 into >= 1024
                                    channels on the panel kernel (A/B) */
-  RETR_TUNE_COUNT = 26
+  RETR_TUNE_ATTN_KEEPPRE = 26,  /* bf16 streaming attention forward with dropout and saved keep
+                                   bits: 0 hashed inside the forward, 1 pregenerated by
+                                   attn_keep_bits_kernel and read by the forward (0.036 ms/step
+                                   slower, profiles/r4_ab_keep_bits.txt) */
+  RETR_TUNE_COUNT = 27
 };
 int retr_tune(int knob, int value);
 

@@ -93,16 +93,26 @@ RETR_DEVICE bool key_masked(uint32_t lo, uint32_t hi, int kc, bool diag, int lim
   return (bit != 0u) | (diag & (kc > lim));
 }
 
+// The padding bits and the causal test are first merged into one 32-bit word per sub-tile (bit
+// j: key 32 sub + j of the lane's phase is masked), then each score is a constant-position bit
+// test + select (3 VALU; was ~6 with the per-score shifts and the causal compare).  The
+// bfe / bfi pair (2 VALU) is not reachable from C: the compiler canonicalises it back to this
+// form, and inline asm that reads the MFMA result would bypass its hazard tracking.
 RETR_DEVICE void mask_tile(f32x16 (&S)[2], unsigned long long pmask, bool diag, int lim, int hh) {
   const unsigned long long pm = pmask >> (4 * hh);
-  const uint32_t lo = (uint32_t)pm, hi = (uint32_t)(pm >> 32);
+  uint32_t w[2] = {(uint32_t)pm, (uint32_t)(pm >> 32)};
+  const uint32_t dm = diag ? ~0u : 0u;
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    const int L = lim - 32 * sub;                       // key j masked when j > L
+    const uint32_t cm = L < 0 ? ~0u : (L >= 31 ? 0u : (~0u << (L + 1)));
+    w[sub] |= cm & dm;
+  }
 #pragma unroll
   for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int kc = sub * 32 + (e & 3) + 8 * (e >> 2);
-      S[sub][e] = key_masked(lo, hi, kc, diag, lim) ? -INFINITY : S[sub][e];
-    }
+    for (int e = 0; e < 16; ++e)
+      S[sub][e] = (w[sub] >> ((e & 3) + 8 * (e >> 2))) & 1u ? -INFINITY : S[sub][e];
 }
 
 // Dropout keep bits saved by the forward for the backward kernels (retr_attention_fwd_dm /
@@ -116,6 +126,42 @@ RETR_DEVICE void store_dmask(uint32_t* dmask, uint32_t wbits, int hh, int bh, in
   const uint32_t full = wbits | (uint32_t)__shfl_xor((int)wbits, 32, 64);
   const int nw = (Lk + 31) / 32;
   if (hh == 0 && qi < Lq && w < nw) dmask[((long)bh * nw + w) * Lq + qi] = full;
+}
+
+// Keep bits of the two 32-key words of 64-key tile t for this lane's query (zero past the
+// last word or query): the DMIN forwards' per-tile loads, one tile ahead.
+RETR_DEVICE void load_dw(uint32_t (&dw)[2], const uint32_t* dmask, int bh, int Lq, int Lk, int qi,
+                         int t) {
+  const int nw = (Lk + 31) / 32, w = 2 * t;
+  const bool ok = qi < Lq;
+  const uint32_t* p = dmask + ((long)bh * nw + w) * Lq + qi;
+  dw[0] = ok && w < nw ? p[0] : 0u;
+  dw[1] = ok && w + 1 < nw ? p[Lq] : 0u;
+}
+
+// Attention-dropout keep bits of a whole (B*H, Lq, Lk) call, one thread per word of the
+// [B*H][ceil(Lk/32)][Lq] layout (store_dmask's): the same (row key, key-pair) hash decisions the
+// hashing forward takes, for every key of the word, so the saved mask is bit-identical either
+// way.  Pure integer VALU (~4 us for the encoder's 20 M scores); run right before a DMIN forward.
+__global__ void __launch_bounds__(256) attn_keep_bits_kernel(uint32_t* dmask, int BH, int Lq,
+                                                             int Lk, DropoutParams dp) {
+  const int nw = (Lk + 31) / 32;
+  const long n = (long)BH * nw * Lq;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int qi = (int)(i % Lq);
+  const long rest = i / Lq;
+  const int w = (int)(rest % nw), bh = (int)(rest / nw);
+  const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
+  const uint32_t rowkey = attn_row_key(dp_seed(dp), (uint32_t)bh * Lq + qi);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int j = 0; j < 32; j += 2) {
+    const uint32_t b = attn_pair_bits(rowkey, 32 * w + j);
+    bits |= (uint32_t)((b & 0xffffu) >= th16) << j;
+    bits |= (uint32_t)((b >> 16) >= th16) << (j + 1);
+  }
+  dmask[i] = bits;
 }
 
 template <int HD>
@@ -164,11 +210,15 @@ struct KVStager {
 // masking, the online-softmax update of (m, l, O) and O^T += V^T drop(P)^T.
 // DROP / MASK compile-time (the kernels branch once per tile, wave-uniformly, on whether the
 // tile holds padded or causal-boundary keys): no per-score runtime selects in the common case.
-template <int HD, bool DROP, bool MASK>
+// DMIN: the keep bits of the tile's two 32-key words come in dw (pregenerated by
+// attn_keep_bits_kernel, the same hash decisions) instead of being hashed here (~9 VALU per
+// score: the pair hash, the 16-bit compare, the bit packing); nothing is stored.
+template <int HD, bool DROP, bool MASK, bool DMIN = false>
 RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
     const char* Kl, const char* Vl, const bf16x8 (&qf)[HD / 16], f32x16 (&O)[HD / 32], float& m,
     float& l, int key0, unsigned long long pmask, bool diag, int qi, int lane,
-    uint32_t rowkey, uint32_t th16, uint32_t* dmask, int bh, int Lq, int Lk) {
+    uint32_t rowkey, uint32_t th16, uint32_t* dmask, int bh, int Lq, int Lk,
+    const uint32_t (&dw)[2] = {0u, 0u}) {
   using TL = Tile<HD>;
   constexpr int KS = HD / 16, DT = HD / 32;
   const int r = lane & 31, hh = lane >> 5;
@@ -213,17 +263,25 @@ RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
     for (int g = 0; g < 4; ++g) {
       const int kk = key0 + sub * 32 + 8 * g + 4 * hh;   // 4 consecutive keys
       uint32_t b01 = 0, b23 = 0;
-      if constexpr (DROP) {
+      if constexpr (DROP && !DMIN) {
         b01 = attn_pair_bits(rowkey, kk);
         b23 = attn_pair_bits(rowkey, kk + 2);
       }
       float pv[4];
+      // S - max for two scores per v_pk_add_f32 (the same per-element differences)
+      const f2v msv = {ms, ms};
+      const f2v d01 = f2v{S[sub][4 * g], S[sub][4 * g + 1]} - msv;
+      const f2v d23 = f2v{S[sub][4 * g + 2], S[sub][4 * g + 3]} - msv;
 #pragma unroll
       for (int e4 = 0; e4 < 4; ++e4) {
-        const int e = 4 * g + e4;
-        float p = __builtin_amdgcn_exp2f(S[sub][e] - ms);
+        float p = __builtin_amdgcn_exp2f(e4 < 2 ? d01[e4] : d23[e4 - 2]);
         l += p;
-        if constexpr (DROP) {
+        if constexpr (DROP && DMIN) {
+          // bit (8 g + 4 hh + e4) of the word as an all-ones / zero mask: v_bfe_i32 + v_and
+          // (a shift / compare form compiles to and + cmp + cndmask)
+          const int km = __builtin_amdgcn_sbfe((int)dw[sub], 8 * g + 4 * hh + e4, 1);
+          p = __builtin_bit_cast(float, __builtin_bit_cast(int, p) & km);
+        } else if constexpr (DROP) {
           const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
           wbits |= (uint32_t)kp << (8 * g + 4 * hh + e4);
           p = kp ? p : 0.f;
@@ -238,7 +296,7 @@ RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
             __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
       }
     }
-    if (DROP && dmask) store_dmask(dmask, wbits, hh, bh, Lq, Lk, qi, key0 / 32 + sub);
+    if (DROP && !DMIN && dmask) store_dmask(dmask, wbits, hh, bh, Lq, Lk, qi, key0 / 32 + sub);
   }
   bf16x8 pf[4];
 #pragma unroll
@@ -303,7 +361,7 @@ RETR_DEVICE void fwd_finish(const f32x16 (&O)[HD / 32], float m, float l, bf16* 
 // ~1.6 waves per SIMD (encoder 400 x 400) or less (cross 128 x 400).  At the end the parities'
 // (m, l, O) go through LDS and parity 0 merges them in parity order (deterministic; the same
 // products as the unsplit kernel, summed in another fixed order).
-template <int HD, int NQ, int KSP, bool DROP>
+template <int HD, int NQ, int KSP, bool DROP, bool DMIN>
 __global__ void __launch_bounds__(NQ * KSP * 64)
 attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
                   bf16* o, long ldo, int H, int Lq, int Lk, int kbr, const unsigned char* kpm,
@@ -335,7 +393,8 @@ attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* 
 
   constexpr bool drop = DROP;
   const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
-  const uint32_t rowkey = drop ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
+  const uint32_t rowkey =
+      drop && !DMIN ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
 
   f32x16 O[DT];
 #pragma unroll
@@ -350,6 +409,8 @@ attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* 
     stg[j].load(kb, ldk, vb, ldv, j * TL::KT, Lk, tid);
     stg[j].store(smem + j * TL::STAGE, tid);
   }
+  uint32_t dw[2] = {0u, 0u};
+  if constexpr (DMIN) load_dw(dw, dmask, b * H + h, Lq, Lk, qi, par);
   __syncthreads();
 
   for (int it = 0; it < nit; ++it) {
@@ -359,6 +420,9 @@ attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* 
       for (int j = 0; j < KSP; ++j) stg[j].load(kb, ldk, vb, ldv, ((it + 1) * KSP + j) * TL::KT, Lk, tid);
     }
     const int t = it * KSP + par;
+    uint32_t dwc[2] = {dw[0], dw[1]};
+    if constexpr (DMIN)
+      if (t + KSP < wtiles) load_dw(dw, dmask, b * H + h, Lq, Lk, qi, t + KSP);
     if (t < wtiles) {
       const int key0 = t * TL::KT;
       bool pad = key0 + lane >= Lk;
@@ -367,11 +431,11 @@ attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* 
       const bool diag = causal && (key0 + TL::KT - 1 > q0);
       const char* Kl = slot + par * TL::STAGE;
       if (pmask || diag)
-        fwd2_tile<HD, DROP, true>(Kl, Kl + TL::BYTES, qf, O, m, l, key0, pmask, diag, qi, lane,
-                                  rowkey, th16, dmask, b * H + h, Lq, Lk);
+        fwd2_tile<HD, DROP, true, DMIN>(Kl, Kl + TL::BYTES, qf, O, m, l, key0, pmask, diag, qi,
+                                        lane, rowkey, th16, dmask, b * H + h, Lq, Lk, dwc);
       else
-        fwd2_tile<HD, DROP, false>(Kl, Kl + TL::BYTES, qf, O, m, l, key0, pmask, diag, qi, lane,
-                                   rowkey, th16, dmask, b * H + h, Lq, Lk);
+        fwd2_tile<HD, DROP, false, DMIN>(Kl, Kl + TL::BYTES, qf, O, m, l, key0, pmask, diag, qi,
+                                         lane, rowkey, th16, dmask, b * H + h, Lq, Lk, dwc);
     }
     if (it + 1 < nit) {
 #pragma unroll
@@ -411,7 +475,7 @@ attn_fwd2s_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* 
   fwd_finish<HD>(O, m, l, o, ldo, b, h, H, qi, Lq, hh, drop, dp.scale, lse);
 }
 
-template <int HD, int NW, bool DROP>
+template <int HD, int NW, bool DROP, bool DMIN>
 __global__ void __launch_bounds__(NW * 64)
 attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v, long ldv,
                  bf16* o, long ldo, int H, int Lq, int Lk, int kbr, const unsigned char* kpm,
@@ -438,7 +502,8 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
 
   constexpr bool drop = DROP;
   const uint32_t th16 = (dp.thresh + 0x8000u) >> 16;
-  const uint32_t rowkey = drop ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
+  const uint32_t rowkey =
+      drop && !DMIN ? attn_row_key(dp_seed(dp), ((uint32_t)b * H + h) * Lq + qi) : 0u;
 
   f32x16 O[DT];
 #pragma unroll
@@ -450,6 +515,8 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
   KVStager<HD, NT> stg;
   stg.load(kb, ldk, vb, ldv, 0, Lk, tid);
   stg.store(smem, tid);
+  uint32_t dw[2] = {0u, 0u};
+  if constexpr (DMIN) load_dw(dw, dmask, b * H + h, Lq, Lk, qi, 0);
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
@@ -457,6 +524,9 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
     const char* Kl = smem + (t & 1) * TL::STAGE;
     const char* Vl = Kl + TL::BYTES;
     if (t + 1 < ntiles) stg.load(kb, ldk, vb, ldv, key0 + TL::KT, Lk, tid);
+    uint32_t dwc[2] = {dw[0], dw[1]};
+    if constexpr (DMIN)
+      if (t + 1 < ntiles) load_dw(dw, dmask, b * H + h, Lq, Lk, qi, t + 1);
     // padding mask of the tile's 64 keys, wave-uniform
     bool pad = key0 + lane >= Lk;
     if (kpm && !pad) pad = kpm[(long)b * Lk + key0 + lane] != 0;
@@ -464,16 +534,30 @@ attn_fwd2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
     const bool diag = causal && (key0 + TL::KT - 1 > q0);
 
     if (pmask || diag)
-      fwd2_tile<HD, DROP, true>(Kl, Vl, qf, O, m, l, key0, pmask, diag, qi, lane, rowkey, th16,
-                                dmask, b * H + h, Lq, Lk);
+      fwd2_tile<HD, DROP, true, DMIN>(Kl, Vl, qf, O, m, l, key0, pmask, diag, qi, lane, rowkey,
+                                      th16, dmask, b * H + h, Lq, Lk, dwc);
     else
-      fwd2_tile<HD, DROP, false>(Kl, Vl, qf, O, m, l, key0, pmask, diag, qi, lane, rowkey, th16,
-                                 dmask, b * H + h, Lq, Lk);
+      fwd2_tile<HD, DROP, false, DMIN>(Kl, Vl, qf, O, m, l, key0, pmask, diag, qi, lane, rowkey,
+                                       th16, dmask, b * H + h, Lq, Lk, dwc);
     if (t + 1 < ntiles) stg.store(smem + ((t + 1) & 1) * TL::STAGE, tid);
     __syncthreads();
   }
 
   fwd_finish<HD>(O, m, l, o, ldo, b, h, H, qi, Lq, hh, drop, dp.scale, lse);
+}
+
+// RETR_TUNE_ATTN_KEEPPRE = 1: pregenerate the call's keep bits (attn_keep_bits_kernel) when
+// dropout is on and the caller saves them (training), and let the forward read them instead of
+// hashing.  Opt-in: the hashing moves out of the forward but is not cheaper, and the extra
+// launch made the graphed step 0.036 ms slower (profiles/r4_ab_keep_bits.txt).
+bool keep_bits_pre(const DropoutParams& dp, uint32_t* dmask, int BH, int Lq, int Lk,
+                   hipStream_t st) {
+  if (dp.thresh == 0 || !dmask || retr_tune_get(RETR_TUNE_ATTN_KEEPPRE) != 1) return false;
+  const long n = (long)BH * ((Lk + 31) / 32) * Lq;
+  if (n == 0) return false;
+  hipLaunchKernelGGL(attn_keep_bits_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     dmask, BH, Lq, Lk, dp);
+  return retr_check_launch("attention_keep_bits") == 0;
 }
 
 template <int HD, int NW>
@@ -485,7 +569,10 @@ int launch_fwd2(const void* q, long ldq, const void* k, long ldk, const void* v,
   const size_t lds = 2 * Tile<HD>::STAGE;
   dim3 grid((Lq + 32 * NW - 1) / (32 * NW), H, B);
   const DropoutParams dp = make_dp(p, seed);
-  auto kern = dp.thresh != 0 ? attn_fwd2_kernel<HD, NW, true> : attn_fwd2_kernel<HD, NW, false>;
+  const bool dmin = keep_bits_pre(dp, dmask, B * H, Lq, Lk, st);
+  auto kern = dp.thresh == 0 ? attn_fwd2_kernel<HD, NW, false, false>
+              : dmin         ? attn_fwd2_kernel<HD, NW, true, true>
+                             : attn_fwd2_kernel<HD, NW, true, false>;
   hipLaunchKernelGGL(kern, grid, dim3(NW * 64), lds, st, (const bf16*)q, ldq, (const bf16*)k, ldk,
                      (const bf16*)v, ldv, (bf16*)o, ldo, H, Lq, Lk, kbr, kpm, causal, qscale, dp,
                      lse, dmask);
@@ -500,8 +587,10 @@ int launch_fwd2s(const void* q, long ldq, const void* k, long ldk, const void* v
   const float qscale = kLog2e / sqrtf((float)HD);
   const size_t lds = 2 * KSP * Tile<HD>::STAGE;
   const DropoutParams dp = make_dp(p, seed);
-  auto kern = dp.thresh != 0 ? attn_fwd2s_kernel<HD, NQ, KSP, true>
-                             : attn_fwd2s_kernel<HD, NQ, KSP, false>;
+  const bool dmin = keep_bits_pre(dp, dmask, B * H, Lq, Lk, st);
+  auto kern = dp.thresh == 0 ? attn_fwd2s_kernel<HD, NQ, KSP, false, false>
+              : dmin         ? attn_fwd2s_kernel<HD, NQ, KSP, true, true>
+                             : attn_fwd2s_kernel<HD, NQ, KSP, true, false>;
   if (lds > 65536)
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);

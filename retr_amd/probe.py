@@ -240,7 +240,7 @@ FAMILY_SYMBOL = {"linear_fwd": "gemm{,2,2_group}_kernel<0,",
                  "conv_fwd": "gemm{,2}_kernel<3, + bottleneck_s1_kernel + stem_pool_kernel",
                  "conv_dgrad": "gemm{,2}_kernel<4,",
                  "conv_wgrad": "gemm{,2}_kernel<5, + conv_wgrad_group_kernel",
-                 "attention_fwd": "attn_fwd{,2,2s}_kernel",
+                 "attention_fwd": "attn_fwd{,2,2s}_kernel + attn_keep_bits_kernel",
                  "attention_bwd": "attn_bwd_"}
 
 
@@ -259,7 +259,7 @@ def family_of_symbol(name):
         return "conv_wgrad"
     if "bottleneck_s1_kernel" in name or "stem_pool_kernel" in name:
         return "conv_fwd"
-    if re.search(r"attn_fwd\d*s?_kernel", name):
+    if re.search(r"attn_fwd\d*s?_kernel", name) or "attn_keep_bits_kernel" in name:
         return "attention_fwd"
     if "attn_bwd_" in name:
         return "attention_bwd"

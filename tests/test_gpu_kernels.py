@@ -962,6 +962,48 @@ def test_attention_saved_dropout_bits_equal_rehash(B, H, Lq, Lk, hd, causal, mas
     assert abs(bits.mean() - (1 - p)) < 0.005, bits.mean()
 
 
+@pytest.mark.parametrize("B,H,Lq,Lk,hd,causal,masked,fs", [
+    (16, 8, 400, 400, 32, False, True, 0), (16, 8, 128, 400, 32, False, False, 0),
+    (16, 8, 128, 128, 32, True, False, 0), (3, 8, 100, 77, 32, False, True, 1),
+    (3, 8, 100, 300, 32, True, True, 4), (2, 8, 130, 200, 64, False, True, 2),
+    (2, 8, 200, 200, 64, True, True, 1)])
+def test_attention_pregenerated_keep_bits(B, H, Lq, Lk, hd, causal, masked, fs):
+    """Training forwards with saved dropout bits: attn_keep_bits_kernel writes every keep word
+    and the streaming forward reads them (RETR_TUNE_ATTN_KEEPPRE 1, opt-in) instead of hashing
+    per score (knob 0, the default: the forward writes the bits itself).  Outputs, log-sum-exp and
+    every word the hashing forward writes are bitwise equal, on the unsplit and key-split
+    kernels (fs: RETR_TUNE_ATTN_FSPLIT), ragged, causal and key-padded shapes, hd 32 / 64."""
+    g = torch.Generator(device="cpu").manual_seed(Lq * 7 + Lk)
+    C, p = H * hd, 0.1
+    bf = torch.bfloat16
+    q, k, v = (torch.randn(B * L, C, generator=g).to(DEV).to(bf) for L in (Lq, Lk, Lk))
+    kpm = None
+    if masked:
+        kpm = torch.zeros(B, Lk, dtype=torch.uint8)
+        kpm[:, Lk - Lk // 5:] = 1
+        kpm = kpm.to(DEV)
+    outs = {}
+    _lib.load().retr_tune(12, fs)
+    try:
+        for pre in (0, 1):
+            _lib.load().retr_tune(26, pre)
+            dm = ops.attn_dmask(B, H, Lq, Lk, p, bf, hd, DEV)
+            dm.fill_(0)
+            o = torch.empty(B * Lq, C, dtype=bf, device=DEV)
+            lse = torch.empty(B * H * Lq, device=DEV)
+            ops.k_attention_fwd(q, k, v, o, B, H, Lq, Lk, hd, kpm, causal, p, 11, lse, None, dm)
+            torch.cuda.synchronize()
+            outs[pre] = (o, lse, dm)
+    finally:
+        _lib.load().retr_tune(26, 0)
+        _lib.load().retr_tune(12, 0)
+    (o1, l1, d1), (o0, l0, d0) = outs[1], outs[0]     # pregenerated, hashing forward
+    assert torch.equal(o0, o1) and torch.equal(l0, l1)
+    w = d0 != 0 if causal else torch.ones_like(d0, dtype=torch.bool)
+    assert torch.equal(d0[w], d1[w])
+    assert w.float().mean().item() > (0.2 if causal else 0.99)   # words the comparison covers
+
+
 @pytest.mark.parametrize("B,H,Lq,Lk,hd,causal,masked", [
     (16, 8, 128, 400, 32, False, True), (16, 8, 128, 128, 32, True, False),
     (3, 8, 100, 77, 32, False, True), (3, 8, 100, 300, 32, True, True),

@@ -73,6 +73,7 @@ VARIANTS = {
     "pg4": {("TUNE", 23): 1, ("TUNE", 24): 4},
     "pg16": {("TUNE", 23): 1, ("TUNE", 24): 16},
     "pconv": {("TUNE", 23): 1, ("TUNE", 25): 1},
+    "kb_on": {("TUNE", 26): 1},
 }
 
 
@@ -90,7 +91,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25):
+    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
