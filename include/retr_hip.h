@@ -66,6 +66,32 @@ int retr_linear_fwd_splitk(int dtype, const void* x, long ldx, const void* w, lo
                            const float* bias, void* y, long ldy, int y_f32, int M, int N, int K,
                            int relu, const float* residual, long ldr, float drop_p,
                            unsigned long long seed, float* ws, int splits, void* stream);
+
+/* LayerNorm of a residual-stream linear's output, produced by that linear's epilogue (the
+ * following pre-norm block's LN, or the stack's final norm: models/ConcatTransformer.py's
+ * norm -> attention / FFN order): y = LN(out) and y2 = LN(out) + pos[row % period] (either may be
+ * null), row statistics mean / rstd for the backward. */
+typedef struct retr_ln_out {
+  const float* gamma;
+  const float* beta;
+  float eps;
+  int y_bf16;           /* y / y2 element type: 1 bf16, 0 fp32 (the fused kernel takes bf16) */
+  void* y;
+  void* y2;
+  long ldy;
+  const float* pos;
+  int period;
+  float* mean;
+  float* rstd;
+} retr_ln_out;
+/* retr_linear_fwd_splitk (fp32 out) + retr_layernorm_fwd of its output in one epilogue launch
+ * after the slices (bf16, N 256 / 512); any other case runs the two calls.  Replaces the
+ * FFResidual output -> next norm pair of models/ConcatTransformer.py:171-257. */
+int retr_linear_fwd_splitk_ln(int dtype, const void* x, long ldx, const void* w, long ldw,
+                              const float* bias, float* y, long ldy, int M, int N, int K, int relu,
+                              const float* residual, long ldr, float drop_p,
+                              unsigned long long seed, float* ws, int splits,
+                              const retr_ln_out* ln, void* stream);
 int retr_linear_dgrad_splitk(int dtype, const void* dy, long lddy, const void* w, long ldw,
                              void* dx, long lddx, int dx_f32, int M, int N, int K,
                              const void* addend, int addend_f32, long lda, const void* gate,

@@ -63,6 +63,12 @@ class ConvUnpackDesc(ctypes.Structure):
                 ("KH", _I), ("KW", _I), ("splits", _I), ("accumulate", _I), ("pad", _I)]
 
 
+class LnOut(ctypes.Structure):
+    """retr_ln_out"""
+    _fields_ = [("gamma", _P), ("beta", _P), ("eps", _F), ("y_bf16", _I), ("y", _P), ("y2", _P),
+                ("ldy", _L), ("pos", _P), ("period", _I), ("mean", _P), ("rstd", _P)]
+
+
 class ConvPackDesc(ctypes.Structure):
     """retr_conv_pack_desc"""
     _fields_ = [("w", _P), ("bn_w", _P), ("bn_b", _P), ("bn_rm", _P), ("bn_rv", _P),
@@ -105,6 +111,8 @@ _SIGS = {
     "retr_ffn_bwd_data": [_P, _L, _P, _P, _L, _P, _P, _L, _P, _L, _I, _I, _I, _P, _I, _P],
     "retr_linear_fwd_splitk": [_I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _I, _P, _L, _F,
                                _U64, _P, _I, _P],
+    "retr_linear_fwd_splitk_ln": [_I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _P, _L, _F,
+                                  _U64, _P, _I, ctypes.POINTER(LnOut), _P],
     "retr_linear_dgrad_splitk": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _L, _P, _L,
                                  _I, _P, _I, _P],
     "retr_linear_wgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _I, _P],

@@ -144,6 +144,129 @@ int norm_splits_k(int K, int BK, int splits) {
 }
 
 
+// The split-K slices alone (fp32 slabs ws[s][M][N]); the caller runs the slab epilogue.
+template <typename T, class LA, class LB>
+int splitk_slabs(const LA& la, const LB& lb, int M, int N, int K, float* ws, int splits,
+                 int fam_dgrad, hipStream_t st, const char* what) {
+  EpiAccF32 acc{ws, (long)N, 0, 0, 1, nullptr};
+  acc.split_stride = (long)M * N;
+  acc.set_vec();
+  if constexpr (sizeof(T) == 2) {
+    return fam_dgrad ? launch_big<kFamLinearDgrad>(la, lb, acc, M, N, K, splits, st, what)
+                     : launch_big<kFamLinearFwd>(la, lb, acc, M, N, K, splits, st, what);
+  } else {
+    return fam_dgrad ? launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, acc, M, N, K, splits, st, what)
+                     : launch_gemm<kFamLinearFwd, T, 64, 64>(la, lb, acc, M, N, K, splits, st, what);
+  }
+}
+
+// Slab epilogue of a residual-stream linear (fp32 out, N = 256 NCH) fused with the LayerNorm
+// that reads its output next (the following pre-norm block's, or the stack's final norm): one
+// wave per row, a lane owns 4 consecutive columns per 256-column chunk.  The slab sum (slice
+// order), the EpiFwd arithmetic (bias, ReLU, dropout, residual) and the LayerNorm (ln_fwd4's
+// statistics and output expressions, norm.hip) are each the unfused kernels' own, so out, LN(out),
+// LN(out) + pos, mean and rstd equal the slab_epilogue_kernel + retr_layernorm_fwd path bitwise;
+// the LayerNorm launch and its re-read of out are gone.
+template <int NCH>
+__global__ void __launch_bounds__(256)
+slab_epilogue_ln_kernel(const float* ws, int splits, int M, EpiFwd<float, float> ep,
+                        retr_ln_out ln) {
+  constexpr int N = 256 * NCH;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const long MN = (long)M * N;
+  const float* p = ws + (long)row * N + 4 * lane;
+  f32x4 v[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // every load of a group of four slices in flight before the adds (slice order kept)
+  int s0 = 0;
+  for (; s0 + 3 < splits; s0 += 4) {
+    f32x4 a[4][NCH];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) a[u][j] = *(const f32x4*)(p + (s0 + u) * MN + 256 * j);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[j][e] += a[u][j][e];
+  }
+  for (; s0 < splits; ++s0)
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const f32x4 a = *(const f32x4*)(p + s0 * MN + 256 * j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] += a[e];
+    }
+  const uint32_t rk = ep.dp.thresh ? drop_row_key(dp_seed(ep.dp), (uint32_t)row) : 0u;
+  const uint32_t th = drop_th16(ep.dp.thresh);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = 4 * lane + 256 * j;
+    if (ep.bias) {
+      const f32x4 b = *(const f32x4*)(ep.bias + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] += b[e];
+    }
+    if (ep.relu == 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = fmaxf(v[j][e], 0.f);
+    }
+    if (ep.dp.thresh) {
+      const uint32_t km = drop_keep4(rk, (uint32_t)c, th);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = ((km >> e) & 1u) ? v[j][e] * ep.dp.scale : 0.f;
+    }
+    if (ep.res) {
+      const f32x4 r = *(const f32x4*)(ep.res + (long)row * ep.ldr + c);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] += r[e];
+    }
+    if (ep.relu == 2) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = fmaxf(v[j][e], 0.f);
+    }
+    *(f32x4*)(ep.out + (long)row * ep.ldo + c) = v[j];
+    s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+  }
+  const float mean = wave_sum(s) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[j][e] - mean;
+      q += d * d;
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / N + ln.eps);
+  const float* pr = ln.pos ? ln.pos + (long)(row % ln.period) * N + 4 * lane : nullptr;
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = 4 * lane + 256 * j;
+    const f32x4 g = *(const f32x4*)(ln.gamma + c), b = *(const f32x4*)(ln.beta + c);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mean) * rstd * g[e] + b[e];
+    if (ln.y)
+      *(bf16x4*)((bf16*)ln.y + (long)row * ln.ldy + c) =
+          bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+    if (ln.y2) {
+      const f32x4 o2 = o + *(const f32x4*)(pr + 256 * j);
+      *(bf16x4*)((bf16*)ln.y2 + (long)row * ln.ldy + c) =
+          bf16x4{(bf16)o2[0], (bf16)o2[1], (bf16)o2[2], (bf16)o2[3]};
+    }
+  }
+  if (lane == 0) {
+    if (ln.mean) ln.mean[row] = mean;
+    if (ln.rstd) ln.rstd[row] = rstd;
+  }
+}
+
 template <typename T, class LA, class LB, class EP>
 int splitk_run(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, float* ws,
                int splits, int fam_dgrad, hipStream_t st, const char* what) {
@@ -162,18 +285,7 @@ int splitk_run(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, fl
                  : launch_splitk_fused<kFamLinearFwd, 64, 64, 2, 2, 2>(la, lb, ep, ws, M, N, K, splits, st, what);
     }
   }
-  EpiAccF32 acc{ws, (long)N, 0, 0, 1, nullptr};
-  acc.split_stride = (long)M * N;
-  acc.set_vec();
-  int e;
-  if constexpr (sizeof(T) == 2) {
-    e = fam_dgrad ? launch_big<kFamLinearDgrad>(la, lb, acc, M, N, K, splits, st, what)
-                  : launch_big<kFamLinearFwd>(la, lb, acc, M, N, K, splits, st, what);
-  } else {
-    e = fam_dgrad ? launch_gemm<kFamLinearDgrad, T, 64, 64>(la, lb, acc, M, N, K, splits, st, what)
-                  : launch_gemm<kFamLinearFwd, T, 64, 64>(la, lb, acc, M, N, K, splits, st, what);
-  }
-  if (e) return e;
+  if (int e = splitk_slabs<T>(la, lb, M, N, K, ws, splits, fam_dgrad, st, what)) return e;
   const long chunks = (long)M * ((N + 7) / 8);
   hipLaunchKernelGGL((slab_epilogue_kernel<EP>), dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0,
                      st, ws, splits, M, N, ep);
@@ -380,6 +492,45 @@ int retr_linear_fwd_splitk(int dtype, const void* x, long ldx, const void* w, lo
   RETR_REQUIRE(K % 4 == 0 && ldx % 4 == 0 && ldw % 4 == 0, "linear_fwd_splitk: K/ld must be %%4");
   return linear_fwd_splitk_t<float, float>(x, ldx, w, ldw, bias, y, ldy, M, N, K, relu, residual,
                                            ldr, drop_p, seed, ws, splits, st);
+}
+
+int retr_linear_fwd_splitk_ln(int dtype, const void* x, long ldx, const void* w, long ldw,
+                              const float* bias, float* y, long ldy, int M, int N, int K, int relu,
+                              const float* residual, long ldr, float drop_p,
+                              unsigned long long seed, float* ws, int splits,
+                              const retr_ln_out* ln, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (M == 0) return 0;
+  RETR_REQUIRE(splits >= 1 && ws != nullptr && ln != nullptr, "linear_fwd_splitk_ln: splits=%d",
+               splits);
+  auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  auto a8 = [](const void* q) { return ((uintptr_t)q & 7) == 0; };
+  const bool fused = dtype == RETR_BF16 && ln->y_bf16 && N % 256 == 0 && N <= 512 &&
+                     K % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0 && ldy % 4 == 0 &&
+                     ldr % 4 == 0 && ln->ldy % 4 == 0 && a16(y) && a16(bias) && a16(residual) &&
+                     a16(ws) && a16(ln->gamma) && a16(ln->beta) && a16(ln->pos) && a8(ln->y) &&
+                     a8(ln->y2) && (ln->pos == nullptr || ln->period > 0);
+  if (!fused) {
+    // two launches with the same results: the split-K linear, then the LayerNorm
+    if (int e = retr_linear_fwd_splitk(dtype, x, ldx, w, ldw, bias, y, ldy, 1, M, N, K, relu,
+                                       residual, ldr, drop_p, seed, ws, splits, stream))
+      return e;
+    return retr_layernorm_fwd(ln->y_bf16 ? RETR_BF16 : RETR_F32, y, ldy, ln->gamma, ln->beta,
+                              ln->eps, M, N, ln->y, ln->ldy, ln->y2, ln->pos, ln->period,
+                              ln->mean, ln->rstd, stream);
+  }
+  DenseK<bf16> la{(const bf16*)x, ldx, M, K};
+  DenseK<bf16> lb{(const bf16*)w, ldw, N, K};
+  splits = norm_splits_k(K, Elem<bf16>::BK, splits);
+  if (int e = splitk_slabs<bf16>(la, lb, M, N, K, ws, splits, 0, st, "linear_fwd_splitk_ln"))
+    return e;
+  EpiFwd<float, float> ep{y, ldy, bias, residual, ldr, relu, make_dp(drop_p, seed), (long)N};
+  const dim3 grid((unsigned)cdiv(M, 4));
+  if (N == 256)
+    hipLaunchKernelGGL(slab_epilogue_ln_kernel<1>, grid, dim3(256), 0, st, ws, splits, M, ep, *ln);
+  else
+    hipLaunchKernelGGL(slab_epilogue_ln_kernel<2>, grid, dim3(256), 0, st, ws, splits, M, ep, *ln);
+  return retr_check_launch("linear_fwd_splitk_ln");
 }
 
 int retr_linear_dgrad_splitk(int dtype, const void* dy, long lddy, const void* w, long ldw,

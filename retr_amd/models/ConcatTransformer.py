@@ -102,7 +102,8 @@ class ConcatTransformer(nn.Module):
         pe, period = self.position_rows(B, S)
         x = src_rows
         atts = []
-        for layer in self.encoder.layers:
+        layers = list(self.encoder.layers)
+        for i, layer in enumerate(layers):
             sa = layer.self_attn
             r = ops.self_attn_block(sa, x, pe, period, B, S, kpm_src, False, self.training,
                                     cdtype, want_probs=want_att)
@@ -112,7 +113,12 @@ class ConcatTransformer(nn.Module):
             else:
                 x = r
             ff = layer.ff
-            x = ops.ffn_block(ff, x, self.training, cdtype)
+            # the LayerNorm that reads this FFN's output, for its down-projection's epilogue
+            if i + 1 < len(layers):
+                nxt = (layers[i + 1].self_attn.norm, pe, period, True, True)
+            else:
+                nxt = (self.encoder.norm, pe, period, True, True) if self.encoder.norm else None
+            x = ops.ffn_block(ff, x, self.training, cdtype, nxt)
         if self.encoder.norm is None:
             # pre_norm=False: the reference builds no encoder norm (:23-24) and the decoder
             # reads the raw residual stream as memory
@@ -132,7 +138,8 @@ class ConcatTransformer(nn.Module):
         kpm_tgt = tgt_mask.contiguous().view(torch.uint8)
         y = ops.embed_ln(self.embeddings, tgt, self.training)
         att_s, att_x = [], []
-        for layer in self.decoder.layers:
+        layers = list(self.decoder.layers)
+        for i, layer in enumerate(layers):
             sa = layer.tgt_self_attn
             r = ops.self_attn_block(sa, y, qpos, T, B, T, kpm_tgt, True, self.training, cdtype,
                                     want_probs=want_att)
@@ -150,7 +157,9 @@ class ConcatTransformer(nn.Module):
             else:
                 y = r
             ff = layer.ff
-            y = ops.ffn_block(ff, y, self.training, cdtype)
+            nxt = ((layers[i + 1].tgt_self_attn.norm, qpos, T, True, True) if i + 1 < len(layers)
+                   else (self.decoder.norm, None, None, True, False))
+            y = ops.ffn_block(ff, y, self.training, cdtype, nxt)
         hs = ops.ln_pos(y, self.decoder.norm, cdtype)
         return hs, att_s, att_x
 

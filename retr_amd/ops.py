@@ -16,6 +16,7 @@ reference computes as separate PyTorch ops:
 Tensors of the residual stream are fp32; GEMM operands are the compute dtype (bf16 or fp32).
 All ops raise on non-HIP tensors (no CPU fallback).
 """
+import ctypes
 import os
 
 import torch
@@ -255,10 +256,35 @@ def _splits(dtype, M, N, K):
 _SPLITS = {}
 
 
-def k_linear_fwd(x, w, bias, y, relu=0, res=None, drop_p=0.0, seed=0):
+def k_linear_fwd(x, w, bias, y, relu=0, res=None, drop_p=0.0, seed=0, ln=None):
+    """``ln`` = (gamma, beta, eps, ln_y, ln_y2, pos, period, mean, rstd): also LayerNorm the
+    (fp32) output -- in the split-K slab epilogue when the linear splits (retr_linear_fwd_splitk_ln),
+    else by a LayerNorm launch after it."""
     M, K = x.shape
     N = w.shape[0]
     splits = _splits(x.dtype, M, N, K)
+    if ln is not None and splits > 1:
+        g, b, eps, ly, ly2, pos, period, mean, rstd = ln
+        posd = pos.detach().contiguous() if pos is not None else None
+        ref = ly if ly is not None else ly2
+        d = _lib.LnOut(ptr(g), ptr(b), float(eps), int(ref.dtype == torch.bfloat16), ptr(ly),
+                       ptr(ly2), ref.stride(0), ptr(posd), int(period or 1), ptr(mean),
+                       ptr(rstd))
+        ws = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+        call("retr_linear_fwd_splitk_ln", dcode(x.dtype), ptr(x), x.stride(0), ptr(w),
+             w.stride(0), ptr(bias), ptr(y), y.stride(0), M, N, K, relu, ptr(res),
+             res.stride(0) if res is not None else 0, drop_p, seed, ptr(ws), splits,
+             ctypes.byref(d), _st())
+        return
+    if ln is not None:
+        k_linear_fwd(x, w, bias, y, relu, res, drop_p, seed)
+        g, b, eps, ly, ly2, pos, period, mean, rstd = ln
+        posd = pos.detach().contiguous() if pos is not None else None
+        ref = ly if ly is not None else ly2
+        call("retr_layernorm_fwd", dcode(ref.dtype), ptr(y), y.stride(0), ptr(g), ptr(b),
+             float(eps), M, N, ptr(ly), ref.stride(0), ptr(ly2), ptr(posd), int(period or 1),
+             ptr(mean), ptr(rstd), _st())
+        return
     if splits > 1:
         # few output tiles, long reduction (FFN down-projection): ordered fp32 slabs + epilogue
         ws = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
@@ -604,14 +630,19 @@ class _LnPos(torch.autograd.Function):
         _lib.require_device(x)
         M, C = x.shape
         dev = x.device
-        y = torch.empty(M, C, dtype=cdtype, device=dev) if mode in ("plain", "both") else None
-        y2 = torch.empty(M, C, dtype=cdtype, device=dev) if mode in ("pos", "both") else None
-        mean = torch.empty(M, dtype=torch.float32, device=dev)
-        rstd = torch.empty_like(mean)
-        posd = pos.detach().contiguous() if pos is not None else None
-        call("retr_layernorm_fwd", dcode(cdtype), ptr(x), x.stride(0), ptr(gamma), ptr(beta),
-             float(eps), M, C, ptr(y), C, ptr(y2), ptr(posd), int(period or 1), ptr(mean),
-             ptr(rstd), _st())
+        got = _ln_take(x, _ln_key(gamma, beta, eps, pos, period, mode in ("plain", "both"),
+                                  mode in ("pos", "both"), cdtype))
+        if got is not None:
+            y, y2, mean, rstd = got
+        else:
+            y = torch.empty(M, C, dtype=cdtype, device=dev) if mode in ("plain", "both") else None
+            y2 = torch.empty(M, C, dtype=cdtype, device=dev) if mode in ("pos", "both") else None
+            mean = torch.empty(M, dtype=torch.float32, device=dev)
+            rstd = torch.empty_like(mean)
+            posd = pos.detach().contiguous() if pos is not None else None
+            call("retr_layernorm_fwd", dcode(cdtype), ptr(x), x.stride(0), ptr(gamma),
+                 ptr(beta), float(eps), M, C, ptr(y), C, ptr(y2), ptr(posd), int(period or 1),
+                 ptr(mean), ptr(rstd), _st())
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.gparams = (gamma, beta, pos)
         ctx.period = period
@@ -663,8 +694,38 @@ def ln_pos(x, norm, cdtype, pos=None, period=None, mode=None, eps=None):
                         norm.eps if eps is None else eps, cdtype, mode)
 
 
+# LayerNorm of a residual-stream tensor produced by the epilogue of the linear that wrote it
+# (retr_linear_fwd_splitk_ln: the FFN down-projection's slab epilogue also normalises its output
+# for the next pre-norm block or the stack's final norm).  The producer tags its output with
+# (key, version, (LN(x), LN(x)+pos, mean, rstd)); the consumer's _ln_fwd takes the tag when the
+# key (the same norm parameters, eps, position table, period and outputs) and the version match,
+# else it launches the LayerNorm as before.  Same bits either way.
+FUSE_LN_NEXT = True
+LN_NEXT_STATS = {"hit": 0, "miss": 0}
+
+
+def _ln_key(gamma, beta, eps, pos, period, plain, with_pos, cdtype):
+    return (id(gamma), id(beta), float(eps), id(pos) if pos is not None else None,
+            int(period or 1) if pos is not None else 1, bool(plain), bool(with_pos), cdtype)
+
+
+def _ln_take(x, key):
+    ent = getattr(x, "_retr_ln", None)
+    if ent is None:
+        return None
+    x._retr_ln = None
+    if ent[0] == key and ent[1] == x._version:
+        LN_NEXT_STATS["hit"] += 1
+        return ent[2]
+    LN_NEXT_STATS["miss"] += 1
+    return None
+
+
 def _ln_fwd(x, gamma, beta, eps, cdtype, pos=None, period=1, plain=True, with_pos=False):
     """LayerNorm kernel: (LN(x) | None, LN(x)+pos[row % period] | None, mean, rstd)."""
+    got = _ln_take(x, _ln_key(gamma, beta, eps, pos, period, plain, with_pos, cdtype))
+    if got is not None:
+        return got
     M, C = x.shape
     dev = x.device
     y = torch.empty(M, C, dtype=cdtype, device=dev) if plain else None
@@ -1040,7 +1101,7 @@ class _FFNBlock(torch.autograd.Function):
     (models/transformer_modules.py:6-11, 77-97) with its pre-norm inside the Function."""
 
     @staticmethod
-    def forward(ctx, x, ln_w, ln_b, eps, w1, b1, w2, b2, drop_res, cdtype):
+    def forward(ctx, x, ln_w, ln_b, eps, w1, b1, w2, b2, drop_res, cdtype, nxt=None):
         _lib.require_device(x)
         n, _, mean, rstd = _ln_fwd(x, ln_w, ln_b, eps, cdtype)
         res = x
@@ -1061,7 +1122,19 @@ class _FFNBlock(torch.autograd.Function):
         else:
             k_linear_fwd(n, w1c, b1.detach(), h, relu=1)
             seed = next_seed()
-            k_linear_fwd(h, w2c, b2.detach(), out, res=res, drop_p=drop_res, seed=seed)
+            lnq = None
+            if nxt is not None and FUSE_LN_NEXT and cdtype == torch.bfloat16:
+                # the next norm's LayerNorm in this linear's epilogue (see _ln_take)
+                g, bb, e2, pos, period, plain, with_pos = nxt
+                ly = torch.empty(M, C, dtype=cdtype, device=dev) if plain else None
+                ly2 = torch.empty(M, C, dtype=cdtype, device=dev) if with_pos else None
+                mean2 = torch.empty(M, dtype=torch.float32, device=dev)
+                rstd2 = torch.empty_like(mean2)
+                lnq = (g, bb, e2, ly, ly2, pos, period, mean2, rstd2)
+            k_linear_fwd(h, w2c, b2.detach(), out, res=res, drop_p=drop_res, seed=seed, ln=lnq)
+            if lnq is not None:
+                out._retr_ln = (_ln_key(g, bb, e2, pos, period, plain, with_pos, cdtype),
+                                out._version, (ly, ly2, mean2, rstd2))
         ctx.splits = splits
         ctx.save_for_backward(n, h, w1, w2, x, ln_w, mean, rstd)
         ctx.gparams = (w1, b1, w2, b2)
@@ -1107,7 +1180,7 @@ class _FFNBlock(torch.autograd.Function):
         else:
             k_linear_wgrad_group(wg)
             dx, dlw, dlb, _ = _ln_bwd(x, ln_w, ctx.ln_b, mean, rstd, dn, None, dout)
-        return dx, dlw, dlb, None, dw1, db1, dw2, db2, None, None
+        return dx, dlw, dlb, None, dw1, db1, dw2, db2, None, None, None
 
 
 def self_attn_block(res_mod, x, pos, period, B, L, kpm, causal, training, cdtype,
@@ -1133,12 +1206,19 @@ def cross_attn_block(res_mod, y, qpos, period, mem_pos, mem, B, Lq, Lk, kpm, tra
                                  _drop_p(training, res_mod.dropout.p), cdtype, want_probs)
 
 
-def ffn_block(res_mod, x, training, cdtype):
-    """res_mod: FFResidual container (.norm, .sublayer = Sequential(Linear, ReLU, Linear))."""
+def ffn_block(res_mod, x, training, cdtype, next_norm=None):
+    """res_mod: FFResidual container (.norm, .sublayer = Sequential(Linear, ReLU, Linear)).
+    ``next_norm`` = (LayerNorm module, pos, period, plain, with_pos) of the LayerNorm that reads
+    the output next (the following pre-norm block's or the stack's final norm): produced in the
+    down-projection's epilogue (see _ln_take)."""
     seq = res_mod.sublayer
+    nxt = None
+    if next_norm is not None:
+        nm, pos, period, plain, with_pos = next_norm
+        nxt = (nm.weight, nm.bias, nm.eps, pos, period, plain, with_pos)
     return _FFNBlock.apply(x, res_mod.norm.weight, res_mod.norm.bias, res_mod.norm.eps,
                            seq[0].weight, seq[0].bias, seq[2].weight, seq[2].bias,
-                           _drop_p(training, res_mod.dropout.p), cdtype)
+                           _drop_p(training, res_mod.dropout.p), cdtype, nxt)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -1556,3 +1556,56 @@ def test_panel_gemm_equals_tile_gemm(M, N, K):
     dref = (dy.float() @ w2.float()) * (gate.float() > 0)
     assert rel_err(outs[1][1].float(), dref) < 1e-2
     assert torch.equal(outs[1][1], outs[1][2])
+
+
+@pytest.mark.parametrize("M,N,K,period,plain,with_pos,drop", [
+    (6400, 256, 2048, 400, True, True, 0.1), (2048, 256, 2048, 128, True, True, 0.1),
+    (2048, 256, 2048, 0, True, False, 0.0), (1000, 256, 1536, 77, False, True, 0.1),
+    (700, 512, 2048, 35, True, True, 0.1)])
+def test_splitk_linear_with_next_layernorm(M, N, K, period, plain, with_pos, drop):
+    """retr_linear_fwd_splitk_ln: the split-K down-projection (bias, dropout, fp32 residual)
+    whose slab epilogue also writes LN(out) / LN(out) + pos[row % period], mean and rstd --
+    bitwise equal to the split-K linear followed by retr_layernorm_fwd (the same slab-sum
+    order, epilogue arithmetic and ln_fwd4 statistics), and LN within bf16 rounding of fp32
+    torch."""
+    bf = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV).to(bf)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV).to(bf)
+    b = torch.randn(N, generator=g).to(DEV)
+    res = torch.randn(M, N, generator=g).to(DEV)
+    gam = (1 + 0.1 * torch.randn(N, generator=g)).to(DEV)
+    bet = (0.1 * torch.randn(N, generator=g)).to(DEV)
+    pos = torch.randn(max(period, 1), N, generator=g).to(DEV) if with_pos else None
+    assert ops._splits(bf, M, N, K) > 1
+    outs = []
+    for fused in (True, False):
+        y = torch.full((M, N), float("nan"), device=DEV)
+        ly = torch.full((M, N), float("nan"), dtype=bf, device=DEV) if plain else None
+        ly2 = torch.full((M, N), float("nan"), dtype=bf, device=DEV) if with_pos else None
+        mean = torch.empty(M, device=DEV)
+        rstd = torch.empty(M, device=DEV)
+        if fused:
+            ops.k_linear_fwd(x, w, b, y, res=res, drop_p=drop, seed=3,
+                             ln=(gam, bet, 1e-5, ly, ly2, pos, period, mean, rstd))
+        else:
+            ops.k_linear_fwd(x, w, b, y, res=res, drop_p=drop, seed=3)
+            ly_, ly2_, mean_, rstd_ = ops._ln_fwd(y, gam, bet, 1e-5, bf, pos, period, plain,
+                                                  with_pos)
+            ly, ly2, mean, rstd = ly_, ly2_, mean_, rstd_
+        torch.cuda.synchronize()
+        outs.append((y, ly, ly2, mean, rstd))
+    for a, c in zip(*outs):
+        assert (a is None) == (c is None)
+        if a is not None:
+            assert torch.equal(a, c)
+    y, ly, ly2, mean, rstd = outs[0]
+    ref = torch.nn.functional.layer_norm(y, (N,), gam, bet, 1e-5)
+    if plain:
+        assert rel_err(ly.float(), ref) < 1e-2
+    if with_pos:
+        rows = torch.arange(M, device=DEV) % period
+        assert rel_err(ly2.float(), ref + pos[rows]) < 1e-2
+    if drop == 0.0:
+        yref = x.float() @ w.float().t() + b + res
+        assert rel_err(y, yref) < 1e-2

@@ -446,3 +446,43 @@ def test_grouped_conv_weight_gradients_match_per_conv_launches():
         else:
             assert torch.equal(g1[n], g0[n]), n
     assert nb > 20
+
+
+def test_next_layernorm_in_ffn_epilogue_matches_separate_launch():
+    """The FFN down-projection's epilogue also produces the LayerNorm that reads its output
+    next (ops.FUSE_LN_NEXT: the following block's pre-norm, the encoder's final LN(x) / LN(x) +
+    pos, the decoder's final norm) -- the consumer takes the tagged result instead of launching
+    its own LayerNorm.  Loss and every gradient bitwise equal to the separate-launch path, and
+    every FFN output was consumed that way (2 + 2 layers: 4 hits per forward)."""
+    from retr_amd import ops
+    cfg = make_config(backbone="ResNet18", hidden=256, layers=(2, 2), vocab=1000, max_pos=16,
+                      ffn=512, dtype="bf16", dropout=0.1)
+    model, crit = build_model(cfg)
+    model.load_state_dict(synthetic_state_dict(model, seed=6))
+    model.to(DEV).train()
+    images, mask = synthetic_images(2, 64, seed=1, pad_band=True)
+    caps, cap_mask = synthetic_captions(2, 16, 1000, seed=2)
+    s = NestedTensor(images.to(DEV), mask.to(DEV))
+    ctr = ops._seed_state["ctr"]
+    res = []
+    try:
+        for fuse in (True, False):
+            ops.FUSE_LN_NEXT = fuse
+            ops._seed_state["ctr"] = ctr
+            h0 = ops.LN_NEXT_STATS["hit"]
+            model.zero_grad(set_to_none=True)
+            out = model(s, caps[:, :-1].to(DEV), cap_mask[:, :-1].to(DEV))
+            loss = crit(out.permute(0, 2, 1), caps[:, 1:].to(DEV))
+            loss.backward()
+            torch.cuda.synchronize()
+            res.append(({n: p.grad.detach().clone() for n, p in model.named_parameters()
+                         if p.grad is not None}, ops.LN_NEXT_STATS["hit"] - h0, loss.item(),
+                        out.detach().clone()))
+    finally:
+        ops.FUSE_LN_NEXT = True
+    (g1, h1, l1, o1), (g0, h0, l0, o0) = res
+    assert h1 == 4 and h0 == 0, (h1, h0)
+    assert l1 == l0 and torch.equal(o1, o0)
+    assert g1.keys() == g0.keys() and len(g1) > 0
+    for n in g1:
+        assert torch.equal(g1[n], g0[n]), n

@@ -74,6 +74,7 @@ VARIANTS = {
     "pg16": {("TUNE", 23): 1, ("TUNE", 24): 16},
     "pconv": {("TUNE", 23): 1, ("TUNE", 25): 1},
     "kb_on": {("TUNE", 26): 1},
+    "lnn_off": {("ATTR", "FUSE_LN_NEXT"): False},
 }
 
 
@@ -86,6 +87,7 @@ def apply(v):
     ops.FUSE_FFN = False
     ops.WGRAD_DEFER = True
     ops.WGRAD_SIDE = False
+    ops.FUSE_LN_NEXT = True
     resnet.CONV_WGRAD_GROUP = True
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
