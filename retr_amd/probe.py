@@ -58,6 +58,9 @@ def flops_of(name, a):
     if name in ("retr_linear_fwd", "retr_linear_fwd_splitk"):
         m, n, k = a[9], a[10], a[11]
         return "linear_fwd", 2.0 * m * n * k
+    if name == "retr_linear_fwd_splitk_ln":     # the LayerNorm in its epilogue: no MFMA work
+        m, n, k = a[8], a[9], a[10]
+        return "linear_fwd", 2.0 * m * n * k
     if name in ("retr_linear_dgrad", "retr_linear_dgrad_splitk"):
         m, n, k = a[8], a[9], a[10]
         return "linear_dgrad", 2.0 * m * n * k
@@ -154,6 +157,11 @@ def bytes_of(name, a):
     if name in ("retr_linear_fwd", "retr_linear_fwd_splitk"):
         yf32, m, n, k, res = a[8], a[9], a[10], a[11], a[13]
         return e * (m * k + n * k) + m * n * (4 if yf32 else e) + (4 * m * n if res else 0)
+    if name == "retr_linear_fwd_splitk_ln":     # fp32 out + the LayerNorm's bf16 outputs
+        m, n, k, res = a[8], a[9], a[10], a[12]
+        ln = getattr(a[18], "_obj", None)
+        nout = (bool(ln.y) + bool(ln.y2)) if ln is not None else 1
+        return e * (m * k + n * k) + 4 * m * n + (4 * m * n if res else 0) + 2 * m * n * nout
     if name in ("retr_linear_dgrad", "retr_linear_dgrad_splitk"):
         dxf32, m, n, k, addend, af32, gate = a[7], a[8], a[9], a[10], a[11], a[12], a[14]
         return (e * (m * n + n * k) + m * k * (4 if dxf32 else e)
@@ -214,6 +222,8 @@ def shape_of(name, a):
         return f"M{a[8]} N{a[9]} K{a[10]} add{int(bool(a[11]))} gate{int(bool(a[14]))} split{a[18]}"
     if name == "retr_linear_fwd_splitk":
         return f"M{a[9]} N{a[10]} K{a[11]} relu{a[12]} res{int(bool(a[13]))} split{a[18]}"
+    if name == "retr_linear_fwd_splitk_ln":
+        return f"M{a[8]} N{a[9]} K{a[10]} relu{a[11]} res{int(bool(a[12]))} split{a[17]} +LN"
     if name == "retr_linear_wgrad":
         return f"M{a[7]} N{a[8]} K{a[9]} db{int(bool(a[10]))} acc{a[11]}"
     if name == "retr_attention_fwd":
@@ -225,7 +235,7 @@ def shape_of(name, a):
 
 TRACKED = ("retr_conv2d_fwd", "retr_conv2d_fwd_out", "retr_conv1x1_fwd_cat",
            "retr_bottleneck_s1_fwd", "retr_stem_pool_fwd", "retr_conv2d_dgrad", "retr_conv2d_wgrad", "retr_linear_fwd",
-           "retr_linear_fwd_splitk",
+           "retr_linear_fwd_splitk", "retr_linear_fwd_splitk_ln",
            "retr_linear_dgrad", "retr_linear_dgrad_splitk", "retr_linear_wgrad",
            "retr_linear_fwd_group", "retr_linear_dgrad_group", "retr_linear_wgrad_group",
            "retr_linear_wgrad_group2", "retr_linear_wgrad_batch", "retr_conv2d_wgrad_group",
