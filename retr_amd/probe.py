@@ -247,8 +247,8 @@ TRACKED = ("retr_conv2d_fwd", "retr_conv2d_fwd_out", "retr_conv1x1_fwd_cat",
 FAMILY_SYMBOL = {"linear_fwd": "gemm{,2,2_group}_kernel<0,",
                  "linear_dgrad": "gemm{,2,2_group}_kernel<1,",
                  "linear_wgrad": "gemm{,2,2_group}_kernel<2, + wgrad_batch_kernel",
-                 "conv_fwd": "gemm{,2}_kernel<3, + bottleneck_s1_kernel + stem_pool_kernel",
-                 "conv_dgrad": "gemm{,2}_kernel<4,",
+                 "conv_fwd": "gemm{,2}_kernel<3, + conv3x3_kernel<..., false> + bottleneck_s1_kernel + stem_pool_kernel",
+                 "conv_dgrad": "gemm{,2}_kernel<4, + conv3x3_kernel<..., true>",
                  "conv_wgrad": "gemm{,2}_kernel<5, + conv_wgrad_group_kernel",
                  "attention_fwd": "attn_fwd{,2,2s}_kernel + attn_keep_bits_kernel",
                  "attention_bwd": "attn_bwd_"}
@@ -263,6 +263,10 @@ def family_of_symbol(name):
     if m:
         return ("linear_fwd", "linear_dgrad", "linear_wgrad", "conv_fwd", "conv_dgrad",
                 "conv_wgrad")[int(m.group(1))]
+    m = re.search(r"conv3x3_kernelI(?:Li\d+E){5}Lb([01])E", name) or \
+        re.search(r"conv3x3_kernel<(?:\d+, ){5}(false|true)", name)
+    if m:                                         # direct 3x3 conv (csrc/conv3x3.hip)
+        return "conv_dgrad" if m.group(1) in ("1", "true") else "conv_fwd"
     if "wgrad_batch_kernel" in name:
         return "linear_wgrad"
     if "conv_wgrad_group_kernel" in name:
