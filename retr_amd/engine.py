@@ -260,13 +260,22 @@ class GraphedTrainStep:
             # the captured update rewrote the bf16 shadow of every parameter it stepped
             self.optimizer.mark_shadow_fresh(self._active)
 
+    def input_buffers(self):
+        """The captured step's static inputs (images, image mask, captions, caption mask), set
+        by the first call: a loader that writes each batch into them and passes them back
+        saves the per-step device-to-device staging copy (78.6 MB of images at cfg2)."""
+        return self.static
+
     def __call__(self, samples, caps, cap_masks):
         nt = samples[0]
         if self.static is None:
             self.static = (nt.tensors.clone(), nt.mask.clone(), caps.clone(), cap_masks.clone())
         else:
             for dst, src in zip(self.static, (nt.tensors, nt.mask, caps, cap_masks)):
-                dst.copy_(src, non_blocking=True)
+                # zero-copy when the caller handed back the step's own input buffers (a loader
+                # that writes each batch into input_buffers()): nothing to stage
+                if src.data_ptr() != dst.data_ptr() or src.shape != dst.shape:
+                    dst.copy_(src, non_blocking=True)
         if self.graph is None:
             opt = self.optimizer
             consume0 = getattr(opt, "consume_grads", None)

@@ -189,6 +189,38 @@ def test_graphed_step_with_fused_adamw_matches_eager():
         assert _rel(a.detach(), b.detach()) < 5e-5, n
 
 
+@pytest.mark.parametrize("deterministic_mode", [True], indirect=True)
+def test_graphed_step_reads_its_own_input_buffers(deterministic_mode):
+    """GraphedTrainStep.input_buffers(): a caller that writes the batch into the captured step's
+    static inputs and passes them back gets the same updates as one passing its own tensors
+    (which the step stages by a copy), including after the buffers are rewritten in place with
+    a new batch."""
+    from retr_amd.engine import GraphedTrainStep
+    cfg, m1, crit = _micro_model()
+    _, m2, _ = _micro_model()
+    o1 = FusedAdamW(_groups(m1, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    o2 = FusedAdamW(_groups(m2, cfg), lr=cfg.lr, weight_decay=cfg.weight_decay)
+    samples, caps, cm = _batch(cfg)
+    m1.train()
+    m2.train()
+    g1 = GraphedTrainStep(m1, crit, o1, 0.1, warmup=2)
+    g2 = GraphedTrainStep(m2, crit, o2, 0.1, warmup=2)
+    l1 = [g1(samples, caps, cm).item()]
+    l2 = [g2(samples, caps, cm).item()]
+    st = g2.input_buffers()
+    own = ((NestedTensor(st[0], st[1]),), st[2], st[3])
+    for i in range(4):
+        if i == 2:       # a new batch: the copy path stages it, the loader path writes in place
+            samples = (NestedTensor(samples[0].tensors.flip(-1).contiguous(),
+                                    samples[0].mask.clone()),)
+            st[0].copy_(samples[0].tensors)
+        l1.append(g1(samples, caps, cm).item())
+        l2.append(g2(*own).item())
+    assert l1 == l2, (l1, l2)
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(a.detach(), b.detach()), n
+
+
 def test_graphed_and_eager_steps_mix_on_one_fused_adamw():
     """Consume mode (the captured update zeroes the gradient arena) belongs to GraphedTrainStep
     only: an eager train_step on the same optimizer between replays still leaves the clipped
