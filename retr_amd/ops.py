@@ -465,6 +465,10 @@ def _wgrad(wg, extra, arena_ok):
             flush_wgrad()
 
 
+# the MLP head's weight gradients join the deferred batch too (else: one launch each + a
+# column-sum launch for the vocabulary bias)
+HEAD_WGRAD_DEFER = True
+
 # The fence's flush on a side stream, overlapping the backbone backward: measured 0.3 ms/step
 # SLOWER in the graphed cfg2 step (profiles/r4_ab_wgrad_defer.txt), so off by default
 WGRAD_SIDE = False
@@ -1360,19 +1364,34 @@ class _MLPHead(torch.autograd.Function):
             dl[:, :V] = dlog.reshape(M, V).to(cdtype)
         w1t, w2t = WEIGHTS.get_t(w1, cdtype), WEIGHTS.get_t(w2, cdtype)
         w3t = WEIGHTS.get_t(w3, cdtype, rows=Vp)
-        (dw1, _), (db1, _), (dw2, _), (db2, _), (dw3, _), (db3, _) = map(grad_buffer,
-                                                                         ctx.gparams)
+        bufs = list(map(grad_buffer, ctx.gparams))
+        (dw1, _), (db1, _), (dw2, _), (db2, _), (dw3, _), (db3, _) = bufs
+        # bf16 with every buffer in the optimizer arena: the three weight gradients (+ biases,
+        # as the batch's all-ones MFMA instead of a column-sum launch over the 125 MB dlogits)
+        # join the deferred batch that the transformer blocks' backward fills (one launch at the
+        # transformer input fence; see _wgrad)
+        defer = (HEAD_WGRAD_DEFER and WGRAD_DEFER and cdtype == torch.bfloat16
+                 and all(a for _, a in bufs))
         ov = _Overlap(OVERLAP["transformer"])
-        with ov.side():
-            k_linear_wgrad(dl, h2, dw3, db3, accumulate=True)  # N = V rows of the padded dl
+        if defer:
+            _wgrad([(dl, h2, dw3, db3, True)], (), True)     # N = V rows of the padded dl
+        else:
+            with ov.side():
+                k_linear_wgrad(dl, h2, dw3, db3, accumulate=True)
         dh2 = torch.empty_like(h2)
         k_linear_dgrad(dl, w3t, dh2, gate=h2)
-        with ov.side():
-            k_linear_wgrad(dh2, h1, dw2, db2, accumulate=True)
+        if defer:
+            _wgrad([(dh2, h1, dw2, db2, True)], (), True)
+        else:
+            with ov.side():
+                k_linear_wgrad(dh2, h1, dw2, db2, accumulate=True)
         dh1 = torch.empty_like(h1)
         k_linear_dgrad(dh2, w2t, dh1, gate=h1)
-        with ov.side():
-            k_linear_wgrad(dh1, hs, dw1, db1, accumulate=True)
+        if defer:
+            _wgrad([(dh1, hs, dw1, db1, True)], (), True)
+        else:
+            with ov.side():
+                k_linear_wgrad(dh1, hs, dw1, db1, accumulate=True)
         dhs = torch.empty_like(hs)
         k_linear_dgrad(dh1, w1t, dhs)
         ov.join()

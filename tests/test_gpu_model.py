@@ -399,9 +399,15 @@ def test_deferred_weight_gradients_match_per_block_launches():
     assert nf1 == 1 and nf0 == 0, (nf1, nf0)
     assert g1.keys() == g0.keys() and len(g1) > 0
     # at these token counts (< 512 per block) the per-block path does not split the reduction
-    # either, so both are the same single fp32 chain per element: bitwise equal everywhere
+    # either, so both are the same single fp32 chain per element: bitwise equal everywhere but
+    # in the MLP head (deferred: the batch kernel, biases as its all-ones MFMA; per-launch: the
+    # single-problem wgrad kernel and a fixed-order column sum -- the same sums in another order)
     for n in g1:
-        assert torch.equal(g1[n], g0[n]), n
+        if n.startswith("mlp."):
+            e = ((g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-30)).item()
+            assert e < 1e-5, (n, e)
+        else:
+            assert torch.equal(g1[n], g0[n]), n
 
 
 def test_grouped_conv_weight_gradients_match_per_conv_launches():

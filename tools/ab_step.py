@@ -75,6 +75,7 @@ VARIANTS = {
     "pconv": {("TUNE", 23): 1, ("TUNE", 25): 1},
     "kb_on": {("TUNE", 26): 1},
     "lnn_off": {("ATTR", "FUSE_LN_NEXT"): False},
+    "hd_off": {("ATTR", "HEAD_WGRAD_DEFER"): False},
 }
 
 
@@ -88,6 +89,7 @@ def apply(v):
     ops.WGRAD_DEFER = True
     ops.WGRAD_SIDE = False
     ops.FUSE_LN_NEXT = True
+    ops.HEAD_WGRAD_DEFER = True
     resnet.CONV_WGRAD_GROUP = True
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
