@@ -550,6 +550,18 @@ int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, f
 /* retr_pos_grad with dpos overwritten (dpos = the sums): no zero fill before a fresh gradient */
 int retr_pos_grad_set(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
                       void* stream);
+/* Several contributions to one position-gradient buffer (the decoder blocks' query-position
+ * gradients, models/ConcatTransformer.py's query_pos used by every decoder layer) in one launch:
+ * dpos (+)= sum over items in order of sum_b d_i[b * period + t] -- bitwise the sequence of
+ * retr_pos_grad calls (the first one retr_pos_grad_set when accumulate is 0). */
+typedef struct retr_pos_item {
+  const void* d;
+  long ld;
+  int M;
+  int pad;
+} retr_pos_item;
+int retr_pos_grad_multi(int dtype, int n, const retr_pos_item* items, int C, int period,
+                        float* dpos, int accumulate, void* stream);
 
 /* ---- fused clip_grad_norm_ + AdamW over flat fp32 arenas --------------------------------
  * Replaces engine.py:80-83 (torch.nn.utils.clip_grad_norm_ + optimizer.step()) with the

@@ -63,6 +63,11 @@ class ConvUnpackDesc(ctypes.Structure):
                 ("KH", _I), ("KW", _I), ("splits", _I), ("accumulate", _I), ("pad", _I)]
 
 
+class PosItem(ctypes.Structure):
+    """retr_pos_item"""
+    _fields_ = [("d", _P), ("ld", _L), ("M", _I), ("pad", _I)]
+
+
 class LnOut(ctypes.Structure):
     """retr_ln_out"""
     _fields_ = [("gamma", _P), ("beta", _P), ("eps", _F), ("y_bf16", _I), ("y", _P), ("y2", _P),
@@ -191,6 +196,7 @@ _SIGS = {
     "retr_sum2": [_I, _P, _P, _L, _P, _P],
     "retr_pos_grad": [_I, _P, _L, _I, _I, _I, _P, _P],
     "retr_pos_grad_set": [_I, _P, _L, _I, _I, _I, _P, _P],
+    "retr_pos_grad_multi": [_I, _I, ctypes.POINTER(PosItem), _I, _I, _P, _I, _P],
     "retr_dec_gemm": [_P, _P, _I, _I, _P, _P, _I, _P, _L, _I, _P, _L, _I, _P, _L, _I, _I, _I, _P],
     "retr_dec_rows": [_P, _P, _I, _P, _I, _I, _P, _P, _P, _F, _P, _P, _P, _P],
     "retr_dec_embed_rows": [_P, _I, _I, _P, _P, _P, _P, _F, _P, _P, _P, _F, _P, _P, _P],

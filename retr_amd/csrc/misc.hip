@@ -256,6 +256,61 @@ __global__ void pos_grad8_kernel(const T* d, long ld, int M, int C, int period, 
   retr::store8<float>(o, cur);
 }
 
+// Several position-gradient contributions into one buffer in one launch (the decoder's query
+// positions: 12 blocks per step).  Thread (j, i) of a block forms item i's batch sum for chunk
+// j exactly as pos_grad8_kernel does (same loop, same order), the sums meet in LDS, and chunk
+// j's thread 0 adds them to dpos in item order: bitwise the sequence of per-item launches.
+constexpr int kPosMulti = 16;                     // items per launch
+struct PosItems {
+  const void* d[kPosMulti];
+  long ld[kPosMulti];
+  int M[kPosMulti];
+  int n;
+};
+template <typename T>
+__global__ void __launch_bounds__(256) pos_grad_multi_kernel(PosItems it, int C, int period,
+                                                             float* dpos, int acc) {
+  __shared__ float sums[kPosMulti][16][8];
+  const int j = threadIdx.x & 15, i = threadIdx.x >> 4;   // 16 chunks x 16 items per block
+  const int c8 = C / 8;
+  const long q = (long)blockIdx.x * 16 + j;
+  const bool okq = q < (long)period * c8;
+  const int c = okq ? (int)(q % c8) * 8 : 0, p = okq ? (int)(q / c8) : 0;
+  if (okq && i < it.n) {
+    const T* d = (const T*)it.d[i];
+    const long ld = it.ld[i];
+    const int M = it.M[i];
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int m = p;
+    for (; m + 7 * period < M; m += 8 * period) {
+      float v[8][8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) retr::load8<T>(d + (long)(m + u * period) * ld + c, v[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += v[u][e];
+    }
+    for (; m < M; m += period) {
+      float v[8];
+      retr::load8<T>(d + (long)m * ld + c, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sums[i][j][e] = s[e];
+  }
+  __syncthreads();
+  if (!okq || i != 0) return;
+  float* o = dpos + (long)p * C + c;
+  float cur[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (acc) retr::load8<float>(o, cur);
+  for (int k = 0; k < it.n; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cur[e] += sums[k][j][e];
+  retr::store8<float>(o, cur);
+}
+
 int grid_for(long total) {
   long g = (total + 255) / 256;
   return (int)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
@@ -376,6 +431,41 @@ int retr_pos_grad(int dtype, const void* d, long ld, int M, int C, int period, f
 int retr_pos_grad_set(int dtype, const void* d, long ld, int M, int C, int period, float* dpos,
                       void* stream) {
   return pos_grad(dtype, d, ld, M, C, period, dpos, 0, stream);
+}
+
+int retr_pos_grad_multi(int dtype, int n, const retr_pos_item* items, int C, int period,
+                        float* dpos, int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  RETR_REQUIRE(n >= 0 && (n == 0 || items) && period > 0, "pos_grad_multi: n=%d period=%d", n,
+               period);
+  bool vec = C % 8 == 0 && ((uintptr_t)dpos & 15) == 0;
+  for (int i = 0; i < n && vec; ++i)
+    vec = items[i].ld % 8 == 0 && ((uintptr_t)items[i].d & 15) == 0;
+  if (!vec) {         // the per-item launches (same results)
+    for (int i = 0; i < n; ++i)
+      if (int e = pos_grad(dtype, items[i].d, items[i].ld, items[i].M, C, period, dpos,
+                           (accumulate || i > 0) ? 1 : 0, stream))
+        return e;
+    return 0;
+  }
+  for (int i0 = 0; i0 < n; i0 += kPosMulti) {
+    PosItems it{};
+    it.n = n - i0 < kPosMulti ? n - i0 : kPosMulti;
+    for (int k = 0; k < it.n; ++k) {
+      it.d[k] = items[i0 + k].d;
+      it.ld[k] = items[i0 + k].ld;
+      it.M[k] = items[i0 + k].M;
+    }
+    const long chunks = (long)period * (C / 8);
+    const int acc = (accumulate || i0 > 0) ? 1 : 0;
+    const dim3 grid((unsigned)((chunks + 15) / 16));
+    if (dtype == RETR_BF16)
+      hipLaunchKernelGGL(pos_grad_multi_kernel<bf16>, grid, dim3(256), 0, st, it, C, period, dpos, acc);
+    else
+      hipLaunchKernelGGL(pos_grad_multi_kernel<float>, grid, dim3(256), 0, st, it, C, period, dpos, acc);
+    if (int e = retr_check_launch("pos_grad_multi")) return e;
+  }
+  return 0;
 }
 
 }  // extern "C"

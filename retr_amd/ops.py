@@ -495,6 +495,7 @@ def flush_wgrad(side=False):
     current one), so the batch overlaps the kernels that follow until the next join."""
     if not side:
         _WQ_STATE["armed"] = False
+    flush_pos()
     if _WQ:
         descs = [d for q in _WQ for d in q[0]]
         xs = [x for q in _WQ for x in q[1]]
@@ -867,12 +868,57 @@ def _ln_bwd_fused(x, gamma, beta, mean, rstd, dy, dy2, addend, prev, cdtype, pos
     extra = [(ws, 2 * C, n, C, dgamma, 1), (ws[C:], 2 * C, n, C, dbeta, 1)] if n > 0 else []
     dpos = None
     if need_dpos and dy2 is not None:
-        dpos, _, last = _shared_grad(pos, lambda: grad_buffer(pos)[0])
-        call("retr_pos_grad", dcode(dy2.dtype), ptr(dy2), dy2.stride(0), M, C, int(period),
-             ptr(dpos), _st())            # adds into the (zeroed or shared) buffer
+        dpos, _, last = _shared_grad(pos, lambda: grad_buffer(pos))
+        dpos, arena = dpos
+        if POS_DEFER and arena and dy2.dtype == torch.bfloat16:
+            _pos_queue(dy2, M, C, int(period), dpos)
+        else:
+            call("retr_pos_grad", dcode(dy2.dtype), ptr(dy2), dy2.stride(0), M, C, int(period),
+                 ptr(dpos), _st())        # adds into the (zeroed or shared) buffer
         if not last:
             dpos = None
     return dx, dgamma, dbeta, dpos, extra, ag and ab
+
+
+# Position gradients of a table several blocks read (the decoder's query positions: 12 blocks)
+# are queued per buffer and summed by one retr_pos_grad_multi launch when the weight-gradient
+# queue flushes (same sums in the same order as one retr_pos_grad per block).  Only for
+# FusedAdamW arena buffers: autograd adopts those as .grad without reading them, so the
+# buffer may be filled later in stream order.
+POS_DEFER = False   # on once measured (tools/ab_step.py pos_on)
+_POSQ = {}     # dpos data_ptr -> [dpos, C, period, [(dy2, M), ...]]
+
+
+def _pos_queue(dy2, M, C, period, dpos):
+    e = _POSQ.get(dpos.data_ptr())
+    if e is None or e[1] != C or e[2] != period:
+        if e is not None:
+            _pos_flush_one(e)
+        e = _POSQ[dpos.data_ptr()] = [dpos, C, period, []]
+    e[3].append((dy2, M))
+    if len(e[3]) == 16:
+        _pos_flush_one(e)
+        del _POSQ[dpos.data_ptr()]
+    if not _WQ_STATE["armed"]:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(flush_wgrad)
+            _WQ_STATE["armed"] = True
+        except RuntimeError:
+            flush_pos()
+
+
+def _pos_flush_one(e):
+    dpos, C, period, items = e
+    arr = (_lib.PosItem * len(items))()
+    for i, (d, M) in enumerate(items):
+        arr[i].d, arr[i].ld, arr[i].M = ptr(d), d.stride(0), M
+    call("retr_pos_grad_multi", BF16, len(items), arr, C, period, ptr(dpos), 1, _st())
+
+
+def flush_pos():
+    for e in list(_POSQ.values()):
+        _pos_flush_one(e)
+    _POSQ.clear()
 
 
 # ---------------------------------------------------------------------------------------------

@@ -1609,3 +1609,32 @@ def test_splitk_linear_with_next_layernorm(M, N, K, period, plain, with_pos, dro
     if drop == 0.0:
         yref = x.float() @ w.float().t() + b + res
         assert rel_err(y, yref) < 1e-2
+
+
+@pytest.mark.parametrize("n,acc,ld_pad", [(12, 1, 0), (12, 0, 0), (17, 1, 0), (3, 1, 8), (1, 0, 0)])
+def test_pos_grad_multi_equals_per_item_launches(n, acc, ld_pad):
+    """retr_pos_grad_multi (the decoder blocks' query-position gradients in one launch) against
+    one retr_pos_grad per item in the same order (the first retr_pos_grad_set when not
+    accumulating): bitwise equal, including more than 16 items (two launches) and row strides
+    wider than C."""
+    import ctypes
+    from retr_amd import _lib as L
+    T, B, C = 128, 16, 256
+    g = torch.Generator(device="cpu").manual_seed(n * 7 + acc)
+    items = [torch.randn(B * T, C + ld_pad, generator=g).to(DEV).to(torch.bfloat16)
+             for _ in range(n)]
+    init = torch.randn(T, C, generator=g).to(DEV)
+    a = init.clone()
+    for i, d in enumerate(items):
+        name = "retr_pos_grad" if (acc or i > 0) else "retr_pos_grad_set"
+        L.call(name, 1, L.ptr(d), d.stride(0), B * T, C, T, L.ptr(a), L.stream())
+    b = init.clone()
+    arr = (L.PosItem * n)()
+    for i, d in enumerate(items):
+        arr[i].d, arr[i].ld, arr[i].M = L.ptr(d), d.stride(0), B * T
+    L.call("retr_pos_grad_multi", 1, n, arr, C, T, L.ptr(b), acc, L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    ref = (init if acc else torch.zeros_like(init)) + sum(
+        d[:, :C].float().view(B, T, C).sum(0) for d in items)
+    assert rel_err(b, ref) < 1e-5

@@ -492,3 +492,41 @@ def test_next_layernorm_in_ffn_epilogue_matches_separate_launch():
     assert g1.keys() == g0.keys() and len(g1) > 0
     for n in g1:
         assert torch.equal(g1[n], g0[n]), n
+
+
+def test_deferred_position_gradients_match_per_block_launches():
+    """The decoder blocks' query-position gradient contributions queued and summed by one
+    retr_pos_grad_multi launch at the weight-gradient flush (ops.POS_DEFER, FusedAdamW arena)
+    against one retr_pos_grad launch per block: every gradient bitwise equal."""
+    from retr_amd import ops
+    from retr_amd.optim import FusedAdamW
+    cfg = make_config(backbone="ResNet18", hidden=256, layers=(2, 2), vocab=1000, max_pos=16,
+                      ffn=512, dtype="bf16", dropout=0.1)
+    model, crit = build_model(cfg)
+    model.load_state_dict(synthetic_state_dict(model, seed=8))
+    model.to(DEV).train()
+    opt = FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+    images, mask = synthetic_images(2, 64, seed=1, pad_band=True)
+    caps, cap_mask = synthetic_captions(2, 16, 1000, seed=2)
+    s = NestedTensor(images.to(DEV), mask.to(DEV))
+    ctr = ops._seed_state["ctr"]
+    res = []
+    try:
+        for defer in (True, False):
+            ops.POS_DEFER = defer
+            ops._seed_state["ctr"] = ctr
+            opt.zero_grad(set_to_none=True)
+            out = model(s, caps[:, :-1].to(DEV), cap_mask[:, :-1].to(DEV))
+            loss = crit(out.permute(0, 2, 1), caps[:, 1:].to(DEV))
+            loss.backward()
+            assert not ops._POSQ
+            torch.cuda.synchronize()
+            res.append({n: p.grad.detach().clone() for n, p in model.named_parameters()
+                        if p.grad is not None})
+    finally:
+        ops.POS_DEFER = False
+    g1, g0 = res
+    assert g1.keys() == g0.keys()
+    assert "embeddings.position_embeddings.weight" in g1
+    for n in g1:
+        assert torch.equal(g1[n], g0[n]), n

@@ -76,6 +76,7 @@ VARIANTS = {
     "kb_on": {("TUNE", 26): 1},
     "lnn_off": {("ATTR", "FUSE_LN_NEXT"): False},
     "hd_off": {("ATTR", "HEAD_WGRAD_DEFER"): False},
+    "pos_on": {("ATTR", "POS_DEFER"): True},
 }
 
 
@@ -90,6 +91,7 @@ def apply(v):
     ops.WGRAD_SIDE = False
     ops.FUSE_LN_NEXT = True
     ops.HEAD_WGRAD_DEFER = True
+    ops.POS_DEFER = False
     resnet.CONV_WGRAD_GROUP = True
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
