@@ -168,7 +168,9 @@ enum {
   RETR_TUNE_LN_BWD = 27,        /* LayerNorm backward (C 256 / 512) rows / waves per block: 0 auto
                                    (32 / 16 at >= 4096 rows, else 8 / 4), 1 32/16, 2 16/8, 3 8/4,
                                    4 16/16, 5 64/16, 6 8/8 (tools/ln_micro.py) */
-  RETR_TUNE_COUNT = 28
+  RETR_TUNE_UNPACK_GRID = 28,   /* retr_conv_wgrad_unpack_group grid cap (blocks walk the
+                                   64-chunk groups): 0 one block per group */
+  RETR_TUNE_COUNT = 29
 };
 int retr_tune(int knob, int value);
 

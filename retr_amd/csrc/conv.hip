@@ -1264,48 +1264,52 @@ __global__ void __launch_bounds__(256) wgrad_unpack_group_kernel(const char* __r
   __shared__ f32x4 red[4][64];
   const CWHead h = *(const CWHead*)table;
   const UPJob* J = (const UPJob*)(table + sizeof(CWHead));
-  const int bid = blockIdx.x;
-  if (bid >= h.total) return;
-  int lo = 0, hi = h.nprob - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (J[mid].blk0 <= bid) lo = mid;
-    else hi = mid - 1;
-  }
-  const UPJob d = J[lo];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c4 = d.Ci / 4;
-  const long total = (long)d.Co * d.KHW * c4;
-  const long slab = (long)d.Co * d.KHW * d.Cp;
-  const long i = (long)(bid - d.blk0) * 64 + lane;
-  int ci = 0, tap = 0, co = 0;
-  f32x4 v = {0.f, 0.f, 0.f, 0.f};
-  if (i < total) {
-    ci = (int)(i % c4) * 4;
-    const long t = i / c4;
-    tap = (int)(t % d.KHW);
-    co = (int)(t / d.KHW);
-    const float* src = d.ws + ((long)co * d.KHW + tap) * d.Cp + ci;
-    int s = w;
-    for (; s + 28 < d.splits; s += 32) {
-      f32x4 u[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) u[k] = *(const f32x4*)(src + (long)(s + 4 * k) * slab);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v += u[k];
+  // a block walks 64-chunk groups bid, bid + gridDim.x, ... (the grid is capped: ~90 k tiny
+  // blocks spent their time in dispatch); every group is summed exactly as before
+  for (int bid = blockIdx.x; bid < h.total; bid += gridDim.x) {
+    int lo = 0, hi = h.nprob - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (J[mid].blk0 <= bid) lo = mid;
+      else hi = mid - 1;
     }
-    for (; s < d.splits; s += 4) v += *(const f32x4*)(src + (long)s * slab);
-  }
-  red[w][lane] = v;
-  __syncthreads();
-  if (w != 0 || i >= total) return;
-  v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-  const float sc = d.scale ? d.scale[co] : 1.f;
-  float* dst = d.grad + ((long)co * d.Ci + ci) * d.KHW + tap;
+    const UPJob d = J[lo];
+    const int c4 = d.Ci / 4;
+    const long total = (long)d.Co * d.KHW * c4;
+    const long slab = (long)d.Co * d.KHW * d.Cp;
+    const long i = (long)(bid - d.blk0) * 64 + lane;
+    int ci = 0, tap = 0, co = 0;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (i < total) {
+      ci = (int)(i % c4) * 4;
+      const long t = i / c4;
+      tap = (int)(t % d.KHW);
+      co = (int)(t / d.KHW);
+      const float* src = d.ws + ((long)co * d.KHW + tap) * d.Cp + ci;
+      int s = w;
+      for (; s + 28 < d.splits; s += 32) {
+        f32x4 u[8];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float x = v[e] * sc;
-    dst[(long)e * d.KHW] = d.accumulate ? dst[(long)e * d.KHW] + x : x;
+        for (int k = 0; k < 8; ++k) u[k] = *(const f32x4*)(src + (long)(s + 4 * k) * slab);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v += u[k];
+      }
+      for (; s < d.splits; s += 4) v += *(const f32x4*)(src + (long)s * slab);
+    }
+    red[w][lane] = v;
+    __syncthreads();
+    if (w == 0 && i < total) {
+      v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+      const float sc = d.scale ? d.scale[co] : 1.f;
+      float* dst = d.grad + ((long)co * d.Ci + ci) * d.KHW + tap;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = v[e] * sc;
+        dst[(long)e * d.KHW] = d.accumulate ? dst[(long)e * d.KHW] + x : x;
+      }
+    }
+    __syncthreads();                             // red[] is rewritten by the next group
   }
 }
 
@@ -1701,7 +1705,12 @@ int retr_conv_wgrad_unpack_group(int n, const retr_conv_unpack_desc* d, void* ta
     hipLaunchKernelGGL(cw_table_put_kernel, dim3(1), dim3(256), 0, st, c, (unsigned*)table);
     if (int e = retr_check_launch("conv_wgrad_unpack_group table")) return e;
   }
-  hipLaunchKernelGGL(wgrad_unpack_group_kernel, dim3(blocks), dim3(256), 0, st,
+  // RETR_TUNE_UNPACK_GRID: cap the grid (the blocks walk the 64-chunk groups); 0 = one block
+  // per group
+  int grid = blocks;
+  const int cap = retr_tune_get(RETR_TUNE_UNPACK_GRID);
+  if (cap > 0 && grid > cap) grid = cap;
+  hipLaunchKernelGGL(wgrad_unpack_group_kernel, dim3(grid), dim3(256), 0, st,
                      (const char*)table);
   return retr_check_launch("conv_wgrad_unpack_group");
 }

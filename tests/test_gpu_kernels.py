@@ -1434,6 +1434,17 @@ def test_conv_wgrad_group_matches_fp32_and_single_path():
         call("retr_conv_wgrad_unpack", ptr(slabs[i]), ptr(scales[i]), ptr(one), co, c, c, k, k,
              0, arr[i].splits, ops._st())
         assert rel_err(outs[i], one) < 1e-6, (geos[i], rel_err(outs[i], one))
+    # a capped grid (RETR_TUNE_UNPACK_GRID: blocks walk the chunk groups): bitwise the same
+    first = [o.clone() for o in outs]
+    for o in outs:
+        o.fill_(float("nan"))
+    try:
+        _lib.load().retr_tune(28, 37)
+        call("retr_conv_wgrad_unpack_group", n, ua, ptr(utab), utab.numel(), ops._st())
+    finally:
+        _lib.load().retr_tune(28, 0)
+    for a, b in zip(first, outs):
+        assert torch.equal(a, b)
     torch.cuda.synchronize()
 
 

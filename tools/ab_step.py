@@ -77,6 +77,8 @@ VARIANTS = {
     "lnn_off": {("ATTR", "FUSE_LN_NEXT"): False},
     "hd_off": {("ATTR", "HEAD_WGRAD_DEFER"): False},
     "pos_on": {("ATTR", "POS_DEFER"): True},
+    "up2k": {("TUNE", 28): 2048},
+    "up8k": {("TUNE", 28): 8192},
 }
 
 
@@ -97,7 +99,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26):
+    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26, 27, 28):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
