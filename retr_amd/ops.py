@@ -885,7 +885,7 @@ def _ln_bwd_fused(x, gamma, beta, mean, rstd, dy, dy2, addend, prev, cdtype, pos
 # queue flushes (same sums in the same order as one retr_pos_grad per block).  Only for
 # FusedAdamW arena buffers: autograd adopts those as .grad without reading them, so the
 # buffer may be filled later in stream order.
-POS_DEFER = False   # on once measured (tools/ab_step.py pos_on)
+POS_DEFER = True    # graphed step 9.670 -> 9.622 ms (profiles/r4_ab_pos_defer.txt)
 _POSQ = {}     # dpos data_ptr -> [dpos, C, period, [(dy2, M), ...]]
 
 

@@ -524,9 +524,9 @@ def test_deferred_position_gradients_match_per_block_launches():
             res.append({n: p.grad.detach().clone() for n, p in model.named_parameters()
                         if p.grad is not None})
     finally:
-        ops.POS_DEFER = False
+        ops.POS_DEFER = True
     g1, g0 = res
     assert g1.keys() == g0.keys()
-    assert "embeddings.position_embeddings.weight" in g1
+    assert any("position_embeddings" in n for n in g1)
     for n in g1:
         assert torch.equal(g1[n], g0[n]), n

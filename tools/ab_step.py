@@ -77,6 +77,7 @@ VARIANTS = {
     "lnn_off": {("ATTR", "FUSE_LN_NEXT"): False},
     "hd_off": {("ATTR", "HEAD_WGRAD_DEFER"): False},
     "pos_on": {("ATTR", "POS_DEFER"): True},
+    "pos_off": {("ATTR", "POS_DEFER"): False},
     "up2k": {("TUNE", 28): 2048},
     "up8k": {("TUNE", 28): 8192},
 }
@@ -93,7 +94,7 @@ def apply(v):
     ops.WGRAD_SIDE = False
     ops.FUSE_LN_NEXT = True
     ops.HEAD_WGRAD_DEFER = True
-    ops.POS_DEFER = False
+    ops.POS_DEFER = True
     resnet.CONV_WGRAD_GROUP = True
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
