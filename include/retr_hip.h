@@ -148,8 +148,12 @@ enum {
   RETR_TUNE_SPLITK_FUSED = 18,  /* split-K forward / data-gradient linears: 0 slabs + a separate
                                    slab-epilogue launch, 1 slice sum + epilogue by each tile's
                                    last-arriving block (csrc/splitk_fused.hpp) */
-  RETR_TUNE_WB_CHUNK = 19,      /* logical blocks per XCD turn in retr_linear_wgrad_batch (0: 4) */
-  RETR_TUNE_CW_CHUNK = 20,      /* logical blocks per XCD turn in retr_conv2d_wgrad_group (0: 4) */
+  RETR_TUNE_WB_CHUNK = 19,      /* retr_linear_wgrad_batch block order: 0 problem-affine pieces
+                                   (one XCD per problem / row-tile run), n > 0 runs of n
+                                   logical blocks per XCD turn (round 4: 4) */
+  RETR_TUNE_CW_CHUNK = 20,      /* retr_conv2d_wgrad_group block order: 0 slice-affine (every tile
+                                   of a K-slice on one XCD), n > 0 runs of n logical blocks per
+                                   XCD turn, -1 runs of 4 (round 4) */
   RETR_TUNE_CONV3X3 = 21,       /* bf16 3x3 stride-1 convs (fwd / dgrad): 0 the direct kernel with
                                    the input halo in LDS on maps >= 32 wide (csrc/conv3x3.hip),
                                    1 the implicit GEMM, 2 the direct kernel on every map >= 16 */

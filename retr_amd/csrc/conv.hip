@@ -1189,37 +1189,64 @@ Geom make_geom(int Nb, int H, int W, int C, int Co, int KH, int KW, int s, int p
 // re-read by the unpacks fall ~5x.  Problems live in a device table (put by table_put launches in
 // stream order); logical blocks go to the XCDs in runs of kCWChunk, the XCDs taking turns, with
 // the longest blocks first.
+//
+// Slice-affine order (round 5, the default): every tile of one K-slice (one pixel range of one
+// conv) runs on ONE XCD, the slices dealt to the XCDs round-robin (longest blocks first).  The
+// tiles of a slice all read the same dY rows and X rows, so that XCD's L2 fetches them from HBM
+// once; in runs of 4 tiles per XCD turn (the round-4 order, still selectable with a positive
+// RETR_TUNE_CW_CHUNK) the 36 tiles of a 3x3 / 256-channel slice were spread over 9 runs on
+// different XCDs and dY came from HBM ~4.5 times (1.89x the algorithmic bytes per step).
 struct CWProb {
   const bf16* dy;
   const bf16* x;
   float* ws;
   Geom g;
   int splits, kchunk, tiles_n, tiles, blk0, vec;
+  int xpre[8];      // slice-affine: blocks of earlier problems in each XCD's queue
+  int s0, pad[3];   // global index of the problem's first slice (slice s0 + i -> XCD (s0+i)%8)
 };
 struct CWHead {
   int nprob, total, pad0, pad1;
+  int xtot[8];      // slice-affine: blocks in each XCD's queue
 };
-static_assert(sizeof(CWProb) == 96 && sizeof(CWHead) == 16, "conv wgrad table");
+static_assert(sizeof(CWProb) == 144 && sizeof(CWHead) == 48, "conv wgrad table");
 constexpr int kCWChunk = 4;
 
 template <int KIND>
 __global__ void __launch_bounds__(KIND ? 512 : 256) conv_wgrad_group_kernel(const char* __restrict__ table,
                                                                             int chunk) {
-  const CWHead h = *(const CWHead*)table;
+  const CWHead& h = *(const CWHead*)table;
   const CWProb* P = (const CWProb*)(table + sizeof(CWHead));
   const int hw = blockIdx.x, xc = hw & 7, q = hw >> 3;
-  const int L = (q / chunk) * (8 * chunk) + xc * chunk + q % chunk;
-  if (L >= h.total) return;
-  int lo = 0, hi = h.nprob - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (P[mid].blk0 <= L) lo = mid;
-    else hi = mid - 1;
+  const int nprob = h.nprob;
+  int lo = 0, split, tile;
+  if (chunk > 0) {                       // runs of `chunk` logical blocks per XCD turn
+    const int L = (q / chunk) * (8 * chunk) + xc * chunk + q % chunk;
+    if (L >= h.total) return;
+    int hi = nprob - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (P[mid].blk0 <= L) lo = mid;
+      else hi = mid - 1;
+    }
+    const int local = L - P[lo].blk0;
+    split = local / P[lo].tiles;
+    tile = local - split * P[lo].tiles;
+  } else {                               // slice-affine
+    if (q >= h.xtot[xc]) return;
+    int hi = nprob - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (P[mid].xpre[xc] <= q) lo = mid;
+      else hi = mid - 1;
+    }
+    const int local = q - P[lo].xpre[xc], T = P[lo].tiles;
+    const int j = local / T;
+    tile = local - j * T;
+    split = (((xc - P[lo].s0) % 8 + 8) % 8) + 8 * j;
   }
   const CWProb d = P[lo];
   const Geom& g = d.g;
-  const int local = L - d.blk0;
-  const int split = local / d.tiles, tile = local - split * d.tiles;
   const int Mp = g.Nb * g.OH * g.OW, R = g.Co, Ncols = g.KH * g.KW * g.C;
   const DenseT<bf16> la{d.dy, (long)g.Co, R, Mp};
   EpiAccF32 ep{d.ws, (long)Ncols, 0, d.vec, 1, nullptr};
@@ -1595,6 +1622,8 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
     CWHead* h = (CWHead*)buf.data();
     CWProb* P = (CWProb*)(buf.data() + sizeof(CWHead));
     int blocks = 0;
+    int xcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int sigma = 0;
     for (size_t j = 0; j < ord.size(); ++j) {
       const retr_conv_wgrad_desc& q = d[ord[j]];
       const Geom g = make_geom(q.Nb, q.H, q.W, q.C, q.Co, q.KH, q.KW, q.stride, q.pad, q.dil);
@@ -1614,9 +1643,18 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
       p.blk0 = blocks;
       p.vec = vec8_ok<float>(q.ws, (long)Ncols) ? 1 : 0;
       blocks += p.tiles * p.splits;
+      p.s0 = sigma;
+      for (int x = 0; x < 8; ++x) p.xpre[x] = xcnt[x];
+      for (int i = 0; i < p.splits; ++i) xcnt[(sigma + i) & 7] += p.tiles;
+      sigma += p.splits;
     }
     h->nprob = (int)ord.size();
     h->total = blocks;
+    int xmax = 0;
+    for (int x = 0; x < 8; ++x) {
+      h->xtot[x] = xcnt[x];
+      xmax = xcnt[x] > xmax ? xcnt[x] : xmax;
+    }
     const int words = (int)((sizeof(CWHead) + ord.size() * sizeof(CWProb) + 3) / 4);
     const unsigned* src = (const unsigned*)buf.data();
     for (int off = 0; off < words; off += 640) {
@@ -1627,9 +1665,11 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
       hipLaunchKernelGGL(cw_table_put_kernel, dim3(1), dim3(256), 0, st, c, (unsigned*)table);
       if (int e = retr_check_launch("conv2d_wgrad_group table")) return e;
     }
+    // RETR_TUNE_CW_CHUNK > 0: the round-4 order in runs of that many blocks per XCD turn;
+    // 0 (default): slice-affine; -1: the round-4 default run length
     int chunk = retr_tune_get(RETR_TUNE_CW_CHUNK);
-    if (chunk <= 0) chunk = kCWChunk;
-    const int grid = cdiv(blocks, 8 * chunk) * 8 * chunk;
+    if (chunk < 0) chunk = kCWChunk;
+    const int grid = chunk > 0 ? cdiv(blocks, 8 * chunk) * 8 * chunk : 8 * xmax;
     constexpr size_t lds = gemm2_lds_bytes<128, 128, 2, 0>();
     if (kind == 0) {
       auto kern = conv_wgrad_group_kernel<0>;

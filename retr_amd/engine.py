@@ -102,9 +102,14 @@ class GraphedTrainStep:
     step counter and lr live on the device); fixed batch shapes.
     """
 
-    def __init__(self, model, criterion, optimizer, max_norm, grad_sync=None, warmup=2):
+    def __init__(self, model, criterion, optimizer, max_norm, grad_sync=None, warmup=2,
+                 consume=True):
         self.model, self.criterion, self.optimizer = model, criterion, optimizer
         self.max_norm, self.grad_sync, self.warmup = max_norm, grad_sync, warmup
+        # FusedAdamW consume mode inside the captured update (see __call__); False keeps the
+        # step's gradients in the arena after each replay (tests read them), at the cost of
+        # one zero fill of the arena before every replay
+        self.consume = bool(consume)
         self.graph = None
         self.graph_opt = None
         self.segments = []        # DP: forward/backward segment graphs (segments[0] is graph)
@@ -274,7 +279,8 @@ class GraphedTrainStep:
             for dst, src in zip(self.static, (nt.tensors, nt.mask, caps, cap_masks)):
                 # zero-copy when the caller handed back the step's own input buffers (a loader
                 # that writes each batch into input_buffers()): nothing to stage
-                if src.data_ptr() != dst.data_ptr() or src.shape != dst.shape:
+                if (src.data_ptr() != dst.data_ptr() or src.shape != dst.shape
+                        or src.stride() != dst.stride() or src.dtype != dst.dtype):
                     dst.copy_(src, non_blocking=True)
         if self.graph is None:
             opt = self.optimizer
@@ -284,7 +290,7 @@ class GraphedTrainStep:
                 # per replay) only for the steps this object runs -- warm-up and capture; the
                 # captured update keeps it on every replay, eager steps outside keep the
                 # optimizer's own setting (p.grad holds the clipped gradient after step())
-                opt.consume_grads = True
+                opt.consume_grads = self.consume
             try:
                 snap = self._snapshot()
                 side = torch.cuda.Stream()

@@ -136,7 +136,7 @@ class ConcatTransformer(nn.Module):
             raise RuntimeError(f"The size of tensor a ({T}) must match the size of tensor b "
                                f"({qpos.shape[0]}) at non-singleton dimension 0")
         kpm_tgt = tgt_mask.contiguous().view(torch.uint8)
-        y = ops.embed_ln(self.embeddings, tgt, self.training)
+        y = ops.embed_ln(self.embeddings, tgt, self.training, shared=True)
         att_s, att_x = [], []
         layers = list(self.decoder.layers)
         for i, layer in enumerate(layers):

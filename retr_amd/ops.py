@@ -22,6 +22,7 @@ import os
 import torch
 
 from . import _lib
+from . import optim as _optim
 from .optim import grad_buffer
 from ._lib import BF16, F32, call, ptr
 
@@ -880,25 +881,29 @@ def _ln_bwd_fused(x, gamma, beta, mean, rstd, dy, dy2, addend, prev, cdtype, pos
     return dx, dgamma, dbeta, dpos, extra, ag and ab
 
 
-# Position gradients of a table several blocks read (the decoder's query positions: 12 blocks)
-# are queued per buffer and summed by one retr_pos_grad_multi launch when the weight-gradient
-# queue flushes (same sums in the same order as one retr_pos_grad per block).  Only for
-# FusedAdamW arena buffers: autograd adopts those as .grad without reading them, so the
-# buffer may be filled later in stream order.
+# Position gradients of a table several blocks read (the decoder's query positions: 12 blocks,
+# plus the DecoderEmbeddings sum, which joins the same shared buffer: _EmbedLN) are queued per
+# buffer and summed by one retr_pos_grad_multi launch when the weight-gradient queue flushes, or
+# when the table's last contributor (the embedding backward) needs the buffer (same sums in the
+# same order as one retr_pos_grad per block).  Only for FusedAdamW arena buffers, which autograd
+# adopts as .grad without reading them -- and only because the queue holds the buffer's ADDRESS,
+# never the tensor: an extra reference makes AccumulateGrad clone the buffer (a read, in stream
+# order before the queued sums land; round 4's lost query-position gradient).
 POS_DEFER = True    # graphed step 9.670 -> 9.622 ms (profiles/r4_ab_pos_defer.txt)
-_POSQ = {}     # dpos data_ptr -> [dpos, C, period, [(dy2, M), ...]]
+_POSQ = {}     # dpos data_ptr -> [dpos data_ptr, C, period, [(dy2, M), ...]]
 
 
 def _pos_queue(dy2, M, C, period, dpos):
-    e = _POSQ.get(dpos.data_ptr())
+    p = dpos.data_ptr()
+    e = _POSQ.get(p)
     if e is None or e[1] != C or e[2] != period:
         if e is not None:
             _pos_flush_one(e)
-        e = _POSQ[dpos.data_ptr()] = [dpos, C, period, []]
+        e = _POSQ[p] = [p, C, period, []]
     e[3].append((dy2, M))
     if len(e[3]) == 16:
         _pos_flush_one(e)
-        del _POSQ[dpos.data_ptr()]
+        del _POSQ[p]
     if not _WQ_STATE["armed"]:
         try:
             torch.autograd.Variable._execution_engine.queue_callback(flush_wgrad)
@@ -912,13 +917,43 @@ def _pos_flush_one(e):
     arr = (_lib.PosItem * len(items))()
     for i, (d, M) in enumerate(items):
         arr[i].d, arr[i].ld, arr[i].M = ptr(d), d.stride(0), M
-    call("retr_pos_grad_multi", BF16, len(items), arr, C, period, ptr(dpos), 1, _st())
+    call("retr_pos_grad_multi", BF16, len(items), arr, C, period, dpos, 1, _st())
 
 
-def flush_pos():
+def flush_pos(addr=None):
+    """Run the queued position-gradient sums (only the buffer at ``addr`` if given)."""
+    if addr is not None:
+        e = _POSQ.pop(addr, None)
+        if e is not None:
+            _pos_flush_one(e)
+        return
     for e in list(_POSQ.values()):
         _pos_flush_one(e)
     _POSQ.clear()
+
+
+def _deferred_overlaps(lo, hi):
+    """True if a queued weight / position gradient writes into the byte range [lo, hi)."""
+    if any(a < hi and lo < b for a, b in _WQ_STATE["ranges"]):
+        return True
+    return any(lo <= p < hi for p in _POSQ)
+
+
+def _on_grad_reuse(p):
+    """optim.grad_buffer hook: parameter ``p``'s arena slot was already handed out this pass
+    and a second contributor is asking for a buffer.  Autograd will add the two (InputBuffer /
+    AccumulateGrad read the arena view), so whatever is still queued for that slot must be in
+    stream order before this contributor's kernels: flush it now."""
+    v = p._retr_grad_view
+    lo = v.data_ptr()
+    hi = lo + v.numel() * v.element_size()
+    if _deferred_overlaps(lo, hi):
+        GRAD_REUSE_STATS["flushes"] += 1
+        flush_wgrad()
+
+
+GRAD_REUSE_STATS = {"flushes": 0}
+_optim.REUSE_HOOK = _on_grad_reuse
 
 
 # ---------------------------------------------------------------------------------------------
@@ -1277,7 +1312,7 @@ def ffn_block(res_mod, x, training, cdtype, next_norm=None):
 
 class _EmbedLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, caps, word, posw, gamma, beta, eps, drop_p, padding_idx):
+    def forward(ctx, caps, word, posw, gamma, beta, eps, drop_p, padding_idx, shared):
         B, T = caps.shape
         C = word.shape[1]
         if T > posw.shape[0]:
@@ -1294,6 +1329,12 @@ class _EmbedLN(torch.autograd.Function):
         ctx.save_for_backward(caps, word, posw, gamma, mean, rstd)
         ctx.gparams = (word, posw, gamma, beta)
         ctx.cfg = (eps, drop_p, seed, padding_idx)
+        # the decoder blocks add their query-position gradients into one shared buffer of the
+        # table (_shared_grad); the embedding's own position sum joins it, so autograd gets ONE
+        # gradient for the parameter (adopted, never read) instead of two to add
+        ctx.shared = bool(shared) and posw.requires_grad
+        if ctx.shared:
+            _share(posw)
         return y
 
     @staticmethod
@@ -1304,21 +1345,36 @@ class _EmbedLN(torch.autograd.Function):
         C = word.shape[1]
         dev = word.device
         dy = dy.contiguous()
-        (dword, _), (dposw, _), (dgamma, _), (dbeta, _) = map(grad_buffer, ctx.gparams)
+        wp, pp, gp, bp = ctx.gparams
+        (dword, _), (dgamma, _), (dbeta, _) = map(grad_buffer, (wp, gp, bp))
+        dposw, last = None, True
+        if ctx.needs_input_grad[2] or ctx.shared:
+            if ctx.shared:
+                (dposw, _), _, last = _shared_grad(pp, lambda: grad_buffer(pp))
+                # the decoder blocks' queued sums land first: (sum of blocks) + embedding, the
+                # order of the per-block launches followed by autograd's add
+                flush_pos(dposw.data_ptr())
+            else:
+                dposw, _ = grad_buffer(pp)
         M = B * T    # workspace: retr_embed_ln_bwd_workspace(B, T, C) bytes
         ws = torch.empty(M * C + 2 * C * ((M + 31) // 32), dtype=torch.float32, device=dev)
         call("retr_embed_ln_bwd", ptr(caps), B, T, C, ptr(word), ptr(posw), ptr(gamma),
              ptr(mean), ptr(rstd), ptr(dy), drop_p, seed, ptr(dword), ptr(dposw), ptr(dgamma),
              ptr(dbeta), -1 if padding_idx is None else int(padding_idx), ptr(ws), _st())
-        return None, dword, dposw, dgamma, dbeta, None, None, None
+        if not (last and ctx.needs_input_grad[2]):
+            dposw = None
+        return None, dword, dposw, dgamma, dbeta, None, None, None, None
 
 
-def embed_ln(emb, caps, training):
-    """emb: DecoderEmbeddings parameter container."""
+def embed_ln(emb, caps, training, shared=False):
+    """emb: DecoderEmbeddings parameter container.  ``shared``: the position table's gradient
+    is also accumulated by the blocks that read it as query positions in this pass
+    (ConcatTransformer.decode, after begin_pass)."""
     p = _drop_p(training, emb.dropout.p)
     we = emb.word_embeddings
     return _EmbedLN.apply(caps, we.weight, emb.position_embeddings.weight, emb.LayerNorm.weight,
-                          emb.LayerNorm.bias, emb.LayerNorm.eps, p, we.padding_idx)
+                          emb.LayerNorm.bias, emb.LayerNorm.eps, p, we.padding_idx,
+                          shared and torch.is_grad_enabled())
 
 
 # ---------------------------------------------------------------------------------------------

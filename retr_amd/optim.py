@@ -68,11 +68,20 @@ def grad_slot(p):
     return a.hand_out(p)
 
 
+# Called with ``p`` when a parameter whose arena slot was already handed out this pass gets a
+# second gradient contributor (ops sets it: flushes deferred sums aimed at that slot, because
+# autograd is about to read the slot to add the two contributions).
+REUSE_HOOK = None
+
+
 def grad_buffer(p, shape=None):
     """(buffer, from_arena): a zeroed fp32 buffer shaped like ``p`` (or ``shape``)."""
     v = grad_slot(p)
     if v is not None:
         return (v if shape is None else v.view(shape)), True
+    a = getattr(p, "_retr_arena", None)
+    if a is not None and REUSE_HOOK is not None and id(p) in a.handed:
+        REUSE_HOOK(p)
     return torch.zeros(shape if shape is not None else p.shape, dtype=torch.float32,
                        device=p.device), False
 

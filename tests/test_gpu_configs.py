@@ -146,13 +146,38 @@ def _seeded_step(model, crit, images, mask, caps, cap_mask, seed_ctr=0, seed_bas
     return out, loss
 
 
-@pytest.mark.parametrize("dropout", [0.0, 0.1])
-def test_cfg2_bf16_full_batch_step(dropout):
+def _attach_arena(model):
+    """The benchmarked optimizer (FusedAdamW): every trainable parameter moves into its arena,
+    so the backward writes weight gradients into arena slots and the deferred paths run
+    (ops.WGRAD_DEFER: the transformer + head weight gradients as one batched launch,
+    ops.POS_DEFER: the query-position sums, resnet.CONV_WGRAD_GROUP)."""
+    from retr_amd.optim import FusedAdamW
+    return FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+
+
+def _assert_adopted(model):
+    """Every trainable gradient IS its arena slot: autograd adopted the buffer the kernels wrote
+    (no second contribution added outside it, no clone taken before a deferred sum landed)."""
+    foreign = [n for n, p in model.named_parameters() if p.requires_grad
+               and (p.grad is None or p.grad.data_ptr() != p._retr_grad_view.data_ptr())]
+    assert not foreign, foreign
+
+
+def _defer_counters():
+    from retr_amd import ops, resnet
+    return (ops.WGRAD_STATS["flushes"], ops.WGRAD_STATS["problems"],
+            resnet.CONV_WGRAD_STATS["grouped"])
+
+
+@pytest.mark.parametrize("dropout,arena", [(0.0, False), (0.1, False), (0.1, True)])
+def test_cfg2_bf16_full_batch_step(dropout, arena):
     """The benchmarked shape (batch 16, 640x640, bf16 operands, dropout 0.1 as timed and 0.0)
     forward + backward against the fp32 HIP model (exact-f32 MFMA; the fp32 path is pinned to
     the CPU oracle at cfg2 / cfg4 batch 1 above) on the same weights, inputs and dropout
     masks: loss within 1e-2 and EVERY trainable gradient within BF16_GRAD_REL (relative L2).
-    Reference step: engine.py:70-80."""
+    ``arena``: with the benchmarked FusedAdamW attached, so the gradients come through the
+    deferred weight-gradient batch, the queued position sums and the grouped conv weight
+    gradients, read from the arena before any step().  Reference step: engine.py:70-80."""
     B = 16
     images, mask = synthetic_images(B, 640, seed=3)
     _, m32, crit, _ = _model(CFG2, "fp32", dropout=dropout)
@@ -163,25 +188,39 @@ def test_cfg2_bf16_full_batch_step(dropout):
     l32 = l32.item()
     del m32
     torch.cuda.empty_cache()
+    opt = _attach_arena(m16) if arena else None
+    c0 = _defer_counters()
     _, l16 = _seeded_step(m16, crit, images, mask, caps, cap_mask, 1000, 12345)
+    c1 = _defer_counters()
     l16 = l16.item()
     assert torch.isfinite(torch.tensor([l16, l32])).all()
     assert abs(l16 - l32) <= 1e-2 * abs(l32), (l16, l32)
+    if arena:
+        _assert_adopted(m16)
+        # one batched transformer + head launch (~90 problems at 6/6), grouped conv wgrads
+        assert c1[0] - c0[0] >= 1 and c1[1] - c0[1] >= 80 and c1[2] - c0[2] > 40, (c0, c1)
     errs = _grad_errors(m16, ref)
     assert len(errs) >= 230, len(errs)
-    _assert_grads(errs, BF16_GRAD_REL, f"cfg2 bf16 B=16 dropout {dropout}")
+    _assert_grads(errs, BF16_GRAD_REL, f"cfg2 bf16 B=16 dropout {dropout} arena {arena}")
+    del opt
 
 
-def test_cfg2_bf16_batch2_vs_oracle():
+@pytest.mark.parametrize("arena", [False, True])
+def test_cfg2_bf16_batch2_vs_oracle(arena):
     """The bf16 training path at cfg2's image size (640x640, R50 6/6 d256; batch 2) against the
     CPU oracle directly: logits within 2e-2 of the oracle's scale, loss within 1e-2, every
-    trainable gradient within BF16_GRAD_REL.  Reference: engine.py:70-80 on
-    models/caption.py:23-47."""
+    trainable gradient within BF16_GRAD_REL.  ``arena``: through the benchmarked FusedAdamW
+    arena (deferred / batched weight and position gradients), gradients read before step().
+    Reference: engine.py:70-80 on models/caption.py:23-47."""
     B = 2
     cfg, model, crit, sd = _model(CFG2, "bf16")
     images, mask = synthetic_images(B, 640, seed=21, pad_band=True)
     caps, cap_mask = synthetic_captions(B, cfg.max_position_embeddings, cfg.vocab_size, seed=22)
+    opt = _attach_arena(model) if arena else None
     out, loss = _seeded_step(model, crit, images, mask, caps, cap_mask)
+    if arena:
+        _assert_adopted(model)
+        del opt
     trainable = {n for n, p in model.named_parameters() if p.requires_grad}
     sdo = {k: (v.clone().requires_grad_(True) if k in trainable else v) for k, v in sd.items()}
     lo = orc.caption_forward(sdo, cfg, images, mask, caps[:, :-1], cap_mask[:, :-1])
@@ -192,6 +231,58 @@ def test_cfg2_bf16_batch2_vs_oracle():
     assert abs(loss.item() - loss_o.item()) <= 1e-2 * abs(loss_o.item())
     errs = _grad_errors(model, {n: sdo[n].grad for n in trainable})
     _assert_grads(errs, BF16_GRAD_REL, "cfg2 bf16 B=2 vs oracle")
+
+
+def test_cfg2_graphed_step_gradients_vs_fp32():
+    """The timed step itself: bench.py's GraphedTrainStep (cfg2, batch 16, bf16, dropout 0.1,
+    FusedAdamW arena, every deferral on) captured and replayed once with consume mode off and
+    no clipping, so the replay's gradients stay in the arena -- against the fp32 HIP model's
+    eager backward on the same weights (the replay runs at the restored pre-warm-up weights),
+    inputs and dropout masks (the capture's per-op seeds and the device step seed bumped
+    once): loss within 1e-2, EVERY trainable gradient within BF16_GRAD_REL.
+    Reference: engine.py:70-83."""
+    from retr_amd import ops
+    from retr_amd.engine import GraphedTrainStep
+    B = 16
+    images, mask = synthetic_images(B, 640, seed=5)
+    cfg, m16, crit, _ = _model(CFG2, "bf16", dropout=0.1)
+    caps, cap_mask = synthetic_captions(B, cfg.max_position_embeddings, cfg.vocab_size, seed=6)
+    opt = _attach_arena(m16)
+    step = GraphedTrainStep(m16, crit, opt, max_norm=0.0, consume=False)
+    box = {}
+    cap = step._capture
+
+    def rec():
+        box["ctr"] = ops._seed_state["ctr"]
+        cap()
+    step._capture = rec
+    base = int(ops.seed_base().item())
+    loss16 = float(step((NestedTensor(images.to(DEV), mask.to(DEV)),), caps.to(DEV),
+                        cap_mask.to(DEV)))
+    torch.cuda.synchronize()
+    names = [n for n, p in m16.named_parameters() if p.requires_grad]
+    g16 = {n: p._retr_grad_view.detach().clone() for n, p in m16.named_parameters()
+           if p.requires_grad}
+    del step, opt, m16
+    torch.cuda.empty_cache()
+    _, m32, _, _ = _model(CFG2, "fp32", dropout=0.1)
+    ops.seed_base().fill_(base)
+    ops.bump_seed()                      # forward_backward's bump, replayed inside the graph
+    _, l32 = _seeded_step(m32, crit, images, mask, caps, cap_mask, box["ctr"], None)
+    l32 = l32.item()
+    assert abs(loss16 - l32) <= 1e-2 * abs(l32), (loss16, l32)
+
+    class _G:                            # _grad_errors reads p.grad / named_parameters
+        def __init__(self, g):
+            self.g = g
+
+        def named_parameters(self):
+            for n in names:
+                yield n, type("P", (), {"requires_grad": True, "grad": self.g[n]})()
+    ref = {n: p.grad.detach() for n, p in m32.named_parameters() if p.requires_grad}
+    errs = _grad_errors(_G(g16), ref)
+    assert len(errs) >= 230, len(errs)
+    _assert_grads(errs, BF16_GRAD_REL, "cfg2 graphed step (one replay) vs fp32")
 
 
 def _recompute_margins(model, samples, ids):

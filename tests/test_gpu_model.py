@@ -521,6 +521,12 @@ def test_deferred_position_gradients_match_per_block_launches():
             loss.backward()
             assert not ops._POSQ
             torch.cuda.synchronize()
+            # the table's 12 query-position contributions and the embedding's own sum meet in
+            # ONE arena buffer that autograd adopts (round 4 lost the queued part: autograd
+            # cloned the buffer before the queued sums were written)
+            foreign = [n for n, p in model.named_parameters() if p.grad is not None
+                       and p.grad.data_ptr() != p._retr_grad_view.data_ptr()]
+            assert not foreign, foreign
             res.append({n: p.grad.detach().clone() for n, p in model.named_parameters()
                         if p.grad is not None})
     finally:
@@ -530,3 +536,126 @@ def test_deferred_position_gradients_match_per_block_launches():
     assert any("position_embeddings" in n for n in g1)
     for n in g1:
         assert torch.equal(g1[n], g0[n]), n
+
+
+def test_position_table_gradient_has_every_contribution():
+    """position_embeddings.weight is read twice by the reference (DecoderEmbeddings,
+    transformer_modules.py:118-127, and as the decoder's query_pos, ConcatTransformer.py:64-65):
+    its gradient through the default bf16 FusedAdamW path (deferred query-position sums) equals
+    the sum of both uses, computed here by differentiating the two uses separately -- a
+    missing contribution (round 4's bug) is an O(1) relative error, far above bf16 noise."""
+    from retr_amd import ops
+    from retr_amd.optim import FusedAdamW
+    cfg = make_config(backbone="ResNet18", hidden=256, layers=(2, 2), vocab=1000, max_pos=16,
+                      ffn=512, dtype="bf16", dropout=0.0)
+    model, crit = build_model(cfg)
+    model.load_state_dict(synthetic_state_dict(model, seed=9))
+    model.to(DEV).train()
+    opt = FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+    images, mask = synthetic_images(2, 64, seed=1, pad_band=True)
+    caps, cap_mask = synthetic_captions(2, 16, 1000, seed=2)
+    s = NestedTensor(images.to(DEV), mask.to(DEV))
+    pw = model.transformer.embeddings.position_embeddings.weight
+
+    def run():
+        opt.zero_grad(set_to_none=True)
+        out = model(s, caps[:, :-1].to(DEV), cap_mask[:, :-1].to(DEV))
+        loss = crit(out.permute(0, 2, 1), caps[:, 1:].to(DEV))
+        loss.backward()
+        torch.cuda.synchronize()
+        return pw.grad.detach().clone()
+
+    full = run()
+    # the per-block launches (POS_DEFER off) give the same bits
+    ops.POS_DEFER = False
+    try:
+        ref = run()
+    finally:
+        ops.POS_DEFER = True
+    assert torch.equal(full, ref)
+    # embedding-only gradient: the same forward with the decoder blocks' query positions
+    # detached (decode() calls ops.self_attn_block / ops.cross_attn_block at run time)
+    saved = ops.self_attn_block, ops.cross_attn_block
+
+    def sab(sa, y, qpos, *a, **k):
+        return saved[0](sa, y, qpos.detach() if qpos is pw else qpos, *a, **k)
+
+    def cab(ca, y, qpos, *a, **k):
+        return saved[1](ca, y, qpos.detach() if qpos is pw else qpos, *a, **k)
+    ops.self_attn_block, ops.cross_attn_block = sab, cab
+    try:
+        emb_only = run()
+    finally:
+        ops.self_attn_block, ops.cross_attn_block = saved
+    # query-position-only gradient: the embedding reads a detached table
+    saved_e = ops.embed_ln
+
+    def el(emb, caps_, training, shared=False):
+        w = emb.position_embeddings.weight
+        emb.position_embeddings.weight = torch.nn.Parameter(w.detach(), requires_grad=False)
+        try:
+            return saved_e(emb, caps_, training, shared=False)
+        finally:
+            emb.position_embeddings.weight = w
+    ops.embed_ln = el
+    try:
+        q_only_g = run()
+    finally:
+        ops.embed_ln = saved_e
+    both = emb_only.double() + q_only_g.double()
+    e = ((full.double() - both).norm() / both.norm()).item()
+    assert e < 1e-5, e
+    # each use really contributes, far above the 1e-5 bound (else the test would be vacuous):
+    # at this size the 4 query-position uses are ~2% of the table's gradient norm
+    assert q_only_g.norm() > 1e-3 * both.norm() and emb_only.norm() > 1e-3 * both.norm()
+
+
+def test_deferred_weight_used_twice_flushes_before_second_contribution():
+    """A parameter with a deferred (queued) weight gradient that gets a second contributor in
+    the same backward: autograd adds the two, reading the first (arena) buffer, so the queue
+    must have run first (optim.REUSE_HOOK -> ops._on_grad_reuse).  The MLP head applied twice
+    in one graph, FusedAdamW arena, bf16: every gradient equals the immediate-launch path
+    (rel 1e-5: batch vs single-problem kernels) and the sum of the two uses' gradients taken one
+    use per backward, and the hook fired."""
+    from retr_amd import ops
+    from retr_amd.models.caption import MLP
+    from retr_amd.optim import FusedAdamW
+    torch.manual_seed(0)
+    B, T, C, V = 2, 16, 64, 1000
+    mlp = MLP(C, 128, V, 3).to(DEV)
+    opt = FusedAdamW(list(mlp.parameters()), lr=1e-4)
+    hs = [torch.randn(B * T, C, device=DEV).to(torch.bfloat16) for _ in range(2)]
+    wts = [torch.randn(B, T, V, device=DEV) for _ in range(2)]
+    res = []
+    try:
+        for defer in (True, False):
+            ops.HEAD_WGRAD_DEFER = defer
+            opt.zero_grad(set_to_none=True)
+            ops.begin_pass()
+            r0 = ops.GRAD_REUSE_STATS["flushes"]
+            loss = sum((ops.mlp_head(mlp, h, B, T, torch.bfloat16).float() * w).sum()
+                       for h, w in zip(hs, wts))
+            loss.backward()
+            torch.cuda.synchronize()
+            res.append(({n: p.grad.detach().clone() for n, p in mlp.named_parameters()},
+                        ops.GRAD_REUSE_STATS["flushes"] - r0))
+    finally:
+        ops.HEAD_WGRAD_DEFER = True
+    (g1, f1), (g0, f0) = res
+    assert f1 >= 1 and f0 == 0, (f1, f0)
+    # every contribution: the sum of the two uses' gradients, each from its own backward (one
+    # use per pass, so nothing is reused or queued twice) -- equal up to the order of the final
+    # fp32 add; a lost use would be an O(1) relative error
+    single = []
+    for h, w in zip(hs, wts):
+        opt.zero_grad(set_to_none=True)
+        ops.begin_pass()
+        (ops.mlp_head(mlp, h, B, T, torch.bfloat16).float() * w).sum().backward()
+        torch.cuda.synchronize()
+        single.append({n: p.grad.detach().clone() for n, p in mlp.named_parameters()})
+    for n in g1:
+        e = ((g1[n] - g0[n]).double().norm() / g0[n].double().norm()).item()
+        assert e < 1e-5, (n, e)
+        r = single[0][n].double() + single[1][n].double()
+        e = ((g1[n].double() - r).norm() / r.norm()).item()
+        assert e < 1e-5, (n, e)

@@ -80,6 +80,11 @@ VARIANTS = {
     "pos_off": {("ATTR", "POS_DEFER"): False},
     "up2k": {("TUNE", 28): 2048},
     "up8k": {("TUNE", 28): 8192},
+    # round 5: slice-affine conv wgrad / problem-affine linear wgrad orders are the defaults;
+    # these restore the round-4 runs of 4 logical blocks per XCD turn
+    "cw_r4": {("TUNE", 20): -1},
+    "wb_r4": {("TUNE", 19): 4},
+    "orders_r4": {("TUNE", 20): -1, ("TUNE", 19): 4},
 }
 
 
