@@ -124,7 +124,8 @@ def train_bench(args, rank, world, device):
 
     for _ in range(args.warmup):
         loss = step()
-    if graph_step is not None and graph_step.input_buffers() is not None:
+    if (graph_step is not None and graph_step.input_buffers() is not None
+            and not args.stage_inputs):
         # the batch lives in the captured step's own input buffers (as a loader writing each
         # batch there would leave it): no per-step device-to-device staging copy
         st = graph_step.input_buffers()
@@ -357,7 +358,26 @@ def _traffic(family):
     ent = d.get("families", {}).get(family)
     if not ent:
         return None, None
-    return ent.get("bytes_per_launch"), d.get("source")
+    return ent, d.get("source")
+
+
+def _traffic_fields(family, calls_per_step, bytes_per_call):
+    """Counted HBM traffic of ``family`` in both units: per kernel DISPATCH (what the --pmc pass
+    measures) and per retr_* API CALL (what the probe times; one call can dispatch several
+    kernels), with the counted / algorithmic ratio per call."""
+    ent, src = _traffic(family)
+    if not ent:
+        return {"traffic": None, "traffic_source": None}
+    out = {"traffic": ent.get("bytes_per_launch"), "traffic_unit": "bytes per dispatch",
+           "traffic_source": src}
+    dps = ent.get("dispatches_per_step")
+    if dps and calls_per_step:
+        per_call = ent["bytes_per_launch"] * dps / calls_per_step
+        out.update({"dispatches_per_step": round(dps, 2),
+                    "traffic_per_call": round(per_call),
+                    "traffic_over_algorithmic": round(per_call / bytes_per_call, 3)
+                    if bytes_per_call else None})
+    return out
 
 
 def _roofline(fam, psteps):
@@ -376,22 +396,23 @@ def _roofline(fam, psteps):
         achieved, peak, unit = d["gbs"], PEAK_HBM_GBS, "GB/s"
     else:
         achieved, peak, unit = d["tflops"], PEAK_BF16_TFLOPS, "TFLOP/s"
-    traffic, tsrc = _traffic(dom_key)
     n = max(1, d["launches"])
+    tf = _traffic_fields(dom_key, d["launches"] / psteps, d["bytes"] / n)
     return {"bound": "hbm" if hbm else "mfma", "kernel": dom_key,
             "kernel_symbol": probe_mod.FAMILY_SYMBOL.get(dom_key, dom_key),
             "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": tsrc,
+            "frac": round(achieved / peak, 4), **tf,
             "intensity_flop_per_byte": round(d["intensity"], 1),
             "ridge_flop_per_byte": probe_mod.RIDGE,
             "tflops": round(d["tflops"], 2), "mfma_frac": round(d["tflops"] / PEAK_BF16_TFLOPS, 4),
             "gbs": round(d["gbs"], 1), "hbm_frac": round(d["gbs"] / PEAK_HBM_GBS, 4),
             "attainable_frac": round(d["attainable_frac"], 4),
             "mfma_busy": _mfma_busy(dom_key),
-            "launches_per_step": d["launches"] // psteps,
+            "api_calls_per_step": d["launches"] // psteps,
             "avg_launch_us": round(d["ms_avg"] * 1e3, 2),
             "flops_per_launch": round(d["flops"] / n, 1),
             "bytes_per_launch": round(d["bytes"] / n),
+            "launch_unit": "one retr_* API call (may dispatch several kernels: dispatches_per_step)",
             "timing": "HIP events around each launch on torch's current stream (the stream "
                       "every retr kernel runs on), device spin in front so the events bracket "
                       "device time only; eager re-run of the step"}
@@ -434,6 +455,9 @@ def main():
                     help="torch.optim.AdamW(capturable) + clip_grad_norm_ instead of the default "
                          "retr_amd FusedAdamW (clip + AdamW kernels over flat arenas)")
     ap.add_argument("--probe-detail", default="", help="write a per-shape kernel table here")
+    ap.add_argument("--stage-inputs", action="store_true",
+                    help="copy the batch into the captured step's input buffers every step "
+                         "(the pre-round-4 timing; default: the batch already sits there)")
     args = ap.parse_args()
     _, size, batch, wl_desc = WORKLOADS[args.workload]
     args.size = args.size or size
@@ -459,7 +483,11 @@ def main():
                     "tflops": round(v["tflops"], 1), "gbs": round(v["gbs"], 1),
                     "bound": "hbm" if v["intensity"] < probe_mod.RIDGE else "mfma",
                     "attainable_frac": round(v["attainable_frac"], 4),
-                    "launches_per_step": v["launches"] // psteps}
+                    "api_calls_per_step": v["launches"] // psteps,
+                    **{f: t for f, t in _traffic_fields(
+                        k, v["launches"] / psteps, v["bytes"] / max(1, v["launches"])).items()
+                       if f in ("dispatches_per_step", "traffic", "traffic_per_call",
+                                "traffic_over_algorithmic")}}
                 for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms_total"])}
     cores, aff = cpu_threads()
     decode = None
@@ -529,6 +557,13 @@ def main():
                         "backend": dist.get_backend() if dist.is_initialized() else None,
                         "dp_schedule": sched},
                "optimizer": "torch.optim.AdamW" if args.torch_adamw else "FusedAdamW",
+               "input_staging": ("per-step device-to-device copy into the captured step's "
+                                 "input buffers (--stage-inputs)" if args.stage_inputs or
+                                 args.eager else
+                                 "none: the batch is resident in the captured step's input "
+                                 "buffers, as a loader writing each batch there leaves it "
+                                 "(since round 4; rounds 1-3 timed a 78.6 MB staging copy "
+                                 "per step, ~45 us)"),
                "decode": decode, "kernel_families": families}
         print(json.dumps(out), flush=True)
     if world > 1:

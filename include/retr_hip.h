@@ -148,12 +148,12 @@ enum {
   RETR_TUNE_SPLITK_FUSED = 18,  /* split-K forward / data-gradient linears: 0 slabs + a separate
                                    slab-epilogue launch, 1 slice sum + epilogue by each tile's
                                    last-arriving block (csrc/splitk_fused.hpp) */
-  RETR_TUNE_WB_CHUNK = 19,      /* retr_linear_wgrad_batch block order: 0 problem-affine pieces
-                                   (one XCD per problem / row-tile run), n > 0 runs of n
-                                   logical blocks per XCD turn (round 4: 4) */
+  RETR_TUNE_WB_CHUNK = 19,      /* retr_linear_wgrad_batch block order: 0 runs of 4 logical
+                                   blocks per XCD turn, n > 0 runs of n, -1 problem-affine pieces
+                                   (one XCD per problem / row-tile run; 0.05 ms/step slower) */
   RETR_TUNE_CW_CHUNK = 20,      /* retr_conv2d_wgrad_group block order: 0 slice-affine (every tile
-                                   of a K-slice on one XCD), n > 0 runs of n logical blocks per
-                                   XCD turn, -1 runs of 4 (round 4) */
+                                   of a K-slice on one XCD, slices to the least-loaded XCD),
+                                   n > 0 runs of n logical blocks per XCD turn, -1 runs of 4 */
   RETR_TUNE_CONV3X3 = 21,       /* bf16 3x3 stride-1 convs (fwd / dgrad): 0 the direct kernel with
                                    the input halo in LDS on maps >= 32 wide (csrc/conv3x3.hip),
                                    1 the implicit GEMM, 2 the direct kernel on every map >= 16 */
@@ -621,6 +621,22 @@ int retr_dec_attn_row(const void* q, const void* k, const void* v, int R, int C,
                       const float* gamma, const float* beta, float eps, const float* pos,
                       const void* wq, const float* bq, void* q2, void* stream);
 /* FFN over hidden units [32 j, 32 j + 32): slabs[j] = relu(n3 W1_j^T + b1_j) W2[:, j]^T (fp32) */
+/* Decode-step attention sub-layers, one wave per (row, head) (csrc/decode_heads.hip; replace
+ * retr_dec_gemm + retr_dec_attn_row x 2 of the fused step, eval_utils/decode.py:53-81 in
+ * KV-cache form).  Self: the head's q|k|v from n / npos and W_in [3C][C], k / v written to the
+ * cache row r * Lmax + i, attention over keys 0..i (beam ancestry anc), then the head's partial
+ * out-projection into slab[h][R][C].  Cross: xo = x + (sum_h slab_in[h] + bo_in) (heads in
+ * order), LN(xo) (+pos), the head's query from wq rows [h hd, (h+1) hd) + bq, attention over
+ * the memory rows (r / kv_group) * Lk + j (kpm masks), the head's partial out-projection into
+ * slab_out[h][R][C].  C 256 | 512, head dim 32 | 64. */
+int retr_dec_self_heads(const void* n, const void* npos, int R, int C, int H, const void* win,
+                        const float* bin, void* kc, void* vc, int i, int Lmax, const int* anc,
+                        const void* wo, float* slab, void* stream);
+int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_in, float* xo,
+                         int R, int C, int H, const float* gamma, const float* beta, float eps,
+                         const float* pos, const void* wq, const float* bq, const void* k,
+                         const void* v, int Lk, int kv_group, const unsigned char* kpm,
+                         const void* wo, float* slab_out, void* stream);
 int retr_dec_ffn(const void* n3, int R, int C, const void* w1, const float* b1, const void* w2,
                  int F, float* slabs, void* stream);
 

@@ -205,6 +205,9 @@ _SIGS = {
     "retr_dec_attn_row": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F,
                           _P, _P, _P, _P, _P],
     "retr_dec_ffn": [_P, _I, _I, _P, _P, _P, _I, _P, _P],
+    "retr_dec_self_heads": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P],
+    "retr_dec_cross_heads": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I,
+                             _P, _P, _P, _P],
     "retr_adamw_sumsq": [_P, _L, _P, _I, _P, _P],
     "retr_adamw_update": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P, _P],
     "retr_adamw_update2": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P, _I, _P],
@@ -232,6 +235,10 @@ def load():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, ctypes.c_int)
+        # RETR_TUNE_<knob>=<value> in the environment presets a tuning knob (A/B runs)
+        for k, v in os.environ.items():
+            if k.startswith("RETR_TUNE_") and k[10:].isdigit():
+                lib.retr_tune(int(k[10:]), int(v))
         _lib = lib
     return _lib
 

@@ -1202,21 +1202,26 @@ struct CWProb {
   float* ws;
   Geom g;
   int splits, kchunk, tiles_n, tiles, blk0, vec;
-  int xpre[8];      // slice-affine: blocks of earlier problems in each XCD's queue
-  int s0, pad[3];   // global index of the problem's first slice (slice s0 + i -> XCD (s0+i)%8)
+};
+struct CWPiece {    // slice-affine order: one K-slice of one problem, all its tiles on one XCD
+  int prob, split, pre, pad;   // pre: position of the slice's first block in its XCD's queue
 };
 struct CWHead {
-  int nprob, total, pad0, pad1;
-  int xtot[8];      // slice-affine: blocks in each XCD's queue
+  int nprob, total, npiece, pad1;
+  int xpiece[8];    // first piece of each XCD (pieces stored XCD by XCD)
+  int xtot[8];      // blocks in each XCD's queue
 };
-static_assert(sizeof(CWProb) == 144 && sizeof(CWHead) == 48, "conv wgrad table");
+static_assert(sizeof(CWProb) == 96 && sizeof(CWHead) == 80 && sizeof(CWPiece) == 16,
+              "conv wgrad table");
 constexpr int kCWChunk = 4;
+constexpr int kCWMaxSlices = 128;   // per problem (the plan caps the split count at 128)
 
 template <int KIND>
 __global__ void __launch_bounds__(KIND ? 512 : 256) conv_wgrad_group_kernel(const char* __restrict__ table,
                                                                             int chunk) {
   const CWHead& h = *(const CWHead*)table;
   const CWProb* P = (const CWProb*)(table + sizeof(CWHead));
+  const CWPiece* Q = (const CWPiece*)(table + sizeof(CWHead) + (size_t)h.nprob * sizeof(CWProb));
   const int hw = blockIdx.x, xc = hw & 7, q = hw >> 3;
   const int nprob = h.nprob;
   int lo = 0, split, tile;
@@ -1232,19 +1237,19 @@ __global__ void __launch_bounds__(KIND ? 512 : 256) conv_wgrad_group_kernel(cons
     const int local = L - P[lo].blk0;
     split = local / P[lo].tiles;
     tile = local - split * P[lo].tiles;
-  } else {                               // slice-affine
+  } else {                               // slice-affine: this XCD's slices in queue order
     if (q >= h.xtot[xc]) return;
-    int hi = nprob - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (P[mid].xpre[xc] <= q) lo = mid;
-      else hi = mid - 1;
+    int a = h.xpiece[xc], b = (xc < 7 ? h.xpiece[xc + 1] : h.npiece) - 1;
+    while (a < b) {
+      const int mid = (a + b + 1) >> 1;
+      if (Q[mid].pre <= q) a = mid;
+      else b = mid - 1;
     }
-    const int local = q - P[lo].xpre[xc], T = P[lo].tiles;
-    const int j = local / T;
-    tile = local - j * T;
-    split = (((xc - P[lo].s0) % 8 + 8) % 8) + 8 * j;
+    lo = Q[a].prob;
+    split = Q[a].split;
+    tile = q - Q[a].pre;
   }
+  if (lo >= nprob || split >= P[lo].splits || tile >= P[lo].tiles) return;   // table guard
   const CWProb d = P[lo];
   const Geom& g = d.g;
   const int Mp = g.Nb * g.OH * g.OW, R = g.Co, Ncols = g.KH * g.KW * g.C;
@@ -1559,7 +1564,8 @@ int retr_conv2d_wgrad_splits(int dtype, int Nb, int H, int W, int C, int Co, int
 }
 
 size_t retr_conv2d_wgrad_group_table_bytes(int n) {
-  return n < 0 ? 0 : sizeof(CWHead) + (size_t)n * sizeof(CWProb);
+  // two kinds, each header + problems + slices, each start 256-byte aligned
+  return n < 0 ? 0 : 2 * (sizeof(CWHead) + 256) + (size_t)n * (sizeof(CWProb) + kCWMaxSlices * sizeof(CWPiece));
 }
 
 int retr_conv2d_wgrad_group_plan(int dtype, int n, retr_conv_wgrad_desc* d) {
@@ -1618,12 +1624,10 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
       return cdiv(g.Nb * g.OH * g.OW, d[i].splits);
     };
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return blk_len(a) > blk_len(b); });
-    std::vector<char> buf(sizeof(CWHead) + ord.size() * sizeof(CWProb) + 16, 0);
+    std::vector<char> buf(sizeof(CWHead) + ord.size() * (sizeof(CWProb) + kCWMaxSlices * sizeof(CWPiece)) + 16, 0);
     CWHead* h = (CWHead*)buf.data();
     CWProb* P = (CWProb*)(buf.data() + sizeof(CWHead));
     int blocks = 0;
-    int xcnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int sigma = 0;
     for (size_t j = 0; j < ord.size(); ++j) {
       const retr_conv_wgrad_desc& q = d[ord[j]];
       const Geom g = make_geom(q.Nb, q.H, q.W, q.C, q.Co, q.KH, q.KW, q.stride, q.pad, q.dil);
@@ -1643,19 +1647,34 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
       p.blk0 = blocks;
       p.vec = vec8_ok<float>(q.ws, (long)Ncols) ? 1 : 0;
       blocks += p.tiles * p.splits;
-      p.s0 = sigma;
-      for (int x = 0; x < 8; ++x) p.xpre[x] = xcnt[x];
-      for (int i = 0; i < p.splits; ++i) xcnt[(sigma + i) & 7] += p.tiles;
-      sigma += p.splits;
     }
     h->nprob = (int)ord.size();
     h->total = blocks;
-    int xmax = 0;
-    for (int x = 0; x < 8; ++x) {
-      h->xtot[x] = xcnt[x];
-      xmax = xcnt[x] > xmax ? xcnt[x] : xmax;
+    // slice-affine pieces: every K-slice to the least-loaded XCD (load = tiles x K-steps), in
+    // order (longest blocks first)
+    std::vector<CWPiece> per[8];
+    long load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (size_t j = 0; j < ord.size(); ++j) {
+      for (int sp = 0; sp < P[j].splits; ++sp) {
+        int best = 0;
+        for (int x = 1; x < 8; ++x)
+          if (load[x] < load[best]) best = x;
+        const int pre = per[best].empty() ? 0 : per[best].back().pre + P[per[best].back().prob].tiles;
+        per[best].push_back(CWPiece{(int)j, sp, pre, 0});
+        load[best] += (long)P[j].tiles * (P[j].kchunk / 64);
+      }
     }
-    const int words = (int)((sizeof(CWHead) + ord.size() * sizeof(CWProb) + 3) / 4);
+    CWPiece* Qd = (CWPiece*)(buf.data() + sizeof(CWHead) + ord.size() * sizeof(CWProb));
+    int npc = 0, xmax = 0;
+    for (int x = 0; x < 8; ++x) {
+      h->xpiece[x] = npc;
+      for (const CWPiece& w : per[x]) Qd[npc++] = w;
+      h->xtot[x] = per[x].empty() ? 0 : per[x].back().pre + P[per[x].back().prob].tiles;
+      xmax = h->xtot[x] > xmax ? h->xtot[x] : xmax;
+    }
+    h->npiece = npc;
+    const size_t used = sizeof(CWHead) + ord.size() * sizeof(CWProb) + (size_t)npc * sizeof(CWPiece);
+    const int words = (int)((used + 3) / 4);
     const unsigned* src = (const unsigned*)buf.data();
     for (int off = 0; off < words; off += 640) {
       CWPut c;
@@ -1691,8 +1710,8 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
     if (int e = retr_check_launch(kind == 0 ? "conv2d_wgrad_group 1x1" : "conv2d_wgrad_group")) return e;
     // the next kind's table must not overwrite this one before the launch has read it: use
     // the second half of the caller's table for kind 1
-    table = (char*)table + (((sizeof(CWHead) + ord.size() * sizeof(CWProb)) + 255) / 256 * 256);
-    table_bytes -= ((sizeof(CWHead) + ord.size() * sizeof(CWProb)) + 255) / 256 * 256;
+    table = (char*)table + (used + 255) / 256 * 256;
+    table_bytes -= (used + 255) / 256 * 256;
   }
   return 0;
 }

@@ -1,0 +1,380 @@
+// Decode-step attention sub-layers as one WAVE per (query row, head) (round 5).
+//
+// csrc/decode.hip's dec_attn_row runs one block per query row: at B = 64 captions that is 64
+// blocks on 256 CUs, and each of them streams the whole out-projection and next-query weights
+// (2 x 128 KB at C = 256) and every head's keys / values through one CU's load pipeline (13.7 /
+// 11.9 us per launch at cfg5, profiles/r4_rocprof_decode.txt).  Here a launch has R x H waves
+// (512 at B = 64, 2 per CU), and each wave reads only its head's slices:
+//
+//   dec_self_heads   q|k|v of head h from LN1(x) (+pos) -- the [q | k | v] projection rows
+//                    of the head (3 x HD x C weights), k / v appended to the cache row -- then
+//                    attention over the cache (beam ancestry), then the head's PARTIAL
+//                    out-projection o_h Wo[:, h]^T into slab[h][r][:] (fp32)
+//   dec_cross_heads  x' = x + (sum_h slab_in[h][r] + b_o) (heads in order; wave h = 0 writes x'),
+//                    LN2(x') + pos, the head's cross query q_h = (.) Wq[h]^T + b_q, attention over
+//                    the image memory (key-padding mask), the head's partial out-projection
+//                    into slab_out[h][r][:]
+//   (retr_dec_rows then sums slab_out in head order + b_o + residual and runs LN3.)
+//
+// The old dec_gemm launch is folded into dec_self_heads.  Roundings follow the unfused path:
+// bf16 q / k / v / attention output (q also rounded after the 1/sqrt(hd) scale), fp32
+// accumulation and residual; the out-projection sums per head and then over heads (a different
+// fp32 order than one 256-term dot).
+#include "common.hpp"
+#include "../../include/retr_hip.h"
+
+namespace {
+
+template <int CTRL>
+RETR_DEVICE float dh_dpp(float s) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s),
+                                                               CTRL, 0xF, 0xF, false));
+}
+// sum over aligned groups of G lanes (G = 4 or 8); every lane of a group ends with the sum
+template <int G>
+RETR_DEVICE float gsum(float s) {
+  static_assert(G == 4 || G == 8, "group of 4 or 8 lanes");
+  s += dh_dpp<0xB1>(s);
+  s += dh_dpp<0x4E>(s);
+  if constexpr (G == 8) s += dh_dpp<0x141>(s);
+  return s;
+}
+
+RETR_DEVICE float bfr(float v) { return (float)(bf16)v; }   // round to bf16 and back
+
+// Projection of one row vector onto HD consecutive weight rows W[row0 .. row0 + HD) (each C
+// bf16): lane = (row group rg = lane / 8, chunk column c = lane % 8); lane c owns the 16-byte
+// chunks c, c + 8, ... of every row (CPL of them) and the matching activation chunks (act, as
+// floats).  out[d] (LDS) = sum_k W[row0 + d][k] act[k] for d < HD.
+template <int C, int HD>
+RETR_DEVICE void head_proj(const bf16* __restrict__ W, int row0, const float (&act)[C / 64][8],
+                           int lane, float* out) {
+  constexpr int CPL = C / 64;                    // chunks per lane per row
+  const int rg = lane >> 3, c = lane & 7;
+  bf16x8 w[HD / 8][CPL];
+#pragma unroll
+  for (int it = 0; it < HD / 8; ++it)
+#pragma unroll
+    for (int m = 0; m < CPL; ++m)
+      w[it][m] = *(const bf16x8*)(W + (long)(row0 + 8 * it + rg) * C + 8 * (c + 8 * m));
+#pragma unroll
+  for (int it = 0; it < HD / 8; ++it) {
+    float s = 0.f;
+#pragma unroll
+    for (int m = 0; m < CPL; ++m)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += (float)w[it][m][e] * act[m][e];
+    s = gsum<8>(s);
+    if (c == 0) out[8 * it + rg] = s;
+  }
+}
+
+// this lane's activation chunks (c + 8 m) of a bf16 row
+template <int C>
+RETR_DEVICE void load_act(const bf16* row, int lane, float (&act)[C / 64][8]) {
+  const int c = lane & 7;
+#pragma unroll
+  for (int m = 0; m < C / 64; ++m) {
+    const bf16x8 v = *(const bf16x8*)(row + 8 * (c + 8 * m));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) act[m][e] = (float)v[e];
+  }
+}
+
+// Online-softmax attention of one wave over keys [0, Lk) in chunks of NPART x KU keys.
+// Lane = (dim group g = lane % NG of 8 dims, key part = lane / NG): key j = j0 + part + NPART u.
+// key_row(j) returns the K/V row of key j, or -1 for the "new" key (its K/V in LDS: kn / vn),
+// or -2 for a masked key.
+template <int HD>
+struct WaveAttn {
+  static constexpr int NG = HD / 8, NPART = 64 / NG, KU = 8, CH = NPART * KU;
+  float mx = -INFINITY, sum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+  template <int C, class RowFn>
+  RETR_DEVICE void run(const bf16* __restrict__ K, const bf16* __restrict__ V, int h, int Lk,
+                       RowFn key_row, const float* qs, const float* kn, const float* vn,
+                       int lane) {
+    const int g = lane % NG, part = lane / NG;
+    float q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) q[e] = qs[8 * g + e];
+    for (int j0 = 0; j0 < Lk; j0 += CH) {
+      long row[KU];
+      bf16x8 kk[KU], vv[KU];
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const int j = j0 + part + NPART * u;
+        row[u] = j < Lk ? key_row(j) : -2;
+        kk[u] = row[u] >= 0 ? *(const bf16x8*)(K + row[u] * C + h * HD + 8 * g) : bf16x8{};
+      }
+#pragma unroll
+      for (int u = 0; u < KU; ++u)
+        vv[u] = row[u] >= 0 ? *(const bf16x8*)(V + row[u] * C + h * HD + 8 * g) : bf16x8{};
+      float sc[KU];
+      float cm = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        float s = 0.f;
+        if (row[u] == -1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s += q[e] * kn[8 * g + e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s += q[e] * (float)kk[u][e];
+        }
+        s = gsum<NG>(s);
+        sc[u] = row[u] == -2 ? -INFINITY : s;
+        cm = fmaxf(cm, sc[u]);
+      }
+      cm = wave_max(cm);
+      const float nm = fmaxf(mx, cm);
+      if (nm != -INFINITY) {
+        const float f = mx == -INFINITY ? 0.f : __expf(mx - nm);
+        sum *= f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] *= f;
+        float cs = 0.f;
+#pragma unroll
+        for (int u = 0; u < KU; ++u) {
+          const float p = sc[u] == -INFINITY ? 0.f : __expf(sc[u] - nm);
+          cs += p;                                 // NG copies of every key: divided out below
+          if (row[u] == -1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] += p * vn[8 * g + e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] += p * (float)vv[u][e];
+          }
+        }
+        sum += wave_sum(cs) * (1.0f / NG);
+        mx = nm;
+      }
+    }
+  }
+  // o[8 g + e] (bf16-rounded, normalised) into LDS from the lanes of part 0
+  RETR_DEVICE void finish(float* os, int lane) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = NG; o < 64; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
+    const float inv = 1.f / sum;                 // a fully masked row gives NaN, as torch
+    if (lane < NG) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) os[8 * lane + e] = bfr(acc[e] * inv);
+    }
+  }
+};
+
+// slab[n] = sum_{d < HD} o[d] Wo[n][h HD + d] for n < C (lane n = lane + 64 m)
+template <int C, int HD>
+RETR_DEVICE void head_outproj(const bf16* __restrict__ Wo, int h, const float* os, float* slab,
+                              int lane) {
+  float o[HD];
+#pragma unroll
+  for (int d = 0; d < HD; ++d) o[d] = os[d];
+#pragma unroll
+  for (int m = 0; m < C / 64; ++m) {
+    const int n = lane + 64 * m;
+    bf16x8 w[HD / 8];
+#pragma unroll
+    for (int t = 0; t < HD / 8; ++t) w[t] = *(const bf16x8*)(Wo + (long)n * C + h * HD + 8 * t);
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < HD / 8; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += o[8 * t + e] * (float)w[t][e];
+    slab[n] = s;
+  }
+}
+
+struct SelfHeadsArgs {
+  const bf16* n;        // LN1(x) [R][C]
+  const bf16* npos;     // LN1(x) + qpos
+  const bf16* win;      // [3C][C]
+  const float* bin;     // [3C]
+  bf16* kc;             // caches [R * Lmax][C]
+  bf16* vc;
+  int i, Lmax;          // this step's position (keys 0..i), cache rows per caption
+  const int* anc;       // [R][Lmax] beam ancestry or null
+  const bf16* wo;       // [C][C]
+  float* slab;          // [H][R][C]
+  int R;
+};
+
+template <int C, int HD>
+__global__ void __launch_bounds__(64) dec_self_heads_kernel(SelfHeadsArgs a, float scale) {
+  constexpr int H = C / HD;
+  __shared__ float qs[HD], ks[HD], vs[HD], os[HD];
+  const int lane = threadIdx.x;
+  const int r = blockIdx.x / H, h = blockIdx.x % H;
+  float act[C / 64][8];
+  load_act<C>(a.npos + (long)r * C, lane, act);
+  head_proj<C, HD>(a.win, h * HD, act, lane, qs);
+  head_proj<C, HD>(a.win, C + h * HD, act, lane, ks);
+  load_act<C>(a.n + (long)r * C, lane, act);
+  head_proj<C, HD>(a.win, 2 * C + h * HD, act, lane, vs);
+  __syncthreads();
+  // bias + bf16 rounding (the unfused path's bf16 q / k / v); k, v appended to the cache
+  if (lane < HD) {
+    const float q = bfr(qs[lane] + a.bin[h * HD + lane]);
+    const float k = bfr(ks[lane] + a.bin[C + h * HD + lane]);
+    const float v = bfr(vs[lane] + a.bin[2 * C + h * HD + lane]);
+    qs[lane] = bfr(q * scale);
+    ks[lane] = k;
+    vs[lane] = v;
+    const long crow = ((long)r * a.Lmax + a.i) * C + h * HD + lane;
+    a.kc[crow] = (bf16)k;
+    a.vc[crow] = (bf16)v;
+  }
+  __syncthreads();
+  const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
+  const int i = a.i, Lmax = a.Lmax;
+  WaveAttn<HD> at;
+  at.template run<C>(a.kc, a.vc, h, i + 1,
+                     [&](int j) -> long {
+                       if (j == i) return -1;
+                       return (long)(ar ? ar[j] : r) * Lmax + j;
+                     },
+                     qs, ks, vs, lane);
+  at.finish(os, lane);
+  __syncthreads();
+  head_outproj<C, HD>(a.wo, h, os, a.slab + ((long)h * a.R + r) * C, lane);
+}
+
+struct CrossHeadsArgs {
+  const float* slab_in;   // [H][R][C] partial out-projections of the self-attention
+  const float* x;         // residual in [R][C]
+  const float* bo_in;     // self out-proj bias
+  float* xo;              // residual out (written by the h = 0 waves)
+  const float* gamma;     // LN2
+  const float* beta;
+  float eps;
+  const float* pos;       // [C] query position row
+  const bf16* wq;         // cross in-projection rows 0..C (queries) [C][C]
+  const float* bq;
+  const bf16* k;          // memory keys / values [(R / kv_group) * Lk][C]
+  const bf16* v;
+  int Lk, kv_group;
+  const unsigned char* kpm;   // [R / kv_group][Lk] or null
+  const bf16* wo;         // cross out-proj [C][C]
+  float* slab_out;        // [H][R][C]
+  int R;
+};
+
+template <int C, int HD>
+__global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, float scale) {
+  constexpr int H = C / HD, PER = C / 64;
+  __shared__ float ts[C];
+  __shared__ float qs[HD], os[HD];
+  const int lane = threadIdx.x;
+  const int r = blockIdx.x / H, h = blockIdx.x % H;
+  const long RC = (long)a.R * C;
+  // x' = x + (sum_h slab_in[h] + b_o), heads in order
+  float v[PER];
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const int n = lane + 64 * m;
+    float t[H];
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) t[hh] = a.slab_in[hh * RC + (long)r * C + n];
+    float s = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) s += t[hh];
+    v[m] = a.x[(long)r * C + n] + (s + a.bo_in[n]);
+  }
+  if (h == 0) {
+#pragma unroll
+    for (int m = 0; m < PER; ++m) a.xo[(long)r * C + lane + 64 * m] = v[m];
+  }
+  // LN2 (+ pos), bf16-rounded like the unfused path's LN output
+  float s = 0.f;
+#pragma unroll
+  for (int m = 0; m < PER; ++m) s += v[m];
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const float d = v[m] - mean;
+    q += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / C + a.eps);
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const int n = lane + 64 * m;
+    const float o = (v[m] - mean) * rstd * a.gamma[n] + a.beta[n];
+    ts[n] = bfr(a.pos ? o + a.pos[n] : o);
+  }
+  __syncthreads();
+  float act[C / 64][8];
+  {
+    const int c = lane & 7;
+#pragma unroll
+    for (int m = 0; m < C / 64; ++m)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) act[m][e] = ts[8 * (c + 8 * m) + e];
+  }
+  head_proj<C, HD>(a.wq, h * HD, act, lane, qs);
+  __syncthreads();
+  if (lane < HD) qs[lane] = bfr(bfr(qs[lane] + a.bq[h * HD + lane]) * scale);
+  __syncthreads();
+  const int kvb = r / a.kv_group, Lk = a.Lk;
+  const unsigned char* km = a.kpm ? a.kpm + (long)kvb * Lk : nullptr;
+  WaveAttn<HD> at;
+  at.template run<C>(a.k, a.v, h, Lk,
+                     [&](int j) -> long {
+                       if (km && km[j]) return -2;
+                       return (long)kvb * Lk + j;
+                     },
+                     qs, nullptr, nullptr, lane);
+  at.finish(os, lane);
+  __syncthreads();
+  head_outproj<C, HD>(a.wo, h, os, a.slab_out + ((long)h * a.R + r) * C, lane);
+}
+
+}  // namespace
+
+extern "C" {
+
+int retr_dec_self_heads(const void* n, const void* npos, int R, int C, int H, const void* win,
+                        const float* bin, void* kc, void* vc, int i, int Lmax, const int* anc,
+                        const void* wo, float* slab, void* stream) {
+  const int hd = H > 0 ? C / H : 0;
+  RETR_REQUIRE((C == 256 || C == 512) && (hd == 32 || hd == 64) && hd * H == C,
+               "dec_self_heads: C=%d H=%d unsupported", C, H);
+  RETR_REQUIRE(i >= 0 && i < Lmax, "dec_self_heads: step %d outside the %d-row cache", i, Lmax);
+  if (R == 0) return 0;
+  SelfHeadsArgs a{(const bf16*)n, (const bf16*)npos, (const bf16*)win, bin, (bf16*)kc,
+                  (bf16*)vc, i, Lmax, anc, (const bf16*)wo, slab, R};
+  const float scale = 1.0f / sqrtf((float)hd);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)(R * H));
+  if (C == 256 && hd == 32) hipLaunchKernelGGL((dec_self_heads_kernel<256, 32>), grid, dim3(64), 0, st, a, scale);
+  else if (C == 256) hipLaunchKernelGGL((dec_self_heads_kernel<256, 64>), grid, dim3(64), 0, st, a, scale);
+  else if (hd == 32) hipLaunchKernelGGL((dec_self_heads_kernel<512, 32>), grid, dim3(64), 0, st, a, scale);
+  else hipLaunchKernelGGL((dec_self_heads_kernel<512, 64>), grid, dim3(64), 0, st, a, scale);
+  return retr_check_launch("dec_self_heads");
+}
+
+int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_in, float* xo,
+                         int R, int C, int H, const float* gamma, const float* beta, float eps,
+                         const float* pos, const void* wq, const float* bq, const void* k,
+                         const void* v, int Lk, int kv_group, const unsigned char* kpm,
+                         const void* wo, float* slab_out, void* stream) {
+  const int hd = H > 0 ? C / H : 0;
+  RETR_REQUIRE((C == 256 || C == 512) && (hd == 32 || hd == 64) && hd * H == C,
+               "dec_cross_heads: C=%d H=%d unsupported", C, H);
+  RETR_REQUIRE(Lk > 0 && kv_group > 0, "dec_cross_heads: Lk=%d kv_group=%d", Lk, kv_group);
+  if (R == 0) return 0;
+  CrossHeadsArgs a{slab_in, x, bo_in, xo, gamma, beta, eps, pos, (const bf16*)wq, bq,
+                   (const bf16*)k, (const bf16*)v, Lk, kv_group, kpm, (const bf16*)wo, slab_out, R};
+  const float scale = 1.0f / sqrtf((float)hd);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)(R * H));
+  if (C == 256 && hd == 32) hipLaunchKernelGGL((dec_cross_heads_kernel<256, 32>), grid, dim3(64), 0, st, a, scale);
+  else if (C == 256) hipLaunchKernelGGL((dec_cross_heads_kernel<256, 64>), grid, dim3(64), 0, st, a, scale);
+  else if (hd == 32) hipLaunchKernelGGL((dec_cross_heads_kernel<512, 32>), grid, dim3(64), 0, st, a, scale);
+  else hipLaunchKernelGGL((dec_cross_heads_kernel<512, 64>), grid, dim3(64), 0, st, a, scale);
+  return retr_check_launch("dec_cross_heads");
+}
+
+}  // extern "C"

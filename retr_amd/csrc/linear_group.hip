@@ -592,7 +592,7 @@ struct WBRow {                // dst[c] (=|+=) sum_s parts[s * stride + c]
   float* dst;
   int stride, nparts, cols, accumulate, blk0, pad;
 };
-// Problem-affine block order (round 5, the default): the tiles of one problem -- or, for a
+// Problem-affine block order (round 5, opt-in: RETR_TUNE_WB_CHUNK = -1): the tiles of one problem -- or, for a
 // problem with more than kWBPieceTiles tiles (the vocabulary head), of one run of whole row
 // tiles -- form a PIECE that runs on ONE XCD; pieces go to the XCDs longest-problem first, each
 // to the XCD with the least work so far.  All tiles of a piece read the same X panels (and a row
@@ -612,7 +612,7 @@ struct WBHead {
 static_assert(sizeof(WBProb) == 64 && sizeof(WBRow) == 40 && sizeof(WBHead) == 96 &&
                   sizeof(WBPiece) == 16, "table");
 
-constexpr int kWBChunk = 4;        // round-4 order: consecutive logical blocks per XCD turn
+constexpr int kWBChunk = 4;        // default order: consecutive logical blocks per XCD turn
 constexpr int kWBPieceTiles = 64;  // one XCD's block slots (32 CUs x 2)
 constexpr int kWBMaxPieces = 16;   // per problem (table bound)
 
@@ -691,8 +691,10 @@ __global__ void __launch_bounds__(256) wgrad_batch_kernel(const char* __restrict
     }
     return;
   }
+  if (lo >= h.nprob) return;                    // table guard
   const WBProb d = P[lo];
   const int tiles_n = d.flags >> 2;
+  if (tile >= tiles_n * ((d.N + BM - 1) / BM)) return;
   using Ld = DenseT<bf16>;
   // dW[n][k] = sum_m dY[m][n] X[m][k]: A(n, m) = dY[m][n], B(k, m) = X[m][k]
   const Ld la{d.dy, d.lddy, d.N, d.M};
@@ -734,8 +736,10 @@ int wgrad_batch_launch(const char* table, int total, int grid_affine, hipStream_
       attr_set = true;
     }
   }
-  // RETR_TUNE_WB_CHUNK > 0: the round-4 order in runs of that many blocks; 0: problem-affine
-  const int chunk = retr_tune_get(RETR_TUNE_WB_CHUNK) > 0 ? retr_tune_get(RETR_TUNE_WB_CHUNK) : 0;
+  // RETR_TUNE_WB_CHUNK: 0 runs of kWBChunk blocks per XCD turn (default), n > 0 runs of n,
+  // -1 problem-affine pieces (measured 0.05 ms/step slower: profiles/r5_ab_wgrad_orders.txt)
+  const int knob = retr_tune_get(RETR_TUNE_WB_CHUNK);
+  const int chunk = knob > 0 ? knob : (knob < 0 ? 0 : kWBChunk);
   const int grid = chunk > 0 ? cdiv(total, 8 * chunk) * 8 * chunk : grid_affine;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, table, chunk);
   return retr_check_launch("linear_wgrad_batch");

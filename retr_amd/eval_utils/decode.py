@@ -43,6 +43,11 @@ def prepare_tokenizer():
     return tokenizer, start_token, end_token
 
 
+# The fused step's attention sub-layers as one wave per (row, head) (csrc/decode_heads.hip);
+# False: the round-4 block-per-row kernels (csrc/decode.hip dec_gemm + dec_attn_row)
+DEC_HEADS = False   # flipped on after GPU validation
+
+
 class _DecodeState:
     """Static device buffers (and captured per-step hipGraphs) for one (B, K, S, T) shape;
     the decoder runs R = B*K rows (K = beams per image, 1 for greedy)."""
@@ -71,6 +76,8 @@ class _DecodeState:
         self.ffh = torch.empty(R, F, dtype=cd, device=dev)
         self.q2 = torch.empty_like(self.n)
         self.slabs = torch.empty(F // 32, R, C, dtype=f32, device=dev)   # fused FFN partials
+        self.hslab = None       # per-head out-projection partials (DEC_HEADS), made on first use
+        self.hslab2 = None
         self.h1 = torch.empty(R, 512, dtype=cd, device=dev)
         self.h2 = torch.empty(R, 512, dtype=cd, device=dev)
         self.Vp = (V + 63) // 64 * 64
@@ -192,7 +199,13 @@ class IncrementalGreedy:
         """Decode step i as five fused launches per decoder layer (csrc/decode.hip):
         [q|k|v] GEMM (+cache append); self-attention + out-proj + residual + LN2 + cross query;
         cross-attention + out-proj + residual + LN3; FFN split over hidden units; ordered slab
-        reduce + residual + the next LayerNorm."""
+        reduce + residual + the next LayerNorm.  With DEC_HEADS (default) the first three are
+        one wave per (row, head) instead (csrc/decode_heads.hip): the head's q|k|v + cache
+        append + self-attention + partial out-projection; the self-attention residual + LN2 +
+        the head's cross query + cross-attention + partial out-projection; then the head
+        partials' ordered sum + residual + LN3 by retr_dec_rows."""
+        if DEC_HEADS:
+            return self._step_heads(st, i, eos_token)
         model, tr, cd = self.model, self.tr, self.cdtype
         S, T, R = st.S, st.T, st.R
         C = st.n.shape[1]
@@ -231,6 +244,64 @@ class IncrementalGreedy:
             call("retr_dec_ffn", ptr(st.o), R, C, ptr(W(f0.weight)), ptr(f0.bias),
                  ptr(W(f2.weight)), F, ptr(st.slabs), s)
             # residual + FFN partials, then the next layer's LN1 (+pos) or the final LN
+            if li + 1 < len(layers):
+                nx, npos = layers[li + 1].tgt_self_attn.norm, ptr(st.npos)
+            else:
+                nx, npos = tr.decoder.norm, None
+            call("retr_dec_rows", ptr(x), ptr(st.slabs), nslab, ptr(f2.bias), R, C, ptr(xa),
+                 ptr(nx.weight), ptr(nx.bias), float(nx.eps), ptr(qp) if npos else None,
+                 ptr(st.n), npos, s)
+            x, xa = xa, x
+        l1, l2, l3 = model.mlp.layers
+        V = l3.weight.shape[0]
+        H1 = l1.weight.shape[0]
+        call("retr_dec_gemm", ptr(st.n), None, R, C, ptr(W(l1.weight)), ptr(l1.bias), H1,
+             ptr(st.h1), H1, 0, None, 0, 0, None, 0, 0, H1, 1, s)
+        k_linear_fwd(st.h1, W(l2.weight), l2.bias.detach(), st.h2, relu=1)
+        k_linear_fwd(st.h2, ops.WEIGHTS.get(l3.weight, cd, rows=st.Vp), st.head_bias, st.logits)
+        self._select(st, i, V, eos_token, s)
+
+    def _step_heads(self, st, i, eos_token):
+        model, tr, cd = self.model, self.tr, self.cdtype
+        S, T, R = st.S, st.T, st.R
+        C = st.n.shape[1]
+        layers = list(tr.decoder.layers)
+        H = layers[0].tgt_self_attn.sublayer.num_heads
+        F = layers[0].ff.sublayer[0].weight.shape[0]
+        W = lambda p: ops.WEIGHTS.get(p, cd)        # noqa: E731
+        if st.hslab is None:
+            st.hslab = torch.empty(H, R, C, dtype=torch.float32, device=st.n.device)
+            st.hslab2 = torch.empty_like(st.hslab)
+        emb = tr.embeddings
+        qp = emb.position_embeddings.weight.detach()[i]
+        s = _st()
+        x, xa = st.y, st.y2
+        n0 = layers[0].tgt_self_attn.norm
+        call("retr_dec_embed_rows", ptr(st.tok), R, C, ptr(emb.word_embeddings.weight), ptr(qp),
+             ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias), float(emb.LayerNorm.eps), ptr(x),
+             ptr(n0.weight), ptr(n0.bias), float(n0.eps), ptr(st.n), ptr(st.npos), s)
+        anc = ptr(st.anc) if self.beam else None
+        nslab = F // 32
+        for li, layer in enumerate(layers):
+            sa, ca, ff = layer.tgt_self_attn, layer.tgt_src_cross_attn, layer.ff
+            sub, csub = sa.sublayer, ca.sublayer
+            call("retr_dec_self_heads", ptr(st.n), ptr(st.npos), R, C, H,
+                 ptr(W(sub.in_proj_weight)), ptr(sub.in_proj_bias), ptr(st.kc[li]),
+                 ptr(st.vc[li]), i, T, anc, ptr(W(sub.out_proj.weight)), ptr(st.hslab), s)
+            call("retr_dec_cross_heads", ptr(st.hslab), ptr(x), ptr(sub.out_proj.bias), ptr(xa),
+                 R, C, H, ptr(ca.norm.weight), ptr(ca.norm.bias), float(ca.norm.eps), ptr(qp),
+                 ptr(W(csub.in_proj_weight)), ptr(csub.in_proj_bias), ptr(st.kx[li]),
+                 ptr(st.vx[li]), S, st.K, ptr(st.kpm), ptr(W(csub.out_proj.weight)),
+                 ptr(st.hslab2), s)
+            x, xa = xa, x
+            # cross-attention residual (head partials in order) + LN3 -> the FFN input
+            call("retr_dec_rows", ptr(x), ptr(st.hslab2), H, ptr(csub.out_proj.bias), R, C,
+                 ptr(xa), ptr(ff.norm.weight), ptr(ff.norm.bias), float(ff.norm.eps), None,
+                 ptr(st.o), None, s)
+            x, xa = xa, x
+            f0, f2 = ff.sublayer[0], ff.sublayer[2]
+            call("retr_dec_ffn", ptr(st.o), R, C, ptr(W(f0.weight)), ptr(f0.bias),
+                 ptr(W(f2.weight)), F, ptr(st.slabs), s)
             if li + 1 < len(layers):
                 nx, npos = layers[li + 1].tgt_self_attn.norm, ptr(st.npos)
             else:

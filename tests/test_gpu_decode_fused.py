@@ -254,3 +254,129 @@ def test_greedy_select_matches_argmax_and_update(B):
             assert torch.equal(u, v)
         assert int(b[4][0]) == (eos if all_eos else 500)
         assert int(b[2][0]) == (step if all_eos else -1)
+
+
+@pytest.mark.parametrize("C,H", [(256, 8), (512, 8)])
+@pytest.mark.parametrize("beam", [False, True])
+def test_dec_heads_self_cross_rows(C, H, beam):
+    """One wave per (row, head) (csrc/decode_heads.hip): the self sub-layer (the head's q|k|v
+    from LN1(x) (+pos), cache append at position i, attention over keys 0..i with beam ancestry,
+    partial out-projection per head), the cross sub-layer (self residual from the head partials,
+    LN2 + pos, the head's query, attention over the masked memory with kv_group rows per memory
+    row, partial out-projection), and retr_dec_rows' ordered head sum + residual + LN3 --
+    against fp32 torch on the same bf16 operands (decode.py:53-81, transformer_modules.py:22-74)."""
+    hd = C // H
+    R, T, i, S, Kb = 6, 16, 9, 37, (3 if beam else 1)
+    g = _g(C + 2 * beam)
+    sc = 1.0 / math.sqrt(hd)
+    bf = lambda t: t.to(DEV).bfloat16()                       # noqa: E731
+    n = bf(torch.randn(R, C, generator=g))
+    npos = bf(torch.randn(R, C, generator=g))
+    win = bf(torch.randn(3 * C, C, generator=g) / math.sqrt(C))
+    bin_ = torch.randn(3 * C, generator=g).to(DEV) * 0.1
+    kc = bf(torch.randn(R * T, C, generator=g))
+    vc = bf(torch.randn(R * T, C, generator=g))
+    kc0, vc0 = kc.clone(), vc.clone()
+    anc = torch.randint(0, R, (R, T), generator=g, dtype=torch.int32).to(DEV) if beam else None
+    wo = bf(torch.randn(C, C, generator=g) / math.sqrt(C))
+    slab = torch.empty(H, R, C, device=DEV)
+    call("retr_dec_self_heads", ptr(n), ptr(npos), R, C, H, ptr(win), ptr(bin_), ptr(kc), ptr(vc),
+         i, T, ptr(anc), ptr(wo), ptr(slab), ops._st())
+    wf = win.float()
+    q = (npos.float() @ wf[:C].t() + bin_[:C]).bfloat16().float()
+    k = (npos.float() @ wf[C:2 * C].t() + bin_[C:2 * C]).bfloat16().float()
+    v = (n.float() @ wf[2 * C:].t() + bin_[2 * C:]).bfloat16().float()
+    kv, vv = kc.view(R, T, C), vc.view(R, T, C)
+    # the new cache row, and nothing else written
+    assert _rel(kv[:, i].float(), k) < 1e-2 and _rel(vv[:, i].float(), v) < 1e-2
+    others = torch.ones(T, dtype=torch.bool)
+    others[i] = False
+    assert torch.equal(kv[:, others], kc0.view(R, T, C)[:, others])
+    assert torch.equal(vv[:, others], vc0.view(R, T, C)[:, others])
+    kf, vf = kc.float().cpu(), vc.float().cpu()
+    for r in range(R):
+        rows = [(int(anc[r, j]) if beam else r) * T + j for j in range(i)] + [r * T + i]
+        o = _attn_ref(q[r].cpu().view(H, hd), kf[rows].view(-1, H, hd), vf[rows].view(-1, H, hd),
+                      None, sc).bfloat16().float()              # [H, hd]
+        for h in range(H):
+            ref = o[h] @ wo.float().cpu()[:, h * hd:(h + 1) * hd].t()
+            assert _rel(slab[h, r], ref) < 1e-2, (r, h)
+    # cross sub-layer on those partials
+    x = torch.randn(R, C, generator=g).to(DEV)
+    bo = torch.randn(C, generator=g).to(DEV) * 0.1
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV) * 0.1
+    pos = torch.randn(C, generator=g).to(DEV)
+    wq = bf(torch.randn(3 * C, C, generator=g) / math.sqrt(C))
+    bq = torch.randn(3 * C, generator=g).to(DEV) * 0.1
+    B = R // Kb
+    km = bf(torch.randn(B * S, C, generator=g))
+    vm = bf(torch.randn(B * S, C, generator=g))
+    kpm = torch.zeros(B, S, dtype=torch.uint8)
+    kpm[B - 1, -9:] = 1
+    kpm = kpm.to(DEV)
+    wo2 = bf(torch.randn(C, C, generator=g) / math.sqrt(C))
+    xo = torch.empty(R, C, device=DEV)
+    slab2 = torch.empty(H, R, C, device=DEV)
+    call("retr_dec_cross_heads", ptr(slab), ptr(x), ptr(bo), ptr(xo), R, C, H, ptr(gamma),
+         ptr(beta), 1e-5, ptr(pos), ptr(wq), ptr(bq), ptr(km), ptr(vm), S, Kb, ptr(kpm), ptr(wo2),
+         ptr(slab2), ops._st())
+    ref_xo = x + (slab.sum(0) + bo)
+    assert _rel(xo, ref_xo) < 1e-6
+    t = (F.layer_norm(ref_xo, (C,), gamma, beta, 1e-5) + pos).bfloat16().float()
+    q2 = (t @ wq.float()[:C].t() + bq[:C]).bfloat16().float()
+    kmf, vmf = km.float().cpu(), vm.float().cpu()
+    for r in range(R):
+        b = r // Kb
+        idx = torch.arange(b * S, (b + 1) * S)
+        o = _attn_ref(q2[r].cpu().view(H, hd), kmf[idx].view(-1, H, hd), vmf[idx].view(-1, H, hd),
+                      kpm[b].bool().cpu(), sc).bfloat16().float()
+        for h in range(H):
+            ref = o[h] @ wo2.float().cpu()[:, h * hd:(h + 1) * hd].t()
+            assert _rel(slab2[h, r], ref) < 2e-2, (r, h)
+    # the head partials' ordered sum + residual + LN3
+    b2 = torch.randn(C, generator=g).to(DEV) * 0.1
+    x3 = torch.empty(R, C, device=DEV)
+    n3 = torch.empty(R, C, dtype=torch.bfloat16, device=DEV)
+    call("retr_dec_rows", ptr(xo), ptr(slab2), H, ptr(b2), R, C, ptr(x3), ptr(gamma), ptr(beta),
+         1e-5, None, ptr(n3), None, ops._st())
+    ref3 = xo + (slab2.sum(0) + b2)
+    assert _rel(x3, ref3) < 1e-6
+    assert _rel(n3.float(), F.layer_norm(ref3, (C,), gamma, beta, 1e-5)) < 1e-2
+
+
+def test_dec_heads_step_matches_block_per_row_step():
+    """The decode step with the per-(row, head) attention sub-layers (DEC_HEADS) against the
+    round-4 block-per-row kernels on the cfg5 model: first-step logits within bf16 rounding
+    (only fp32 summation order differs), greedy ids equal up to near-ties, graphs == eager."""
+    from bench import build, cfg5
+    from retr_amd.eval_utils import decode as dec
+    from retr_amd.synthetic import synthetic_images
+    model, _ = build(cfg5(), DEV)
+    model.eval()
+    B, T = 16, 128
+    img, mask = synthetic_images(B, 224, seed=12, pad_band=True)
+    s = NestedTensor(img.to(DEV), mask.to(DEV))
+    res = {}
+    try:
+        for heads in (True, False):
+            dec.DEC_HEADS = heads
+            model._retr_decode_states = {}
+            g = dec.IncrementalGreedy(model)
+            ids = g(s, T, 101, 102)
+            st = next(v for k, v in model._retr_decode_states.items() if k[0] == "IncrementalGreedy")
+            with torch.no_grad():
+                g._reset(st, 101)
+                g._step(st, 0, 102)
+                torch.cuda.synchronize()
+                res[heads] = (ids, st.logits.float().clone())
+            if heads:
+                assert st.hslab is not None
+                ids_e = dec.IncrementalGreedy(model, use_graphs=False)(s, T, 101, 102)
+                assert torch.equal(ids, ids_e)
+    finally:
+        dec.DEC_HEADS = True
+        model._retr_decode_states = {}
+    (i1, l1), (i0, l0) = res[True], res[False]
+    assert _rel(l1, l0) < 2e-2
+    assert (i1 == i0).float().mean().item() > 0.3

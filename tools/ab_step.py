@@ -83,8 +83,8 @@ VARIANTS = {
     # round 5: slice-affine conv wgrad / problem-affine linear wgrad orders are the defaults;
     # these restore the round-4 runs of 4 logical blocks per XCD turn
     "cw_r4": {("TUNE", 20): -1},
-    "wb_r4": {("TUNE", 19): 4},
-    "orders_r4": {("TUNE", 20): -1, ("TUNE", 19): 4},
+    "wb_aff": {("TUNE", 19): -1},
+    "orders_aff": {("TUNE", 19): -1},   # with the default (slice-affine) conv order
 }
 
 

@@ -22,7 +22,12 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--beam", type=int, default=1)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--block-per-row", action="store_true",
+                    help="the round-4 attention sub-layers (eval_utils.decode.DEC_HEADS = False)")
     a = ap.parse_args()
+    if a.block_per_row:
+        from retr_amd.eval_utils import decode as dec
+        dec.DEC_HEADS = False
     model, _ = build(cfg5(), "cuda")
     model.eval()
     img, mask = synthetic_images(a.batch, 224, seed=3000)

@@ -109,17 +109,23 @@ def main():
     if out:
         with open(out, "w") as f:
             json.dump(res, f, indent=1)
+    def ghz(e):
+        # GRBM_GUI_ACTIVE / 8 / duration reads above the 2.4 GHz maximum clock when the counter
+        # spans more than the dispatch (short kernels): that quotient is not a clock -- print
+        # "clamp" (the busy fraction used the dispatch duration at 2.4 GHz instead)
+        g = e["clock_ghz"]
+        return "  n/a" if g is None else (f"{g:6.2f}" if g <= 2.4 else " clamp")
     print(f"{'family / kernel':60s} {'n':>5} {'us/disp':>9} {'mfma_busy':>9} {'VALU/MFMA':>9} "
           f"{'GHz':>6}")
     for k, e in sorted(fams.items(), key=lambda kv: -kv[1]["us_per_dispatch"] * kv[1]["dispatches"]):
         print(f"{k:60s} {e['dispatches']:5d} {e['us_per_dispatch']:9.2f} "
               f"{e['mfma_busy'] if e['mfma_busy'] is not None else 0:9.3f} "
-              f"{e['valu_per_mfma'] or 0:9.2f} {e['clock_ghz'] or 0:6.2f}")
+              f"{e['valu_per_mfma'] or 0:9.2f} {ghz(e)}")
     print()
     for k, e in kers.items():
         print(f"{k[:60]:60s} {e['dispatches']:5d} {e['us_per_dispatch']:9.2f} "
               f"{e['mfma_busy'] if e['mfma_busy'] is not None else 0:9.3f} "
-              f"{e['valu_per_mfma'] or 0:9.2f} {e['clock_ghz'] or 0:6.2f}")
+              f"{e['valu_per_mfma'] or 0:9.2f} {ghz(e)}")
 
 
 if __name__ == "__main__":

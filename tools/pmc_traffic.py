@@ -6,7 +6,12 @@ FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads, so it is 
 (MI355X_MICROARCH.md §HBM); WRITE_SIZE is exact for 16-B streaming stores and float atomics.
 
     python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> \
-        --out profiles/pmc_traffic.json --source "<what was run>"
+        --out profiles/pmc_traffic.json --source "<what was run>" [--steps N]
+
+``--steps``: training steps the profiled program ran (bench.py --eager --steps 1 --warmup 1: 2),
+so ``dispatches_per_step`` can be set against bench.py's API calls per step (one retr_* call
+may dispatch several kernels of a family: the attention backward's dQ and dK/dV kernels, the
+two grouped conv weight-gradient kinds).
 """
 import csv
 import json
@@ -37,6 +42,7 @@ def main():
     fetch, write = sys.argv[1], sys.argv[2]
     out = sys.argv[sys.argv.index("--out") + 1]
     src = sys.argv[sys.argv.index("--source") + 1] if "--source" in sys.argv else ""
+    steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else None
     fr, wr = read(fetch, "FETCH_SIZE"), read(write, "WRITE_SIZE")
     fams = {}
     for fam in sorted(set(fr) | set(wr)):
@@ -48,8 +54,10 @@ def main():
         wb = w_kib * 1024 / nw
         fams[fam] = {"bytes_per_launch": round(rd + wb), "read_bytes_per_launch": round(rd),
                      "write_bytes_per_launch": round(wb), "dispatches": [nf, nw]}
+        if steps:
+            fams[fam]["dispatches_per_step"] = nf / steps
     with open(out, "w") as f:
-        json.dump({"source": src, "correction": "read = 2 x FETCH_SIZE KiB (gfx950), "
+        json.dump({"source": src, "steps": steps, "correction": "read = 2 x FETCH_SIZE KiB (gfx950), "
                    "write = WRITE_SIZE KiB", "families": fams}, f, indent=1)
     for k, v in fams.items():
         print(f"{k:15s} {v['bytes_per_launch'] / 1e6:10.2f} MB/launch")
