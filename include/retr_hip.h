@@ -151,9 +151,9 @@ enum {
   RETR_TUNE_WB_CHUNK = 19,      /* retr_linear_wgrad_batch block order: 0 runs of 4 logical
                                    blocks per XCD turn, n > 0 runs of n, -1 problem-affine pieces
                                    (one XCD per problem / row-tile run; 0.05 ms/step slower) */
-  RETR_TUNE_CW_CHUNK = 20,      /* retr_conv2d_wgrad_group block order: 0 slice-affine (every tile
-                                   of a K-slice on one XCD, slices to the least-loaded XCD),
-                                   n > 0 runs of n logical blocks per XCD turn, -1 runs of 4 */
+  RETR_TUNE_CW_CHUNK = 20,      /* retr_conv2d_wgrad_group block order: 0 runs of 4 logical blocks
+                                   per XCD turn, n > 0 runs of n, -1 slice-affine (every tile of
+                                   a K-slice on one XCD, slices to the least-loaded XCD; slower) */
   RETR_TUNE_CONV3X3 = 21,       /* bf16 3x3 stride-1 convs (fwd / dgrad): 0 the direct kernel with
                                    the input halo in LDS on maps >= 32 wide (csrc/conv3x3.hip),
                                    1 the implicit GEMM, 2 the direct kernel on every map >= 16 */
@@ -639,6 +639,13 @@ int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_i
                          const void* wo, float* slab_out, void* stream);
 int retr_dec_ffn(const void* n3, int R, int C, const void* w1, const float* b1, const void* w2,
                  int F, float* slabs, void* stream);
+/* retr_dec_ffn with its input LayerNorm in the prologue: per row x = xin + (sum_j hslab[j] + bo)
+ * (slabs [nslab][R][C] in order), written to xout, FFN input = bf16(LN(x; gamma, beta, eps)) --
+ * the retr_dec_rows launch between the per-head cross-attention partials and the FFN folded in. */
+int retr_dec_ffn_ln(const float* xin, const float* hslab, int nslab, const float* bo,
+                    const float* gamma, const float* beta, float eps, float* xout, int R, int C,
+                    const void* w1, const float* b1, const void* w2, int F, float* slabs,
+                    void* stream);
 
 #ifdef __cplusplus
 }

@@ -1190,7 +1190,7 @@ Geom make_geom(int Nb, int H, int W, int C, int Co, int KH, int KW, int s, int p
 // stream order); logical blocks go to the XCDs in runs of kCWChunk, the XCDs taking turns, with
 // the longest blocks first.
 //
-// Slice-affine order (round 5, the default): every tile of one K-slice (one pixel range of one
+// Slice-affine order (round 5, opt-in: RETR_TUNE_CW_CHUNK = -1; measured slower): every tile of one K-slice (one pixel range of one
 // conv) runs on ONE XCD, the slices dealt to the XCDs round-robin (longest blocks first).  The
 // tiles of a slice all read the same dY rows and X rows, so that XCD's L2 fetches them from HBM
 // once; in runs of 4 tiles per XCD turn (the round-4 order, still selectable with a positive
@@ -1684,10 +1684,10 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
       hipLaunchKernelGGL(cw_table_put_kernel, dim3(1), dim3(256), 0, st, c, (unsigned*)table);
       if (int e = retr_check_launch("conv2d_wgrad_group table")) return e;
     }
-    // RETR_TUNE_CW_CHUNK > 0: the round-4 order in runs of that many blocks per XCD turn;
-    // 0 (default): slice-affine; -1: the round-4 default run length
+    // RETR_TUNE_CW_CHUNK: 0 (default) runs of kCWChunk logical blocks per XCD turn, n > 0 runs
+    // of n, -1 slice-affine (0.17 ms/step slower: profiles/r5_ab_wgrad_orders.txt)
     int chunk = retr_tune_get(RETR_TUNE_CW_CHUNK);
-    if (chunk < 0) chunk = kCWChunk;
+    chunk = chunk > 0 ? chunk : (chunk < 0 ? 0 : kCWChunk);
     const int grid = chunk > 0 ? cdiv(blocks, 8 * chunk) * 8 * chunk : 8 * xmax;
     constexpr size_t lds = gemm2_lds_bytes<128, 128, 2, 0>();
     if (kind == 0) {

@@ -42,33 +42,6 @@ RETR_DEVICE float gsum(float s) {
 
 RETR_DEVICE float bfr(float v) { return (float)(bf16)v; }   // round to bf16 and back
 
-// Projection of one row vector onto HD consecutive weight rows W[row0 .. row0 + HD) (each C
-// bf16): lane = (row group rg = lane / 8, chunk column c = lane % 8); lane c owns the 16-byte
-// chunks c, c + 8, ... of every row (CPL of them) and the matching activation chunks (act, as
-// floats).  out[d] (LDS) = sum_k W[row0 + d][k] act[k] for d < HD.
-template <int C, int HD>
-RETR_DEVICE void head_proj(const bf16* __restrict__ W, int row0, const float (&act)[C / 64][8],
-                           int lane, float* out) {
-  constexpr int CPL = C / 64;                    // chunks per lane per row
-  const int rg = lane >> 3, c = lane & 7;
-  bf16x8 w[HD / 8][CPL];
-#pragma unroll
-  for (int it = 0; it < HD / 8; ++it)
-#pragma unroll
-    for (int m = 0; m < CPL; ++m)
-      w[it][m] = *(const bf16x8*)(W + (long)(row0 + 8 * it + rg) * C + 8 * (c + 8 * m));
-#pragma unroll
-  for (int it = 0; it < HD / 8; ++it) {
-    float s = 0.f;
-#pragma unroll
-    for (int m = 0; m < CPL; ++m)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s += (float)w[it][m][e] * act[m][e];
-    s = gsum<8>(s);
-    if (c == 0) out[8 * it + rg] = s;
-  }
-}
-
 // this lane's activation chunks (c + 8 m) of a bf16 row
 template <int C>
 RETR_DEVICE void load_act(const bf16* row, int lane, float (&act)[C / 64][8]) {
@@ -81,49 +54,60 @@ RETR_DEVICE void load_act(const bf16* row, int lane, float (&act)[C / 64][8]) {
   }
 }
 
-// Online-softmax attention of one wave over keys [0, Lk) in chunks of NPART x KU keys.
-// Lane = (dim group g = lane % NG of 8 dims, key part = lane / NG): key j = j0 + part + NPART u.
-// key_row(j) returns the K/V row of key j, or -1 for the "new" key (its K/V in LDS: kn / vn),
-// or -2 for a masked key.
-template <int HD>
+// Attention of one wave over keys [0, Lk), Lk <= NCH x CH: every key / value load is issued
+// by load() (at kernel start: they depend on nothing computed in the step), then compute() runs
+// an online softmax over the NCH chunks.  Lane = (dim group g = lane % NG of 8 dims, key part =
+// lane / NG): key j = CH c + part + NPART u.  key_row(j) gives the K/V row of key j, -1 for the
+// step's own key (its K/V in LDS: kn / vn) or -2 for a masked key.
+template <int HD, int NCH>
 struct WaveAttn {
   static constexpr int NG = HD / 8, NPART = 64 / NG, KU = 8, CH = NPART * KU;
+  long row[NCH][KU];
+  bf16x8 kk[NCH][KU], vv[NCH][KU];
   float mx = -INFINITY, sum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   template <int C, class RowFn>
-  RETR_DEVICE void run(const bf16* __restrict__ K, const bf16* __restrict__ V, int h, int Lk,
-                       RowFn key_row, const float* qs, const float* kn, const float* vn,
-                       int lane) {
+  RETR_DEVICE void load(const bf16* __restrict__ K, const bf16* __restrict__ V, int h, int Lk,
+                        RowFn key_row, int lane) {
     const int g = lane % NG, part = lane / NG;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const int j = CH * c + part + NPART * u;
+        row[c][u] = j < Lk ? key_row(j) : -2;
+        kk[c][u] = row[c][u] >= 0 ? *(const bf16x8*)(K + row[c][u] * C + h * HD + 8 * g)
+                                  : bf16x8{};
+      }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int u = 0; u < KU; ++u)
+        vv[c][u] = row[c][u] >= 0 ? *(const bf16x8*)(V + row[c][u] * C + h * HD + 8 * g)
+                                  : bf16x8{};
+  }
+
+  RETR_DEVICE void compute(const float* qs, const float* kn, const float* vn, int lane) {
+    const int g = lane % NG;
     float q[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) q[e] = qs[8 * g + e];
-    for (int j0 = 0; j0 < Lk; j0 += CH) {
-      long row[KU];
-      bf16x8 kk[KU], vv[KU];
 #pragma unroll
-      for (int u = 0; u < KU; ++u) {
-        const int j = j0 + part + NPART * u;
-        row[u] = j < Lk ? key_row(j) : -2;
-        kk[u] = row[u] >= 0 ? *(const bf16x8*)(K + row[u] * C + h * HD + 8 * g) : bf16x8{};
-      }
-#pragma unroll
-      for (int u = 0; u < KU; ++u)
-        vv[u] = row[u] >= 0 ? *(const bf16x8*)(V + row[u] * C + h * HD + 8 * g) : bf16x8{};
+    for (int c = 0; c < NCH; ++c) {
       float sc[KU];
       float cm = -INFINITY;
 #pragma unroll
       for (int u = 0; u < KU; ++u) {
         float s = 0.f;
-        if (row[u] == -1) {
+        if (row[c][u] == -1) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) s += q[e] * kn[8 * g + e];
         } else {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) s += q[e] * (float)kk[u][e];
+          for (int e = 0; e < 8; ++e) s += q[e] * (float)kk[c][u][e];
         }
         s = gsum<NG>(s);
-        sc[u] = row[u] == -2 ? -INFINITY : s;
+        sc[u] = row[c][u] == -2 ? -INFINITY : s;
         cm = fmaxf(cm, sc[u]);
       }
       cm = wave_max(cm);
@@ -138,12 +122,12 @@ struct WaveAttn {
         for (int u = 0; u < KU; ++u) {
           const float p = sc[u] == -INFINITY ? 0.f : __expf(sc[u] - nm);
           cs += p;                                 // NG copies of every key: divided out below
-          if (row[u] == -1) {
+          if (row[c][u] == -1) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) acc[e] += p * vn[8 * g + e];
           } else {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) acc[e] += p * (float)vv[u][e];
+            for (int e = 0; e < 8; ++e) acc[e] += p * (float)vv[c][u][e];
           }
         }
         sum += wave_sum(cs) * (1.0f / NG);
@@ -165,27 +149,63 @@ struct WaveAttn {
   }
 };
 
-// slab[n] = sum_{d < HD} o[d] Wo[n][h HD + d] for n < C (lane n = lane + 64 m)
+// The head's weight slices, loaded up front: rows [row0, row0 + HD) of W (C columns each) in
+// head_proj's lane layout
 template <int C, int HD>
-RETR_DEVICE void head_outproj(const bf16* __restrict__ Wo, int h, const float* os, float* slab,
-                              int lane) {
-  float o[HD];
+struct ProjW {
+  static constexpr int CPL = C / 64;
+  bf16x8 w[HD / 8][CPL];
+  RETR_DEVICE void load(const bf16* __restrict__ W, int row0, int lane) {
+    const int rg = lane >> 3, c = lane & 7;
 #pragma unroll
-  for (int d = 0; d < HD; ++d) o[d] = os[d];
+    for (int it = 0; it < HD / 8; ++it)
 #pragma unroll
-  for (int m = 0; m < C / 64; ++m) {
-    const int n = lane + 64 * m;
-    bf16x8 w[HD / 8];
-#pragma unroll
-    for (int t = 0; t < HD / 8; ++t) w[t] = *(const bf16x8*)(Wo + (long)n * C + h * HD + 8 * t);
-    float s = 0.f;
-#pragma unroll
-    for (int t = 0; t < HD / 8; ++t)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) s += o[8 * t + e] * (float)w[t][e];
-    slab[n] = s;
+      for (int m = 0; m < CPL; ++m)
+        w[it][m] = *(const bf16x8*)(W + (long)(row0 + 8 * it + rg) * C + 8 * (c + 8 * m));
   }
-}
+  // out[d] (LDS) = sum_k W[row0 + d][k] act[k]
+  RETR_DEVICE void dot(const float (&act)[CPL][8], int lane, float* out) const {
+    const int rg = lane >> 3, c = lane & 7;
+#pragma unroll
+    for (int it = 0; it < HD / 8; ++it) {
+      float s = 0.f;
+#pragma unroll
+      for (int m = 0; m < CPL; ++m)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (float)w[it][m][e] * act[m][e];
+      s = gsum<8>(s);
+      if (c == 0) out[8 * it + rg] = s;
+    }
+  }
+};
+
+// The head's out-projection column slice Wo[n][h HD .. h HD + HD) for n = lane + 64 m
+template <int C, int HD>
+struct OutW {
+  bf16x8 w[C / 64][HD / 8];
+  RETR_DEVICE void load(const bf16* __restrict__ Wo, int h, int lane) {
+#pragma unroll
+    for (int m = 0; m < C / 64; ++m)
+#pragma unroll
+      for (int t = 0; t < HD / 8; ++t)
+        w[m][t] = *(const bf16x8*)(Wo + (long)(lane + 64 * m) * C + h * HD + 8 * t);
+  }
+  // slab[n] = sum_{d < HD} o[d] Wo[n][h HD + d]
+  RETR_DEVICE void apply(const float* os, float* slab, int lane) const {
+    float o[HD];
+#pragma unroll
+    for (int d = 0; d < HD; ++d) o[d] = os[d];
+#pragma unroll
+    for (int m = 0; m < C / 64; ++m) {
+      float s = 0.f;
+#pragma unroll
+      for (int t = 0; t < HD / 8; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += o[8 * t + e] * (float)w[m][t][e];
+      slab[lane + 64 * m] = s;
+    }
+  }
+};
 
 struct SelfHeadsArgs {
   const bf16* n;        // LN1(x) [R][C]
@@ -201,44 +221,60 @@ struct SelfHeadsArgs {
   int R;
 };
 
-template <int C, int HD>
+template <int C, int HD, int NCH>
 __global__ void __launch_bounds__(64) dec_self_heads_kernel(SelfHeadsArgs a, float scale) {
   constexpr int H = C / HD;
   __shared__ float qs[HD], ks[HD], vs[HD], os[HD];
   const int lane = threadIdx.x;
   const int r = blockIdx.x / H, h = blockIdx.x % H;
-  float act[C / 64][8];
-  load_act<C>(a.npos + (long)r * C, lane, act);
-  head_proj<C, HD>(a.win, h * HD, act, lane, qs);
-  head_proj<C, HD>(a.win, C + h * HD, act, lane, ks);
-  load_act<C>(a.n + (long)r * C, lane, act);
-  head_proj<C, HD>(a.win, 2 * C + h * HD, act, lane, vs);
+  const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
+  const int i = a.i, Lmax = a.Lmax;
+  // every global load first: activations, the head's q|k|v and out-projection weight slices,
+  // the cached keys / values of positions < i (one dependent memory round trip per launch)
+  float actp[C / 64][8], actn[C / 64][8];
+  load_act<C>(a.npos + (long)r * C, lane, actp);
+  load_act<C>(a.n + (long)r * C, lane, actn);
+  ProjW<C, HD> wq, wk, wv;
+  wq.load(a.win, h * HD, lane);
+  wk.load(a.win, C + h * HD, lane);
+  wv.load(a.win, 2 * C + h * HD, lane);
+  WaveAttn<HD, NCH> at;
+  at.template load<C>(a.kc, a.vc, h, i + 1,
+                      [&](int j) -> long {
+                        if (j == i) return -1;
+                        return (long)(ar ? ar[j] : r) * Lmax + j;
+                      },
+                      lane);
+  OutW<C, HD> wo;
+  wo.load(a.wo, h, lane);
+  const float bq = lane < HD ? a.bin[h * HD + lane] : 0.f;
+  const float bk = lane < HD ? a.bin[C + h * HD + lane] : 0.f;
+  const float bv = lane < HD ? a.bin[2 * C + h * HD + lane] : 0.f;
+  wq.dot(actp, lane, qs);
+  wk.dot(actp, lane, ks);
+  wv.dot(actn, lane, vs);
   __syncthreads();
   // bias + bf16 rounding (the unfused path's bf16 q / k / v); k, v appended to the cache
+  float q = 0.f, k = 0.f, v = 0.f;
   if (lane < HD) {
-    const float q = bfr(qs[lane] + a.bin[h * HD + lane]);
-    const float k = bfr(ks[lane] + a.bin[C + h * HD + lane]);
-    const float v = bfr(vs[lane] + a.bin[2 * C + h * HD + lane]);
+    q = bfr(qs[lane] + bq);
+    k = bfr(ks[lane] + bk);
+    v = bfr(vs[lane] + bv);
+  }
+  __syncthreads();
+  if (lane < HD) {
     qs[lane] = bfr(q * scale);
     ks[lane] = k;
     vs[lane] = v;
-    const long crow = ((long)r * a.Lmax + a.i) * C + h * HD + lane;
+    const long crow = ((long)r * Lmax + i) * C + h * HD + lane;
     a.kc[crow] = (bf16)k;
     a.vc[crow] = (bf16)v;
   }
   __syncthreads();
-  const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
-  const int i = a.i, Lmax = a.Lmax;
-  WaveAttn<HD> at;
-  at.template run<C>(a.kc, a.vc, h, i + 1,
-                     [&](int j) -> long {
-                       if (j == i) return -1;
-                       return (long)(ar ? ar[j] : r) * Lmax + j;
-                     },
-                     qs, ks, vs, lane);
+  at.compute(qs, ks, vs, lane);
   at.finish(os, lane);
   __syncthreads();
-  head_outproj<C, HD>(a.wo, h, os, a.slab + ((long)h * a.R + r) * C, lane);
+  wo.apply(os, a.slab + ((long)h * a.R + r) * C, lane);
 }
 
 struct CrossHeadsArgs {
@@ -261,7 +297,7 @@ struct CrossHeadsArgs {
   int R;
 };
 
-template <int C, int HD>
+template <int C, int HD, int NCH>
 __global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, float scale) {
   constexpr int H = C / HD, PER = C / 64;
   __shared__ float ts[C];
@@ -269,18 +305,42 @@ __global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, f
   const int lane = threadIdx.x;
   const int r = blockIdx.x / H, h = blockIdx.x % H;
   const long RC = (long)a.R * C;
+  const int kvb = r / a.kv_group, Lk = a.Lk;
+  const unsigned char* km = a.kpm ? a.kpm + (long)kvb * Lk : nullptr;
+  // every global load first: the memory keys / values, the head's query and out-projection
+  // weight slices, the self-attention head partials and the row operands
+  WaveAttn<HD, NCH> at;
+  at.template load<C>(a.k, a.v, h, Lk,
+                      [&](int j) -> long {
+                        if (km && km[j]) return -2;
+                        return (long)kvb * Lk + j;
+                      },
+                      lane);
+  ProjW<C, HD> wq;
+  wq.load(a.wq, h * HD, lane);
+  OutW<C, HD> wo;
+  wo.load(a.wo, h, lane);
+  const float bq = lane < HD ? a.bq[h * HD + lane] : 0.f;
+  float t[PER][H], xv[PER], bo[PER], gm[PER], bt[PER], ps[PER];
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const int n = lane + 64 * m;
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) t[m][hh] = a.slab_in[hh * RC + (long)r * C + n];
+    xv[m] = a.x[(long)r * C + n];
+    bo[m] = a.bo_in[n];
+    gm[m] = a.gamma[n];
+    bt[m] = a.beta[n];
+    ps[m] = a.pos ? a.pos[n] : 0.f;
+  }
   // x' = x + (sum_h slab_in[h] + b_o), heads in order
   float v[PER];
 #pragma unroll
   for (int m = 0; m < PER; ++m) {
-    const int n = lane + 64 * m;
-    float t[H];
-#pragma unroll
-    for (int hh = 0; hh < H; ++hh) t[hh] = a.slab_in[hh * RC + (long)r * C + n];
     float s = 0.f;
 #pragma unroll
-    for (int hh = 0; hh < H; ++hh) s += t[hh];
-    v[m] = a.x[(long)r * C + n] + (s + a.bo_in[n]);
+    for (int hh = 0; hh < H; ++hh) s += t[m][hh];
+    v[m] = xv[m] + (s + bo[m]);
   }
   if (h == 0) {
 #pragma unroll
@@ -300,9 +360,8 @@ __global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, f
   const float rstd = 1.0f / sqrtf(wave_sum(q) / C + a.eps);
 #pragma unroll
   for (int m = 0; m < PER; ++m) {
-    const int n = lane + 64 * m;
-    const float o = (v[m] - mean) * rstd * a.gamma[n] + a.beta[n];
-    ts[n] = bfr(a.pos ? o + a.pos[n] : o);
+    const float o = (v[m] - mean) * rstd * gm[m] + bt[m];
+    ts[lane + 64 * m] = bfr(a.pos ? o + ps[m] : o);
   }
   __syncthreads();
   float act[C / 64][8];
@@ -313,22 +372,17 @@ __global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, f
 #pragma unroll
       for (int e = 0; e < 8; ++e) act[m][e] = ts[8 * (c + 8 * m) + e];
   }
-  head_proj<C, HD>(a.wq, h * HD, act, lane, qs);
+  wq.dot(act, lane, qs);
   __syncthreads();
-  if (lane < HD) qs[lane] = bfr(bfr(qs[lane] + a.bq[h * HD + lane]) * scale);
+  float qv = 0.f;
+  if (lane < HD) qv = bfr(bfr(qs[lane] + bq) * scale);
   __syncthreads();
-  const int kvb = r / a.kv_group, Lk = a.Lk;
-  const unsigned char* km = a.kpm ? a.kpm + (long)kvb * Lk : nullptr;
-  WaveAttn<HD> at;
-  at.template run<C>(a.k, a.v, h, Lk,
-                     [&](int j) -> long {
-                       if (km && km[j]) return -2;
-                       return (long)kvb * Lk + j;
-                     },
-                     qs, nullptr, nullptr, lane);
+  if (lane < HD) qs[lane] = qv;
+  __syncthreads();
+  at.compute(qs, nullptr, nullptr, lane);
   at.finish(os, lane);
   __syncthreads();
-  head_outproj<C, HD>(a.wo, h, os, a.slab_out + ((long)h * a.R + r) * C, lane);
+  wo.apply(os, a.slab_out + ((long)h * a.R + r) * C, lane);
 }
 
 }  // namespace
@@ -348,10 +402,18 @@ int retr_dec_self_heads(const void* n, const void* npos, int R, int C, int H, co
   const float scale = 1.0f / sqrtf((float)hd);
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(R * H));
-  if (C == 256 && hd == 32) hipLaunchKernelGGL((dec_self_heads_kernel<256, 32>), grid, dim3(64), 0, st, a, scale);
-  else if (C == 256) hipLaunchKernelGGL((dec_self_heads_kernel<256, 64>), grid, dim3(64), 0, st, a, scale);
-  else if (hd == 32) hipLaunchKernelGGL((dec_self_heads_kernel<512, 32>), grid, dim3(64), 0, st, a, scale);
-  else hipLaunchKernelGGL((dec_self_heads_kernel<512, 64>), grid, dim3(64), 0, st, a, scale);
+  // all of a wave's key / value loads are issued up front: chunks of 128 (hd 32) or 64 keys
+  const int ch = hd == 32 ? 128 : 64, nch = cdiv(i + 1, ch);
+  RETR_REQUIRE(nch <= 4, "dec_self_heads: %d keys (at most %d)", i + 1, 4 * ch);
+#define SH(CV, HDV, NC) hipLaunchKernelGGL((dec_self_heads_kernel<CV, HDV, NC>), grid, dim3(64), 0, st, a, scale)
+#define SH_N(CV, HDV) \
+  if (nch == 1) SH(CV, HDV, 1); else if (nch == 2) SH(CV, HDV, 2); else SH(CV, HDV, 4);
+  if (C == 256 && hd == 32) { SH_N(256, 32) }
+  else if (C == 256) { SH_N(256, 64) }
+  else if (hd == 32) { SH_N(512, 32) }
+  else { SH_N(512, 64) }
+#undef SH_N
+#undef SH
   return retr_check_launch("dec_self_heads");
 }
 
@@ -370,10 +432,17 @@ int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_i
   const float scale = 1.0f / sqrtf((float)hd);
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(R * H));
-  if (C == 256 && hd == 32) hipLaunchKernelGGL((dec_cross_heads_kernel<256, 32>), grid, dim3(64), 0, st, a, scale);
-  else if (C == 256) hipLaunchKernelGGL((dec_cross_heads_kernel<256, 64>), grid, dim3(64), 0, st, a, scale);
-  else if (hd == 32) hipLaunchKernelGGL((dec_cross_heads_kernel<512, 32>), grid, dim3(64), 0, st, a, scale);
-  else hipLaunchKernelGGL((dec_cross_heads_kernel<512, 64>), grid, dim3(64), 0, st, a, scale);
+  const int ch = hd == 32 ? 128 : 64, nch = cdiv(Lk, ch);
+  RETR_REQUIRE(nch <= 4, "dec_cross_heads: %d memory keys (at most %d)", Lk, 4 * ch);
+#define XH(CV, HDV, NC) hipLaunchKernelGGL((dec_cross_heads_kernel<CV, HDV, NC>), grid, dim3(64), 0, st, a, scale)
+#define XH_N(CV, HDV) \
+  if (nch == 1) XH(CV, HDV, 1); else if (nch == 2) XH(CV, HDV, 2); else XH(CV, HDV, 4);
+  if (C == 256 && hd == 32) { XH_N(256, 32) }
+  else if (C == 256) { XH_N(256, 64) }
+  else if (hd == 32) { XH_N(512, 32) }
+  else { XH_N(512, 64) }
+#undef XH_N
+#undef XH
   return retr_check_launch("dec_cross_heads");
 }
 

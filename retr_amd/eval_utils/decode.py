@@ -46,6 +46,8 @@ def prepare_tokenizer():
 # The fused step's attention sub-layers as one wave per (row, head) (csrc/decode_heads.hip);
 # False: the round-4 block-per-row kernels (csrc/decode.hip dec_gemm + dec_attn_row)
 DEC_HEADS = False   # flipped on after GPU validation
+# (with DEC_HEADS) the cross-attention residual + LN3 in the FFN kernel's prologue
+DEC_FFN_LN = True
 
 
 class _DecodeState:
@@ -294,14 +296,19 @@ class IncrementalGreedy:
                  ptr(st.vx[li]), S, st.K, ptr(st.kpm), ptr(W(csub.out_proj.weight)),
                  ptr(st.hslab2), s)
             x, xa = xa, x
-            # cross-attention residual (head partials in order) + LN3 -> the FFN input
-            call("retr_dec_rows", ptr(x), ptr(st.hslab2), H, ptr(csub.out_proj.bias), R, C,
-                 ptr(xa), ptr(ff.norm.weight), ptr(ff.norm.bias), float(ff.norm.eps), None,
-                 ptr(st.o), None, s)
-            x, xa = xa, x
             f0, f2 = ff.sublayer[0], ff.sublayer[2]
-            call("retr_dec_ffn", ptr(st.o), R, C, ptr(W(f0.weight)), ptr(f0.bias),
-                 ptr(W(f2.weight)), F, ptr(st.slabs), s)
+            if DEC_FFN_LN:
+                # cross-attention residual (head partials in order) + LN3 in the FFN's prologue
+                call("retr_dec_ffn_ln", ptr(x), ptr(st.hslab2), H, ptr(csub.out_proj.bias),
+                     ptr(ff.norm.weight), ptr(ff.norm.bias), float(ff.norm.eps), ptr(xa), R, C,
+                     ptr(W(f0.weight)), ptr(f0.bias), ptr(W(f2.weight)), F, ptr(st.slabs), s)
+            else:
+                call("retr_dec_rows", ptr(x), ptr(st.hslab2), H, ptr(csub.out_proj.bias), R, C,
+                     ptr(xa), ptr(ff.norm.weight), ptr(ff.norm.bias), float(ff.norm.eps), None,
+                     ptr(st.o), None, s)
+                call("retr_dec_ffn", ptr(st.o), R, C, ptr(W(f0.weight)), ptr(f0.bias),
+                     ptr(W(f2.weight)), F, ptr(st.slabs), s)
+            x, xa = xa, x
             if li + 1 < len(layers):
                 nx, npos = layers[li + 1].tgt_self_attn.norm, ptr(st.npos)
             else:

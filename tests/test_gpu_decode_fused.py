@@ -358,6 +358,7 @@ def test_dec_heads_step_matches_block_per_row_step():
     img, mask = synthetic_images(B, 224, seed=12, pad_band=True)
     s = NestedTensor(img.to(DEV), mask.to(DEV))
     res = {}
+    old = dec.DEC_HEADS
     try:
         for heads in (True, False):
             dec.DEC_HEADS = heads
@@ -375,8 +376,37 @@ def test_dec_heads_step_matches_block_per_row_step():
                 ids_e = dec.IncrementalGreedy(model, use_graphs=False)(s, T, 101, 102)
                 assert torch.equal(ids, ids_e)
     finally:
-        dec.DEC_HEADS = True
+        dec.DEC_HEADS = old
         model._retr_decode_states = {}
     (i1, l1), (i0, l0) = res[True], res[False]
     assert _rel(l1, l0) < 2e-2
     assert (i1 == i0).float().mean().item() > 0.3
+
+
+@pytest.mark.parametrize("R", [7, 64])
+def test_dec_ffn_ln_matches_rows_then_ffn(R):
+    """retr_dec_ffn_ln (the FFN input LayerNorm of the head partials in the FFN prologue) against
+    retr_dec_rows (ordered head-partial sum + residual + LN) followed by retr_dec_ffn: the
+    residual bitwise equal, the FFN partial slabs within bf16 rounding of the LN output."""
+    C, Fh, H = 256, 2048, 8
+    g = _g(R + 7)
+    x = torch.randn(R, C, generator=g).to(DEV)
+    hs = torch.randn(H, R, C, generator=g).to(DEV)
+    bo = torch.randn(C, generator=g).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV)
+    w1 = (torch.randn(Fh, C, generator=g) / 16).to(DEV).bfloat16()
+    b1 = torch.randn(Fh, generator=g).to(DEV)
+    w2 = (torch.randn(C, Fh, generator=g) / 45).to(DEV).bfloat16()
+    xo0, xo1 = torch.empty(R, C, device=DEV), torch.empty(R, C, device=DEV)
+    n3 = torch.empty(R, C, dtype=torch.bfloat16, device=DEV)
+    s0 = torch.empty(Fh // 32, R, C, device=DEV)
+    s1 = torch.empty_like(s0)
+    st = ops._st()
+    call("retr_dec_rows", ptr(x), ptr(hs), H, ptr(bo), R, C, ptr(xo0), ptr(gamma), ptr(beta),
+         1e-5, None, ptr(n3), None, st)
+    call("retr_dec_ffn", ptr(n3), R, C, ptr(w1), ptr(b1), ptr(w2), Fh, ptr(s0), st)
+    call("retr_dec_ffn_ln", ptr(x), ptr(hs), H, ptr(bo), ptr(gamma), ptr(beta), 1e-5, ptr(xo1), R,
+         C, ptr(w1), ptr(b1), ptr(w2), Fh, ptr(s1), st)
+    assert torch.equal(xo0, xo1)
+    assert _rel(s1, s0) < 1e-2

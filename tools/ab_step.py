@@ -82,9 +82,9 @@ VARIANTS = {
     "up8k": {("TUNE", 28): 8192},
     # round 5: slice-affine conv wgrad / problem-affine linear wgrad orders are the defaults;
     # these restore the round-4 runs of 4 logical blocks per XCD turn
-    "cw_r4": {("TUNE", 20): -1},
+    "cw_aff": {("TUNE", 20): -1},
     "wb_aff": {("TUNE", 19): -1},
-    "orders_aff": {("TUNE", 19): -1},   # with the default (slice-affine) conv order
+    "orders_aff": {("TUNE", 19): -1, ("TUNE", 20): -1},
 }
 
 

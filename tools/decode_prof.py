@@ -25,9 +25,8 @@ def main():
     ap.add_argument("--block-per-row", action="store_true",
                     help="the round-4 attention sub-layers (eval_utils.decode.DEC_HEADS = False)")
     a = ap.parse_args()
-    if a.block_per_row:
-        from retr_amd.eval_utils import decode as dec
-        dec.DEC_HEADS = False
+    from retr_amd.eval_utils import decode as dec
+    dec.DEC_HEADS = not a.block_per_row
     model, _ = build(cfg5(), "cuda")
     model.eval()
     img, mask = synthetic_images(a.batch, 224, seed=3000)
