@@ -42,16 +42,29 @@ RETR_DEVICE float gsum(float s) {
 
 RETR_DEVICE float bfr(float v) { return (float)(bf16)v; }   // round to bf16 and back
 
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+// sum_e a[e] b[e] over 8 bf16 pairs by v_dot2c_f32_bf16, two independent chains (a single wave
+// per SIMD: every dependent VALU op exposes its latency)
+RETR_DEVICE float dot8(const bf16x8& a, const bf16x8& b) {
+  float s0 = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{a[0], a[1]}, bf16x2{b[0], b[1]}, 0.f, false);
+  float s1 = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{a[2], a[3]}, bf16x2{b[2], b[3]}, 0.f, false);
+  s0 = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{a[4], a[5]}, bf16x2{b[4], b[5]}, s0, false);
+  s1 = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{a[6], a[7]}, bf16x2{b[6], b[7]}, s1, false);
+  return s0 + s1;
+}
+RETR_DEVICE bf16x8 to_bf8(const float* v) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = (bf16)v[e];
+  return r;
+}
+
 // this lane's activation chunks (c + 8 m) of a bf16 row
 template <int C>
-RETR_DEVICE void load_act(const bf16* row, int lane, float (&act)[C / 64][8]) {
+RETR_DEVICE void load_act(const bf16* row, int lane, bf16x8 (&act)[C / 64]) {
   const int c = lane & 7;
 #pragma unroll
-  for (int m = 0; m < C / 64; ++m) {
-    const bf16x8 v = *(const bf16x8*)(row + 8 * (c + 8 * m));
-#pragma unroll
-    for (int e = 0; e < 8; ++e) act[m][e] = (float)v[e];
-  }
+  for (int m = 0; m < C / 64; ++m) act[m] = *(const bf16x8*)(row + 8 * (c + 8 * m));
 }
 
 // Attention of one wave over keys [0, Lk), Lk <= NCH x CH: every key / value load is issued
@@ -89,23 +102,15 @@ struct WaveAttn {
 
   RETR_DEVICE void compute(const float* qs, const float* kn, const float* vn, int lane) {
     const int g = lane % NG;
-    float q[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) q[e] = qs[8 * g + e];
+    const bf16x8 q = to_bf8(qs + 8 * g);            // bf16-rounded values: exact
+    const bf16x8 knb = kn ? to_bf8(kn + 8 * g) : bf16x8{};
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       float sc[KU];
       float cm = -INFINITY;
 #pragma unroll
       for (int u = 0; u < KU; ++u) {
-        float s = 0.f;
-        if (row[c][u] == -1) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) s += q[e] * kn[8 * g + e];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) s += q[e] * (float)kk[c][u][e];
-        }
+        float s = dot8(q, row[c][u] == -1 ? knb : kk[c][u]);
         s = gsum<NG>(s);
         sc[u] = row[c][u] == -2 ? -INFINITY : s;
         cm = fmaxf(cm, sc[u]);
@@ -163,17 +168,20 @@ struct ProjW {
       for (int m = 0; m < CPL; ++m)
         w[it][m] = *(const bf16x8*)(W + (long)(row0 + 8 * it + rg) * C + 8 * (c + 8 * m));
   }
-  // out[d] (LDS) = sum_k W[row0 + d][k] act[k]
-  RETR_DEVICE void dot(const float (&act)[CPL][8], int lane, float* out) const {
+  // out[d] (LDS) = sum_k W[row0 + d][k] act[k]  (one dot8 chain pair per chunk, chunks summed
+  // pairwise)
+  RETR_DEVICE void dot(const bf16x8 (&act)[CPL], int lane, float* out) const {
     const int rg = lane >> 3, c = lane & 7;
 #pragma unroll
     for (int it = 0; it < HD / 8; ++it) {
-      float s = 0.f;
+      float p[CPL];
 #pragma unroll
-      for (int m = 0; m < CPL; ++m)
+      for (int m = 0; m < CPL; ++m) p[m] = dot8(w[it][m], act[m]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s += (float)w[it][m][e] * act[m][e];
-      s = gsum<8>(s);
+      for (int st = 1; st < CPL; st <<= 1)
+#pragma unroll
+        for (int m = 0; m + st < CPL; m += 2 * st) p[m] += p[m + st];
+      const float s = gsum<8>(p[0]);
       if (c == 0) out[8 * it + rg] = s;
     }
   }
@@ -192,17 +200,19 @@ struct OutW {
   }
   // slab[n] = sum_{d < HD} o[d] Wo[n][h HD + d]
   RETR_DEVICE void apply(const float* os, float* slab, int lane) const {
-    float o[HD];
+    bf16x8 o[HD / 8];                               // bf16-rounded attention output: exact
 #pragma unroll
-    for (int d = 0; d < HD; ++d) o[d] = os[d];
+    for (int t = 0; t < HD / 8; ++t) o[t] = to_bf8(os + 8 * t);
 #pragma unroll
     for (int m = 0; m < C / 64; ++m) {
-      float s = 0.f;
+      float p[HD / 8];
 #pragma unroll
-      for (int t = 0; t < HD / 8; ++t)
+      for (int t = 0; t < HD / 8; ++t) p[t] = dot8(o[t], w[m][t]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s += o[8 * t + e] * (float)w[m][t][e];
-      slab[lane + 64 * m] = s;
+      for (int st = 1; st < HD / 8; st <<= 1)
+#pragma unroll
+        for (int t = 0; t + st < HD / 8; t += 2 * st) p[t] += p[t + st];
+      slab[lane + 64 * m] = p[0];
     }
   }
 };
@@ -231,7 +241,7 @@ __global__ void __launch_bounds__(64) dec_self_heads_kernel(SelfHeadsArgs a, flo
   const int i = a.i, Lmax = a.Lmax;
   // every global load first: activations, the head's q|k|v and out-projection weight slices,
   // the cached keys / values of positions < i (one dependent memory round trip per launch)
-  float actp[C / 64][8], actn[C / 64][8];
+  bf16x8 actp[C / 64], actn[C / 64];
   load_act<C>(a.npos + (long)r * C, lane, actp);
   load_act<C>(a.n + (long)r * C, lane, actn);
   ProjW<C, HD> wq, wk, wv;
@@ -364,13 +374,11 @@ __global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, f
     ts[lane + 64 * m] = bfr(a.pos ? o + ps[m] : o);
   }
   __syncthreads();
-  float act[C / 64][8];
+  bf16x8 act[C / 64];                               // bf16-rounded LN output: exact
   {
     const int c = lane & 7;
 #pragma unroll
-    for (int m = 0; m < C / 64; ++m)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) act[m][e] = ts[8 * (c + 8 * m) + e];
+    for (int m = 0; m < C / 64; ++m) act[m] = to_bf8(ts + 8 * (c + 8 * m));
   }
   wq.dot(act, lane, qs);
   __syncthreads();

@@ -45,9 +45,9 @@ def prepare_tokenizer():
 
 # The fused step's attention sub-layers as one wave per (row, head) (csrc/decode_heads.hip);
 # False: the round-4 block-per-row kernels (csrc/decode.hip dec_gemm + dec_attn_row)
-DEC_HEADS = False   # flipped on after GPU validation
+DEC_HEADS = True
 # (with DEC_HEADS) the cross-attention residual + LN3 in the FFN kernel's prologue
-DEC_FFN_LN = True
+DEC_FFN_LN = False
 
 
 class _DecodeState:
