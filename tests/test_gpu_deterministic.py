@@ -85,7 +85,7 @@ def test_embed_ln_backward_matches_autograd(padding_idx):
     beta = torch.randn(C, generator=g)
     dy = torch.randn(B * T, C, generator=g)
     ps = [t.to(DEV).requires_grad_(True) for t in (word, posw, gamma, beta)]
-    y = ops._EmbedLN.apply(caps.to(DEV), *ps, 1e-12, 0.0, padding_idx)
+    y = ops._EmbedLN.apply(caps.to(DEV), *ps, 1e-12, 0.0, padding_idx, False)
     y.backward(dy.to(DEV))
     rs = [t.clone().requires_grad_(True) for t in (word, posw, gamma, beta)]
     e = rs[0][caps] + rs[1][:T].unsqueeze(0)
@@ -103,7 +103,7 @@ def test_embed_ln_backward_matches_autograd(padding_idx):
     first = [p.grad.clone() for p in ps]
     for p in ps:
         p.grad = None
-    ops._EmbedLN.apply(caps.to(DEV), *ps, 1e-12, 0.0, padding_idx).backward(dy.to(DEV))
+    ops._EmbedLN.apply(caps.to(DEV), *ps, 1e-12, 0.0, padding_idx, False).backward(dy.to(DEV))
     for a, p in zip(first, ps):
         assert torch.equal(a, p.grad)
 
