@@ -816,111 +816,113 @@ dec_ffn_kernel(const bf16* n3, int R, const bf16* w1, const float* b1, const bf1
 }
 
 // ---- dec_ffn_ln: dec_ffn with the FFN's input LayerNorm in its prologue -----------------------
-// The wave's 16 rows: x = xin + (sum_j hslab[j] + bo) (slabs in order) -> xout (hidden chunk 0's
-// blocks write it), n3 = bf16(LN3(x)) into LDS as the FFN1 A operand -- instead of a retr_dec_rows
-// launch between the attention and the FFN (csrc/decode_heads.hip's per-head partials).
-template <int PER>
-__global__ void __launch_bounds__(64)
+// Block = 4 waves over the same 16 rows x 32 hidden units as dec_ffn.  Wave w: rows 4w..4w+3 of
+// x = xin + (sum_j hslab[j] + bo) (slabs in order; hidden chunk 0's blocks write x to xout) and
+// n3 = bf16(LN3(x)) into LDS; waves 0 / 1 then the FFN1 column tile w (16 hidden units), and every
+// wave 4 of the 16 FFN2 column tiles -- instead of a retr_dec_rows launch between the per-head
+// cross-attention partials (csrc/decode_heads.hip) and the FFN.
+template <int PER, int MAXS>
+__global__ void __launch_bounds__(256)
 dec_ffn_ln_kernel(const float* xin, const float* hslab, int nslab, const float* bo,
                   const float* gamma, const float* beta, float eps, float* xout, int R,
                   const bf16* w1, const float* b1, const bf16* w2, int F, float* slabs) {
   constexpr int C = PER * 64;
   constexpr int HS = 32 + 8, AS = C + 8;
   constexpr int CPL = C / 64;                     // consecutive columns per lane
+  constexpr int NT = C / 16, NTW = NT / 4;        // FFN2 column tiles, per wave
+  typedef __attribute__((ext_vector_type(4))) float f4v;
   __shared__ __attribute__((aligned(16))) bf16 Hs[16 * HS];     // relu(h) [16 rows][32 units]
   __shared__ __attribute__((aligned(16))) bf16 As[16 * AS];     // LN3 rows [16][C]
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j0 = blockIdx.x * 32, r0 = blockIdx.y * 16;
-  constexpr int NT = C / 16;
-  u32x4 w1f[2][C / 32], w2f[NT];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
+  // weights first: FFN1 column tile w (waves 0, 1), FFN2 column tiles 4w .. 4w + 3
+  u32x4 w1f[C / 32], w2f[NTW];
+  if (w < 2) {
 #pragma unroll
     for (int ks = 0; ks < C / 32; ++ks)
-      w1f[t][ks] = *(const u32x4*)(w1 + (long)(j0 + 16 * t + (lane & 15)) * C + 32 * ks +
-                                   8 * (lane >> 4));
+      w1f[ks] = *(const u32x4*)(w1 + (long)(j0 + 16 * w + (lane & 15)) * C + 32 * ks +
+                                8 * (lane >> 4));
+  }
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
-    w2f[t] = *(const u32x4*)(w2 + (long)(16 * t + (lane & 15)) * F + j0 + 8 * (lane >> 4));
-  const float b1v[2] = {b1[j0 + (lane & 15)], b1[j0 + 16 + (lane & 15)]};
+  for (int t = 0; t < NTW; ++t)
+    w2f[t] = *(const u32x4*)(w2 + (long)(16 * (NTW * w + t) + (lane & 15)) * F + j0 +
+                             8 * (lane >> 4));
+  const float b1v = w < 2 ? b1[j0 + 16 * w + (lane & 15)] : 0.f;
+  const long RC = (long)R * C;
+  const int c0 = CPL * lane;
   float bb[CPL], gm[CPL], bt[CPL];
 #pragma unroll
-  for (int e = 0; e < CPL; ++e) {
-    const int c = CPL * lane + e;
-    bb[e] = bo[c];
-    gm[e] = gamma[c];
-    bt[e] = beta[c];
+  for (int e = 0; e < CPL; e += 4) {
+    *(f4v*)(bb + e) = *(const f4v*)(bo + c0 + e);
+    *(f4v*)(gm + e) = *(const f4v*)(gamma + c0 + e);
+    *(f4v*)(bt + e) = *(const f4v*)(beta + c0 + e);
   }
-  const long RC = (long)R * C;
-  constexpr int RB = 4;                           // rows per load batch
-#pragma unroll 1
-  for (int rb = 0; rb < 16; rb += RB) {
-    float v[RB][CPL];
+  // the wave's 4 rows: every slab / residual load in flight at once
+  float t[4][MAXS][CPL], xv[4][CPL];
 #pragma unroll
-    for (int q = 0; q < RB; ++q) {
-      const int r = r0 + rb + q;
-      const int rr = r < R ? r : R - 1;
-      float s[CPL];
+  for (int q = 0; q < 4; ++q) {
+    const int r = r0 + 4 * w + q;
+    const int rr = r < R ? r : R - 1;
 #pragma unroll
-      for (int e = 0; e < CPL; ++e) s[e] = 0.f;
-      for (int j = 0; j < nslab; ++j) {
-        const float* src = hslab + j * RC + (long)rr * C + CPL * lane;
+    for (int j = 0; j < MAXS; ++j)
 #pragma unroll
-        for (int e = 0; e < CPL; ++e) s[e] += src[e];
-      }
-      const float* xr = xin + (long)rr * C + CPL * lane;
+      for (int e = 0; e < CPL; e += 4)
+        *(f4v*)(&t[q][j][e]) = j < nslab ? *(const f4v*)(hslab + j * RC + (long)rr * C + c0 + e)
+                                         : f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int e = 0; e < CPL; ++e) v[q][e] = xr[e] + (s[e] + bb[e]);
+    for (int e = 0; e < CPL; e += 4) *(f4v*)(&xv[q][e]) = *(const f4v*)(xin + (long)rr * C + c0 + e);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = r0 + 4 * w + q;
+    float v[CPL];
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < MAXS; ++j)
+        if (j < nslab) s += t[q][j][e];
+      v[e] = xv[q][e] + (s + bb[e]);
     }
+    float sm = 0.f;
 #pragma unroll
-    for (int q = 0; q < RB; ++q) {
-      const int r = r0 + rb + q;
-      float sm = 0.f;
+    for (int e = 0; e < CPL; ++e) sm += v[e];
+    const float mean = wave_sum(sm) / C;
+    float qq = 0.f;
 #pragma unroll
-      for (int e = 0; e < CPL; ++e) sm += v[q][e];
-      const float mean = wave_sum(sm) / C;
-      float qq = 0.f;
+    for (int e = 0; e < CPL; ++e) {
+      const float d = v[e] - mean;
+      qq += d * d;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(qq) / C + eps);
 #pragma unroll
-      for (int e = 0; e < CPL; ++e) {
-        const float d = v[q][e] - mean;
-        qq += d * d;
-      }
-      const float rstd = 1.0f / sqrtf(wave_sum(qq) / C + eps);
+    for (int e = 0; e < CPL; ++e)
+      As[(4 * w + q) * AS + c0 + e] = (bf16)((v[e] - mean) * rstd * gm[e] + bt[e]);
+    if (blockIdx.x == 0 && r < R) {
 #pragma unroll
-      for (int e = 0; e < CPL; ++e)
-        As[(rb + q) * AS + CPL * lane + e] = (bf16)((v[q][e] - mean) * rstd * gm[e] + bt[e]);
-      if (blockIdx.x == 0 && r < R) {
-#pragma unroll
-        for (int e = 0; e < CPL; ++e) xout[(long)r * C + CPL * lane + e] = v[q][e];
-      }
+      for (int e = 0; e < CPL; e += 4) *(f4v*)(xout + (long)r * C + c0 + e) = *(f4v*)(v + e);
     }
   }
   __syncthreads();
-  u32x4 af[C / 32];
+  if (w < 2) {
+    f4 h = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int ks = 0; ks < C / 32; ++ks)
-    af[ks] = *(const u32x4*)(As + (lane & 15) * AS + 32 * ks + 8 * (lane >> 4));
-  f4 h[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int ks = 0; ks < C / 32; ++ks) {
-    h[0] = mfma16(af[ks], w1f[0][ks], h[0]);
-    h[1] = mfma16(af[ks], w1f[1][ks], h[1]);
-  }
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int jj = 16 * t + (lane & 15);
-    const float b = b1v[t];
+    for (int ks = 0; ks < C / 32; ++ks) {
+      const u32x4 af = *(const u32x4*)(As + (lane & 15) * AS + 32 * ks + 8 * (lane >> 4));
+      h = mfma16(af, w1f[ks], h);
+    }
+    const int jj = 16 * w + (lane & 15);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      Hs[(4 * (lane >> 4) + e) * HS + jj] = (bf16)fmaxf(h[t][e] + b, 0.f);
+      Hs[(4 * (lane >> 4) + e) * HS + jj] = (bf16)fmaxf(h[e] + b1v, 0.f);
   }
   __syncthreads();
   const u32x4 a0 = *(const u32x4*)(Hs + (lane & 15) * HS + 8 * (lane >> 4));
   float* slab = slabs + (long)blockIdx.x * R * C;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int n = 16 * t + (lane & 15);
-    const f4 acc = mfma16(a0, w2f[t], f4{0.f, 0.f, 0.f, 0.f});
+  for (int t2 = 0; t2 < NTW; ++t2) {
+    const int n = 16 * (NTW * w + t2) + (lane & 15);
+    const f4 acc = mfma16(a0, w2f[t2], f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int r = r0 + 4 * (lane >> 4) + e;
@@ -1048,17 +1050,17 @@ int retr_dec_ffn_ln(const float* xin, const float* hslab, int nslab, const float
                     const float* gamma, const float* beta, float eps, float* xout, int R, int C,
                     const void* w1, const float* b1, const void* w2, int F, float* slabs,
                     void* stream) {
-  RETR_REQUIRE((C == 256 || C == 512) && F % 32 == 0 && nslab >= 0, "dec_ffn_ln: C=%d F=%d",
-               C, F);
+  RETR_REQUIRE((C == 256 || C == 512) && F % 32 == 0 && nslab >= 0 && nslab <= 16,
+               "dec_ffn_ln: C=%d F=%d nslab=%d (<= 16)", C, F, nslab);
   if (R == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(F / 32, cdiv(R, 16));
-  if (C == 256)
-    hipLaunchKernelGGL(dec_ffn_ln_kernel<4>, grid, dim3(64), 0, st, xin, hslab, nslab, bo, gamma,
-                       beta, eps, xout, R, (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
-  else
-    hipLaunchKernelGGL(dec_ffn_ln_kernel<8>, grid, dim3(64), 0, st, xin, hslab, nslab, bo, gamma,
-                       beta, eps, xout, R, (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
+#define FL(P, MS) hipLaunchKernelGGL((dec_ffn_ln_kernel<P, MS>), grid, dim3(256), 0, st, xin, hslab, \
+                                     nslab, bo, gamma, beta, eps, xout, R, (const bf16*)w1, b1,    \
+                                     (const bf16*)w2, F, slabs)
+  if (C == 256) { if (nslab <= 8) FL(4, 8); else FL(4, 16); }
+  else { if (nslab <= 8) FL(8, 8); else FL(8, 16); }
+#undef FL
   return retr_check_launch("dec_ffn_ln");
 }
 

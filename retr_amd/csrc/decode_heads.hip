@@ -67,28 +67,28 @@ RETR_DEVICE void load_act(const bf16* row, int lane, bf16x8 (&act)[C / 64]) {
   for (int m = 0; m < C / 64; ++m) act[m] = *(const bf16x8*)(row + 8 * (c + 8 * m));
 }
 
-// Attention of one wave over keys [0, Lk), Lk <= NCH x CH: every key / value load is issued
-// by load() (at kernel start: they depend on nothing computed in the step), then compute() runs
-// an online softmax over the NCH chunks.  Lane = (dim group g = lane % NG of 8 dims, key part =
-// lane / NG): key j = CH c + part + NPART u.  key_row(j) gives the K/V row of key j, -1 for the
-// step's own key (its K/V in LDS: kn / vn) or -2 for a masked key.
-template <int HD, int NCH>
+// Attention of one wave over its key range [j0, j1), at most NCH x CH keys: every key / value load
+// is issued by load() (at kernel start: they depend on nothing computed in the step), then
+// compute() runs an online softmax over the NCH chunks.  Lane = (dim group g = lane % NG of 8
+// dims, key part = lane / NG): key j = j0 + CH c + part + NPART u.  key_row(j) gives the K/V row
+// of key j, -1 for the step's own key (its K/V in LDS: kn / vn) or -2 for a masked key.
+template <int HD, int NCH, int KU>
 struct WaveAttn {
-  static constexpr int NG = HD / 8, NPART = 64 / NG, KU = 8, CH = NPART * KU;
+  static constexpr int NG = HD / 8, NPART = 64 / NG, CH = NPART * KU;
   long row[NCH][KU];
   bf16x8 kk[NCH][KU], vv[NCH][KU];
   float mx = -INFINITY, sum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   template <int C, class RowFn>
-  RETR_DEVICE void load(const bf16* __restrict__ K, const bf16* __restrict__ V, int h, int Lk,
-                        RowFn key_row, int lane) {
+  RETR_DEVICE void load(const bf16* __restrict__ K, const bf16* __restrict__ V, int h, int j0,
+                        int j1, RowFn key_row, int lane) {
     const int g = lane % NG, part = lane / NG;
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int u = 0; u < KU; ++u) {
-        const int j = CH * c + part + NPART * u;
-        row[c][u] = j < Lk ? key_row(j) : -2;
+        const int j = j0 + CH * c + part + NPART * u;
+        row[c][u] = j < j1 ? key_row(j) : -2;
         kk[c][u] = row[c][u] >= 0 ? *(const bf16x8*)(K + row[c][u] * C + h * HD + 8 * g)
                                   : bf16x8{};
       }
@@ -140,40 +140,61 @@ struct WaveAttn {
       }
     }
   }
-  // o[8 g + e] (bf16-rounded, normalised) into LDS from the lanes of part 0
-  RETR_DEVICE void finish(float* os, int lane) {
+  // this wave's (max, sum, unnormalised P V) into LDS slot w
+  RETR_DEVICE void publish(float* mxs, float* sms, float* accs, int w, int lane) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
 #pragma unroll
       for (int o = NG; o < 64; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
-    const float inv = 1.f / sum;                 // a fully masked row gives NaN, as torch
+    if (lane == 0) {
+      mxs[w] = mx;
+      sms[w] = sum;
+    }
     if (lane < NG) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) os[8 * lane + e] = bfr(acc[e] * inv);
+      for (int e = 0; e < 8; ++e) accs[w * HD + 8 * lane + e] = acc[e];
     }
   }
 };
 
-// The head's weight slices, loaded up front: rows [row0, row0 + HD) of W (C columns each) in
-// head_proj's lane layout
-template <int C, int HD>
+// o[d] (bf16-rounded, normalised) from NW waves' partial softmax states, for d = lane < HD
+template <int HD, int NW>
+RETR_DEVICE void merge_heads(const float* mxs, const float* sms, const float* accs, float* os,
+                             int lane) {
+  if (lane >= HD) return;
+  float M = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) M = fmaxf(M, mxs[w]);
+  float num = 0.f, den = 0.f;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const float f = mxs[w] == -INFINITY ? 0.f : __expf(mxs[w] - M);
+    num += accs[w * HD + lane] * f;
+    den += sms[w] * f;
+  }
+  os[lane] = bfr(num * (1.f / den));               // a fully masked row gives NaN, as torch
+}
+
+// ND of a head's projection rows, [row0, row0 + ND) of W (C columns each), loaded up front in
+// the dot's lane layout: lane = (row group rg = lane / 8, chunk column c = lane % 8), lane c owns
+// the 16-byte chunks c, c + 8, ... of every row
+template <int C, int ND>
 struct ProjW {
   static constexpr int CPL = C / 64;
-  bf16x8 w[HD / 8][CPL];
+  bf16x8 w[ND / 8][CPL];
   RETR_DEVICE void load(const bf16* __restrict__ W, int row0, int lane) {
     const int rg = lane >> 3, c = lane & 7;
 #pragma unroll
-    for (int it = 0; it < HD / 8; ++it)
+    for (int it = 0; it < ND / 8; ++it)
 #pragma unroll
       for (int m = 0; m < CPL; ++m)
         w[it][m] = *(const bf16x8*)(W + (long)(row0 + 8 * it + rg) * C + 8 * (c + 8 * m));
   }
-  // out[d] (LDS) = sum_k W[row0 + d][k] act[k]  (one dot8 chain pair per chunk, chunks summed
-  // pairwise)
+  // out[d] (LDS) = sum_k W[row0 + d][k] act[k]  (one dot8 per chunk, chunks summed pairwise)
   RETR_DEVICE void dot(const bf16x8 (&act)[CPL], int lane, float* out) const {
     const int rg = lane >> 3, c = lane & 7;
 #pragma unroll
-    for (int it = 0; it < HD / 8; ++it) {
+    for (int it = 0; it < ND / 8; ++it) {
       float p[CPL];
 #pragma unroll
       for (int m = 0; m < CPL; ++m) p[m] = dot8(w[it][m], act[m]);
@@ -187,24 +208,24 @@ struct ProjW {
   }
 };
 
-// The head's out-projection column slice Wo[n][h HD .. h HD + HD) for n = lane + 64 m
-template <int C, int HD>
+// NM groups of 64 out-projection rows (n = lane + 64 (m0 + m)), the head's HD columns of each
+template <int C, int HD, int NM>
 struct OutW {
-  bf16x8 w[C / 64][HD / 8];
-  RETR_DEVICE void load(const bf16* __restrict__ Wo, int h, int lane) {
+  bf16x8 w[NM][HD / 8];
+  RETR_DEVICE void load(const bf16* __restrict__ Wo, int h, int m0, int lane) {
 #pragma unroll
-    for (int m = 0; m < C / 64; ++m)
+    for (int m = 0; m < NM; ++m)
 #pragma unroll
       for (int t = 0; t < HD / 8; ++t)
-        w[m][t] = *(const bf16x8*)(Wo + (long)(lane + 64 * m) * C + h * HD + 8 * t);
+        w[m][t] = *(const bf16x8*)(Wo + (long)(lane + 64 * (m0 + m)) * C + h * HD + 8 * t);
   }
   // slab[n] = sum_{d < HD} o[d] Wo[n][h HD + d]
-  RETR_DEVICE void apply(const float* os, float* slab, int lane) const {
+  RETR_DEVICE void apply(const float* os, float* slab, int m0, int lane) const {
     bf16x8 o[HD / 8];                               // bf16-rounded attention output: exact
 #pragma unroll
     for (int t = 0; t < HD / 8; ++t) o[t] = to_bf8(os + 8 * t);
 #pragma unroll
-    for (int m = 0; m < C / 64; ++m) {
+    for (int m = 0; m < NM; ++m) {
       float p[HD / 8];
 #pragma unroll
       for (int t = 0; t < HD / 8; ++t) p[t] = dot8(o[t], w[m][t]);
@@ -212,7 +233,7 @@ struct OutW {
       for (int st = 1; st < HD / 8; st <<= 1)
 #pragma unroll
         for (int t = 0; t + st < HD / 8; t += 2 * st) p[t] += p[t + st];
-      slab[lane + 64 * m] = p[0];
+      slab[lane + 64 * (m0 + m)] = p[0];
     }
   }
 };
@@ -231,67 +252,75 @@ struct SelfHeadsArgs {
   int R;
 };
 
-template <int C, int HD, int NCH>
-__global__ void __launch_bounds__(64) dec_self_heads_kernel(SelfHeadsArgs a, float scale) {
-  constexpr int H = C / HD;
+// One block of NW waves per (row, head): wave w computes rows [w HD / NW, (w + 1) HD / NW) of
+// the head's q, k, v, attends over keys [w KPW, (w + 1) KPW), and computes out-projection rows
+// n in its NM-group share; the waves' softmax states merge through LDS.
+template <int C, int HD, int NW, int NCH, int KU>
+__global__ void __launch_bounds__(64 * NW) dec_self_heads_kernel(SelfHeadsArgs a, float scale) {
+  constexpr int H = C / HD, ND = HD / NW, NM = C / 64 / NW;
+  constexpr int KPW = NCH * (64 / (HD / 8)) * KU;  // keys per wave
   __shared__ float qs[HD], ks[HD], vs[HD], os[HD];
-  const int lane = threadIdx.x;
+  __shared__ float mxs[NW], sms[NW], accs[NW * HD];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = blockIdx.x / H, h = blockIdx.x % H;
   const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
   const int i = a.i, Lmax = a.Lmax;
-  // every global load first: activations, the head's q|k|v and out-projection weight slices,
-  // the cached keys / values of positions < i (one dependent memory round trip per launch)
+  // every global load first: activations, this wave's q|k|v and out-projection weight rows,
+  // its cached keys / values of positions < i (one dependent memory round trip per launch)
   bf16x8 actp[C / 64], actn[C / 64];
   load_act<C>(a.npos + (long)r * C, lane, actp);
   load_act<C>(a.n + (long)r * C, lane, actn);
-  ProjW<C, HD> wq, wk, wv;
-  wq.load(a.win, h * HD, lane);
-  wk.load(a.win, C + h * HD, lane);
-  wv.load(a.win, 2 * C + h * HD, lane);
-  WaveAttn<HD, NCH> at;
-  at.template load<C>(a.kc, a.vc, h, i + 1,
+  ProjW<C, ND> wq, wk, wv;
+  wq.load(a.win, h * HD + w * ND, lane);
+  wk.load(a.win, C + h * HD + w * ND, lane);
+  wv.load(a.win, 2 * C + h * HD + w * ND, lane);
+  WaveAttn<HD, NCH, KU> at;
+  at.template load<C>(a.kc, a.vc, h, w * KPW, min(i + 1, (w + 1) * KPW),
                       [&](int j) -> long {
                         if (j == i) return -1;
                         return (long)(ar ? ar[j] : r) * Lmax + j;
                       },
                       lane);
-  OutW<C, HD> wo;
-  wo.load(a.wo, h, lane);
-  const float bq = lane < HD ? a.bin[h * HD + lane] : 0.f;
-  const float bk = lane < HD ? a.bin[C + h * HD + lane] : 0.f;
-  const float bv = lane < HD ? a.bin[2 * C + h * HD + lane] : 0.f;
-  wq.dot(actp, lane, qs);
-  wk.dot(actp, lane, ks);
-  wv.dot(actn, lane, vs);
+  OutW<C, HD, NM> wo;
+  wo.load(a.wo, h, w * NM, lane);
+  const int d = w * ND + lane;
+  const float bq = lane < ND ? a.bin[h * HD + d] : 0.f;
+  const float bk = lane < ND ? a.bin[C + h * HD + d] : 0.f;
+  const float bv = lane < ND ? a.bin[2 * C + h * HD + d] : 0.f;
+  wq.dot(actp, lane, qs + w * ND);
+  wk.dot(actp, lane, ks + w * ND);
+  wv.dot(actn, lane, vs + w * ND);
   __syncthreads();
   // bias + bf16 rounding (the unfused path's bf16 q / k / v); k, v appended to the cache
   float q = 0.f, k = 0.f, v = 0.f;
-  if (lane < HD) {
-    q = bfr(qs[lane] + bq);
-    k = bfr(ks[lane] + bk);
-    v = bfr(vs[lane] + bv);
+  if (lane < ND) {
+    q = bfr(qs[d] + bq);
+    k = bfr(ks[d] + bk);
+    v = bfr(vs[d] + bv);
   }
   __syncthreads();
-  if (lane < HD) {
-    qs[lane] = bfr(q * scale);
-    ks[lane] = k;
-    vs[lane] = v;
-    const long crow = ((long)r * Lmax + i) * C + h * HD + lane;
+  if (lane < ND) {
+    qs[d] = bfr(q * scale);
+    ks[d] = k;
+    vs[d] = v;
+    const long crow = ((long)r * Lmax + i) * C + h * HD + d;
     a.kc[crow] = (bf16)k;
     a.vc[crow] = (bf16)v;
   }
   __syncthreads();
   at.compute(qs, ks, vs, lane);
-  at.finish(os, lane);
+  at.publish(mxs, sms, accs, w, lane);
   __syncthreads();
-  wo.apply(os, a.slab + ((long)h * a.R + r) * C, lane);
+  merge_heads<HD, NW>(mxs, sms, accs, os, lane);
+  __syncthreads();
+  wo.apply(os, a.slab + ((long)h * a.R + r) * C, w * NM, lane);
 }
 
 struct CrossHeadsArgs {
   const float* slab_in;   // [H][R][C] partial out-projections of the self-attention
   const float* x;         // residual in [R][C]
   const float* bo_in;     // self out-proj bias
-  float* xo;              // residual out (written by the h = 0 waves)
+  float* xo;              // residual out (written by the h = 0 blocks)
   const float* gamma;     // LN2
   const float* beta;
   float eps;
@@ -307,30 +336,32 @@ struct CrossHeadsArgs {
   int R;
 };
 
-template <int C, int HD, int NCH>
-__global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, float scale) {
-  constexpr int H = C / HD, PER = C / 64;
+template <int C, int HD, int NW, int NCH, int KU>
+__global__ void __launch_bounds__(64 * NW) dec_cross_heads_kernel(CrossHeadsArgs a, float scale) {
+  constexpr int H = C / HD, PER = C / 64, ND = HD / NW, NM = C / 64 / NW;
+  constexpr int KPW = NCH * (64 / (HD / 8)) * KU;
   __shared__ float ts[C];
   __shared__ float qs[HD], os[HD];
-  const int lane = threadIdx.x;
+  __shared__ float mxs[NW], sms[NW], accs[NW * HD];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = blockIdx.x / H, h = blockIdx.x % H;
   const long RC = (long)a.R * C;
   const int kvb = r / a.kv_group, Lk = a.Lk;
   const unsigned char* km = a.kpm ? a.kpm + (long)kvb * Lk : nullptr;
-  // every global load first: the memory keys / values, the head's query and out-projection
-  // weight slices, the self-attention head partials and the row operands
-  WaveAttn<HD, NCH> at;
-  at.template load<C>(a.k, a.v, h, Lk,
+  // every global load first: this wave's memory keys / values, query and out-projection weight
+  // rows, the self-attention head partials and the row operands
+  WaveAttn<HD, NCH, KU> at;
+  at.template load<C>(a.k, a.v, h, w * KPW, min(Lk, (w + 1) * KPW),
                       [&](int j) -> long {
                         if (km && km[j]) return -2;
                         return (long)kvb * Lk + j;
                       },
                       lane);
-  ProjW<C, HD> wq;
-  wq.load(a.wq, h * HD, lane);
-  OutW<C, HD> wo;
-  wo.load(a.wo, h, lane);
-  const float bq = lane < HD ? a.bq[h * HD + lane] : 0.f;
+  ProjW<C, ND> wq;
+  wq.load(a.wq, h * HD + w * ND, lane);
+  OutW<C, HD, NM> wo;
+  wo.load(a.wo, h, w * NM, lane);
+  const float bq = lane < ND ? a.bq[h * HD + w * ND + lane] : 0.f;
   float t[PER][H], xv[PER], bo[PER], gm[PER], bt[PER], ps[PER];
 #pragma unroll
   for (int m = 0; m < PER; ++m) {
@@ -343,7 +374,7 @@ __global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, f
     bt[m] = a.beta[n];
     ps[m] = a.pos ? a.pos[n] : 0.f;
   }
-  // x' = x + (sum_h slab_in[h] + b_o), heads in order
+  // x' = x + (sum_h slab_in[h] + b_o), heads in order (every wave: no wait on another)
   float v[PER];
 #pragma unroll
   for (int m = 0; m < PER; ++m) {
@@ -352,7 +383,7 @@ __global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, f
     for (int hh = 0; hh < H; ++hh) s += t[m][hh];
     v[m] = xv[m] + (s + bo[m]);
   }
-  if (h == 0) {
+  if (h == 0 && w == 0) {
 #pragma unroll
     for (int m = 0; m < PER; ++m) a.xo[(long)r * C + lane + 64 * m] = v[m];
   }
@@ -364,14 +395,16 @@ __global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, f
   float q = 0.f;
 #pragma unroll
   for (int m = 0; m < PER; ++m) {
-    const float d = v[m] - mean;
-    q += d * d;
+    const float dd = v[m] - mean;
+    q += dd * dd;
   }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / C + a.eps);
+  if (w == 0) {
 #pragma unroll
-  for (int m = 0; m < PER; ++m) {
-    const float o = (v[m] - mean) * rstd * gm[m] + bt[m];
-    ts[lane + 64 * m] = bfr(a.pos ? o + ps[m] : o);
+    for (int m = 0; m < PER; ++m) {
+      const float o = (v[m] - mean) * rstd * gm[m] + bt[m];
+      ts[lane + 64 * m] = bfr(a.pos ? o + ps[m] : o);
+    }
   }
   __syncthreads();
   bf16x8 act[C / 64];                               // bf16-rounded LN output: exact
@@ -380,17 +413,19 @@ __global__ void __launch_bounds__(64) dec_cross_heads_kernel(CrossHeadsArgs a, f
 #pragma unroll
     for (int m = 0; m < C / 64; ++m) act[m] = to_bf8(ts + 8 * (c + 8 * m));
   }
-  wq.dot(act, lane, qs);
+  wq.dot(act, lane, qs + w * ND);
   __syncthreads();
   float qv = 0.f;
-  if (lane < HD) qv = bfr(bfr(qs[lane] + bq) * scale);
+  if (lane < ND) qv = bfr(bfr(qs[w * ND + lane] + bq) * scale);
   __syncthreads();
-  if (lane < HD) qs[lane] = qv;
+  if (lane < ND) qs[w * ND + lane] = qv;
   __syncthreads();
   at.compute(qs, nullptr, nullptr, lane);
-  at.finish(os, lane);
+  at.publish(mxs, sms, accs, w, lane);
   __syncthreads();
-  wo.apply(os, a.slab_out + ((long)h * a.R + r) * C, lane);
+  merge_heads<HD, NW>(mxs, sms, accs, os, lane);
+  __syncthreads();
+  wo.apply(os, a.slab_out + ((long)h * a.R + r) * C, w * NM, lane);
 }
 
 }  // namespace
@@ -410,12 +445,17 @@ int retr_dec_self_heads(const void* n, const void* npos, int R, int C, int H, co
   const float scale = 1.0f / sqrtf((float)hd);
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(R * H));
-  // all of a wave's key / value loads are issued up front: chunks of 128 (hd 32) or 64 keys
-  const int ch = hd == 32 ? 128 : 64, nch = cdiv(i + 1, ch);
-  RETR_REQUIRE(nch <= 4, "dec_self_heads: %d keys (at most %d)", i + 1, 4 * ch);
-#define SH(CV, HDV, NC) hipLaunchKernelGGL((dec_self_heads_kernel<CV, HDV, NC>), grid, dim3(64), 0, st, a, scale)
-#define SH_N(CV, HDV) \
-  if (nch == 1) SH(CV, HDV, 1); else if (nch == 2) SH(CV, HDV, 2); else SH(CV, HDV, 4);
+  // two waves per (row, head) for up to 128 / 64 keys (hd 32 / 64), else one wave with every
+  // key / value load of up to 4 chunks in flight
+  const int np = 64 / (hd / 8), nk = i + 1;
+#define SH(CV, HDV, NW, NC, KU) \
+  hipLaunchKernelGGL((dec_self_heads_kernel<CV, HDV, NW, NC, KU>), grid, dim3(64 * NW), 0, st, a, scale)
+#define SH_N(CV, HDV)                                           \
+  if (nk <= 2 * np * 4) SH(CV, HDV, 2, 1, 4);                    \
+  else if (nk <= np * 8) SH(CV, HDV, 1, 1, 8);                   \
+  else if (nk <= 2 * np * 8) SH(CV, HDV, 1, 2, 8);               \
+  else SH(CV, HDV, 1, 4, 8);
+  RETR_REQUIRE(nk <= 4 * np * 8, "dec_self_heads: %d keys (at most %d)", nk, 4 * np * 8);
   if (C == 256 && hd == 32) { SH_N(256, 32) }
   else if (C == 256) { SH_N(256, 64) }
   else if (hd == 32) { SH_N(512, 32) }
@@ -440,11 +480,13 @@ int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_i
   const float scale = 1.0f / sqrtf((float)hd);
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(R * H));
-  const int ch = hd == 32 ? 128 : 64, nch = cdiv(Lk, ch);
-  RETR_REQUIRE(nch <= 4, "dec_cross_heads: %d memory keys (at most %d)", Lk, 4 * ch);
-#define XH(CV, HDV, NC) hipLaunchKernelGGL((dec_cross_heads_kernel<CV, HDV, NC>), grid, dim3(64), 0, st, a, scale)
+  // two waves per (row, head), each over up to 2 chunks of 8 keys per lane part
+  const int np = 64 / (hd / 8), per = np * 8;
+#define XH(CV, HDV, NC) \
+  hipLaunchKernelGGL((dec_cross_heads_kernel<CV, HDV, 2, NC, 8>), grid, dim3(128), 0, st, a, scale)
 #define XH_N(CV, HDV) \
-  if (nch == 1) XH(CV, HDV, 1); else if (nch == 2) XH(CV, HDV, 2); else XH(CV, HDV, 4);
+  if (Lk <= 2 * per) XH(CV, HDV, 1); else XH(CV, HDV, 2);
+  RETR_REQUIRE(Lk <= 4 * per, "dec_cross_heads: %d memory keys (at most %d)", Lk, 4 * per);
   if (C == 256 && hd == 32) { XH_N(256, 32) }
   else if (C == 256) { XH_N(256, 64) }
   else if (hd == 32) { XH_N(512, 32) }

@@ -47,7 +47,7 @@ def prepare_tokenizer():
 # False: the round-4 block-per-row kernels (csrc/decode.hip dec_gemm + dec_attn_row)
 DEC_HEADS = True
 # (with DEC_HEADS) the cross-attention residual + LN3 in the FFN kernel's prologue
-DEC_FFN_LN = False
+DEC_FFN_LN = True
 
 
 class _DecodeState:
