@@ -297,7 +297,9 @@ class IncrementalGreedy:
                  ptr(st.hslab2), s)
             x, xa = xa, x
             f0, f2 = ff.sublayer[0], ff.sublayer[2]
-            if DEC_FFN_LN:
+            if DEC_FFN_LN and R <= 64:
+                # (every FFN block re-derives its 16 rows' LayerNorm: beyond 64 rows the
+                # repeated slab reads cost more than the separate launch saves)
                 # cross-attention residual (head partials in order) + LN3 in the FFN's prologue
                 call("retr_dec_ffn_ln", ptr(x), ptr(st.hslab2), H, ptr(csub.out_proj.bias),
                      ptr(ff.norm.weight), ptr(ff.norm.bias), float(ff.norm.eps), ptr(xa), R, C,
