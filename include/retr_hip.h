@@ -174,7 +174,10 @@ enum {
                                    4 16/16, 5 64/16, 6 8/8 (tools/ln_micro.py) */
   RETR_TUNE_UNPACK_GRID = 28,   /* retr_conv_wgrad_unpack_group grid cap (blocks walk the
                                    64-chunk groups): 0 one block per group */
-  RETR_TUNE_COUNT = 29
+  RETR_TUNE_CW_WAVES = 29,      /* retr_conv2d_wgrad_group wave layout of the 128x128 tile (sweeps):
+                                   0 kind 0 (1x1) 4 waves / kind 1 (3x3, strided) 8 waves, 1 both
+                                   4 waves (64x64 per wave), 2 both 8 waves (32x64 per wave) */
+  RETR_TUNE_COUNT = 30
 };
 int retr_tune(int knob, int value);
 
@@ -632,6 +635,15 @@ int retr_dec_attn_row(const void* q, const void* k, const void* v, int R, int C,
 int retr_dec_self_heads(const void* n, const void* npos, int R, int C, int H, const void* win,
                         const float* bin, void* kc, void* vc, int i, int Lmax, const int* anc,
                         const void* wo, float* slab, void* stream);
+/* retr_dec_self_heads with the layer's LN1 in its prologue (xin != NULL; n / npos ignored):
+ * x = xin + (sum_j slabs[j] + b2) (the previous layer's FFN partials [nslab][R][C]), written to
+ * xout, n = bf16(LN1(x)), npos = bf16(LN1(x) + qpos) -- the retr_dec_rows launch between decoder
+ * layers folded in. */
+int retr_dec_self_heads_ln(const void* n, const void* npos, int R, int C, int H, const void* win,
+                           const float* bin, void* kc, void* vc, int i, int Lmax, const int* anc,
+                           const void* wo, float* slab, const float* xin, const float* slabs,
+                           int nslab, const float* b2, const float* gamma, const float* beta,
+                           float eps, const float* qpos, float* xout, void* stream);
 int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_in, float* xo,
                          int R, int C, int H, const float* gamma, const float* beta, float eps,
                          const float* pos, const void* wq, const float* bq, const void* k,
@@ -646,6 +658,11 @@ int retr_dec_ffn_ln(const float* xin, const float* hslab, int nslab, const float
                     const float* gamma, const float* beta, float eps, float* xout, int R, int C,
                     const void* w1, const float* b1, const void* w2, int F, float* slabs,
                     void* stream);
+/* retr_dec_ffn_ln over 64 hidden units per block: slabs [F / 64][R][C] */
+int retr_dec_ffn_ln64(const float* xin, const float* hslab, int nslab, const float* bo,
+                      const float* gamma, const float* beta, float eps, float* xout, int R, int C,
+                      const void* w1, const float* b1, const void* w2, int F, float* slabs,
+                      void* stream);
 
 #ifdef __cplusplus
 }

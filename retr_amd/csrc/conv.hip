@@ -1216,9 +1216,9 @@ static_assert(sizeof(CWProb) == 96 && sizeof(CWHead) == 80 && sizeof(CWPiece) ==
 constexpr int kCWChunk = 4;
 constexpr int kCWMaxSlices = 128;   // per problem (the plan caps the split count at 128)
 
-template <int KIND>
-__global__ void __launch_bounds__(KIND ? 512 : 256) conv_wgrad_group_kernel(const char* __restrict__ table,
-                                                                            int chunk) {
+template <int KIND, int NW>
+__global__ void __launch_bounds__(NW * 64) conv_wgrad_group_kernel(const char* __restrict__ table,
+                                                                   int chunk) {
   const CWHead& h = *(const CWHead*)table;
   const CWProb* P = (const CWProb*)(table + sizeof(CWHead));
   const CWPiece* Q = (const CWPiece*)(table + sizeof(CWHead) + (size_t)h.nprob * sizeof(CWProb));
@@ -1257,17 +1257,18 @@ __global__ void __launch_bounds__(KIND ? 512 : 256) conv_wgrad_group_kernel(cons
   EpiAccF32 ep{d.ws, (long)Ncols, 0, d.vec, 1, nullptr};
   ep.split_stride = (long)R * Ncols;
   ep.split = split;
+  constexpr int WM = NW == 8 ? 4 : 2;
   if constexpr (KIND == 0) {
     const DenseT<bf16> lb{d.x, (long)g.C, Ncols, Mp};
-    gemm2_tile<kFamConvWgrad, 128, 128, 2, 2, 2, 0>(la, lb, ep, R, Ncols, Mp, d.kchunk, d.tiles_n,
-                                                    tile, split);
+    gemm2_tile<kFamConvWgrad, 128, 128, WM, 2, 2, 0>(la, lb, ep, R, Ncols, Mp, d.kchunk,
+                                                     d.tiles_n, tile, split);
   } else {
     constexpr int BK = 64;
     const int qq = BK / g.OW, rr = BK % g.OW;
     const ConvWgradB32<bf16> lb{d.x, g, Ncols, Mp, qq, rr, (qq * g.s * g.W + rr * g.s) * g.C,
                                 g.s * g.W * g.C - g.OW * g.s * g.C, (g.H - g.OH * g.s) * g.W * g.C};
-    gemm2_tile<kFamConvWgrad, 128, 128, 4, 2, 2, 0>(la, lb, ep, R, Ncols, Mp, d.kchunk, d.tiles_n,
-                                                    tile, split);
+    gemm2_tile<kFamConvWgrad, 128, 128, WM, 2, 2, 0>(la, lb, ep, R, Ncols, Mp, d.kchunk,
+                                                     d.tiles_n, tile, split);
   }
 }
 
@@ -1690,22 +1691,19 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
     chunk = chunk > 0 ? chunk : (chunk < 0 ? 0 : kCWChunk);
     const int grid = chunk > 0 ? cdiv(blocks, 8 * chunk) * 8 * chunk : 8 * xmax;
     constexpr size_t lds = gemm2_lds_bytes<128, 128, 2, 0>();
+    const int wl = retr_tune_get(RETR_TUNE_CW_WAVES);
+    const int nw = wl == 1 ? 4 : wl == 2 ? 8 : (kind == 0 ? 4 : 8);
+    auto launch = [&](auto kern, int threads) {
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, st, (const char*)table, chunk);
+    };
     if (kind == 0) {
-      auto kern = conv_wgrad_group_kernel<0>;
-      static bool attr0 = false;
-      if (lds > 65536 && !attr0) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr0 = true;
-      }
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, (const char*)table, chunk);
+      if (nw == 4) launch(conv_wgrad_group_kernel<0, 4>, 256);
+      else launch(conv_wgrad_group_kernel<0, 8>, 512);
     } else {
-      auto kern = conv_wgrad_group_kernel<1>;
-      static bool attr1 = false;
-      if (lds > 65536 && !attr1) {
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        attr1 = true;
-      }
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, (const char*)table, chunk);
+      if (nw == 4) launch(conv_wgrad_group_kernel<1, 4>, 256);
+      else launch(conv_wgrad_group_kernel<1, 8>, 512);
     }
     if (int e = retr_check_launch(kind == 0 ? "conv2d_wgrad_group 1x1" : "conv2d_wgrad_group")) return e;
     // the next kind's table must not overwrite this one before the launch has read it: use

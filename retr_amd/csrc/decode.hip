@@ -821,23 +821,25 @@ dec_ffn_kernel(const bf16* n3, int R, const bf16* w1, const float* b1, const bf1
 // n3 = bf16(LN3(x)) into LDS; waves 0 / 1 then the FFN1 column tile w (16 hidden units), and every
 // wave 4 of the 16 FFN2 column tiles -- instead of a retr_dec_rows launch between the per-head
 // cross-attention partials (csrc/decode_heads.hip) and the FFN.
-template <int PER, int MAXS>
+template <int PER, int MAXS, int HB>
 __global__ void __launch_bounds__(256)
 dec_ffn_ln_kernel(const float* xin, const float* hslab, int nslab, const float* bo,
                   const float* gamma, const float* beta, float eps, float* xout, int R,
                   const bf16* w1, const float* b1, const bf16* w2, int F, float* slabs) {
   constexpr int C = PER * 64;
-  constexpr int HS = 32 + 8, AS = C + 8;
+  constexpr int HS = HB + 8, AS = C + 8;
   constexpr int CPL = C / 64;                     // consecutive columns per lane
   constexpr int NT = C / 16, NTW = NT / 4;        // FFN2 column tiles, per wave
+  constexpr int T1 = HB / 16;                     // FFN1 column tiles (waves 0 .. T1-1)
+  constexpr int K2 = HB / 32;                     // FFN2 K-steps
   typedef __attribute__((ext_vector_type(4))) float f4v;
-  __shared__ __attribute__((aligned(16))) bf16 Hs[16 * HS];     // relu(h) [16 rows][32 units]
+  __shared__ __attribute__((aligned(16))) bf16 Hs[16 * HS];     // relu(h) [16 rows][HB units]
   __shared__ __attribute__((aligned(16))) bf16 As[16 * AS];     // LN3 rows [16][C]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j0 = blockIdx.x * 32, r0 = blockIdx.y * 16;
-  // weights first: FFN1 column tile w (waves 0, 1), FFN2 column tiles 4w .. 4w + 3
-  u32x4 w1f[C / 32], w2f[NTW];
-  if (w < 2) {
+  const int j0 = blockIdx.x * HB, r0 = blockIdx.y * 16;
+  // weights first: FFN1 column tile w (waves 0 .. T1-1), FFN2 column tiles 4w .. 4w + 3
+  u32x4 w1f[C / 32], w2f[NTW][K2];
+  if (w < T1) {
 #pragma unroll
     for (int ks = 0; ks < C / 32; ++ks)
       w1f[ks] = *(const u32x4*)(w1 + (long)(j0 + 16 * w + (lane & 15)) * C + 32 * ks +
@@ -845,9 +847,11 @@ dec_ffn_ln_kernel(const float* xin, const float* hslab, int nslab, const float* 
   }
 #pragma unroll
   for (int t = 0; t < NTW; ++t)
-    w2f[t] = *(const u32x4*)(w2 + (long)(16 * (NTW * w + t) + (lane & 15)) * F + j0 +
-                             8 * (lane >> 4));
-  const float b1v = w < 2 ? b1[j0 + 16 * w + (lane & 15)] : 0.f;
+#pragma unroll
+    for (int k2 = 0; k2 < K2; ++k2)
+      w2f[t][k2] = *(const u32x4*)(w2 + (long)(16 * (NTW * w + t) + (lane & 15)) * F + j0 +
+                                   32 * k2 + 8 * (lane >> 4));
+  const float b1v = w < T1 ? b1[j0 + 16 * w + (lane & 15)] : 0.f;
   const long RC = (long)R * C;
   const int c0 = CPL * lane;
   float bb[CPL], gm[CPL], bt[CPL];
@@ -904,7 +908,7 @@ dec_ffn_ln_kernel(const float* xin, const float* hslab, int nslab, const float* 
     }
   }
   __syncthreads();
-  if (w < 2) {
+  if (w < T1) {
     f4 h = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < C / 32; ++ks) {
@@ -917,12 +921,17 @@ dec_ffn_ln_kernel(const float* xin, const float* hslab, int nslab, const float* 
       Hs[(4 * (lane >> 4) + e) * HS + jj] = (bf16)fmaxf(h[e] + b1v, 0.f);
   }
   __syncthreads();
-  const u32x4 a0 = *(const u32x4*)(Hs + (lane & 15) * HS + 8 * (lane >> 4));
+  u32x4 a0[K2];
+#pragma unroll
+  for (int k2 = 0; k2 < K2; ++k2)
+    a0[k2] = *(const u32x4*)(Hs + (lane & 15) * HS + 32 * k2 + 8 * (lane >> 4));
   float* slab = slabs + (long)blockIdx.x * R * C;
 #pragma unroll
   for (int t2 = 0; t2 < NTW; ++t2) {
     const int n = 16 * (NTW * w + t2) + (lane & 15);
-    const f4 acc = mfma16(a0, w2f[t2], f4{0.f, 0.f, 0.f, 0.f});
+    f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k2 = 0; k2 < K2; ++k2) acc = mfma16(a0[k2], w2f[t2][k2], acc);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int r = r0 + 4 * (lane >> 4) + e;
@@ -1055,13 +1064,31 @@ int retr_dec_ffn_ln(const float* xin, const float* hslab, int nslab, const float
   if (R == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(F / 32, cdiv(R, 16));
-#define FL(P, MS) hipLaunchKernelGGL((dec_ffn_ln_kernel<P, MS>), grid, dim3(256), 0, st, xin, hslab, \
-                                     nslab, bo, gamma, beta, eps, xout, R, (const bf16*)w1, b1,    \
-                                     (const bf16*)w2, F, slabs)
+#define FL(P, MS) hipLaunchKernelGGL((dec_ffn_ln_kernel<P, MS, 32>), grid, dim3(256), 0, st, xin, \
+                                     hslab, nslab, bo, gamma, beta, eps, xout, R,                  \
+                                     (const bf16*)w1, b1, (const bf16*)w2, F, slabs)
   if (C == 256) { if (nslab <= 8) FL(4, 8); else FL(4, 16); }
   else { if (nslab <= 8) FL(8, 8); else FL(8, 16); }
 #undef FL
   return retr_check_launch("dec_ffn_ln");
+}
+
+int retr_dec_ffn_ln64(const float* xin, const float* hslab, int nslab, const float* bo,
+                      const float* gamma, const float* beta, float eps, float* xout, int R, int C,
+                      const void* w1, const float* b1, const void* w2, int F, float* slabs,
+                      void* stream) {
+  RETR_REQUIRE((C == 256 || C == 512) && F % 64 == 0 && nslab >= 0 && nslab <= 16,
+               "dec_ffn_ln64: C=%d F=%d nslab=%d (<= 16)", C, F, nslab);
+  if (R == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(F / 64, cdiv(R, 16));
+#define FL(P, MS) hipLaunchKernelGGL((dec_ffn_ln_kernel<P, MS, 64>), grid, dim3(256), 0, st, xin, \
+                                     hslab, nslab, bo, gamma, beta, eps, xout, R,                  \
+                                     (const bf16*)w1, b1, (const bf16*)w2, F, slabs)
+  if (C == 256) { if (nslab <= 8) FL(4, 8); else FL(4, 16); }
+  else { if (nslab <= 8) FL(8, 8); else FL(8, 16); }
+#undef FL
+  return retr_check_launch("dec_ffn_ln64");
 }
 
 #ifdef RETR_DEC_TIMING

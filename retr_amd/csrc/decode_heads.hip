@@ -250,6 +250,18 @@ struct SelfHeadsArgs {
   const bf16* wo;       // [C][C]
   float* slab;          // [H][R][C]
   int R;
+  // LN1 prologue (xin != null; n / npos unused): x = xin + (sum_j slabs[j] + b2) (the previous
+  // layer's FFN partials [nslab][R][C]) -> xout (block h = 0), n = bf16(LN1(x)), npos =
+  // bf16(LN1(x) + qpos) -- instead of a retr_dec_rows launch between the layers
+  const float* xin;
+  const float* slabs;
+  int nslab;
+  const float* b2;
+  const float* gamma;
+  const float* beta;
+  float eps;
+  const float* qpos;
+  float* xout;
 };
 
 // One block of NW waves per (row, head): wave w computes rows [w HD / NW, (w + 1) HD / NW) of
@@ -259,17 +271,49 @@ template <int C, int HD, int NW, int NCH, int KU>
 __global__ void __launch_bounds__(64 * NW) dec_self_heads_kernel(SelfHeadsArgs a, float scale) {
   constexpr int H = C / HD, ND = HD / NW, NM = C / 64 / NW;
   constexpr int KPW = NCH * (64 / (HD / 8)) * KU;  // keys per wave
+  constexpr int CPL = C / 64;
+  typedef __attribute__((ext_vector_type(4))) float f4v;
   __shared__ float qs[HD], ks[HD], vs[HD], os[HD];
   __shared__ float mxs[NW], sms[NW], accs[NW * HD];
+  __shared__ __attribute__((aligned(16))) float part[NW][C];   // LN1 prologue slab partials
+  __shared__ __attribute__((aligned(16))) bf16 lnb[2][C];      // LN1 prologue n / npos
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = blockIdx.x / H, h = blockIdx.x % H;
   const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
   const int i = a.i, Lmax = a.Lmax;
-  // every global load first: activations, this wave's q|k|v and out-projection weight rows,
-  // its cached keys / values of positions < i (one dependent memory round trip per launch)
+  const bool pro = a.xin != nullptr;
+  // every global load first (one dependent memory round trip per launch): the LN1 prologue's
+  // slab share (wave w: slabs [w S / NW, (w + 1) S / NW)), activations, this wave's q|k|v and
+  // out-projection weight rows, its cached keys / values of positions < i
+  const int c0 = CPL * lane;
+  float ps[CPL];
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) ps[e] = 0.f;
+  if (pro) {
+    const long RC = (long)a.R * C;
+    const int s0 = w * a.nslab / NW, s1 = (w + 1) * a.nslab / NW;
+    for (int j = s0; j < s1; j += 8) {
+      f4v t[8][CPL / 4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int e = 0; e < CPL / 4; ++e)
+          t[u][e] = j + u < s1 ? *(const f4v*)(a.slabs + (j + u) * RC + (long)r * C + c0 + 4 * e)
+                               : f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int e = 0; e < CPL / 4; ++e)
+#pragma unroll
+          for (int f = 0; f < 4; ++f)
+            if (j + u < s1) ps[4 * e + f] += t[u][e][f];
+    }
+  }
   bf16x8 actp[C / 64], actn[C / 64];
-  load_act<C>(a.npos + (long)r * C, lane, actp);
-  load_act<C>(a.n + (long)r * C, lane, actn);
+  if (!pro) {
+    load_act<C>(a.npos + (long)r * C, lane, actp);
+    load_act<C>(a.n + (long)r * C, lane, actn);
+  }
   ProjW<C, ND> wq, wk, wv;
   wq.load(a.win, h * HD + w * ND, lane);
   wk.load(a.win, C + h * HD + w * ND, lane);
@@ -287,6 +331,57 @@ __global__ void __launch_bounds__(64 * NW) dec_self_heads_kernel(SelfHeadsArgs a
   const float bq = lane < ND ? a.bin[h * HD + d] : 0.f;
   const float bk = lane < ND ? a.bin[C + h * HD + d] : 0.f;
   const float bv = lane < ND ? a.bin[2 * C + h * HD + d] : 0.f;
+  if (pro) {
+    // x = xin + (slab partials in wave order + b2); LN1 (+ qpos) -> LDS (bf16)
+    float xv[CPL], b2[CPL], gm[CPL], bt[CPL], qp[CPL];
+#pragma unroll
+    for (int e = 0; e < CPL; e += 4) {
+      *(f4v*)(xv + e) = *(const f4v*)(a.xin + (long)r * C + c0 + e);
+      *(f4v*)(b2 + e) = *(const f4v*)(a.b2 + c0 + e);
+      *(f4v*)(gm + e) = *(const f4v*)(a.gamma + c0 + e);
+      *(f4v*)(bt + e) = *(const f4v*)(a.beta + c0 + e);
+      *(f4v*)(qp + e) = *(const f4v*)(a.qpos + c0 + e);
+    }
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) part[w][c0 + e] = ps[e];
+    __syncthreads();
+    float v[CPL], sm = 0.f;
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+      float t = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) t += part[ww][c0 + e];
+      v[e] = xv[e] + (t + b2[e]);
+      sm += v[e];
+    }
+    if (h == 0 && w == 0) {
+#pragma unroll
+      for (int e = 0; e < CPL; e += 4) *(f4v*)(a.xout + (long)r * C + c0 + e) = *(f4v*)(v + e);
+    }
+    const float mean = wave_sum(sm) / C;
+    float q2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+      const float dd = v[e] - mean;
+      q2 += dd * dd;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q2) / C + a.eps);
+    if (w == 0) {
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) {
+        const float o = (v[e] - mean) * rstd * gm[e] + bt[e];
+        lnb[0][c0 + e] = (bf16)o;
+        lnb[1][c0 + e] = (bf16)(o + qp[e]);
+      }
+    }
+    __syncthreads();
+    const int c = lane & 7;
+#pragma unroll
+    for (int m = 0; m < C / 64; ++m) {
+      actn[m] = *(const bf16x8*)(&lnb[0][8 * (c + 8 * m)]);
+      actp[m] = *(const bf16x8*)(&lnb[1][8 * (c + 8 * m)]);
+    }
+  }
   wq.dot(actp, lane, qs + w * ND);
   wk.dot(actp, lane, ks + w * ND);
   wv.dot(actn, lane, vs + w * ND);
@@ -435,13 +530,26 @@ extern "C" {
 int retr_dec_self_heads(const void* n, const void* npos, int R, int C, int H, const void* win,
                         const float* bin, void* kc, void* vc, int i, int Lmax, const int* anc,
                         const void* wo, float* slab, void* stream) {
+  return retr_dec_self_heads_ln(n, npos, R, C, H, win, bin, kc, vc, i, Lmax, anc, wo, slab,
+                                nullptr, nullptr, 0, nullptr, nullptr, nullptr, 0.f, nullptr,
+                                nullptr, stream);
+}
+
+int retr_dec_self_heads_ln(const void* n, const void* npos, int R, int C, int H, const void* win,
+                           const float* bin, void* kc, void* vc, int i, int Lmax, const int* anc,
+                           const void* wo, float* slab, const float* xin, const float* slabs,
+                           int nslab, const float* b2, const float* gamma, const float* beta,
+                           float eps, const float* qpos, float* xout, void* stream) {
+  RETR_REQUIRE(xin == nullptr || (slabs && b2 && gamma && beta && qpos && xout && nslab >= 0),
+               "dec_self_heads_ln: incomplete LayerNorm prologue operands");
   const int hd = H > 0 ? C / H : 0;
   RETR_REQUIRE((C == 256 || C == 512) && (hd == 32 || hd == 64) && hd * H == C,
                "dec_self_heads: C=%d H=%d unsupported", C, H);
   RETR_REQUIRE(i >= 0 && i < Lmax, "dec_self_heads: step %d outside the %d-row cache", i, Lmax);
   if (R == 0) return 0;
   SelfHeadsArgs a{(const bf16*)n, (const bf16*)npos, (const bf16*)win, bin, (bf16*)kc,
-                  (bf16*)vc, i, Lmax, anc, (const bf16*)wo, slab, R};
+                  (bf16*)vc, i, Lmax, anc, (const bf16*)wo, slab, R, xin, slabs, nslab, b2,
+                  gamma, beta, eps, qpos, xout};
   const float scale = 1.0f / sqrtf((float)hd);
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(R * H));

@@ -48,6 +48,8 @@ def prepare_tokenizer():
 DEC_HEADS = True
 # (with DEC_HEADS) the cross-attention residual + LN3 in the FFN kernel's prologue
 DEC_FFN_LN = True
+# (with DEC_FFN_LN) the FFN residual + the next layer's LN1 in the self-attention prologue
+DEC_FOLD_ROWS = True
 
 
 class _DecodeState:
@@ -284,23 +286,46 @@ class IncrementalGreedy:
              ptr(n0.weight), ptr(n0.bias), float(n0.eps), ptr(st.n), ptr(st.npos), s)
         anc = ptr(st.anc) if self.beam else None
         nslab = F // 32
+        # three launches per layer (up to 64 rows): the FFN residual + next LN1 in the next
+        # layer's self-attention prologue, the cross residual + LN3 in the FFN prologue
+        fold = DEC_FFN_LN and DEC_FOLD_ROWS and R <= 64 and F % 64 == 0
         for li, layer in enumerate(layers):
             sa, ca, ff = layer.tgt_self_attn, layer.tgt_src_cross_attn, layer.ff
             sub, csub = sa.sublayer, ca.sublayer
-            call("retr_dec_self_heads", ptr(st.n), ptr(st.npos), R, C, H,
-                 ptr(W(sub.in_proj_weight)), ptr(sub.in_proj_bias), ptr(st.kc[li]),
-                 ptr(st.vc[li]), i, T, anc, ptr(W(sub.out_proj.weight)), ptr(st.hslab), s)
+            f0, f2 = ff.sublayer[0], ff.sublayer[2]
+            if fold and li > 0:
+                pf2 = layers[li - 1].ff.sublayer[2]
+                call("retr_dec_self_heads_ln", None, None, R, C, H,
+                     ptr(W(sub.in_proj_weight)), ptr(sub.in_proj_bias), ptr(st.kc[li]),
+                     ptr(st.vc[li]), i, T, anc, ptr(W(sub.out_proj.weight)), ptr(st.hslab),
+                     ptr(x), ptr(st.slabs), F // 64, ptr(pf2.bias), ptr(sa.norm.weight),
+                     ptr(sa.norm.bias), float(sa.norm.eps), ptr(qp), ptr(xa), s)
+                x, xa = xa, x
+            else:
+                call("retr_dec_self_heads", ptr(st.n), ptr(st.npos), R, C, H,
+                     ptr(W(sub.in_proj_weight)), ptr(sub.in_proj_bias), ptr(st.kc[li]),
+                     ptr(st.vc[li]), i, T, anc, ptr(W(sub.out_proj.weight)), ptr(st.hslab), s)
             call("retr_dec_cross_heads", ptr(st.hslab), ptr(x), ptr(sub.out_proj.bias), ptr(xa),
                  R, C, H, ptr(ca.norm.weight), ptr(ca.norm.bias), float(ca.norm.eps), ptr(qp),
                  ptr(W(csub.in_proj_weight)), ptr(csub.in_proj_bias), ptr(st.kx[li]),
                  ptr(st.vx[li]), S, st.K, ptr(st.kpm), ptr(W(csub.out_proj.weight)),
                  ptr(st.hslab2), s)
             x, xa = xa, x
-            f0, f2 = ff.sublayer[0], ff.sublayer[2]
+            if fold:
+                call("retr_dec_ffn_ln64", ptr(x), ptr(st.hslab2), H, ptr(csub.out_proj.bias),
+                     ptr(ff.norm.weight), ptr(ff.norm.bias), float(ff.norm.eps), ptr(xa), R, C,
+                     ptr(W(f0.weight)), ptr(f0.bias), ptr(W(f2.weight)), F, ptr(st.slabs), s)
+                x, xa = xa, x
+                if li + 1 == len(layers):
+                    nx = tr.decoder.norm
+                    call("retr_dec_rows", ptr(x), ptr(st.slabs), F // 64, ptr(f2.bias), R, C,
+                         ptr(xa), ptr(nx.weight), ptr(nx.bias), float(nx.eps), None, ptr(st.n),
+                         None, s)
+                    x, xa = xa, x
+                continue
             if DEC_FFN_LN and R <= 64:
                 # (every FFN block re-derives its 16 rows' LayerNorm: beyond 64 rows the
                 # repeated slab reads cost more than the separate launch saves)
-                # cross-attention residual (head partials in order) + LN3 in the FFN's prologue
                 call("retr_dec_ffn_ln", ptr(x), ptr(st.hslab2), H, ptr(csub.out_proj.bias),
                      ptr(ff.norm.weight), ptr(ff.norm.bias), float(ff.norm.eps), ptr(xa), R, C,
                      ptr(W(f0.weight)), ptr(f0.bias), ptr(W(f2.weight)), F, ptr(st.slabs), s)

@@ -410,3 +410,80 @@ def test_dec_ffn_ln_matches_rows_then_ffn(R):
          C, ptr(w1), ptr(b1), ptr(w2), Fh, ptr(s1), st)
     assert torch.equal(xo0, xo1)
     assert _rel(s1, s0) < 1e-2
+
+
+def test_dec_self_heads_ln_matches_rows_then_heads():
+    """retr_dec_self_heads_ln (the previous layer's FFN partials + residual + LN1 (+qpos) in the
+    self-attention prologue) against retr_dec_rows followed by retr_dec_self_heads: the
+    residual, the cache row and the head partials within fp32 reassociation / bf16 rounding."""
+    C, H, R, T, i, ns = 256, 8, 64, 16, 5, 32
+    g = _g(99)
+    bf = lambda t: t.to(DEV).bfloat16()                       # noqa: E731
+    x = torch.randn(R, C, generator=g).to(DEV)
+    slabs = torch.randn(ns, R, C, generator=g).to(DEV) * 0.1
+    b2 = torch.randn(C, generator=g).to(DEV) * 0.1
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV) * 0.1
+    qp = torch.randn(C, generator=g).to(DEV)
+    win = bf(torch.randn(3 * C, C, generator=g) / math.sqrt(C))
+    bin_ = torch.randn(3 * C, generator=g).to(DEV) * 0.1
+    wo = bf(torch.randn(C, C, generator=g) / math.sqrt(C))
+    kc0 = bf(torch.randn(R * T, C, generator=g))
+    vc0 = bf(torch.randn(R * T, C, generator=g))
+    st = ops._st()
+    # reference: rows then heads
+    x1 = torch.empty(R, C, device=DEV)
+    n = torch.empty(R, C, dtype=torch.bfloat16, device=DEV)
+    npos = torch.empty_like(n)
+    call("retr_dec_rows", ptr(x), ptr(slabs), ns, ptr(b2), R, C, ptr(x1), ptr(gamma), ptr(beta),
+         1e-5, ptr(qp), ptr(n), ptr(npos), st)
+    kc1, vc1 = kc0.clone(), vc0.clone()
+    s1 = torch.empty(H, R, C, device=DEV)
+    call("retr_dec_self_heads", ptr(n), ptr(npos), R, C, H, ptr(win), ptr(bin_), ptr(kc1),
+         ptr(vc1), i, T, None, ptr(wo), ptr(s1), st)
+    # fused prologue
+    x2 = torch.empty(R, C, device=DEV)
+    kc2, vc2 = kc0.clone(), vc0.clone()
+    s2 = torch.empty(H, R, C, device=DEV)
+    call("retr_dec_self_heads_ln", None, None, R, C, H, ptr(win), ptr(bin_), ptr(kc2), ptr(vc2), i,
+         T, None, ptr(wo), ptr(s2), ptr(x), ptr(slabs), ns, ptr(b2), ptr(gamma), ptr(beta), 1e-5,
+         ptr(qp), ptr(x2), st)
+    assert _rel(x2, x1) < 1e-6
+    assert _rel(kc2.float(), kc1.float()) < 1e-2 and _rel(vc2.float(), vc1.float()) < 1e-2
+    assert _rel(s2, s1) < 2e-2
+
+
+@pytest.mark.parametrize("fold", [False, True])
+def test_dec_fold_rows_step_matches(fold):
+    """The three-launch decoder layer (DEC_FOLD_ROWS: FFN residual + next LN1 in the self prologue,
+    cross residual + LN3 in the FFN prologue, 64 hidden units per FFN block) against the
+    five-launch one on the cfg5 model: first-step logits within bf16 rounding, graphs == eager."""
+    from bench import build, cfg5
+    from retr_amd.eval_utils import decode as dec
+    from retr_amd.synthetic import synthetic_images
+    model, _ = build(cfg5(), DEV)
+    model.eval()
+    B, T = 16, 128
+    img, mask = synthetic_images(B, 224, seed=13, pad_band=True)
+    s = NestedTensor(img.to(DEV), mask.to(DEV))
+    old = (dec.DEC_HEADS, dec.DEC_FFN_LN, dec.DEC_FOLD_ROWS)
+    res = []
+    try:
+        for f in (fold, False):
+            dec.DEC_HEADS, dec.DEC_FFN_LN, dec.DEC_FOLD_ROWS = True, True, f
+            model._retr_decode_states = {}
+            gr = dec.IncrementalGreedy(model)
+            ids = gr(s, T, 101, 102)
+            st = next(v for k, v in model._retr_decode_states.items() if k[0] == "IncrementalGreedy")
+            with torch.no_grad():
+                gr._reset(st, 101)
+                gr._step(st, 0, 102)
+                torch.cuda.synchronize()
+                res.append(st.logits.float().clone())
+            if f:
+                ids_e = dec.IncrementalGreedy(model, use_graphs=False)(s, T, 101, 102)
+                assert torch.equal(ids, ids_e)
+    finally:
+        dec.DEC_HEADS, dec.DEC_FFN_LN, dec.DEC_FOLD_ROWS = old
+        model._retr_decode_states = {}
+    assert _rel(res[0], res[1]) < 2e-2

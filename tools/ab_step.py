@@ -85,6 +85,8 @@ VARIANTS = {
     "cw_aff": {("TUNE", 20): -1},
     "wb_aff": {("TUNE", 19): -1},
     "orders_aff": {("TUNE", 19): -1, ("TUNE", 20): -1},
+    "cw_w4": {("TUNE", 29): 1},
+    "cw_w8": {("TUNE", 29): 2},
 }
 
 
@@ -105,7 +107,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26, 27, 28):
+    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--beam", type=int, default=1)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--fold", type=int, default=None,
+                    help="1 / 0: eval_utils.decode.DEC_FOLD_ROWS (default: the module's)")
     ap.add_argument("--ffn-ln", type=int, default=None,
                     help="1 / 0: eval_utils.decode.DEC_FFN_LN (default: the module's)")
     ap.add_argument("--block-per-row", action="store_true",
@@ -31,6 +33,8 @@ def main():
     dec.DEC_HEADS = not a.block_per_row
     if a.ffn_ln is not None:
         dec.DEC_FFN_LN = bool(a.ffn_ln)
+    if a.fold is not None:
+        dec.DEC_FOLD_ROWS = bool(a.fold)
     model, _ = build(cfg5(), "cuda")
     model.eval()
     img, mask = synthetic_images(a.batch, 224, seed=3000)
