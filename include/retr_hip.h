@@ -649,6 +649,20 @@ int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_i
                          const float* pos, const void* wq, const float* bq, const void* k,
                          const void* v, int Lk, int kv_group, const unsigned char* kpm,
                          const void* wo, float* slab_out, void* stream);
+/* Multi-row variants (beam search): rb rows x one head per block, the head's weight slices (and
+ * the memory keys / values when kv_group % rb == 0) staged in LDS once per block.  Same operands
+ * and results as retr_dec_self_heads_ln / retr_dec_cross_heads; C = 256, H = 8, rb in {1, 2, 4,
+ * 5} (1 = the per-(row, head) kernels), R % rb == 0, at most 128 self / 256 memory keys. */
+int retr_dec_self_heads_mr(const void* n, const void* npos, int R, int C, int H, const void* win,
+                           const float* bin, void* kc, void* vc, int i, int Lmax, const int* anc,
+                           const void* wo, float* slab, const float* xin, const float* slabs,
+                           int nslab, const float* b2, const float* gamma, const float* beta,
+                           float eps, const float* qpos, float* xout, int rb, void* stream);
+int retr_dec_cross_heads_mr(const float* slab_in, const float* x, const float* bo_in, float* xo,
+                            int R, int C, int H, const float* gamma, const float* beta, float eps,
+                            const float* pos, const void* wq, const float* bq, const void* k,
+                            const void* v, int Lk, int kv_group, const unsigned char* kpm,
+                            const void* wo, float* slab_out, int rb, void* stream);
 int retr_dec_ffn(const void* n3, int R, int C, const void* w1, const float* b1, const void* w2,
                  int F, float* slabs, void* stream);
 /* retr_dec_ffn with its input LayerNorm in the prologue: per row x = xin + (sum_j hslab[j] + bo)

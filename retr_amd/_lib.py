@@ -212,6 +212,10 @@ _SIGS = {
     "retr_dec_self_heads": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P],
     "retr_dec_cross_heads": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I,
                              _P, _P, _P, _P],
+    "retr_dec_self_heads_mr": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _I,
+                               _P, _P, _P, _F, _P, _P, _I, _P],
+    "retr_dec_cross_heads_mr": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I,
+                                _P, _P, _P, _I, _P],
     "retr_adamw_sumsq": [_P, _L, _P, _I, _P, _P],
     "retr_adamw_update": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P, _P],
     "retr_adamw_update2": [_P, _P, _P, _P, _L, _P, _D, _D, _F, _P, _F, _P, _I, _F, _P, _I, _P],

@@ -182,13 +182,13 @@ template <int C, int ND>
 struct ProjW {
   static constexpr int CPL = C / 64;
   bf16x8 w[ND / 8][CPL];
-  RETR_DEVICE void load(const bf16* __restrict__ W, int row0, int lane) {
+  RETR_DEVICE void load(const bf16* __restrict__ W, int row0, int lane, int ld = C) {
     const int rg = lane >> 3, c = lane & 7;
 #pragma unroll
     for (int it = 0; it < ND / 8; ++it)
 #pragma unroll
       for (int m = 0; m < CPL; ++m)
-        w[it][m] = *(const bf16x8*)(W + (long)(row0 + 8 * it + rg) * C + 8 * (c + 8 * m));
+        w[it][m] = *(const bf16x8*)(W + (long)(row0 + 8 * it + rg) * ld + 8 * (c + 8 * m));
   }
   // out[d] (LDS) = sum_k W[row0 + d][k] act[k]  (one dot8 per chunk, chunks summed pairwise)
   RETR_DEVICE void dot(const bf16x8 (&act)[CPL], int lane, float* out) const {
@@ -212,12 +212,12 @@ struct ProjW {
 template <int C, int HD, int NM>
 struct OutW {
   bf16x8 w[NM][HD / 8];
-  RETR_DEVICE void load(const bf16* __restrict__ Wo, int h, int m0, int lane) {
+  RETR_DEVICE void load(const bf16* __restrict__ Wo, int h, int m0, int lane, int ld = C) {
 #pragma unroll
     for (int m = 0; m < NM; ++m)
 #pragma unroll
       for (int t = 0; t < HD / 8; ++t)
-        w[m][t] = *(const bf16x8*)(Wo + (long)(lane + 64 * (m0 + m)) * C + h * HD + 8 * t);
+        w[m][t] = *(const bf16x8*)(Wo + (long)(lane + 64 * (m0 + m)) * ld + h * HD + 8 * t);
   }
   // slab[n] = sum_{d < HD} o[d] Wo[n][h HD + d]
   RETR_DEVICE void apply(const float* os, float* slab, int m0, int lane) const {
@@ -523,6 +523,307 @@ __global__ void __launch_bounds__(64 * NW) dec_cross_heads_kernel(CrossHeadsArgs
   wo.apply(os, a.slab_out + ((long)h * a.R + r) * C, w * NM, lane);
 }
 
+// ---- multi-row blocks (beam search: the K beams of an image share every weight slice and, in
+// the cross sub-layer, the memory keys / values) -----------------------------------------------
+// A block = RB consecutive rows x one head, two waves per row (the layout of the kernels above).
+// The head's weight slices (and, with KVS, the memory K / V of the rows' image) are staged in LDS
+// once per block instead of once per (row, head): at beam 5 (R = 320) the per-(row, head) blocks
+// moved ~80 KB (self) / ~66 KB (cross) each through their CU, ~170 MB per launch.  C = 256,
+// head dim 32.
+constexpr int MR_C = 256, MR_HD = 32, MR_H = MR_C / MR_HD;
+constexpr int MR_WLD = MR_C + 8;                  // staged projection rows (bank offset 16 B)
+constexpr int MR_OLD = MR_HD + 8;                 // staged out-projection rows (80 B)
+
+// rows [row0, row0 + nrows) x [col0, col0 + ncols) of a bf16 matrix (ld elements) staged into LDS
+// rows of dld elements, 16-byte chunks over the block's NT threads: load() issues every chunk
+// (at most N per thread) before store() writes any, so the staging costs one memory round trip
+template <int N, int NT>
+struct Stager {
+  bf16x8 t[N];
+  int cpr, total;
+  RETR_DEVICE void load(const bf16* __restrict__ src, long ld, int row0, int col0, int nrows,
+                        int ncols, int tid) {
+    cpr = ncols / 8;
+    total = nrows * cpr;
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+      const int q = tid + it * NT, rr = q / cpr, cc = q - rr * cpr;
+      if (q < total) t[it] = *(const bf16x8*)(src + (long)(row0 + rr) * ld + col0 + 8 * cc);
+    }
+  }
+  RETR_DEVICE void store(bf16* dst, int dld, int tid) const {
+#pragma unroll
+    for (int it = 0; it < N; ++it) {
+      const int q = tid + it * NT, rr = q / cpr, cc = q - rr * cpr;
+      if (q < total) *(bf16x8*)(dst + rr * dld + 8 * cc) = t[it];
+    }
+  }
+};
+
+template <int RB>
+__global__ void __launch_bounds__(128 * RB) dec_self_heads_mr_kernel(SelfHeadsArgs a, float scale) {
+  constexpr int C = MR_C, HD = MR_HD, H = MR_H, NW = 2, ND = HD / NW, NM = C / 64 / NW;
+  constexpr int CPL = C / 64;
+  constexpr int KPW = (64 / (HD / 8)) * 4;        // keys per wave (2 x 64 = 128)
+  typedef __attribute__((ext_vector_type(4))) float f4v;
+  __shared__ __attribute__((aligned(16))) bf16 wi_s[3 * HD * MR_WLD];
+  __shared__ __attribute__((aligned(16))) bf16 wo_s[C * MR_OLD];
+  __shared__ float qs[RB][HD], ks[RB][HD], vs[RB][HD], os[RB][HD];
+  __shared__ float mxs[RB][NW], sms[RB][NW], accs[RB][NW * HD];
+  __shared__ __attribute__((aligned(16))) float part[RB][NW][C];
+  __shared__ __attribute__((aligned(16))) bf16 lnb[RB][2][C];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, rr = wv >> 1, w = wv & 1;
+  const int g = blockIdx.x / H, h = blockIdx.x % H;
+  const int r = g * RB + rr;
+  const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
+  const int i = a.i, Lmax = a.Lmax;
+  const bool pro = a.xin != nullptr;
+  const int c0 = CPL * lane;
+  constexpr int NT = 128 * RB;
+  // the head's q | k | v rows and out-projection columns, staged once per block
+  Stager<(HD * C / 8 + NT - 1) / NT, NT> sq, sk, sv;
+  Stager<(C * HD / 8 + NT - 1) / NT, NT> so;
+  sq.load(a.win, C, h * HD, 0, HD, C, tid);
+  sk.load(a.win, C, C + h * HD, 0, HD, C, tid);
+  sv.load(a.win, C, 2 * C + h * HD, 0, HD, C, tid);
+  so.load(a.wo, C, 0, h * HD, C, HD, tid);
+  // the row's own operands: prologue slab share, activations, cached keys / values
+  float ps[CPL];
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) ps[e] = 0.f;
+  if (pro) {
+    const long RC = (long)a.R * C;
+    const int s0 = w * a.nslab / NW, s1 = (w + 1) * a.nslab / NW;
+    for (int j = s0; j < s1; j += 8) {
+      f4v t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        t[u] = j + u < s1 ? *(const f4v*)(a.slabs + (j + u) * RC + (long)r * C + c0)
+                          : f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+          if (j + u < s1) ps[f] += t[u][f];
+    }
+  }
+  bf16x8 actp[C / 64], actn[C / 64];
+  if (!pro) {
+    load_act<C>(a.npos + (long)r * C, lane, actp);
+    load_act<C>(a.n + (long)r * C, lane, actn);
+  }
+  WaveAttn<HD, 1, 4> at;
+  at.template load<C>(a.kc, a.vc, h, w * KPW, min(i + 1, (w + 1) * KPW),
+                      [&](int j) -> long {
+                        if (j == i) return -1;
+                        return (long)(ar ? ar[j] : r) * Lmax + j;
+                      },
+                      lane);
+  const int d = w * ND + lane;
+  const float bq = lane < ND ? a.bin[h * HD + d] : 0.f;
+  const float bk = lane < ND ? a.bin[C + h * HD + d] : 0.f;
+  const float bv = lane < ND ? a.bin[2 * C + h * HD + d] : 0.f;
+  sq.store(wi_s, MR_WLD, tid);
+  sk.store(wi_s + HD * MR_WLD, MR_WLD, tid);
+  sv.store(wi_s + 2 * HD * MR_WLD, MR_WLD, tid);
+  so.store(wo_s, MR_OLD, tid);
+  if (pro) {
+    float xv[CPL], b2[CPL], gm[CPL], bt[CPL], qp[CPL];
+    *(f4v*)xv = *(const f4v*)(a.xin + (long)r * C + c0);
+    *(f4v*)b2 = *(const f4v*)(a.b2 + c0);
+    *(f4v*)gm = *(const f4v*)(a.gamma + c0);
+    *(f4v*)bt = *(const f4v*)(a.beta + c0);
+    *(f4v*)qp = *(const f4v*)(a.qpos + c0);
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) part[rr][w][c0 + e] = ps[e];
+    __syncthreads();
+    float v[CPL], sm = 0.f;
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+      v[e] = xv[e] + ((part[rr][0][c0 + e] + part[rr][1][c0 + e]) + b2[e]);
+      sm += v[e];
+    }
+    if (h == 0 && w == 0) *(f4v*)(a.xout + (long)r * C + c0) = *(f4v*)v;
+    const float mean = wave_sum(sm) / C;
+    float q2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+      const float dd = v[e] - mean;
+      q2 += dd * dd;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q2) / C + a.eps);
+    if (w == 0) {
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) {
+        const float o = (v[e] - mean) * rstd * gm[e] + bt[e];
+        lnb[rr][0][c0 + e] = (bf16)o;
+        lnb[rr][1][c0 + e] = (bf16)(o + qp[e]);
+      }
+    }
+  }
+  __syncthreads();                                   // staged weights (and LN1) visible
+  if (pro) {
+    const int c = lane & 7;
+#pragma unroll
+    for (int m = 0; m < C / 64; ++m) {
+      actn[m] = *(const bf16x8*)(&lnb[rr][0][8 * (c + 8 * m)]);
+      actp[m] = *(const bf16x8*)(&lnb[rr][1][8 * (c + 8 * m)]);
+    }
+  }
+  {
+    ProjW<C, ND> pw;                                 // one slice at a time (LDS reads are cheap)
+    pw.load(wi_s, w * ND, lane, MR_WLD);
+    pw.dot(actp, lane, qs[rr] + w * ND);
+    pw.load(wi_s + HD * MR_WLD, w * ND, lane, MR_WLD);
+    pw.dot(actp, lane, ks[rr] + w * ND);
+    pw.load(wi_s + 2 * HD * MR_WLD, w * ND, lane, MR_WLD);
+    pw.dot(actn, lane, vs[rr] + w * ND);
+  }
+  __syncthreads();
+  float q = 0.f, k = 0.f, v = 0.f;
+  if (lane < ND) {
+    q = bfr(qs[rr][d] + bq);
+    k = bfr(ks[rr][d] + bk);
+    v = bfr(vs[rr][d] + bv);
+  }
+  __syncthreads();
+  if (lane < ND) {
+    qs[rr][d] = bfr(q * scale);
+    ks[rr][d] = k;
+    vs[rr][d] = v;
+    const long crow = ((long)r * Lmax + i) * C + h * HD + d;
+    a.kc[crow] = (bf16)k;
+    a.vc[crow] = (bf16)v;
+  }
+  __syncthreads();
+  at.compute(qs[rr], ks[rr], vs[rr], lane);
+  at.publish(mxs[rr], sms[rr], accs[rr], w, lane);
+  __syncthreads();
+  merge_heads<HD, NW>(mxs[rr], sms[rr], accs[rr], os[rr], lane);
+  __syncthreads();
+  OutW<C, HD, NM> wo;
+  wo.load(wo_s, 0, w * NM, lane, MR_OLD);
+  wo.apply(os[rr], a.slab + ((long)h * a.R + r) * C, w * NM, lane);
+}
+
+// KVS: the block's rows read the same memory rows (beam: kv_group a multiple of RB), whose keys /
+// values for this head are staged in LDS once (Lk <= 256)
+template <int RB, bool KVS>
+__global__ void __launch_bounds__(128 * RB) dec_cross_heads_mr_kernel(CrossHeadsArgs a, float scale) {
+  constexpr int C = MR_C, HD = MR_HD, H = MR_H, PER = C / 64, NW = 2, ND = HD / NW, NM = C / 64 / NW;
+  constexpr int KPW = (64 / (HD / 8)) * 8;        // keys per wave (2 x 128 = 256)
+  constexpr int KMAX = 2 * KPW;
+  __shared__ __attribute__((aligned(16))) bf16 wq_s[HD * MR_WLD];
+  __shared__ __attribute__((aligned(16))) bf16 wo_s[C * MR_OLD];
+  __shared__ __attribute__((aligned(16))) bf16 k_s[KVS ? KMAX * HD : 8];
+  __shared__ __attribute__((aligned(16))) bf16 v_s[KVS ? KMAX * HD : 8];
+  __shared__ float ts[RB][C];
+  __shared__ float qs[RB][HD], os[RB][HD];
+  __shared__ float mxs[RB][NW], sms[RB][NW], accs[RB][NW * HD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, rr = wv >> 1, w = wv & 1;
+  const int g = blockIdx.x / H, h = blockIdx.x % H;
+  const int r = g * RB + rr;
+  const long RC = (long)a.R * C;
+  const int kvb = r / a.kv_group, Lk = a.Lk;
+  const unsigned char* km = a.kpm ? a.kpm + (long)kvb * Lk : nullptr;
+  constexpr int NT = 128 * RB;
+  Stager<(HD * C / 8 + NT - 1) / NT, NT> sq;
+  Stager<(C * HD / 8 + NT - 1) / NT, NT> so;
+  Stager<KVS ? (KMAX * HD / 8 + NT - 1) / NT : 1, NT> skk, svv;
+  sq.load(a.wq, C, h * HD, 0, HD, C, tid);
+  so.load(a.wo, C, 0, h * HD, C, HD, tid);
+  if constexpr (KVS) {
+    skk.load(a.k, C, kvb * Lk, h * HD, Lk, HD, tid);
+    svv.load(a.v, C, kvb * Lk, h * HD, Lk, HD, tid);
+  }
+  WaveAttn<HD, 1, 8> at;
+  if constexpr (!KVS)
+    at.template load<C>(a.k, a.v, h, w * KPW, min(Lk, (w + 1) * KPW),
+                        [&](int j) -> long {
+                          if (km && km[j]) return -2;
+                          return (long)kvb * Lk + j;
+                        },
+                        lane);
+  const float bq = lane < ND ? a.bq[h * HD + w * ND + lane] : 0.f;
+  float t[PER][H], xv[PER], bo[PER], gm[PER], bt[PER], ps[PER];
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const int n = lane + 64 * m;
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) t[m][hh] = a.slab_in[hh * RC + (long)r * C + n];
+    xv[m] = a.x[(long)r * C + n];
+    bo[m] = a.bo_in[n];
+    gm[m] = a.gamma[n];
+    bt[m] = a.beta[n];
+    ps[m] = a.pos ? a.pos[n] : 0.f;
+  }
+  sq.store(wq_s, MR_WLD, tid);
+  so.store(wo_s, MR_OLD, tid);
+  if constexpr (KVS) {
+    skk.store(k_s, HD, tid);
+    svv.store(v_s, HD, tid);
+  }
+  float v[PER];
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    float s = 0.f;
+#pragma unroll
+    for (int hh = 0; hh < H; ++hh) s += t[m][hh];
+    v[m] = xv[m] + (s + bo[m]);
+  }
+  if (h == 0 && w == 0) {
+#pragma unroll
+    for (int m = 0; m < PER; ++m) a.xo[(long)r * C + lane + 64 * m] = v[m];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int m = 0; m < PER; ++m) s += v[m];
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    const float dd = v[m] - mean;
+    q += dd * dd;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / C + a.eps);
+  if (w == 0) {
+#pragma unroll
+    for (int m = 0; m < PER; ++m) {
+      const float o = (v[m] - mean) * rstd * gm[m] + bt[m];
+      ts[rr][lane + 64 * m] = bfr(a.pos ? o + ps[m] : o);
+    }
+  }
+  __syncthreads();                                   // staged slices + LN2 rows visible
+  if constexpr (KVS)
+    at.template load<HD>(k_s, v_s, 0, w * KPW, min(Lk, (w + 1) * KPW),
+                         [&](int j) -> long { return (km && km[j]) ? -2 : (long)j; }, lane);
+  bf16x8 act[C / 64];
+  {
+    const int c = lane & 7;
+#pragma unroll
+    for (int m = 0; m < C / 64; ++m) act[m] = to_bf8(ts[rr] + 8 * (c + 8 * m));
+  }
+  {
+    ProjW<C, ND> wq;
+    wq.load(wq_s, w * ND, lane, MR_WLD);
+    wq.dot(act, lane, qs[rr] + w * ND);
+  }
+  __syncthreads();
+  float qv = 0.f;
+  if (lane < ND) qv = bfr(bfr(qs[rr][w * ND + lane] + bq) * scale);
+  __syncthreads();
+  if (lane < ND) qs[rr][w * ND + lane] = qv;
+  __syncthreads();
+  at.compute(qs[rr], nullptr, nullptr, lane);
+  at.publish(mxs[rr], sms[rr], accs[rr], w, lane);
+  __syncthreads();
+  merge_heads<HD, NW>(mxs[rr], sms[rr], accs[rr], os[rr], lane);
+  __syncthreads();
+  OutW<C, HD, NM> wo;
+  wo.load(wo_s, 0, w * NM, lane, MR_OLD);
+  wo.apply(os[rr], a.slab_out + ((long)h * a.R + r) * C, w * NM, lane);
+}
+
 }  // namespace
 
 extern "C" {
@@ -602,6 +903,72 @@ int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_i
 #undef XH_N
 #undef XH
   return retr_check_launch("dec_cross_heads");
+}
+
+// Multi-row blocks (rb rows x one head, 128 rb threads): the head's weight slices are staged in
+// LDS once per block, and the memory keys / values too when the block's rows share an image
+// (kv_group % rb == 0).  C = 256, head dim 32, rb in {2, 4, 5}, R % rb == 0, at most 128 self /
+// 256 memory keys; other shapes take the per-(row, head) kernels above (rb = 1).
+int retr_dec_self_heads_mr(const void* n, const void* npos, int R, int C, int H, const void* win,
+                           const float* bin, void* kc, void* vc, int i, int Lmax, const int* anc,
+                           const void* wo, float* slab, const float* xin, const float* slabs,
+                           int nslab, const float* b2, const float* gamma, const float* beta,
+                           float eps, const float* qpos, float* xout, int rb, void* stream) {
+  if (rb == 1)
+    return retr_dec_self_heads_ln(n, npos, R, C, H, win, bin, kc, vc, i, Lmax, anc, wo, slab, xin,
+                                  slabs, nslab, b2, gamma, beta, eps, qpos, xout, stream);
+  RETR_REQUIRE(xin == nullptr || (slabs && b2 && gamma && beta && qpos && xout && nslab >= 0),
+               "dec_self_heads_mr: incomplete LayerNorm prologue operands");
+  RETR_REQUIRE(C == MR_C && H == MR_H, "dec_self_heads_mr: C=%d H=%d (needs C=256, H=8)", C, H);
+  RETR_REQUIRE(rb == 2 || rb == 4 || rb == 5, "dec_self_heads_mr: rb=%d", rb);
+  RETR_REQUIRE(R % rb == 0, "dec_self_heads_mr: R=%d not a multiple of rb=%d", R, rb);
+  RETR_REQUIRE(i >= 0 && i < Lmax, "dec_self_heads_mr: step %d outside the %d-row cache", i, Lmax);
+  RETR_REQUIRE(i + 1 <= 128, "dec_self_heads_mr: %d keys (at most 128)", i + 1);
+  if (R == 0) return 0;
+  SelfHeadsArgs a{(const bf16*)n, (const bf16*)npos, (const bf16*)win, bin, (bf16*)kc,
+                  (bf16*)vc, i, Lmax, anc, (const bf16*)wo, slab, R, xin, slabs, nslab, b2,
+                  gamma, beta, eps, qpos, xout};
+  const float scale = 1.0f / sqrtf((float)MR_HD);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)(R / rb * H));
+#define SM(RBV) hipLaunchKernelGGL((dec_self_heads_mr_kernel<RBV>), grid, dim3(128 * RBV), 0, st, a, scale)
+  if (rb == 2) SM(2);
+  else if (rb == 4) SM(4);
+  else SM(5);
+#undef SM
+  return retr_check_launch("dec_self_heads_mr");
+}
+
+int retr_dec_cross_heads_mr(const float* slab_in, const float* x, const float* bo_in, float* xo,
+                            int R, int C, int H, const float* gamma, const float* beta, float eps,
+                            const float* pos, const void* wq, const float* bq, const void* k,
+                            const void* v, int Lk, int kv_group, const unsigned char* kpm,
+                            const void* wo, float* slab_out, int rb, void* stream) {
+  if (rb == 1)
+    return retr_dec_cross_heads(slab_in, x, bo_in, xo, R, C, H, gamma, beta, eps, pos, wq, bq, k,
+                                v, Lk, kv_group, kpm, wo, slab_out, stream);
+  RETR_REQUIRE(C == MR_C && H == MR_H, "dec_cross_heads_mr: C=%d H=%d (needs C=256, H=8)", C, H);
+  RETR_REQUIRE(rb == 2 || rb == 4 || rb == 5, "dec_cross_heads_mr: rb=%d", rb);
+  RETR_REQUIRE(R % rb == 0, "dec_cross_heads_mr: R=%d not a multiple of rb=%d", R, rb);
+  RETR_REQUIRE(Lk > 0 && Lk <= 256 && kv_group > 0,
+               "dec_cross_heads_mr: Lk=%d (1..256) kv_group=%d", Lk, kv_group);
+  if (R == 0) return 0;
+  CrossHeadsArgs a{slab_in, x, bo_in, xo, gamma, beta, eps, pos, (const bf16*)wq, bq,
+                   (const bf16*)k, (const bf16*)v, Lk, kv_group, kpm, (const bf16*)wo, slab_out, R};
+  const float scale = 1.0f / sqrtf((float)MR_HD);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)(R / rb * H));
+  const bool kvs = kv_group % rb == 0;
+#define XM(RBV)                                                                                   \
+  if (kvs) hipLaunchKernelGGL((dec_cross_heads_mr_kernel<RBV, true>), grid, dim3(128 * RBV), 0, st, \
+                              a, scale);                                                          \
+  else hipLaunchKernelGGL((dec_cross_heads_mr_kernel<RBV, false>), grid, dim3(128 * RBV), 0, st, a, \
+                          scale);
+  if (rb == 2) { XM(2) }
+  else if (rb == 4) { XM(4) }
+  else { XM(5) }
+#undef XM
+  return retr_check_launch("dec_cross_heads_mr");
 }
 
 }  // extern "C"

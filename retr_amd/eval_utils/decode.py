@@ -51,6 +51,23 @@ DEC_FFN_LN = True
 # (with DEC_FFN_LN) the FFN residual + the next layer's LN1 in the self-attention prologue
 DEC_FOLD_ROWS = True
 
+# Rows per block of the attention sub-layer kernels: None = automatic (beam groups of K rows
+# share the head's staged weights and memory keys / values: K in {2, 4, 5}), else an int for
+# every launch (1 = a block per (row, head)).
+DEC_ROWS_PER_BLOCK = None
+
+
+def _rows_per_block(R, C, H, K, nkeys, S):
+    """(self, cross) rows per block for retr_dec_self_heads_mr / retr_dec_cross_heads_mr."""
+    if C != 256 or H != 8:
+        return 1, 1
+    rb = DEC_ROWS_PER_BLOCK
+    if rb is None:
+        rb = K if K in (2, 4, 5) else 1
+    if rb == 1 or R % rb:
+        return 1, 1
+    return (rb if nkeys <= 128 else 1), (rb if S <= 256 else 1)
+
 
 class _DecodeState:
     """Static device buffers (and captured per-step hipGraphs) for one (B, K, S, T) shape;
@@ -289,27 +306,29 @@ class IncrementalGreedy:
         # three launches per layer (up to 64 rows): the FFN residual + next LN1 in the next
         # layer's self-attention prologue, the cross residual + LN3 in the FFN prologue
         fold = DEC_FFN_LN and DEC_FOLD_ROWS and R <= 64 and F % 64 == 0
+        rbs, rbx = _rows_per_block(R, C, H, st.K, i + 1, S)
         for li, layer in enumerate(layers):
             sa, ca, ff = layer.tgt_self_attn, layer.tgt_src_cross_attn, layer.ff
             sub, csub = sa.sublayer, ca.sublayer
             f0, f2 = ff.sublayer[0], ff.sublayer[2]
             if fold and li > 0:
                 pf2 = layers[li - 1].ff.sublayer[2]
-                call("retr_dec_self_heads_ln", None, None, R, C, H,
+                call("retr_dec_self_heads_mr", None, None, R, C, H,
                      ptr(W(sub.in_proj_weight)), ptr(sub.in_proj_bias), ptr(st.kc[li]),
                      ptr(st.vc[li]), i, T, anc, ptr(W(sub.out_proj.weight)), ptr(st.hslab),
                      ptr(x), ptr(st.slabs), F // 64, ptr(pf2.bias), ptr(sa.norm.weight),
-                     ptr(sa.norm.bias), float(sa.norm.eps), ptr(qp), ptr(xa), s)
+                     ptr(sa.norm.bias), float(sa.norm.eps), ptr(qp), ptr(xa), rbs, s)
                 x, xa = xa, x
             else:
-                call("retr_dec_self_heads", ptr(st.n), ptr(st.npos), R, C, H,
+                call("retr_dec_self_heads_mr", ptr(st.n), ptr(st.npos), R, C, H,
                      ptr(W(sub.in_proj_weight)), ptr(sub.in_proj_bias), ptr(st.kc[li]),
-                     ptr(st.vc[li]), i, T, anc, ptr(W(sub.out_proj.weight)), ptr(st.hslab), s)
-            call("retr_dec_cross_heads", ptr(st.hslab), ptr(x), ptr(sub.out_proj.bias), ptr(xa),
-                 R, C, H, ptr(ca.norm.weight), ptr(ca.norm.bias), float(ca.norm.eps), ptr(qp),
-                 ptr(W(csub.in_proj_weight)), ptr(csub.in_proj_bias), ptr(st.kx[li]),
+                     ptr(st.vc[li]), i, T, anc, ptr(W(sub.out_proj.weight)), ptr(st.hslab),
+                     None, None, 0, None, None, None, 0.0, None, None, rbs, s)
+            call("retr_dec_cross_heads_mr", ptr(st.hslab), ptr(x), ptr(sub.out_proj.bias),
+                 ptr(xa), R, C, H, ptr(ca.norm.weight), ptr(ca.norm.bias), float(ca.norm.eps),
+                 ptr(qp), ptr(W(csub.in_proj_weight)), ptr(csub.in_proj_bias), ptr(st.kx[li]),
                  ptr(st.vx[li]), S, st.K, ptr(st.kpm), ptr(W(csub.out_proj.weight)),
-                 ptr(st.hslab2), s)
+                 ptr(st.hslab2), rbx, s)
             x, xa = xa, x
             if fold:
                 call("retr_dec_ffn_ln64", ptr(x), ptr(st.hslab2), H, ptr(csub.out_proj.bias),

@@ -487,3 +487,95 @@ def test_dec_fold_rows_step_matches(fold):
         dec.DEC_HEADS, dec.DEC_FFN_LN, dec.DEC_FOLD_ROWS = old
         model._retr_decode_states = {}
     assert _rel(res[0], res[1]) < 2e-2
+
+
+@pytest.mark.parametrize("rb,kv_group,prologue", [(5, 5, False), (5, 5, True), (2, 1, False),
+                                                  (4, 2, True), (4, 8, False)])
+def test_dec_heads_multi_row_matches_per_row(rb, kv_group, prologue):
+    """retr_dec_self_heads_mr / retr_dec_cross_heads_mr (rb rows x one head per block, weight
+    slices -- and memory keys / values when kv_group % rb == 0 -- staged in LDS) against the
+    per-(row, head) kernels on the same operands: identical arithmetic, so every output (head
+    partials, cache rows, residual) is bit-identical; beam ancestry, masked memory keys."""
+    C, H = 256, 8
+    R, T, i, S = 40, 32, 21, 197
+    g = _g(rb * 10 + kv_group + prologue)
+    bf = lambda t: t.to(DEV).bfloat16()                       # noqa: E731
+    n = bf(torch.randn(R, C, generator=g))
+    npos = bf(torch.randn(R, C, generator=g))
+    win = bf(torch.randn(3 * C, C, generator=g) / math.sqrt(C))
+    bin_ = torch.randn(3 * C, generator=g).to(DEV) * 0.1
+    kc = bf(torch.randn(R * T, C, generator=g))
+    vc = bf(torch.randn(R * T, C, generator=g))
+    anc = torch.randint(0, R, (R, T), generator=g, dtype=torch.int32).to(DEV)
+    wo = bf(torch.randn(C, C, generator=g) / math.sqrt(C))
+    nsl = 4
+    xin = torch.randn(R, C, generator=g).to(DEV)
+    slabs = torch.randn(nsl, R, C, generator=g).to(DEV) * 0.3
+    b2 = torch.randn(C, generator=g).to(DEV) * 0.1
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV) * 0.1
+    qpos = torch.randn(C, generator=g).to(DEV)
+    outs = []
+    for r_b in (1, rb):
+        kc1, vc1 = kc.clone(), vc.clone()
+        slab = torch.full((H, R, C), float("nan"), device=DEV)
+        xout = torch.full((R, C), float("nan"), device=DEV)
+        if prologue:
+            call("retr_dec_self_heads_mr", None, None, R, C, H, ptr(win), ptr(bin_), ptr(kc1),
+                 ptr(vc1), i, T, ptr(anc), ptr(wo), ptr(slab), ptr(xin), ptr(slabs), nsl, ptr(b2),
+                 ptr(gamma), ptr(beta), 1e-5, ptr(qpos), ptr(xout), r_b, ops._st())
+        else:
+            call("retr_dec_self_heads_mr", ptr(n), ptr(npos), R, C, H, ptr(win), ptr(bin_),
+                 ptr(kc1), ptr(vc1), i, T, ptr(anc), ptr(wo), ptr(slab), None, None, 0, None,
+                 None, None, 0.0, None, None, r_b, ops._st())
+        B = R // kv_group
+        km = bf(torch.randn(B * S, C, generator=_g(7)))
+        vm = bf(torch.randn(B * S, C, generator=_g(8)))
+        kpm = torch.zeros(B, S, dtype=torch.uint8)
+        kpm[B - 1, -13:] = 1
+        kpm = kpm.to(DEV)
+        x = torch.randn(R, C, generator=_g(9)).to(DEV)
+        wq = bf(torch.randn(3 * C, C, generator=_g(10)) / math.sqrt(C))
+        bq = torch.randn(3 * C, generator=_g(11)).to(DEV) * 0.1
+        wo2 = bf(torch.randn(C, C, generator=_g(12)) / math.sqrt(C))
+        xo = torch.full((R, C), float("nan"), device=DEV)
+        slab2 = torch.full((H, R, C), float("nan"), device=DEV)
+        call("retr_dec_cross_heads_mr", ptr(slab), ptr(x), ptr(b2), ptr(xo), R, C, H, ptr(gamma),
+             ptr(beta), 1e-5, ptr(qpos), ptr(wq), ptr(bq), ptr(km), ptr(vm), S, kv_group,
+             ptr(kpm), ptr(wo2), ptr(slab2), r_b, ops._st())
+        torch.cuda.synchronize()
+        outs.append((slab, kc1, vc1, xo, slab2) + ((xout,) if prologue else ()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert not torch.isnan(outs[1][-1]).any()
+
+
+def test_dec_multi_row_beam_step_matches():
+    """Beam 5 decode with the multi-row attention blocks (the automatic choice: a block per beam
+    group x head) against a block per (row, head) on the cfg5 model: identical captions and
+    first-step logits (bit-identical kernels), graphs == eager."""
+    from bench import build, cfg5
+    from retr_amd.eval_utils import decode as dec
+    from retr_amd.synthetic import synthetic_images
+    model, _ = build(cfg5(), DEV)
+    model.eval()
+    B, T = 8, 128
+    img, mask = synthetic_images(B, 224, seed=17, pad_band=True)
+    s = NestedTensor(img.to(DEV), mask.to(DEV))
+    old = dec.DEC_ROWS_PER_BLOCK
+    res = []
+    try:
+        for rb in (None, 1):
+            dec.DEC_ROWS_PER_BLOCK = rb
+            model._retr_decode_states = {}
+            bm = dec.IncrementalBeam(model, 5)
+            ids = bm(s, T, 101, 102)
+            res.append(ids)
+            if rb is None:
+                assert dec._rows_per_block(B * 5, 256, 8, 5, 1, 197) == (5, 5)
+                ids_e = dec.IncrementalBeam(model, 5, use_graphs=False)(s, T, 101, 102)
+                assert torch.equal(ids, ids_e)
+    finally:
+        dec.DEC_ROWS_PER_BLOCK = old
+        model._retr_decode_states = {}
+    assert torch.equal(res[0], res[1])
