@@ -157,6 +157,135 @@ topk_kernel(const T* x, long ld, int V, int* idx_out, float* lp_out) {
   }
 }
 
+// Register-resident variant for rows of up to 512 x 8 x 8 = 32768 words (the 30522-word
+// vocabulary): 512 threads, each holds its 8 chunks of 8 in registers.  Pass 1 gives the row's
+// log-sum-exp and every wave's maximum; the K-th largest wave maximum tau is a lower bound of the
+// K-th best word (K distinct waves each hold a word >= tau), so pass 2 offers only words >= tau to
+// the private lists -- a handful per row instead of a compare-and-shift chain per chunk, which
+// left topk_kernel VALU-bound at ~37 us for 320 rows.  Same (value desc, index asc) result.
+constexpr int kT2 = 512, kT2W = kT2 / 64, kT2C = 8;
+template <typename T, int K>
+__global__ void __launch_bounds__(kT2)
+topk_reg_kernel(const T* x, long ld, int V, int* idx_out, float* lp_out) {
+  static_assert(K <= kT2W, "tau needs K distinct waves");
+  __shared__ float wmax[kT2W], wsum[kT2W];
+  __shared__ float rv[kT2W];
+  __shared__ int ri[kT2W], rt[kT2W];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const T* xr = x + (long)row * ld;
+  const int V8 = V / 8;
+  float v[kT2C][8];
+#pragma unroll
+  for (int u = 0; u < kT2C; ++u) {
+    const int c = tid + u * kT2;
+    if (c < V8) {
+      load8f<T>(xr + 8 * c, v[u]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i = 8 * c + e;
+        v[u][e] = (c == V8 && i < V) ? to_f(xr[i]) : -INFINITY;
+      }
+    }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < kT2C; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx = fmaxf(mx, v[u][e]);
+  float sum = 0.f;
+  if (mx != -INFINITY) {
+#pragma unroll
+    for (int u = 0; u < kT2C; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += __expf(v[u][e] - mx);
+  }
+  const float gm = wave_max(mx);
+  float s = (mx == -INFINITY) ? 0.f : sum * __expf(mx - gm);
+  s = wave_sum(s);
+  if (lane == 0) wmax[wave] = gm, wsum[wave] = s;
+  __syncthreads();
+  float bm = wmax[0];
+#pragma unroll
+  for (int w = 1; w < kT2W; ++w) bm = fmaxf(bm, wmax[w]);
+  float bs = 0.f;
+#pragma unroll
+  for (int w = 0; w < kT2W; ++w) bs += wmax[w] == -INFINITY ? 0.f : wsum[w] * __expf(wmax[w] - bm);
+  const float lse = bm + __logf(bs);
+  // tau = K-th largest wave maximum (counting equal maxima of distinct waves)
+  float tau = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < kT2W; ++w) {
+    int above = 0;
+#pragma unroll
+    for (int q = 0; q < kT2W; ++q) above += (wmax[q] > wmax[w] || (wmax[q] == wmax[w] && q < w));
+    if (above == K - 1) tau = wmax[w];
+  }
+  float tv[K];
+  int ti[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) tv[k] = -INFINITY, ti[k] = 0x7fffffff;
+#pragma unroll
+  for (int u = 0; u < kT2C; ++u) {
+    float cm = v[u][0];
+#pragma unroll
+    for (int e = 1; e < 8; ++e) cm = fmaxf(cm, v[u][e]);
+    if (cm >= tau) {
+      const int base = 8 * (tid + u * kT2);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float cv0 = v[u][e];
+        if (base + e >= V || cv0 < tau || !better(cv0, base + e, tv[K - 1], ti[K - 1])) continue;
+        float cv = cv0;
+        int ci = base + e;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if (better(cv, ci, tv[k], ti[k])) {
+            const float tvk = tv[k];
+            const int tik = ti[k];
+            tv[k] = cv;
+            ti[k] = ci;
+            cv = tvk;
+            ci = tik;
+          }
+        }
+      }
+    }
+  }
+  for (int k = 0; k < K; ++k) {
+    float bv = tv[0];
+    int bi = ti[0];
+    int who = tid;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(bv, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64), w2 = __shfl_xor(who, o, 64);
+      if (better(v2, i2, bv, bi)) bv = v2, bi = i2, who = w2;
+    }
+    __syncthreads();
+    if (lane == 0) rv[wave] = bv, ri[wave] = bi, rt[wave] = who;
+    __syncthreads();
+    float cv = rv[0];
+    int ci = ri[0], cw = rt[0];
+#pragma unroll
+    for (int w = 1; w < kT2W; ++w)
+      if (better(rv[w], ri[w], cv, ci)) cv = rv[w], ci = ri[w], cw = rt[w];
+    if (tid == cw) {
+#pragma unroll
+      for (int q = 0; q < K - 1; ++q) {
+        tv[q] = tv[q + 1];
+        ti[q] = ti[q + 1];
+      }
+      tv[K - 1] = -INFINITY;
+      ti[K - 1] = 0x7fffffff;
+    }
+    if (tid == 0) {
+      idx_out[(long)row * K + k] = ci;
+      if (lp_out) lp_out[(long)row * K + k] = cv - lse;
+    }
+  }
+}
+
 // One block per image b: select the K surviving beams from the candidates, then reorder the
 // token history and the cache-ancestry rows in LDS and append step i's token.
 __global__ void __launch_bounds__(64)
@@ -257,8 +386,15 @@ int retr_topk_rows(int dtype, const void* x, long ld, int M, int V, int K, int* 
   RETR_REQUIRE(ld % 8 == 0 && V >= K, "topk_rows: row stride %%8 and V >= K");
   if (M == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  const bool reg = V <= kT2 * kT2C * 8;
 #define TOPK(KK)                                                                                 \
-  if (dtype == RETR_BF16)                                                                        \
+  if (reg && dtype == RETR_BF16)                                                                 \
+    hipLaunchKernelGGL((topk_reg_kernel<bf16, KK>), dim3(M), dim3(kT2), 0, st, (const bf16*)x,   \
+                       ld, V, idx, logprob);                                                     \
+  else if (reg)                                                                                  \
+    hipLaunchKernelGGL((topk_reg_kernel<float, KK>), dim3(M), dim3(kT2), 0, st, (const float*)x, \
+                       ld, V, idx, logprob);                                                     \
+  else if (dtype == RETR_BF16)                                                                   \
     hipLaunchKernelGGL((topk_kernel<bf16, KK>), dim3(M), dim3(kThreads), 0, st, (const bf16*)x,  \
                        ld, V, idx, logprob);                                                     \
   else                                                                                           \

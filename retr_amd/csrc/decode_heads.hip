@@ -77,21 +77,52 @@ struct WaveAttn {
   static constexpr int NG = HD / 8, NPART = 64 / NG, CH = NPART * KU;
   long row[NCH][KU];
   bf16x8 kk[NCH][KU], vv[NCH][KU];
+  bool mk[NCH][KU] = {};                            // key-padding flags (load_mask)
   float mx = -INFINITY, sum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
-  template <int C, class RowFn>
-  RETR_DEVICE void load(const bf16* __restrict__ K, const bf16* __restrict__ V, int h, int j0,
-                        int j1, RowFn key_row, int lane) {
-    const int g = lane % NG, part = lane / NG;
+  // key-padding flags of the wave's keys, loaded BEFORE (and independently of) the keys /
+  // values: a mask test inside key_row would make every K / V address wait for its mask byte
+  RETR_DEVICE void load_mask(const unsigned char* km, int j0, int j1, int lane) {
+    if (!km) return;
+    const int part = lane / NG;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const int j = j0 + CH * c + part + NPART * u;
+        mk[c][u] = j < j1 && km[j] != 0;
+      }
+  }
+
+  // the K / V rows of the wave's keys (key_row may read memory: the beam ancestry table) --
+  // called first in a kernel, so that waiting for those reads does not wait for later loads
+  template <class RowFn>
+  RETR_DEVICE void set_rows(int j0, int j1, RowFn key_row, int lane) {
+    const int part = lane / NG;
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int u = 0; u < KU; ++u) {
         const int j = j0 + CH * c + part + NPART * u;
         row[c][u] = j < j1 ? key_row(j) : -2;
+      }
+  }
+  template <int C, class RowFn>
+  RETR_DEVICE void load(const bf16* __restrict__ K, const bf16* __restrict__ V, int h, int j0,
+                        int j1, RowFn key_row, int lane) {
+    set_rows(j0, j1, key_row, lane);
+    load_rows<C>(K, V, h, lane);
+  }
+  template <int C>
+  RETR_DEVICE void load_rows(const bf16* __restrict__ K, const bf16* __restrict__ V, int h,
+                             int lane) {
+    const int g = lane % NG;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int u = 0; u < KU; ++u)
         kk[c][u] = row[c][u] >= 0 ? *(const bf16x8*)(K + row[c][u] * C + h * HD + 8 * g)
                                   : bf16x8{};
-      }
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -112,7 +143,7 @@ struct WaveAttn {
       for (int u = 0; u < KU; ++u) {
         float s = dot8(q, row[c][u] == -1 ? knb : kk[c][u]);
         s = gsum<NG>(s);
-        sc[u] = row[c][u] == -2 ? -INFINITY : s;
+        sc[u] = (row[c][u] == -2 || mk[c][u]) ? -INFINITY : s;
         cm = fmaxf(cm, sc[u]);
       }
       cm = wave_max(cm);
@@ -131,8 +162,9 @@ struct WaveAttn {
 #pragma unroll
             for (int e = 0; e < 8; ++e) acc[e] += p * vn[8 * g + e];
           } else {
+            const bf16x8 vs = mk[c][u] ? bf16x8{} : vv[c][u];   // as an unloaded masked key
 #pragma unroll
-            for (int e = 0; e < 8; ++e) acc[e] += p * (float)vv[c][u][e];
+            for (int e = 0; e < 8; ++e) acc[e] += p * (float)vs[e];
           }
         }
         sum += wave_sum(cs) * (1.0f / NG);
@@ -282,6 +314,13 @@ __global__ void __launch_bounds__(64 * NW) dec_self_heads_kernel(SelfHeadsArgs a
   const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
   const int i = a.i, Lmax = a.Lmax;
   const bool pro = a.xin != nullptr;
+  WaveAttn<HD, NCH, KU> at;
+  at.set_rows(w * KPW, min(i + 1, (w + 1) * KPW),
+              [&](int j) -> long {
+                if (j == i) return -1;
+                return (long)(ar ? ar[j] : r) * Lmax + j;
+              },
+              lane);
   // every global load first (one dependent memory round trip per launch): the LN1 prologue's
   // slab share (wave w: slabs [w S / NW, (w + 1) S / NW)), activations, this wave's q|k|v and
   // out-projection weight rows, its cached keys / values of positions < i
@@ -318,13 +357,7 @@ __global__ void __launch_bounds__(64 * NW) dec_self_heads_kernel(SelfHeadsArgs a
   wq.load(a.win, h * HD + w * ND, lane);
   wk.load(a.win, C + h * HD + w * ND, lane);
   wv.load(a.win, 2 * C + h * HD + w * ND, lane);
-  WaveAttn<HD, NCH, KU> at;
-  at.template load<C>(a.kc, a.vc, h, w * KPW, min(i + 1, (w + 1) * KPW),
-                      [&](int j) -> long {
-                        if (j == i) return -1;
-                        return (long)(ar ? ar[j] : r) * Lmax + j;
-                      },
-                      lane);
+  at.template load_rows<C>(a.kc, a.vc, h, lane);
   OutW<C, HD, NM> wo;
   wo.load(a.wo, h, w * NM, lane);
   const int d = w * ND + lane;
@@ -446,12 +479,9 @@ __global__ void __launch_bounds__(64 * NW) dec_cross_heads_kernel(CrossHeadsArgs
   // every global load first: this wave's memory keys / values, query and out-projection weight
   // rows, the self-attention head partials and the row operands
   WaveAttn<HD, NCH, KU> at;
+  at.load_mask(km, w * KPW, min(Lk, (w + 1) * KPW), lane);
   at.template load<C>(a.k, a.v, h, w * KPW, min(Lk, (w + 1) * KPW),
-                      [&](int j) -> long {
-                        if (km && km[j]) return -2;
-                        return (long)kvb * Lk + j;
-                      },
-                      lane);
+                      [&](int j) -> long { return (long)kvb * Lk + j; }, lane);
   ProjW<C, ND> wq;
   wq.load(a.wq, h * HD + w * ND, lane);
   OutW<C, HD, NM> wo;
@@ -579,6 +609,13 @@ __global__ void __launch_bounds__(128 * RB) dec_self_heads_mr_kernel(SelfHeadsAr
   const int i = a.i, Lmax = a.Lmax;
   const bool pro = a.xin != nullptr;
   const int c0 = CPL * lane;
+  WaveAttn<HD, 1, 4> at;
+  at.set_rows(w * KPW, min(i + 1, (w + 1) * KPW),
+              [&](int j) -> long {
+                if (j == i) return -1;
+                return (long)(ar ? ar[j] : r) * Lmax + j;
+              },
+              lane);
   constexpr int NT = 128 * RB;
   // the head's q | k | v rows and out-projection columns, staged once per block
   Stager<(HD * C / 8 + NT - 1) / NT, NT> sq, sk, sv;
@@ -612,13 +649,7 @@ __global__ void __launch_bounds__(128 * RB) dec_self_heads_mr_kernel(SelfHeadsAr
     load_act<C>(a.npos + (long)r * C, lane, actp);
     load_act<C>(a.n + (long)r * C, lane, actn);
   }
-  WaveAttn<HD, 1, 4> at;
-  at.template load<C>(a.kc, a.vc, h, w * KPW, min(i + 1, (w + 1) * KPW),
-                      [&](int j) -> long {
-                        if (j == i) return -1;
-                        return (long)(ar ? ar[j] : r) * Lmax + j;
-                      },
-                      lane);
+  at.template load_rows<C>(a.kc, a.vc, h, lane);
   const int d = w * ND + lane;
   const float bq = lane < ND ? a.bin[h * HD + d] : 0.f;
   const float bk = lane < ND ? a.bin[C + h * HD + d] : 0.f;
@@ -737,13 +768,10 @@ __global__ void __launch_bounds__(128 * RB) dec_cross_heads_mr_kernel(CrossHeads
     svv.load(a.v, C, kvb * Lk, h * HD, Lk, HD, tid);
   }
   WaveAttn<HD, 1, 8> at;
+  at.load_mask(km, w * KPW, min(Lk, (w + 1) * KPW), lane);
   if constexpr (!KVS)
     at.template load<C>(a.k, a.v, h, w * KPW, min(Lk, (w + 1) * KPW),
-                        [&](int j) -> long {
-                          if (km && km[j]) return -2;
-                          return (long)kvb * Lk + j;
-                        },
-                        lane);
+                        [&](int j) -> long { return (long)kvb * Lk + j; }, lane);
   const float bq = lane < ND ? a.bq[h * HD + w * ND + lane] : 0.f;
   float t[PER][H], xv[PER], bo[PER], gm[PER], bt[PER], ps[PER];
 #pragma unroll
@@ -796,7 +824,7 @@ __global__ void __launch_bounds__(128 * RB) dec_cross_heads_mr_kernel(CrossHeads
   __syncthreads();                                   // staged slices + LN2 rows visible
   if constexpr (KVS)
     at.template load<HD>(k_s, v_s, 0, w * KPW, min(Lk, (w + 1) * KPW),
-                         [&](int j) -> long { return (km && km[j]) ? -2 : (long)j; }, lane);
+                         [&](int j) -> long { return (long)j; }, lane);
   bf16x8 act[C / 64];
   {
     const int c = lane & 7;

@@ -118,3 +118,36 @@ def test_beam_cfg5_shape_bf16():
     assert float((s5 >= gs - 1e-3).float().mean()) >= 0.9, (s5 - gs)
     assert float((s5 - gs).mean()) >= 0.0
     assert b5.shape == (B, T) and bool((b5[:, 0] == 101).all())
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("V,K", [(30522, 5), (30522, 8), (1003, 1), (1003, 3), (40000, 5)])
+def test_topk_rows_matches_torch(dtype, V, K):
+    """retr_topk_rows (csrc/beam.hip; register-resident kernel up to 32768 words, the streaming
+    one beyond): the K best words per row by (value desc, index asc) -- exact indices, planted
+    ties and a row whose best words sit in one wave -- and log-softmax values within 1e-5."""
+    from retr_amd import ops
+    from retr_amd._lib import call, ptr
+    dev = "cuda"
+    M, ld = 37, (V + 15) // 8 * 8
+    g = torch.Generator().manual_seed(V + K)
+    x = torch.randn(M, ld, generator=g) * 3
+    x[0, 100] = x[0, 7000 % V] = x[0, 29000 % V] = 20.0         # ties -> ascending index
+    x[1, 64:64 + 4 * K] = 15.0 + torch.arange(4 * K).float() / 64  # best words in one chunk run
+    x[2, V - 1] = 30.0                                           # last (possibly partial) chunk
+    t = x.bfloat16() if dtype == "bf16" else x
+    xd = t.to(dev)
+    idx = torch.empty(M, K, dtype=torch.int32, device=dev)
+    lp = torch.empty(M, K, dtype=torch.float32, device=dev)
+    call("retr_topk_rows", 1 if dtype == "bf16" else 0, ptr(xd), ld, M, V, K, ptr(idx), ptr(lp),
+         ops._st())
+    torch.cuda.synchronize()
+    xf = t.float()[:, :V]
+    ref_lp = torch.log_softmax(xf.double(), -1)
+    for r in range(M):
+        order = sorted(range(V), key=lambda i: (-float(xf[r, i]), i))[:K] if r < 3 else None
+        if order is None:                                       # stable sort: index asc on ties
+            vals, ids = torch.sort(xf[r], descending=True, stable=True)
+            order = ids[:K].tolist()
+        assert idx[r].tolist() == order, r
+        assert torch.allclose(lp[r].double().cpu(), ref_lp[r, order], atol=1e-5), r
