@@ -177,7 +177,10 @@ enum {
   RETR_TUNE_CW_WAVES = 29,      /* retr_conv2d_wgrad_group wave layout of the 128x128 tile (sweeps):
                                    0 kind 0 (1x1) 4 waves / kind 1 (3x3, strided) 8 waves, 1 both
                                    4 waves (64x64 per wave), 2 both 8 waves (32x64 per wave) */
-  RETR_TUNE_COUNT = 30
+  RETR_TUNE_DEC_ORDER = 30,     /* decode attention blocks (retr_dec_*_heads*): 0 a row's (or beam
+                                   group's) head blocks on one XCD (its L2 holds the row's partial
+                                   slabs and whole K / V cache lines), 1 block b = (b / H, b % H) */
+  RETR_TUNE_COUNT = 31
 };
 int retr_tune(int knob, int value);
 

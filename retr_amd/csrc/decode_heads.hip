@@ -59,6 +59,22 @@ RETR_DEVICE bf16x8 to_bf8(const float* v) {
   return r;
 }
 
+// (row unit, head) of block b.  Hardware dispatches block b to XCD b % 8; with every head block
+// of a row on one XCD that XCD's L2 serves the row's partial slabs to all its heads (they were
+// fetched into all eight L2s) and the 128-byte K / V cache lines the row's heads share (a head's
+// 32 dimensions are half a line), at the price of every XCD reading every head's weight slices
+// (a few hundred KB per launch).  Needs units % 8 == 0, else row-major.
+RETR_DEVICE void dec_block_rh(int b, int units, int H, bool xcd, int& r, int& h) {
+  if ((units & 7) == 0 && xcd) {
+    const int x = b & 7, q = b >> 3;
+    r = x * (units >> 3) + q / H;
+    h = q % H;
+  } else {
+    r = b / H;
+    h = b % H;
+  }
+}
+
 // this lane's activation chunks (c + 8 m) of a bf16 row
 template <int C>
 RETR_DEVICE void load_act(const bf16* row, int lane, bf16x8 (&act)[C / 64]) {
@@ -294,6 +310,7 @@ struct SelfHeadsArgs {
   float eps;
   const float* qpos;
   float* xout;
+  bool xcd = true;      // dec_block_rh order (RETR_TUNE_DEC_ORDER)
 };
 
 // One block of NW waves per (row, head): wave w computes rows [w HD / NW, (w + 1) HD / NW) of
@@ -310,7 +327,8 @@ __global__ void __launch_bounds__(64 * NW) dec_self_heads_kernel(SelfHeadsArgs a
   __shared__ __attribute__((aligned(16))) float part[NW][C];   // LN1 prologue slab partials
   __shared__ __attribute__((aligned(16))) bf16 lnb[2][C];      // LN1 prologue n / npos
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = blockIdx.x / H, h = blockIdx.x % H;
+  int r, h;
+  dec_block_rh(blockIdx.x, a.R, H, a.xcd, r, h);
   const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
   const int i = a.i, Lmax = a.Lmax;
   const bool pro = a.xin != nullptr;
@@ -462,6 +480,7 @@ struct CrossHeadsArgs {
   const bf16* wo;         // cross out-proj [C][C]
   float* slab_out;        // [H][R][C]
   int R;
+  bool xcd = true;        // dec_block_rh order (RETR_TUNE_DEC_ORDER)
 };
 
 template <int C, int HD, int NW, int NCH, int KU>
@@ -472,7 +491,8 @@ __global__ void __launch_bounds__(64 * NW) dec_cross_heads_kernel(CrossHeadsArgs
   __shared__ float qs[HD], os[HD];
   __shared__ float mxs[NW], sms[NW], accs[NW * HD];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r = blockIdx.x / H, h = blockIdx.x % H;
+  int r, h;
+  dec_block_rh(blockIdx.x, a.R, H, a.xcd, r, h);
   const long RC = (long)a.R * C;
   const int kvb = r / a.kv_group, Lk = a.Lk;
   const unsigned char* km = a.kpm ? a.kpm + (long)kvb * Lk : nullptr;
@@ -603,7 +623,8 @@ __global__ void __launch_bounds__(128 * RB) dec_self_heads_mr_kernel(SelfHeadsAr
   __shared__ __attribute__((aligned(16))) float part[RB][NW][C];
   __shared__ __attribute__((aligned(16))) bf16 lnb[RB][2][C];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, rr = wv >> 1, w = wv & 1;
-  const int g = blockIdx.x / H, h = blockIdx.x % H;
+  int g, h;
+  dec_block_rh(blockIdx.x, a.R / RB, H, a.xcd, g, h);
   const int r = g * RB + rr;
   const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
   const int i = a.i, Lmax = a.Lmax;
@@ -752,7 +773,8 @@ __global__ void __launch_bounds__(128 * RB) dec_cross_heads_mr_kernel(CrossHeads
   __shared__ float qs[RB][HD], os[RB][HD];
   __shared__ float mxs[RB][NW], sms[RB][NW], accs[RB][NW * HD];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, rr = wv >> 1, w = wv & 1;
-  const int g = blockIdx.x / H, h = blockIdx.x % H;
+  int g, h;
+  dec_block_rh(blockIdx.x, a.R / RB, H, a.xcd, g, h);
   const int r = g * RB + rr;
   const long RC = (long)a.R * C;
   const int kvb = r / a.kv_group, Lk = a.Lk;
@@ -879,6 +901,7 @@ int retr_dec_self_heads_ln(const void* n, const void* npos, int R, int C, int H,
   SelfHeadsArgs a{(const bf16*)n, (const bf16*)npos, (const bf16*)win, bin, (bf16*)kc,
                   (bf16*)vc, i, Lmax, anc, (const bf16*)wo, slab, R, xin, slabs, nslab, b2,
                   gamma, beta, eps, qpos, xout};
+  a.xcd = retr_tune_get(RETR_TUNE_DEC_ORDER) == 0;
   const float scale = 1.0f / sqrtf((float)hd);
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(R * H));
@@ -914,6 +937,7 @@ int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_i
   if (R == 0) return 0;
   CrossHeadsArgs a{slab_in, x, bo_in, xo, gamma, beta, eps, pos, (const bf16*)wq, bq,
                    (const bf16*)k, (const bf16*)v, Lk, kv_group, kpm, (const bf16*)wo, slab_out, R};
+  a.xcd = retr_tune_get(RETR_TUNE_DEC_ORDER) == 0;
   const float scale = 1.0f / sqrtf((float)hd);
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(R * H));
@@ -956,6 +980,7 @@ int retr_dec_self_heads_mr(const void* n, const void* npos, int R, int C, int H,
   SelfHeadsArgs a{(const bf16*)n, (const bf16*)npos, (const bf16*)win, bin, (bf16*)kc,
                   (bf16*)vc, i, Lmax, anc, (const bf16*)wo, slab, R, xin, slabs, nslab, b2,
                   gamma, beta, eps, qpos, xout};
+  a.xcd = retr_tune_get(RETR_TUNE_DEC_ORDER) == 0;
   const float scale = 1.0f / sqrtf((float)MR_HD);
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(R / rb * H));
@@ -983,6 +1008,7 @@ int retr_dec_cross_heads_mr(const float* slab_in, const float* x, const float* b
   if (R == 0) return 0;
   CrossHeadsArgs a{slab_in, x, bo_in, xo, gamma, beta, eps, pos, (const bf16*)wq, bq,
                    (const bf16*)k, (const bf16*)v, Lk, kv_group, kpm, (const bf16*)wo, slab_out, R};
+  a.xcd = retr_tune_get(RETR_TUNE_DEC_ORDER) == 0;
   const float scale = 1.0f / sqrtf((float)MR_HD);
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)(R / rb * H));
