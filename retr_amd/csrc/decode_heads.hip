@@ -587,24 +587,26 @@ constexpr int MR_OLD = MR_HD + 8;                 // staged out-projection rows 
 // rows [row0, row0 + nrows) x [col0, col0 + ncols) of a bf16 matrix (ld elements) staged into LDS
 // rows of dld elements, 16-byte chunks over the block's NT threads: load() issues every chunk
 // (at most N per thread) before store() writes any, so the staging costs one memory round trip
-template <int N, int NT>
+template <int N, int NT, int NCOLS>
 struct Stager {
+  static constexpr int CPR = NCOLS / 8;           // 16-byte chunks per row (power of two)
+  static_assert((CPR & (CPR - 1)) == 0, "chunks per row");
   bf16x8 t[N];
-  int cpr, total;
+  int total;
   RETR_DEVICE void load(const bf16* __restrict__ src, long ld, int row0, int col0, int nrows,
-                        int ncols, int tid) {
-    cpr = ncols / 8;
-    total = nrows * cpr;
+                        int tid) {
+    total = nrows * CPR;
+    const bf16* base = src + (long)row0 * ld + col0;
 #pragma unroll
     for (int it = 0; it < N; ++it) {
-      const int q = tid + it * NT, rr = q / cpr, cc = q - rr * cpr;
-      if (q < total) t[it] = *(const bf16x8*)(src + (long)(row0 + rr) * ld + col0 + 8 * cc);
+      const int q = tid + it * NT, rr = q / CPR, cc = q % CPR;
+      if (q < total) t[it] = *(const bf16x8*)(base + rr * ld + 8 * cc);
     }
   }
   RETR_DEVICE void store(bf16* dst, int dld, int tid) const {
 #pragma unroll
     for (int it = 0; it < N; ++it) {
-      const int q = tid + it * NT, rr = q / cpr, cc = q - rr * cpr;
+      const int q = tid + it * NT, rr = q / CPR, cc = q % CPR;
       if (q < total) *(bf16x8*)(dst + rr * dld + 8 * cc) = t[it];
     }
   }
@@ -639,12 +641,12 @@ __global__ void __launch_bounds__(128 * RB) dec_self_heads_mr_kernel(SelfHeadsAr
               lane);
   constexpr int NT = 128 * RB;
   // the head's q | k | v rows and out-projection columns, staged once per block
-  Stager<(HD * C / 8 + NT - 1) / NT, NT> sq, sk, sv;
-  Stager<(C * HD / 8 + NT - 1) / NT, NT> so;
-  sq.load(a.win, C, h * HD, 0, HD, C, tid);
-  sk.load(a.win, C, C + h * HD, 0, HD, C, tid);
-  sv.load(a.win, C, 2 * C + h * HD, 0, HD, C, tid);
-  so.load(a.wo, C, 0, h * HD, C, HD, tid);
+  Stager<(HD * C / 8 + NT - 1) / NT, NT, C> sq, sk, sv;
+  Stager<(C * HD / 8 + NT - 1) / NT, NT, HD> so;
+  sq.load(a.win, C, h * HD, 0, HD, tid);
+  sk.load(a.win, C, C + h * HD, 0, HD, tid);
+  sv.load(a.win, C, 2 * C + h * HD, 0, HD, tid);
+  so.load(a.wo, C, 0, h * HD, C, tid);
   // the row's own operands: prologue slab share, activations, cached keys / values
   float ps[CPL];
 #pragma unroll
@@ -780,14 +782,14 @@ __global__ void __launch_bounds__(128 * RB) dec_cross_heads_mr_kernel(CrossHeads
   const int kvb = r / a.kv_group, Lk = a.Lk;
   const unsigned char* km = a.kpm ? a.kpm + (long)kvb * Lk : nullptr;
   constexpr int NT = 128 * RB;
-  Stager<(HD * C / 8 + NT - 1) / NT, NT> sq;
-  Stager<(C * HD / 8 + NT - 1) / NT, NT> so;
-  Stager<KVS ? (KMAX * HD / 8 + NT - 1) / NT : 1, NT> skk, svv;
-  sq.load(a.wq, C, h * HD, 0, HD, C, tid);
-  so.load(a.wo, C, 0, h * HD, C, HD, tid);
+  Stager<(HD * C / 8 + NT - 1) / NT, NT, C> sq;
+  Stager<(C * HD / 8 + NT - 1) / NT, NT, HD> so;
+  Stager<KVS ? (KMAX * HD / 8 + NT - 1) / NT : 1, NT, HD> skk, svv;
+  sq.load(a.wq, C, h * HD, 0, HD, tid);
+  so.load(a.wo, C, 0, h * HD, C, tid);
   if constexpr (KVS) {
-    skk.load(a.k, C, kvb * Lk, h * HD, Lk, HD, tid);
-    svv.load(a.v, C, kvb * Lk, h * HD, Lk, HD, tid);
+    skk.load(a.k, C, kvb * Lk, h * HD, Lk, tid);
+    svv.load(a.v, C, kvb * Lk, h * HD, Lk, tid);
   }
   WaveAttn<HD, 1, 8> at;
   at.load_mask(km, w * KPW, min(Lk, (w + 1) * KPW), lane);
