@@ -1216,7 +1216,7 @@ static_assert(sizeof(CWProb) == 96 && sizeof(CWHead) == 80 && sizeof(CWPiece) ==
 constexpr int kCWChunk = 4;
 constexpr int kCWMaxSlices = 128;   // per problem (the plan caps the split count at 128)
 
-template <int KIND, int NW>
+template <int KIND, int NW, int BN = 128>
 __global__ void __launch_bounds__(NW * 64) conv_wgrad_group_kernel(const char* __restrict__ table,
                                                                    int chunk) {
   const CWHead& h = *(const CWHead*)table;
@@ -1257,18 +1257,21 @@ __global__ void __launch_bounds__(NW * 64) conv_wgrad_group_kernel(const char* _
   EpiAccF32 ep{d.ws, (long)Ncols, 0, d.vec, 1, nullptr};
   ep.split_stride = (long)R * Ncols;
   ep.split = split;
-  constexpr int WM = NW == 8 ? 4 : 2;
+  // 128 x 128: 4 waves (2 x 2) or 8 (4 x 2); 128 x 256 (opt-in): 8 waves (2 x 4) of 64 x 64, the
+  // dY panel re-read by half as many column tiles, fp32 epilogue in two row bands
+  constexpr int WM = BN == 256 ? 2 : (NW == 8 ? 4 : 2), WN = NW / WM;
+  constexpr int EPB = BN == 256 ? 2 : 0;
   if constexpr (KIND == 0) {
     const DenseT<bf16> lb{d.x, (long)g.C, Ncols, Mp};
-    gemm2_tile<kFamConvWgrad, 128, 128, WM, 2, 2, 0>(la, lb, ep, R, Ncols, Mp, d.kchunk,
-                                                     d.tiles_n, tile, split);
+    gemm2_tile<kFamConvWgrad, 128, BN, WM, WN, 2, EPB>(la, lb, ep, R, Ncols, Mp, d.kchunk,
+                                                       d.tiles_n, tile, split);
   } else {
     constexpr int BK = 64;
     const int qq = BK / g.OW, rr = BK % g.OW;
     const ConvWgradB32<bf16> lb{d.x, g, Ncols, Mp, qq, rr, (qq * g.s * g.W + rr * g.s) * g.C,
                                 g.s * g.W * g.C - g.OW * g.s * g.C, (g.H - g.OH * g.s) * g.W * g.C};
-    gemm2_tile<kFamConvWgrad, 128, 128, WM, 2, 2, 0>(la, lb, ep, R, Ncols, Mp, d.kchunk,
-                                                     d.tiles_n, tile, split);
+    gemm2_tile<kFamConvWgrad, 128, BN, WM, WN, 2, EPB>(la, lb, ep, R, Ncols, Mp, d.kchunk,
+                                                       d.tiles_n, tile, split);
   }
 }
 
@@ -1619,6 +1622,9 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
         ord.push_back(i);
       }
     if (ord.empty()) continue;
+    // RETR_TUNE_CW_WAVES 3: the 128 x 256 tile for this kind (sweeps)
+    const int wl = retr_tune_get(RETR_TUNE_CW_WAVES);
+    const int bn = wl == 3 ? 256 : 128;
     auto blk_len = [&](int i) {
       const Geom g = make_geom(d[i].Nb, d[i].H, d[i].W, d[i].C, d[i].Co, d[i].KH, d[i].KW,
                                d[i].stride, d[i].pad, d[i].dil);
@@ -1643,7 +1649,7 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
       p.splits = cdiv(Mp, p.kchunk);
       RETR_REQUIRE(p.splits == q.splits, "conv2d_wgrad_group[%d]: splits %d != plan %d", ord[j],
                    p.splits, q.splits);
-      p.tiles_n = cdiv(Ncols, 128);
+      p.tiles_n = cdiv(Ncols, bn);
       p.tiles = cdiv(g.Co, 128) * p.tiles_n;
       p.blk0 = blocks;
       p.vec = vec8_ok<float>(q.ws, (long)Ncols) ? 1 : 0;
@@ -1690,20 +1696,23 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
     int chunk = retr_tune_get(RETR_TUNE_CW_CHUNK);
     chunk = chunk > 0 ? chunk : (chunk < 0 ? 0 : kCWChunk);
     const int grid = chunk > 0 ? cdiv(blocks, 8 * chunk) * 8 * chunk : 8 * xmax;
-    constexpr size_t lds = gemm2_lds_bytes<128, 128, 2, 0>();
-    const int wl = retr_tune_get(RETR_TUNE_CW_WAVES);
     const int nw = wl == 1 ? 4 : wl == 2 ? 8 : (kind == 0 ? 4 : 8);
-    auto launch = [&](auto kern, int threads) {
+    auto launch = [&](auto kern, int threads, size_t lds) {
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, st, (const char*)table, chunk);
     };
-    if (kind == 0) {
-      if (nw == 4) launch(conv_wgrad_group_kernel<0, 4>, 256);
-      else launch(conv_wgrad_group_kernel<0, 8>, 512);
+    constexpr size_t lds = gemm2_lds_bytes<128, 128, 2, 0>();
+    constexpr size_t lds256 = gemm2_lds_bytes<128, 256, 2, 2>();
+    if (bn == 256) {
+      if (kind == 0) launch(conv_wgrad_group_kernel<0, 8, 256>, 512, lds256);
+      else launch(conv_wgrad_group_kernel<1, 8, 256>, 512, lds256);
+    } else if (kind == 0) {
+      if (nw == 4) launch(conv_wgrad_group_kernel<0, 4>, 256, lds);
+      else launch(conv_wgrad_group_kernel<0, 8>, 512, lds);
     } else {
-      if (nw == 4) launch(conv_wgrad_group_kernel<1, 4>, 256);
-      else launch(conv_wgrad_group_kernel<1, 8>, 512);
+      if (nw == 4) launch(conv_wgrad_group_kernel<1, 4>, 256, lds);
+      else launch(conv_wgrad_group_kernel<1, 8>, 512, lds);
     }
     if (int e = retr_check_launch(kind == 0 ? "conv2d_wgrad_group 1x1" : "conv2d_wgrad_group")) return e;
     // the next kind's table must not overwrite this one before the launch has read it: use

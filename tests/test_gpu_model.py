@@ -659,3 +659,35 @@ def test_deferred_weight_used_twice_flushes_before_second_contribution():
         r = single[0][n].double() + single[1][n].double()
         e = ((g1[n].double() - r).norm() / r.norm()).item()
         assert e < 1e-5, (n, e)
+
+
+def test_grouped_conv_wgrad_tile_layouts_bitwise():
+    """The grouped conv weight-gradient launches under every tile layout (RETR_TUNE_CW_WAVES:
+    128 x 128 on 4 or 8 waves, 128 x 256 on 8 waves) give bitwise-equal gradients: the same
+    K-slices, each output element's MFMA chain over the slice in the same order."""
+    from retr_amd import _lib, resnet
+    cfg = make_config(backbone="ResNet50", hidden=64, layers=(1, 1), vocab=1000, max_pos=16,
+                      ffn=128, dtype="bf16", dropout=0.0)
+    model, crit = build_model(cfg)
+    model.load_state_dict(synthetic_state_dict(model, seed=6))
+    model.to(DEV).train()
+    images, mask = synthetic_images(2, 256, seed=3, pad_band=True)
+    caps, cap_mask = synthetic_captions(2, 16, 1000, seed=4)
+    s = NestedTensor(images.to(DEV), mask.to(DEV))
+    res = []
+    try:
+        resnet.CONV_WGRAD_GROUP = True
+        for layout in (0, 1, 2, 3):
+            _lib.load().retr_tune(29, layout)
+            model.zero_grad(set_to_none=True)
+            out = model(s, caps[:, :-1].to(DEV), cap_mask[:, :-1].to(DEV))
+            crit(out.permute(0, 2, 1), caps[:, 1:].to(DEV)).backward()
+            torch.cuda.synchronize()
+            res.append({n: p.grad.detach().clone() for n, p in model.named_parameters()
+                        if p.grad is not None and n.startswith("backbone")})
+    finally:
+        _lib.load().retr_tune(29, 0)
+    assert len(res[0]) > 20
+    for r in res[1:]:
+        for n in res[0]:
+            assert torch.equal(r[n], res[0][n]), n

@@ -87,6 +87,7 @@ VARIANTS = {
     "orders_aff": {("TUNE", 19): -1, ("TUNE", 20): -1},
     "cw_w4": {("TUNE", 29): 1},
     "cw_w8": {("TUNE", 29): 2},
+    "cw_256": {("TUNE", 29): 3},
 }
 
 
