@@ -652,6 +652,16 @@ int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_i
                          const float* pos, const void* wq, const float* bq, const void* k,
                          const void* v, int Lk, int kv_group, const unsigned char* kpm,
                          const void* wo, float* slab_out, void* stream);
+/* retr_dec_self_heads_ln for the first decoder layer with the DecoderEmbeddings in the prologue:
+ * x = LN(word[tok[r]] + qpos; ge, be, epse) -> xout (models/transformer_modules.py:118-127), then
+ * LN1 (gamma, beta, eps) and the self sub-layer -- replaces retr_dec_embed_rows +
+ * retr_dec_self_heads.  Head dim 32, at most 128 keys. */
+int retr_dec_self_heads_embed(const long long* tok, const float* word, const float* ge,
+                              const float* be, float epse, int R, int C, int H, const void* win,
+                              const float* bin, void* kc, void* vc, int i, int Lmax,
+                              const int* anc, const void* wo, float* slab, const float* gamma,
+                              const float* beta, float eps, const float* qpos, float* xout,
+                              void* stream);
 /* Multi-row variants (beam search): rb rows x one head per block, the head's weight slices (and
  * the memory keys / values when kv_group % rb == 0) staged in LDS once per block.  Same operands
  * and results as retr_dec_self_heads_ln / retr_dec_cross_heads; C = 256, H = 8, rb in {1, 2, 4,

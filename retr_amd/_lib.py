@@ -212,6 +212,8 @@ _SIGS = {
     "retr_dec_self_heads": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P],
     "retr_dec_cross_heads": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I,
                              _P, _P, _P, _P],
+    "retr_dec_self_heads_embed": [_P, _P, _P, _P, _F, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P,
+                                  _P, _P, _P, _P, _F, _P, _P, _P],
     "retr_dec_self_heads_mr": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _I,
                                _P, _P, _P, _F, _P, _P, _I, _P],
     "retr_dec_cross_heads_mr": [_P, _P, _P, _P, _I, _I, _I, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I,

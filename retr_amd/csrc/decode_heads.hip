@@ -311,6 +311,14 @@ struct SelfHeadsArgs {
   const float* qpos;
   float* xout;
   bool xcd = true;      // dec_block_rh order (RETR_TUNE_DEC_ORDER)
+  // embedding prologue (tok != null, layer 0; xin / slabs unused): x = LN_e(word[tok] + qpos)
+  // (DecoderEmbeddings) -> xout (block h = 0), then LN1 as above -- instead of a
+  // retr_dec_embed_rows launch before the first layer
+  const long long* tok = nullptr;
+  const float* word = nullptr;
+  const float* ge = nullptr;
+  const float* be = nullptr;
+  float epse = 0.f;
 };
 
 // One block of NW waves per (row, head): wave w computes rows [w HD / NW, (w + 1) HD / NW) of
@@ -331,7 +339,9 @@ __global__ void __launch_bounds__(64 * NW) dec_self_heads_kernel(SelfHeadsArgs a
   dec_block_rh(blockIdx.x, a.R, H, a.xcd, r, h);
   const int* ar = a.anc ? a.anc + (long)r * a.Lmax : nullptr;
   const int i = a.i, Lmax = a.Lmax;
-  const bool pro = a.xin != nullptr;
+  const bool emb = a.tok != nullptr;
+  const bool pro = a.xin != nullptr || emb;
+  const long long tokr = emb ? a.tok[r] : 0;
   WaveAttn<HD, NCH, KU> at;
   at.set_rows(w * KPW, min(i + 1, (w + 1) * KPW),
               [&](int j) -> long {
@@ -346,7 +356,10 @@ __global__ void __launch_bounds__(64 * NW) dec_self_heads_kernel(SelfHeadsArgs a
   float ps[CPL];
 #pragma unroll
   for (int e = 0; e < CPL; ++e) ps[e] = 0.f;
-  if (pro) {
+  if (emb) {                                   // the token's word-embedding chunk
+#pragma unroll
+    for (int e = 0; e < CPL; e += 4) *(f4v*)(ps + e) = *(const f4v*)(a.word + tokr * C + c0 + e);
+  } else if (pro) {
     const long RC = (long)a.R * C;
     const int s0 = w * a.nslab / NW, s1 = (w + 1) * a.nslab / NW;
     for (int j = s0; j < s1; j += 8) {
@@ -383,27 +396,55 @@ __global__ void __launch_bounds__(64 * NW) dec_self_heads_kernel(SelfHeadsArgs a
   const float bk = lane < ND ? a.bin[C + h * HD + d] : 0.f;
   const float bv = lane < ND ? a.bin[2 * C + h * HD + d] : 0.f;
   if (pro) {
-    // x = xin + (slab partials in wave order + b2); LN1 (+ qpos) -> LDS (bf16)
+    // x = xin + (slab partials in wave order + b2), or the token embedding; LN1 (+ qpos) -> LDS
     float xv[CPL], b2[CPL], gm[CPL], bt[CPL], qp[CPL];
 #pragma unroll
     for (int e = 0; e < CPL; e += 4) {
-      *(f4v*)(xv + e) = *(const f4v*)(a.xin + (long)r * C + c0 + e);
-      *(f4v*)(b2 + e) = *(const f4v*)(a.b2 + c0 + e);
+      if (emb) {
+        *(f4v*)(xv + e) = *(const f4v*)(a.ge + c0 + e);
+        *(f4v*)(b2 + e) = *(const f4v*)(a.be + c0 + e);
+      } else {
+        *(f4v*)(xv + e) = *(const f4v*)(a.xin + (long)r * C + c0 + e);
+        *(f4v*)(b2 + e) = *(const f4v*)(a.b2 + c0 + e);
+      }
       *(f4v*)(gm + e) = *(const f4v*)(a.gamma + c0 + e);
       *(f4v*)(bt + e) = *(const f4v*)(a.beta + c0 + e);
       *(f4v*)(qp + e) = *(const f4v*)(a.qpos + c0 + e);
     }
-#pragma unroll
-    for (int e = 0; e < CPL; ++e) part[w][c0 + e] = ps[e];
-    __syncthreads();
     float v[CPL], sm = 0.f;
+    if (emb) {
+      // DecoderEmbeddings: LN_e(word + position) (ps holds the word chunk; xv / b2 = ge / be)
+      float u[CPL], su = 0.f;
 #pragma unroll
-    for (int e = 0; e < CPL; ++e) {
-      float t = 0.f;
+      for (int e = 0; e < CPL; ++e) {
+        u[e] = ps[e] + qp[e];
+        su += u[e];
+      }
+      const float me = wave_sum(su) / C;
+      float qe = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < NW; ++ww) t += part[ww][c0 + e];
-      v[e] = xv[e] + (t + b2[e]);
-      sm += v[e];
+      for (int e = 0; e < CPL; ++e) {
+        const float dd = u[e] - me;
+        qe += dd * dd;
+      }
+      const float re = 1.0f / sqrtf(wave_sum(qe) / C + a.epse);
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) {
+        v[e] = (u[e] - me) * re * xv[e] + b2[e];
+        sm += v[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) part[w][c0 + e] = ps[e];
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) {
+        float t = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) t += part[ww][c0 + e];
+        v[e] = xv[e] + (t + b2[e]);
+        sm += v[e];
+      }
     }
     if (h == 0 && w == 0) {
 #pragma unroll
@@ -925,6 +966,39 @@ int retr_dec_self_heads_ln(const void* n, const void* npos, int R, int C, int H,
 #undef SH_N
 #undef SH
   return retr_check_launch("dec_self_heads");
+}
+
+int retr_dec_self_heads_embed(const long long* tok, const float* word, const float* ge,
+                              const float* be, float epse, int R, int C, int H, const void* win,
+                              const float* bin, void* kc, void* vc, int i, int Lmax,
+                              const int* anc, const void* wo, float* slab, const float* gamma,
+                              const float* beta, float eps, const float* qpos, float* xout,
+                              void* stream) {
+  RETR_REQUIRE(tok && word && ge && be && gamma && beta && qpos && xout,
+               "dec_self_heads_embed: missing operands");
+  const int hd = H > 0 ? C / H : 0;
+  RETR_REQUIRE((C == 256 || C == 512) && hd == 32 && hd * H == C,
+               "dec_self_heads_embed: C=%d H=%d unsupported", C, H);
+  RETR_REQUIRE(i >= 0 && i < Lmax && i + 1 <= 128,
+               "dec_self_heads_embed: step %d (cache %d rows, at most 128 keys)", i, Lmax);
+  if (R == 0) return 0;
+  SelfHeadsArgs a{nullptr, nullptr, (const bf16*)win, bin, (bf16*)kc, (bf16*)vc, i, Lmax, anc,
+                  (const bf16*)wo, slab, R, nullptr, nullptr, 0, nullptr, gamma, beta, eps, qpos,
+                  xout};
+  a.xcd = retr_tune_get(RETR_TUNE_DEC_ORDER) == 0;
+  a.tok = tok;
+  a.word = word;
+  a.ge = ge;
+  a.be = be;
+  a.epse = epse;
+  const float scale = 1.0f / sqrtf((float)hd);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)(R * H));
+  if (C == 256)
+    hipLaunchKernelGGL((dec_self_heads_kernel<256, 32, 2, 1, 4>), grid, dim3(128), 0, st, a, scale);
+  else
+    hipLaunchKernelGGL((dec_self_heads_kernel<512, 32, 2, 1, 4>), grid, dim3(128), 0, st, a, scale);
+  return retr_check_launch("dec_self_heads_embed");
 }
 
 int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_in, float* xo,

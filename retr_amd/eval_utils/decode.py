@@ -50,6 +50,8 @@ DEC_HEADS = True
 DEC_FFN_LN = True
 # (with DEC_FFN_LN) the FFN residual + the next layer's LN1 in the self-attention prologue
 DEC_FOLD_ROWS = True
+# (with DEC_FOLD_ROWS) the decoder embeddings + first LN1 in the first self-attention launch
+DEC_EMBED_FOLD = False   # measured neutral (0.248 ms/step either way): the token -> word-row load is a dependent round trip
 
 # Rows per block of the attention sub-layer kernels: None = automatic (beam groups of K rows
 # share the head's staged weights and memory keys / values: K in {2, 4, 5}), else an int for
@@ -298,20 +300,31 @@ class IncrementalGreedy:
         s = _st()
         x, xa = st.y, st.y2
         n0 = layers[0].tgt_self_attn.norm
-        call("retr_dec_embed_rows", ptr(st.tok), R, C, ptr(emb.word_embeddings.weight), ptr(qp),
-             ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias), float(emb.LayerNorm.eps), ptr(x),
-             ptr(n0.weight), ptr(n0.bias), float(n0.eps), ptr(st.n), ptr(st.npos), s)
         anc = ptr(st.anc) if self.beam else None
         nslab = F // 32
         # three launches per layer (up to 64 rows): the FFN residual + next LN1 in the next
         # layer's self-attention prologue, the cross residual + LN3 in the FFN prologue
         fold = DEC_FFN_LN and DEC_FOLD_ROWS and R <= 64 and F % 64 == 0
         rbs, rbx = _rows_per_block(R, C, H, st.K, i + 1, S)
+        # the embeddings + first LN1 in the first self-attention launch (per-row blocks)
+        embed = fold and DEC_EMBED_FOLD and rbs == 1 and C // H == 32 and i < 128
+        if not embed:
+            call("retr_dec_embed_rows", ptr(st.tok), R, C, ptr(emb.word_embeddings.weight),
+                 ptr(qp), ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias),
+                 float(emb.LayerNorm.eps), ptr(x), ptr(n0.weight), ptr(n0.bias), float(n0.eps),
+                 ptr(st.n), ptr(st.npos), s)
         for li, layer in enumerate(layers):
             sa, ca, ff = layer.tgt_self_attn, layer.tgt_src_cross_attn, layer.ff
             sub, csub = sa.sublayer, ca.sublayer
             f0, f2 = ff.sublayer[0], ff.sublayer[2]
-            if fold and li > 0:
+            if embed and li == 0:
+                call("retr_dec_self_heads_embed", ptr(st.tok), ptr(emb.word_embeddings.weight),
+                     ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias),
+                     float(emb.LayerNorm.eps), R, C, H, ptr(W(sub.in_proj_weight)),
+                     ptr(sub.in_proj_bias), ptr(st.kc[li]), ptr(st.vc[li]), i, T, anc,
+                     ptr(W(sub.out_proj.weight)), ptr(st.hslab), ptr(n0.weight), ptr(n0.bias),
+                     float(n0.eps), ptr(qp), ptr(x), s)
+            elif fold and li > 0:
                 pf2 = layers[li - 1].ff.sublayer[2]
                 call("retr_dec_self_heads_mr", None, None, R, C, H,
                      ptr(W(sub.in_proj_weight)), ptr(sub.in_proj_bias), ptr(st.kc[li]),

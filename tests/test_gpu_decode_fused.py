@@ -562,11 +562,12 @@ def test_dec_multi_row_beam_step_matches():
     B, T = 8, 128
     img, mask = synthetic_images(B, 224, seed=17, pad_band=True)
     s = NestedTensor(img.to(DEV), mask.to(DEV))
-    old = dec.DEC_ROWS_PER_BLOCK
+    old = dec.DEC_ROWS_PER_BLOCK, dec.DEC_EMBED_FOLD
     res = []
     try:
         for rb in (None, 1):
-            dec.DEC_ROWS_PER_BLOCK = rb
+            # (the embedding fold runs on per-row blocks only: off for both, same arithmetic)
+            dec.DEC_ROWS_PER_BLOCK, dec.DEC_EMBED_FOLD = rb, False
             model._retr_decode_states = {}
             bm = dec.IncrementalBeam(model, 5)
             ids = bm(s, T, 101, 102)
@@ -576,6 +577,84 @@ def test_dec_multi_row_beam_step_matches():
                 ids_e = dec.IncrementalBeam(model, 5, use_graphs=False)(s, T, 101, 102)
                 assert torch.equal(ids, ids_e)
     finally:
-        dec.DEC_ROWS_PER_BLOCK = old
+        dec.DEC_ROWS_PER_BLOCK, dec.DEC_EMBED_FOLD = old
         model._retr_decode_states = {}
     assert torch.equal(res[0], res[1])
+
+
+def test_dec_self_heads_embed_matches_embed_rows_then_heads():
+    """retr_dec_self_heads_embed (DecoderEmbeddings + LN1 in the first self-attention launch)
+    against retr_dec_embed_rows + retr_dec_self_heads on the same operands: residual x within
+    fp32 reassociation of the LayerNorm sums, head partials and cache rows within bf16 rounding."""
+    C, H, R, T, i, V = 256, 8, 16, 32, 11, 500
+    g = _g(77)
+    bf = lambda t: t.to(DEV).bfloat16()                       # noqa: E731
+    tok = torch.randint(0, V, (R,), generator=g).to(DEV)
+    word = torch.randn(V, C, generator=g).to(DEV)
+    qp = torch.randn(C, generator=g).to(DEV)
+    ge, g1 = [(torch.rand(C, generator=g) + 0.5).to(DEV) for _ in range(2)]
+    be, b1 = [(torch.randn(C, generator=g) * 0.1).to(DEV) for _ in range(2)]
+    win = bf(torch.randn(3 * C, C, generator=g) / math.sqrt(C))
+    bin_ = torch.randn(3 * C, generator=g).to(DEV) * 0.1
+    kc = bf(torch.randn(R * T, C, generator=g))
+    vc = bf(torch.randn(R * T, C, generator=g))
+    wo = bf(torch.randn(C, C, generator=g) / math.sqrt(C))
+    outs = []
+    for fused in (True, False):
+        k1, v1 = kc.clone(), vc.clone()
+        x = torch.full((R, C), float("nan"), device=DEV)
+        slab = torch.full((H, R, C), float("nan"), device=DEV)
+        if fused:
+            call("retr_dec_self_heads_embed", ptr(tok), ptr(word), ptr(ge), ptr(be), 1e-12, R, C,
+                 H, ptr(win), ptr(bin_), ptr(k1), ptr(v1), i, T, None, ptr(wo), ptr(slab),
+                 ptr(g1), ptr(b1), 1e-5, ptr(qp), ptr(x), ops._st())
+        else:
+            n = torch.empty(R, C, dtype=torch.bfloat16, device=DEV)
+            npos = torch.empty_like(n)
+            call("retr_dec_embed_rows", ptr(tok), R, C, ptr(word), ptr(qp), ptr(ge), ptr(be),
+                 1e-12, ptr(x), ptr(g1), ptr(b1), 1e-5, ptr(n), ptr(npos), ops._st())
+            call("retr_dec_self_heads", ptr(n), ptr(npos), R, C, H, ptr(win), ptr(bin_),
+                 ptr(k1), ptr(v1), i, T, None, ptr(wo), ptr(slab), ops._st())
+        torch.cuda.synchronize()
+        outs.append((x, slab, k1, v1))
+    (x1, s1, k1, v1), (x0, s0, k0, v0) = outs
+    ref = F.layer_norm(word[tok] + qp, (C,), ge, be, 1e-12)
+    assert _rel(x0, ref) < 1e-5 and _rel(x1, ref) < 1e-5
+    assert _rel(s1, s0) < 2e-2
+    assert _rel(k1.float(), k0.float()) < 1e-2 and _rel(v1.float(), v0.float()) < 1e-2
+
+
+@pytest.mark.parametrize("embed", [True, False])
+def test_dec_embed_fold_step_matches(embed):
+    """The decode step with the embeddings folded into the first self-attention launch
+    (DEC_EMBED_FOLD) against the separate embed launch on the cfg5 model: first-step logits
+    within bf16 rounding, graphs == eager."""
+    from bench import build, cfg5
+    from retr_amd.eval_utils import decode as dec
+    from retr_amd.synthetic import synthetic_images
+    model, _ = build(cfg5(), DEV)
+    model.eval()
+    B, T = 16, 128
+    img, mask = synthetic_images(B, 224, seed=21, pad_band=True)
+    s = NestedTensor(img.to(DEV), mask.to(DEV))
+    old = dec.DEC_EMBED_FOLD
+    res = []
+    try:
+        for f in (embed, False):
+            dec.DEC_EMBED_FOLD = f
+            model._retr_decode_states = {}
+            gr = dec.IncrementalGreedy(model)
+            ids = gr(s, T, 101, 102)
+            st = next(v for k, v in model._retr_decode_states.items() if k[0] == "IncrementalGreedy")
+            with torch.no_grad():
+                gr._reset(st, 101)
+                gr._step(st, 0, 102)
+                torch.cuda.synchronize()
+                res.append(st.logits.float().clone())
+            if f:
+                ids_e = dec.IncrementalGreedy(model, use_graphs=False)(s, T, 101, 102)
+                assert torch.equal(ids, ids_e)
+    finally:
+        dec.DEC_EMBED_FOLD = old
+        model._retr_decode_states = {}
+    assert _rel(res[0], res[1]) < 2e-2
