@@ -180,9 +180,10 @@ enum {
   RETR_TUNE_DEC_ORDER = 30,     /* decode attention blocks (retr_dec_*_heads*): 0 a row's (or beam
                                    group's) head blocks on one XCD (its L2 holds the row's partial
                                    slabs and whole K / V cache lines), 1 block b = (b / H, b % H) */
-  RETR_TUNE_DEC_WAVES = 31,     /* per-(row, head) decode attention blocks (C 256, hd 32, <= 128
-                                   self / 256 memory keys): 0 four waves (greedy 0.250 -> 0.244
-                                   ms/step), 1 two */
+  RETR_TUNE_DEC_WAVES = 31,     /* decode wave layouts (C 256): 0 four waves per (row, head)
+                                   attention block (hd 32, <= 128 self / 256 memory keys; greedy
+                                   0.250 -> 0.244 ms/step) and eight per FFN block; 1 two / four
+                                   (round-5 kernels as first built); 2 four / four */
   RETR_TUNE_COUNT = 32
 };
 int retr_tune(int knob, int value);

@@ -821,15 +821,16 @@ dec_ffn_kernel(const bf16* n3, int R, const bf16* w1, const float* b1, const bf1
 // n3 = bf16(LN3(x)) into LDS; waves 0 / 1 then the FFN1 column tile w (16 hidden units), and every
 // wave 4 of the 16 FFN2 column tiles -- instead of a retr_dec_rows launch between the per-head
 // cross-attention partials (csrc/decode_heads.hip) and the FFN.
-template <int PER, int MAXS, int HB>
-__global__ void __launch_bounds__(256)
+template <int PER, int MAXS, int HB, int NWV = 4>
+__global__ void __launch_bounds__(64 * NWV)
 dec_ffn_ln_kernel(const float* xin, const float* hslab, int nslab, const float* bo,
                   const float* gamma, const float* beta, float eps, float* xout, int R,
                   const bf16* w1, const float* b1, const bf16* w2, int F, float* slabs) {
   constexpr int C = PER * 64;
   constexpr int HS = HB + 8, AS = C + 8;
   constexpr int CPL = C / 64;                     // consecutive columns per lane
-  constexpr int NT = C / 16, NTW = NT / 4;        // FFN2 column tiles, per wave
+  constexpr int NT = C / 16, NTW = NT / NWV;      // FFN2 column tiles, per wave
+  constexpr int RPW = 16 / NWV;                   // LayerNorm rows per wave
   constexpr int T1 = HB / 16;                     // FFN1 column tiles (waves 0 .. T1-1)
   constexpr int K2 = HB / 32;                     // FFN2 K-steps
   typedef __attribute__((ext_vector_type(4))) float f4v;
@@ -861,11 +862,11 @@ dec_ffn_ln_kernel(const float* xin, const float* hslab, int nslab, const float* 
     *(f4v*)(gm + e) = *(const f4v*)(gamma + c0 + e);
     *(f4v*)(bt + e) = *(const f4v*)(beta + c0 + e);
   }
-  // the wave's 4 rows: every slab / residual load in flight at once
-  float t[4][MAXS][CPL], xv[4][CPL];
+  // the wave's RPW rows: every slab / residual load in flight at once
+  float t[RPW][MAXS][CPL], xv[RPW][CPL];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = r0 + 4 * w + q;
+  for (int q = 0; q < RPW; ++q) {
+    const int r = r0 + RPW * w + q;
     const int rr = r < R ? r : R - 1;
 #pragma unroll
     for (int j = 0; j < MAXS; ++j)
@@ -877,8 +878,8 @@ dec_ffn_ln_kernel(const float* xin, const float* hslab, int nslab, const float* 
     for (int e = 0; e < CPL; e += 4) *(f4v*)(&xv[q][e]) = *(const f4v*)(xin + (long)rr * C + c0 + e);
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = r0 + 4 * w + q;
+  for (int q = 0; q < RPW; ++q) {
+    const int r = r0 + RPW * w + q;
     float v[CPL];
 #pragma unroll
     for (int e = 0; e < CPL; ++e) {
@@ -901,7 +902,7 @@ dec_ffn_ln_kernel(const float* xin, const float* hslab, int nslab, const float* 
     const float rstd = 1.0f / sqrtf(wave_sum(qq) / C + eps);
 #pragma unroll
     for (int e = 0; e < CPL; ++e)
-      As[(4 * w + q) * AS + c0 + e] = (bf16)((v[e] - mean) * rstd * gm[e] + bt[e]);
+      As[(RPW * w + q) * AS + c0 + e] = (bf16)((v[e] - mean) * rstd * gm[e] + bt[e]);
     if (blockIdx.x == 0 && r < R) {
 #pragma unroll
       for (int e = 0; e < CPL; e += 4) *(f4v*)(xout + (long)r * C + c0 + e) = *(f4v*)(v + e);
@@ -1082,10 +1083,23 @@ int retr_dec_ffn_ln64(const float* xin, const float* hslab, int nslab, const flo
   if (R == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(F / 64, cdiv(R, 16));
+  // 8 waves (2 LayerNorm rows, 2 FFN2 column tiles each) unless RETR_TUNE_DEC_WAVES asks for 4
+  const int kn = retr_tune_get(RETR_TUNE_DEC_WAVES);
+  const bool w8 = C == 256 && nslab <= 8 && kn != 1 && kn != 2;
+  if (w8 && kn == 3) {                     // sweeps: 16 waves (one LayerNorm row, one FFN2 tile)
+    hipLaunchKernelGGL((dec_ffn_ln_kernel<4, 8, 64, 16>), grid, dim3(1024), 0, st, xin, hslab,
+                       nslab, bo, gamma, beta, eps, xout, R, (const bf16*)w1, b1,
+                       (const bf16*)w2, F, slabs);
+    return retr_check_launch("dec_ffn_ln64");
+  }
 #define FL(P, MS) hipLaunchKernelGGL((dec_ffn_ln_kernel<P, MS, 64>), grid, dim3(256), 0, st, xin, \
                                      hslab, nslab, bo, gamma, beta, eps, xout, R,                  \
                                      (const bf16*)w1, b1, (const bf16*)w2, F, slabs)
-  if (C == 256) { if (nslab <= 8) FL(4, 8); else FL(4, 16); }
+  if (w8)
+    hipLaunchKernelGGL((dec_ffn_ln_kernel<4, 8, 64, 8>), grid, dim3(512), 0, st, xin, hslab, nslab,
+                       bo, gamma, beta, eps, xout, R, (const bf16*)w1, b1, (const bf16*)w2, F,
+                       slabs);
+  else if (C == 256) { if (nslab <= 8) FL(4, 8); else FL(4, 16); }
   else { if (nslab <= 8) FL(8, 8); else FL(8, 16); }
 #undef FL
   return retr_check_launch("dec_ffn_ln64");

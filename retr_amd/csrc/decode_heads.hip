@@ -959,7 +959,7 @@ int retr_dec_self_heads_ln(const void* n, const void* npos, int R, int C, int H,
   else if (nk <= 2 * np * 8) SH(CV, HDV, 1, 2, 8);               \
   else SH(CV, HDV, 1, 4, 8);
   RETR_REQUIRE(nk <= 4 * np * 8, "dec_self_heads: %d keys (at most %d)", nk, 4 * np * 8);
-  if (C == 256 && hd == 32 && nk <= 128 && retr_tune_get(RETR_TUNE_DEC_WAVES) == 0)
+  if (C == 256 && hd == 32 && nk <= 128 && retr_tune_get(RETR_TUNE_DEC_WAVES) != 1)
     SH(256, 32, 4, 1, 2);
   else if (C == 256 && hd == 32) { SH_N(256, 32) }
   else if (C == 256) { SH_N(256, 64) }
@@ -1026,7 +1026,7 @@ int retr_dec_cross_heads(const float* slab_in, const float* x, const float* bo_i
 #define XH_N(CV, HDV) \
   if (Lk <= 2 * per) XH(CV, HDV, 1); else XH(CV, HDV, 2);
   RETR_REQUIRE(Lk <= 4 * per, "dec_cross_heads: %d memory keys (at most %d)", Lk, 4 * per);
-  if (C == 256 && hd == 32 && Lk <= 256 && retr_tune_get(RETR_TUNE_DEC_WAVES) == 0)
+  if (C == 256 && hd == 32 && Lk <= 256 && retr_tune_get(RETR_TUNE_DEC_WAVES) != 1)
     hipLaunchKernelGGL((dec_cross_heads_kernel<256, 32, 4, 1, 4>), grid, dim3(256), 0, st, a, scale);
   else if (C == 256 && hd == 32) { XH_N(256, 32) }
   else if (C == 256) { XH_N(256, 64) }

@@ -7,7 +7,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from retr_amd import ops
+from retr_amd import _lib, ops
 from retr_amd._lib import call, ptr
 from retr_amd.models.utils import NestedTensor
 
@@ -516,6 +516,7 @@ def test_dec_heads_multi_row_matches_per_row(rb, kv_group, prologue):
     beta = torch.randn(C, generator=g).to(DEV) * 0.1
     qpos = torch.randn(C, generator=g).to(DEV)
     outs = []
+    _lib.load().retr_tune(31, 1)          # the per-row kernels' two-wave layout (the mr layout)
     for r_b in (1, rb):
         kc1, vc1 = kc.clone(), vc.clone()
         slab = torch.full((H, R, C), float("nan"), device=DEV)
@@ -545,6 +546,7 @@ def test_dec_heads_multi_row_matches_per_row(rb, kv_group, prologue):
              ptr(kpm), ptr(wo2), ptr(slab2), r_b, ops._st())
         torch.cuda.synchronize()
         outs.append((slab, kc1, vc1, xo, slab2) + ((xout,) if prologue else ()))
+    _lib.load().retr_tune(31, 0)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
     assert not torch.isnan(outs[1][-1]).any()
@@ -568,6 +570,7 @@ def test_dec_multi_row_beam_step_matches():
         for rb in (None, 1):
             # (the embedding fold runs on per-row blocks only: off for both, same arithmetic)
             dec.DEC_ROWS_PER_BLOCK, dec.DEC_EMBED_FOLD = rb, False
+            _lib.load().retr_tune(31, 1)    # two-wave per-row kernels: the mr kernels' arithmetic
             model._retr_decode_states = {}
             bm = dec.IncrementalBeam(model, 5)
             ids = bm(s, T, 101, 102)
@@ -578,6 +581,7 @@ def test_dec_multi_row_beam_step_matches():
                 assert torch.equal(ids, ids_e)
     finally:
         dec.DEC_ROWS_PER_BLOCK, dec.DEC_EMBED_FOLD = old
+        _lib.load().retr_tune(31, 0)
         model._retr_decode_states = {}
     assert torch.equal(res[0], res[1])
 
