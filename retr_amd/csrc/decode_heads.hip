@@ -188,6 +188,47 @@ struct WaveAttn {
       }
     }
   }
+  // compute() over keys / values resident in LDS ([keys][HD] images, key j of the wave at row
+  // j): the same arithmetic, each key's K / V read inside the loops instead of held in registers
+  // from load() (NCH = 1)
+  RETR_DEVICE void compute_lds(const float* qs, const bf16* Ks, const bf16* Vs, int j0, int j1,
+                               int lane) {
+    static_assert(NCH == 1, "one chunk");
+    const int g = lane % NG, part = lane / NG;
+    const bf16x8 q = to_bf8(qs + 8 * g);
+    float sc[KU];
+    float cm = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int j = j0 + part + NPART * u;
+      const bool ok = j < j1 && !mk[0][u];
+      const bf16x8 kk8 = ok ? *(const bf16x8*)(Ks + j * HD + 8 * g) : bf16x8{};
+      float sv = dot8(q, kk8);
+      sv = gsum<NG>(sv);
+      sc[u] = ok ? sv : -INFINITY;
+      cm = fmaxf(cm, sc[u]);
+    }
+    cm = wave_max(cm);
+    const float nm = fmaxf(mx, cm);
+    if (nm != -INFINITY) {
+      const float f = mx == -INFINITY ? 0.f : __expf(mx - nm);
+      sum *= f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] *= f;
+      float cs = 0.f;
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const int j = j0 + part + NPART * u;
+        const float p = sc[u] == -INFINITY ? 0.f : __expf(sc[u] - nm);
+        cs += p;
+        const bf16x8 vv8 = sc[u] == -INFINITY ? bf16x8{} : *(const bf16x8*)(Vs + j * HD + 8 * g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += p * (float)vv8[e];
+      }
+      sum += wave_sum(cs) * (1.0f / NG);
+      mx = nm;
+    }
+  }
   // this wave's (max, sum, unnormalised P V) into LDS slot w
   RETR_DEVICE void publish(float* mxs, float* sms, float* accs, int w, int lane) {
 #pragma unroll
@@ -887,9 +928,7 @@ __global__ void __launch_bounds__(128 * RB) dec_cross_heads_mr_kernel(CrossHeads
     }
   }
   __syncthreads();                                   // staged slices + LN2 rows visible
-  if constexpr (KVS)
-    at.template load<HD>(k_s, v_s, 0, w * KPW, min(Lk, (w + 1) * KPW),
-                         [&](int j) -> long { return (long)j; }, lane);
+
   bf16x8 act[C / 64];
   {
     const int c = lane & 7;
@@ -907,7 +946,10 @@ __global__ void __launch_bounds__(128 * RB) dec_cross_heads_mr_kernel(CrossHeads
   __syncthreads();
   if (lane < ND) qs[rr][w * ND + lane] = qv;
   __syncthreads();
-  at.compute(qs[rr], nullptr, nullptr, lane);
+  if constexpr (KVS)
+    at.compute_lds(qs[rr], k_s, v_s, w * KPW, min(Lk, (w + 1) * KPW), lane);
+  else
+    at.compute(qs[rr], nullptr, nullptr, lane);
   at.publish(mxs[rr], sms[rr], accs[rr], w, lane);
   __syncthreads();
   merge_heads<HD, NW>(mxs[rr], sms[rr], accs[rr], os[rr], lane);

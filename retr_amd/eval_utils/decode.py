@@ -50,6 +50,8 @@ DEC_HEADS = True
 DEC_FFN_LN = True
 # (with DEC_FFN_LN) the FFN residual + the next layer's LN1 in the self-attention prologue
 DEC_FOLD_ROWS = True
+# rows up to which the folded (three-launch) layer is used (beyond: five launches per layer)
+DEC_FOLD_MAX_ROWS = 512
 # (with DEC_FOLD_ROWS) the decoder embeddings + first LN1 in the first self-attention launch
 DEC_EMBED_FOLD = False   # measured neutral (0.248 ms/step either way): the token -> word-row load is a dependent round trip
 
@@ -304,7 +306,7 @@ class IncrementalGreedy:
         nslab = F // 32
         # three launches per layer (up to 64 rows): the FFN residual + next LN1 in the next
         # layer's self-attention prologue, the cross residual + LN3 in the FFN prologue
-        fold = DEC_FFN_LN and DEC_FOLD_ROWS and R <= 64 and F % 64 == 0
+        fold = DEC_FFN_LN and DEC_FOLD_ROWS and R <= DEC_FOLD_MAX_ROWS and F % 64 == 0
         rbs, rbx = _rows_per_block(R, C, H, st.K, i + 1, S)
         # the embeddings + first LN1 in the first self-attention launch (per-row blocks)
         embed = fold and DEC_EMBED_FOLD and rbs == 1 and C // H == 32 and i < 128

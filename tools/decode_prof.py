@@ -26,6 +26,8 @@ def main():
                     help="1 / 0: eval_utils.decode.DEC_FOLD_ROWS (default: the module's)")
     ap.add_argument("--ffn-ln", type=int, default=None,
                     help="1 / 0: eval_utils.decode.DEC_FFN_LN (default: the module's)")
+    ap.add_argument("--fold-max-rows", type=int, default=None,
+                    help="eval_utils.decode.DEC_FOLD_MAX_ROWS (default: the module's)")
     ap.add_argument("--rows-per-block", type=int, default=None,
                     help="eval_utils.decode.DEC_ROWS_PER_BLOCK (default: automatic)")
     ap.add_argument("--block-per-row", action="store_true",
@@ -38,6 +40,8 @@ def main():
     if a.fold is not None:
         dec.DEC_FOLD_ROWS = bool(a.fold)
     dec.DEC_ROWS_PER_BLOCK = a.rows_per_block
+    if a.fold_max_rows is not None:
+        dec.DEC_FOLD_MAX_ROWS = a.fold_max_rows
     model, _ = build(cfg5(), "cuda")
     model.eval()
     img, mask = synthetic_images(a.batch, 224, seed=3000)
