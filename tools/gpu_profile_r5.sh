@@ -35,6 +35,9 @@ echo "pmc mfma done"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/dec -o run -- \
   python3 tools/decode_prof.py --reps 2 > $OUT/dec_prof.log 2>&1 || { echo "dec trace failed $?"; exit 1; }
 echo "dec trace done"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/decb -o run -- \
+  python3 tools/decode_prof.py --reps 2 --beam 5 > $OUT/decb_prof.log 2>&1 || { echo "beam trace failed $?"; exit 1; }
+echo "beam trace done"
 # summaries here (the raw traces are large): families / step breakdown / PMC tables
 T=$(find $OUT/trace -name "*.db" | head -1)
 python tools/rocprof_families.py $T > $OUT/rocprof_families.txt 2>&1
@@ -42,6 +45,8 @@ python tools/prof_step.py $T > $OUT/rocprof_step_breakdown.txt 2>&1
 python tools/prof_summary.py $T --top 60 > $OUT/rocprof_summary.txt 2>&1
 D=$(find $OUT/dec -name "*kernel_trace.csv" | head -1)
 python tools/prof_summary.py $D --top 30 > $OUT/rocprof_decode.txt 2>&1
+DB=$(find $OUT/decb -name "*kernel_trace.csv" | head -1)
+python tools/prof_summary.py $DB --top 30 > $OUT/rocprof_decode_beam.txt 2>&1
 F=$(find $OUT/pmc_fetch -name "*counter_collection.csv" | head -1)
 W=$(find $OUT/pmc_write -name "*counter_collection.csv" | head -1)
 M=$(find $OUT/pmc_mfma -name "*counter_collection.csv" | head -1)
@@ -49,5 +54,5 @@ python tools/pmc_traffic.py $F $W --out $OUT/pmc_traffic.json --steps 2 \
   --source "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) of bench.py --eager --steps 1 --warmup 1 --no-decode (round 5 final tree, $TAG)" > $OUT/pmc_traffic.txt 2>&1
 python tools/pmc_mfma.py $M --out $OUT/pmc_mfma.json --by-kernel 30 \
   --source "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_* of bench.py --eager --steps 1 --warmup 1 --no-decode ($TAG)" > $OUT/pmc_mfma.txt 2>&1
-rm -f $T $D $F $W $M
+rm -f $T $D $DB $F $W $M
 echo "summaries done"
