@@ -694,6 +694,12 @@ int retr_dec_ffn_ln64(const float* xin, const float* hslab, int nslab, const flo
                       const float* gamma, const float* beta, float eps, float* xout, int R, int C,
                       const void* w1, const float* b1, const void* w2, int F, float* slabs,
                       void* stream);
+/* ... over 128 hidden units per block (C = 256): slabs [F / 128][R][C] -- half the blocks that
+ * each re-derive their 16 rows' LayerNorm (beam rows) */
+int retr_dec_ffn_ln128(const float* xin, const float* hslab, int nslab, const float* bo,
+                       const float* gamma, const float* beta, float eps, float* xout, int R,
+                       int C, const void* w1, const float* b1, const void* w2, int F,
+                       float* slabs, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1105,6 +1105,20 @@ int retr_dec_ffn_ln64(const float* xin, const float* hslab, int nslab, const flo
   return retr_check_launch("dec_ffn_ln64");
 }
 
+int retr_dec_ffn_ln128(const float* xin, const float* hslab, int nslab, const float* bo,
+                       const float* gamma, const float* beta, float eps, float* xout, int R,
+                       int C, const void* w1, const float* b1, const void* w2, int F,
+                       float* slabs, void* stream) {
+  RETR_REQUIRE(C == 256 && F % 128 == 0 && nslab >= 0 && nslab <= 8,
+               "dec_ffn_ln128: C=%d F=%d nslab=%d (C 256, nslab <= 8)", C, F, nslab);
+  if (R == 0) return 0;
+  // 8 waves: FFN1 column tile w (16 hidden units) each, 2 FFN2 column tiles x 4 K-steps each
+  hipLaunchKernelGGL((dec_ffn_ln_kernel<4, 8, 128, 8>), dim3(F / 128, cdiv(R, 16)), dim3(512), 0,
+                     (hipStream_t)stream, xin, hslab, nslab, bo, gamma, beta, eps, xout, R,
+                     (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
+  return retr_check_launch("dec_ffn_ln128");
+}
+
 #ifdef RETR_DEC_TIMING
 int retr_dec_timing_read(long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dec_t), sizeof(long long) * 16);

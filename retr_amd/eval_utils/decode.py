@@ -52,6 +52,8 @@ DEC_FFN_LN = True
 DEC_FOLD_ROWS = True
 # rows up to which the folded (three-launch) layer is used (beyond: five launches per layer)
 DEC_FOLD_MAX_ROWS = 512
+# rows beyond which the folded FFN runs 128 hidden units per block
+DEC_FFN_HB128_ROWS = 64
 # (with DEC_FOLD_ROWS) the decoder embeddings + first LN1 in the first self-attention launch
 DEC_EMBED_FOLD = False   # measured neutral (0.248 ms/step either way): the token -> word-row load is a dependent round trip
 
@@ -308,6 +310,9 @@ class IncrementalGreedy:
         # layer's self-attention prologue, the cross residual + LN3 in the FFN prologue
         fold = DEC_FFN_LN and DEC_FOLD_ROWS and R <= DEC_FOLD_MAX_ROWS and F % 64 == 0
         rbs, rbx = _rows_per_block(R, C, H, st.K, i + 1, S)
+        # hidden units per folded-FFN block: 128 beyond DEC_FFN_HB128_ROWS rows (half the blocks
+        # re-deriving each row group's LayerNorm, half the partial slabs), else 64
+        hb = 128 if (R > DEC_FFN_HB128_ROWS and C == 256 and F % 128 == 0 and H <= 8) else 64
         # the embeddings + first LN1 in the first self-attention launch (per-row blocks)
         embed = fold and DEC_EMBED_FOLD and rbs == 1 and C // H == 32 and i < 128
         if not embed:
@@ -331,7 +336,7 @@ class IncrementalGreedy:
                 call("retr_dec_self_heads_mr", None, None, R, C, H,
                      ptr(W(sub.in_proj_weight)), ptr(sub.in_proj_bias), ptr(st.kc[li]),
                      ptr(st.vc[li]), i, T, anc, ptr(W(sub.out_proj.weight)), ptr(st.hslab),
-                     ptr(x), ptr(st.slabs), F // 64, ptr(pf2.bias), ptr(sa.norm.weight),
+                     ptr(x), ptr(st.slabs), F // hb, ptr(pf2.bias), ptr(sa.norm.weight),
                      ptr(sa.norm.bias), float(sa.norm.eps), ptr(qp), ptr(xa), rbs, s)
                 x, xa = xa, x
             else:
@@ -346,13 +351,14 @@ class IncrementalGreedy:
                  ptr(st.hslab2), rbx, s)
             x, xa = xa, x
             if fold:
-                call("retr_dec_ffn_ln64", ptr(x), ptr(st.hslab2), H, ptr(csub.out_proj.bias),
+                call("retr_dec_ffn_ln128" if hb == 128 else "retr_dec_ffn_ln64", ptr(x),
+                     ptr(st.hslab2), H, ptr(csub.out_proj.bias),
                      ptr(ff.norm.weight), ptr(ff.norm.bias), float(ff.norm.eps), ptr(xa), R, C,
                      ptr(W(f0.weight)), ptr(f0.bias), ptr(W(f2.weight)), F, ptr(st.slabs), s)
                 x, xa = xa, x
                 if li + 1 == len(layers):
                     nx = tr.decoder.norm
-                    call("retr_dec_rows", ptr(x), ptr(st.slabs), F // 64, ptr(f2.bias), R, C,
+                    call("retr_dec_rows", ptr(x), ptr(st.slabs), F // hb, ptr(f2.bias), R, C,
                          ptr(xa), ptr(nx.weight), ptr(nx.bias), float(nx.eps), None, ptr(st.n),
                          None, s)
                     x, xa = xa, x

@@ -662,3 +662,36 @@ def test_dec_embed_fold_step_matches(embed):
         dec.DEC_EMBED_FOLD = old
         model._retr_decode_states = {}
     assert _rel(res[0], res[1]) < 2e-2
+
+
+@pytest.mark.parametrize("R", [5, 320])
+def test_dec_ffn_ln_hidden_block_widths_agree(R):
+    """retr_dec_ffn_ln64 / retr_dec_ffn_ln128 (64 / 128 hidden units per block) against
+    retr_dec_rows + retr_dec_ffn: the residual bitwise equal, the sum of each variant's partial
+    slabs (the FFN output before its bias) within bf16 rounding of the LN output."""
+    C, Fh, H = 256, 2048, 8
+    g = _g(R + 11)
+    x = torch.randn(R, C, generator=g).to(DEV)
+    hs = torch.randn(H, R, C, generator=g).to(DEV)
+    bo = torch.randn(C, generator=g).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    beta = torch.randn(C, generator=g).to(DEV)
+    w1 = (torch.randn(Fh, C, generator=g) / 16).to(DEV).bfloat16()
+    b1 = torch.randn(Fh, generator=g).to(DEV)
+    w2 = (torch.randn(C, Fh, generator=g) / 45).to(DEV).bfloat16()
+    st = ops._st()
+    xo0 = torch.empty(R, C, device=DEV)
+    n3 = torch.empty(R, C, dtype=torch.bfloat16, device=DEV)
+    s0 = torch.empty(Fh // 32, R, C, device=DEV)
+    call("retr_dec_rows", ptr(x), ptr(hs), H, ptr(bo), R, C, ptr(xo0), ptr(gamma), ptr(beta),
+         1e-5, None, ptr(n3), None, st)
+    call("retr_dec_ffn", ptr(n3), R, C, ptr(w1), ptr(b1), ptr(w2), Fh, ptr(s0), st)
+    ref = s0.sum(0)
+    for name, hb in (("retr_dec_ffn_ln64", 64), ("retr_dec_ffn_ln128", 128)):
+        xo = torch.full((R, C), float("nan"), device=DEV)
+        sl = torch.full((Fh // hb, R, C), float("nan"), device=DEV)
+        call(name, ptr(x), ptr(hs), H, ptr(bo), ptr(gamma), ptr(beta), 1e-5, ptr(xo), R, C,
+             ptr(w1), ptr(b1), ptr(w2), Fh, ptr(sl), st)
+        torch.cuda.synchronize()
+        assert torch.equal(xo, xo0), name
+        assert _rel(sl.sum(0), ref) < 1e-2, name
