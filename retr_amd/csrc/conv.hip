@@ -1149,26 +1149,43 @@ __global__ void __launch_bounds__(256) conv_pack_tiled_group_kernel(PackGroup g)
   constexpr int ROW = 64 * KHW;                  // one co row of the tile
   constexpr int LDR = ROW + 2;                   // odd dword stride: the co-fastest reads below
   constexpr int TOT = 64 * ROW;                  // hit 64 distinct banks
-#pragma unroll 8
-  for (int e = tid; e < TOT; e += 256) {
-    const int r = e / ROW, j = e - r * ROW;
-    tile[r * LDR + j] = from_f<T>(d.w[((long)(co0 + r) * Cp + ci0) * KHW + j] * sc[r]);
+  // fp32 rows in 16-byte loads (a row's 64 KHW floats are contiguous and 16-byte aligned)
+  constexpr int R4 = ROW / 4;
+  static_assert(ROW % 4 == 0, "pack row");
+#pragma unroll 4
+  for (int f = tid; f < 64 * R4; f += 256) {
+    const int r = f / R4, j = 4 * (f - r * R4);
+    const float4 v = *(const float4*)(d.w + ((long)(co0 + r) * Cp + ci0) * KHW + j);
+    const float s = sc[r];
+    tile[r * LDR + j] = from_f<T>(v.x * s);
+    tile[r * LDR + j + 1] = from_f<T>(v.y * s);
+    tile[r * LDR + j + 2] = from_f<T>(v.z * s);
+    tile[r * LDR + j + 3] = from_f<T>(v.w * s);
   }
   __syncthreads();
+  // both images in 16-byte stores: VEC consecutive ci (image 1) / co (image 2) per store
+  constexpr int VEC = 16 / sizeof(T), NV = 64 / VEC;
+  typedef __attribute__((ext_vector_type(4))) unsigned int u4;
   T* wout = (T*)d.w_out;
-#pragma unroll 8
-  for (int e = tid; e < TOT; e += 256) {
-    const int ci = e & 63, q = e >> 6;
+#pragma unroll 4
+  for (int e = tid; e < 64 * KHW * NV; e += 256) {
+    const int cc = e % NV, q = e / NV;
     const int tap = q % KHW, r = q / KHW;
-    wout[((long)(co0 + r) * KHW + tap) * Cp + ci0 + ci] = tile[r * LDR + ci * KHW + tap];
+    T v[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) v[k] = tile[r * LDR + (cc * VEC + k) * KHW + tap];
+    *(u4*)(wout + ((long)(co0 + r) * KHW + tap) * Cp + ci0 + cc * VEC) = *(const u4*)v;
   }
   if (!d.wt_out) return;
   T* wt = (T*)d.wt_out;
-#pragma unroll 8
-  for (int e = tid; e < TOT; e += 256) {
-    const int r = e & 63, q = e >> 6;
+#pragma unroll 4
+  for (int e = tid; e < 64 * KHW * NV; e += 256) {
+    const int rc = e % NV, q = e / NV;
     const int tap = q % KHW, ci = q / KHW;
-    wt[((long)(ci0 + ci) * KHW + tap) * Co + co0 + r] = tile[r * LDR + ci * KHW + tap];
+    T v[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) v[k] = tile[(rc * VEC + k) * LDR + ci * KHW + tap];
+    *(u4*)(wt + ((long)(ci0 + ci) * KHW + tap) * Co + co0 + rc * VEC) = *(const u4*)v;
   }
 }
 

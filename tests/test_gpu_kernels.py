@@ -706,8 +706,11 @@ def test_argmax_split_matches_single_pass():
     assert int(a[3]) == 100 and int(a[5]) == 29999
 
 
-def test_conv_pack_group_matches_single():
-    """Grouped weight packing (one launch for many convs) == per-conv retr_conv_pack."""
+@pytest.mark.parametrize("dt", [1, 0])
+def test_conv_pack_group_matches_single(dt):
+    """Grouped weight packing (one launch for many convs; the tiled kernel's 16-byte loads and
+    stores) == per-conv retr_conv_pack, bf16 and fp32 images."""
+    odt = torch.bfloat16 if dt == 1 else torch.float32
     shapes = [(64, 3, 7, 8), (128, 64, 3, 64), (256, 128, 1, 128), (512, 512, 3, 512)]
     arr = (_lib.ConvPackDesc * len(shapes))()
     outs, refs, keep = [], [], []
@@ -716,11 +719,11 @@ def test_conv_pack_group_matches_single():
         bw, bb = torch.rand(co, device=DEV) + 0.5, torch.randn(co, device=DEV)
         rm, rv = torch.randn(co, device=DEV), torch.rand(co, device=DEV) + 0.5
         keep += [w, bw, bb, rm, rv]
-        o = [torch.empty(co, k, k, cp, dtype=torch.bfloat16, device=DEV),
-             torch.empty(cp, k, k, co, dtype=torch.bfloat16, device=DEV),
+        o = [torch.empty(co, k, k, cp, dtype=odt, device=DEV),
+             torch.empty(cp, k, k, co, dtype=odt, device=DEV),
              torch.empty(co, device=DEV), torch.empty(co, device=DEV)]
         r = [torch.empty_like(t) for t in o]
-        call("retr_conv_pack", 1, ptr(w), ptr(bw), ptr(bb), ptr(rm), ptr(rv), None, co, ci, k, k,
+        call("retr_conv_pack", dt, ptr(w), ptr(bw), ptr(bb), ptr(rm), ptr(rv), None, co, ci, k, k,
              cp, ptr(r[0]), ptr(r[1]), ptr(r[2]), ptr(r[3]), ops._st())
         d = arr[i]
         d.w, d.bn_w, d.bn_b, d.bn_rm, d.bn_rv = ptr(w), ptr(bw), ptr(bb), ptr(rm), ptr(rv)
@@ -728,7 +731,7 @@ def test_conv_pack_group_matches_single():
         d.Co, d.Ci, d.KH, d.KW, d.Cp = co, ci, k, k, cp
         outs.append(o)
         refs.append(r)
-    call("retr_conv_pack_group", 1, len(shapes), arr, ops._st())
+    call("retr_conv_pack_group", dt, len(shapes), arr, ops._st())
     for o, r in zip(outs, refs):
         for a, b in zip(o, r):
             assert torch.equal(a, b)
