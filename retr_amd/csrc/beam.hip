@@ -286,9 +286,10 @@ topk_reg_kernel(const T* x, long ld, int V, int* idx_out, float* lp_out) {
   }
 }
 
-// One block per image b: select the K surviving beams from the candidates, then reorder the
-// token history and the cache-ancestry rows in LDS and append step i's token.
-__global__ void __launch_bounds__(64)
+// One block per image b: select the K surviving beams from the candidates (the first wave),
+// then reorder the token history and the cache-ancestry rows in LDS and append step i's token
+// (all four waves: the K x T row copies in a quarter of the dependent passes of one wave).
+__global__ void __launch_bounds__(256)
 beam_select_kernel(const int* cand_tok, const float* cand_lp, int B, int K, int i, int T,
                    long long eos, float* scores, unsigned char* finished, long long* hist,
                    int* anc, long long* tok, unsigned char* item_done, const int* done) {
@@ -422,7 +423,7 @@ int retr_beam_select(const int* cand_tok, const float* cand_lp, int B, int K, in
   size_t lds = 128 + (size_t)K * T * (sizeof(long long) + sizeof(int));
   RETR_REQUIRE(lds <= 65536, "beam_select: K*T too large");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(beam_select_kernel, dim3(B), dim3(64), lds, st, cand_tok, cand_lp, B, K, i,
+  hipLaunchKernelGGL(beam_select_kernel, dim3(B), dim3(256), lds, st, cand_tok, cand_lp, B, K, i,
                      T, eos, scores, finished, hist, anc, tok, item_done, done);
   if (int e = retr_check_launch("beam_select")) return e;
   hipLaunchKernelGGL(beam_done_kernel, dim3(1), dim3(256), 0, st, item_done, B, i, done);
