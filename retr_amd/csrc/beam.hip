@@ -252,6 +252,35 @@ topk_reg_kernel(const T* x, long ld, int V, int* idx_out, float* lp_out) {
       }
     }
   }
+  // the candidates (at least K, usually few): gathered into LDS and ranked by one wave --
+  // instead of K rounds of a block-wide argmax (two barriers each); more than 64 (ties at the
+  // threshold) take the rounds below
+  __shared__ float cvs[64];
+  __shared__ int cis[64];
+  __shared__ int ncand;
+  if (tid == 0) ncand = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (ti[k] != 0x7fffffff) {
+      const int slot = atomicAdd(&ncand, 1);
+      if (slot < 64) cvs[slot] = tv[k], cis[slot] = ti[k];
+    }
+  __syncthreads();
+  const int nc = ncand;
+  if (nc <= 64) {
+    if (wave == 0 && lane < nc) {
+      const float mv = cvs[lane];
+      const int mi = cis[lane];
+      int rank = 0;
+      for (int q = 0; q < nc; ++q) rank += better(cvs[q], cis[q], mv, mi) ? 1 : 0;
+      if (rank < K) {
+        idx_out[(long)row * K + rank] = mi;
+        if (lp_out) lp_out[(long)row * K + rank] = mv - lse;
+      }
+    }
+    return;
+  }
   for (int k = 0; k < K; ++k) {
     float bv = tv[0];
     int bi = ti[0];
