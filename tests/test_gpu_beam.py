@@ -135,6 +135,7 @@ def test_topk_rows_matches_torch(dtype, V, K):
     x[0, 100] = x[0, 7000 % V] = x[0, 29000 % V] = 20.0         # ties -> ascending index
     x[1, 64:64 + 4 * K] = 15.0 + torch.arange(4 * K).float() / 64  # best words in one chunk run
     x[2, V - 1] = 30.0                                           # last (possibly partial) chunk
+    x[3, torch.arange(7, V, max(1, V // 200))] = 25.0            # > 64 tied candidates
     t = x.bfloat16() if dtype == "bf16" else x
     xd = t.to(dev)
     idx = torch.empty(M, K, dtype=torch.int32, device=dev)
@@ -145,7 +146,7 @@ def test_topk_rows_matches_torch(dtype, V, K):
     xf = t.float()[:, :V]
     ref_lp = torch.log_softmax(xf.double(), -1)
     for r in range(M):
-        order = sorted(range(V), key=lambda i: (-float(xf[r, i]), i))[:K] if r < 3 else None
+        order = sorted(range(V), key=lambda i: (-float(xf[r, i]), i))[:K] if r < 4 else None
         if order is None:                                       # stable sort: index asc on ties
             vals, ids = torch.sort(xf[r], descending=True, stable=True)
             order = ids[:K].tolist()
