@@ -28,6 +28,7 @@ def main():
                     help="1 / 0: eval_utils.decode.DEC_FFN_LN (default: the module's)")
     ap.add_argument("--fold-max-rows", type=int, default=None,
                     help="eval_utils.decode.DEC_FOLD_MAX_ROWS (default: the module's)")
+    ap.add_argument("--fp32", action="store_true", help="cfg5 in fp32 parity mode")
     ap.add_argument("--rows-per-block", type=int, default=None,
                     help="eval_utils.decode.DEC_ROWS_PER_BLOCK (default: automatic)")
     ap.add_argument("--block-per-row", action="store_true",
@@ -42,7 +43,7 @@ def main():
     dec.DEC_ROWS_PER_BLOCK = a.rows_per_block
     if a.fold_max_rows is not None:
         dec.DEC_FOLD_MAX_ROWS = a.fold_max_rows
-    model, _ = build(cfg5(), "cuda")
+    model, _ = build(cfg5("fp32") if a.fp32 else cfg5(), "cuda")
     model.eval()
     img, mask = synthetic_images(a.batch, 224, seed=3000)
     samples = [NestedTensor(img.cuda(), mask.cuda())]

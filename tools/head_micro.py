@@ -22,7 +22,7 @@ def main():
         b = torch.randn(N, device="cuda")
         y = torch.empty(M, N, device="cuda")
         out = []
-        for tile in (0, 1, 2, 4, 6, 8, 9):
+        for tile in tuple(int(t) for t in os.environ.get("HEAD_TILES", "0,1,2,4,6,8,9").split(",")):
             load().retr_tune(6, tile)
             t = timeit(lambda: call("retr_linear_fwd", 1, ptr(x), K, ptr(w), K, ptr(b), ptr(y), N,
                                     1, M, N, K, 0, None, 0, 0.0, 0, stream()))
