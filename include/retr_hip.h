@@ -682,6 +682,12 @@ int retr_dec_cross_heads_mr(const float* slab_in, const float* x, const float* b
                             const void* wo, float* slab_out, int rb, void* stream);
 int retr_dec_ffn(const void* n3, int R, int C, const void* w1, const float* b1, const void* w2,
                  int F, float* slabs, void* stream);
+/* fp32 parity-mode decode linear for few rows: y = x W^T (+ bias) (ReLU) (+ res), exact-f32 MFMA,
+ * one 16 x 16 tile per block with K split over its 4 waves (summed in wave order); M <= 64,
+ * K % 16 == 0, 16-byte aligned x / w rows. */
+int retr_dec_linear_f32(const float* x, long ldx, const float* w, long ldw, const float* bias,
+                        float* y, long ldy, int M, int N, int K, int relu, const float* res,
+                        long ldr, void* stream);
 /* retr_dec_ffn with its input LayerNorm in the prologue: per row x = xin + (sum_j hslab[j] + bo)
  * (slabs [nslab][R][C] in order), written to xout, FFN input = bf16(LN(x; gamma, beta, eps)) --
  * the retr_dec_rows launch between the per-head cross-attention partials and the FFN folded in. */

@@ -108,6 +108,59 @@ dec_gemm_kernel(const bf16* a_plain, const bf16* a_pos, int R, const bf16* w, co
   }
 }
 
+// ---- dec_linear_f32: the fp32 parity-mode decode step's linears (M <= 64 rows) ---------------
+// y[m][n] = x[m][:] . w[n][:] (+ b[n]) (ReLU) (+ res[m][n]) in exact fp32 (16x16x4 f32 MFMA).
+// Block = one 16 x 16 output tile, its four waves split K in quarters (wave w: the 16-column
+// blocks of K numbered w mod 4); within a 16-column block lane group g feeds columns
+// k0 + 4 g .. + 3 to the four MFMA steps (each step covers four distinct k, every k once), from
+// one 16-byte load of x and of w per lane.  The waves' partial tiles are added in wave order.
+// The generic GEMM ran these as 8-block grids (12.7 us per call, 50 calls per step).
+__global__ void __launch_bounds__(256)
+dec_linear_f32_kernel(const float* x, long ldx, const float* w, long ldw, const float* bias,
+                      float* y, long ldy, int M, int N, int K, int relu, const float* res,
+                      long ldr) {
+  __shared__ f4 red[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n0 = 16 * blockIdx.x, m0 = 16 * blockIdx.y;
+  const int rr = lane & 15, g = lane >> 4;
+  const int m = m0 + rr, n = n0 + rr;
+  const float* xr = x + (long)(m < M ? m : M - 1) * ldx + 4 * g;
+  const float* wr = w + (long)(n < N ? n : N - 1) * ldw + 4 * g;
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  const int nb = K / 16;                          // 16-column blocks of K
+  constexpr int U = 4;                            // blocks per wave in flight
+  for (int b0 = wv; b0 < nb; b0 += 4 * U) {
+    f4 xa[U], wa[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = b0 + 4 * u;
+      xa[u] = b < nb ? *(const f4*)(xr + 16 * b) : f4{0.f, 0.f, 0.f, 0.f};
+      wa[u] = b < nb ? *(const f4*)(wr + 16 * b) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[u][s], wa[u][s], acc, 0, 0, 0);
+  }
+  red[wv][lane] = acc;
+  __syncthreads();
+  if (wv != 0) return;
+  const f4 t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  const int col = n0 + (lane & 15);
+  if (col >= N) return;
+  const float bb = bias ? bias[col] : 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int row = m0 + 4 * (lane >> 4) + e;
+    if (row >= M) continue;
+    float v = t[e] + bb;
+    if (relu) v = fmaxf(v, 0.f);
+    if (res) v += res[(long)row * ldr + col];
+    y[(long)row * ldy + col] = v;
+  }
+}
+
 // ---- dec_rows: residual update + LayerNorm, one block per row ---------------------------------
 // x = xin (+ b2 + sum_j slabs[j], slabs in order); xout = x (if given); n = LN(x) (bf16),
 // npos = LN(x) + pos (bf16, if given).
@@ -1117,6 +1170,18 @@ int retr_dec_ffn_ln128(const float* xin, const float* hslab, int nslab, const fl
                      (hipStream_t)stream, xin, hslab, nslab, bo, gamma, beta, eps, xout, R,
                      (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
   return retr_check_launch("dec_ffn_ln128");
+}
+
+int retr_dec_linear_f32(const float* x, long ldx, const float* w, long ldw, const float* bias,
+                        float* y, long ldy, int M, int N, int K, int relu, const float* res,
+                        long ldr, void* stream) {
+  RETR_REQUIRE(M >= 0 && M <= 64 && N > 0 && K > 0 && K % 16 == 0 && ldx % 4 == 0 &&
+                   ldw % 4 == 0 && (((uintptr_t)x | (uintptr_t)w) & 15) == 0,
+               "dec_linear_f32: M=%d N=%d K=%d (M <= 64, K %% 16, 16-byte rows)", M, N, K);
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(dec_linear_f32_kernel, dim3(cdiv(N, 16), cdiv(M, 16)), dim3(256), 0,
+                     (hipStream_t)stream, x, ldx, w, ldw, bias, y, ldy, M, N, K, relu, res, ldr);
+  return retr_check_launch("dec_linear_f32");
 }
 
 #ifdef RETR_DEC_TIMING

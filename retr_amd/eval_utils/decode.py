@@ -50,6 +50,8 @@ DEC_HEADS = True
 DEC_FFN_LN = True
 # (with DEC_FFN_LN) the FFN residual + the next layer's LN1 in the self-attention prologue
 DEC_FOLD_ROWS = True
+# fp32 parity mode: the step's linears on the skinny exact-f32 kernel
+DEC_F32_SKINNY = True
 # rows up to which the folded (three-launch) layer is used (beyond: five launches per layer)
 DEC_FOLD_MAX_ROWS = 512
 # rows beyond which the folded FFN runs 128 hidden units per block
@@ -164,6 +166,19 @@ class IncrementalGreedy:
                 and C // H in (32, 64) and H % 4 == 0 and F % 32 == 0 and st.S <= 512
                 and st.T <= 512 and self.model.mlp.layers[0].weight.shape[0] % 32 == 0)
 
+    def _lin(self, x, w, bias, y, relu=0, res=None):
+        """The unfused step's linears; the fp32 parity mode's (few rows) on the skinny exact-f32
+        kernel (csrc/decode.hip dec_linear_f32), everything else on the generic GEMM."""
+        M, K = x.shape
+        if (DEC_F32_SKINNY and x.dtype == torch.float32 and y.dtype == torch.float32
+                and M <= 64 and K % 16 == 0 and x.stride(1) == 1 and w.stride(1) == 1
+                and x.stride(0) % 4 == 0 and w.stride(0) % 4 == 0):
+            call("retr_dec_linear_f32", ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(bias),
+                 ptr(y), y.stride(0), M, w.shape[0], K, int(relu), ptr(res),
+                 res.stride(0) if res is not None else 0, _st())
+            return
+        k_linear_fwd(x, w, bias, y, relu=relu, res=res)
+
     def _step(self, st, i, eos_token):
         """Kernels of decode step i (reads token i, writes caption column i+1)."""
         if self._fusable(st):
@@ -187,13 +202,13 @@ class IncrementalGreedy:
             w = ops.WEIGHTS.get(sub.in_proj_weight, cd)
             b = sub.in_proj_bias.detach()
             self._ln(y, sa.norm, y=st.n, y2=st.npos, pos=qp)
-            k_linear_fwd(st.npos, w[:C], b[:C], st.q)
-            k_linear_fwd(st.npos, w[C:2 * C], b[C:2 * C], st.kc[li][i::T])
-            k_linear_fwd(st.n, w[2 * C:], b[2 * C:], st.vc[li][i::T])
+            self._lin(st.npos, w[:C], b[:C], st.q)
+            self._lin(st.npos, w[C:2 * C], b[C:2 * C], st.kc[li][i::T])
+            self._lin(st.n, w[2 * C:], b[2 * C:], st.vc[li][i::T])
             call("retr_attention_decode", dcode(cd), ptr(st.q), C, ptr(st.kc[li]), C,
                  ptr(st.vc[li]), C, ptr(st.o), C, R, H, i + 1, T, hd, None, 1,
                  ptr(st.anc) if self.beam else None, s)
-            k_linear_fwd(st.o, ops.WEIGHTS.get(sub.out_proj.weight, cd),
+            self._lin(st.o, ops.WEIGHTS.get(sub.out_proj.weight, cd),
                          sub.out_proj.bias.detach(), y2, res=y)
             y, y2 = y2, y
             ca = layer.tgt_src_cross_attn
@@ -201,24 +216,24 @@ class IncrementalGreedy:
             w = ops.WEIGHTS.get(sub.in_proj_weight, cd)
             b = sub.in_proj_bias.detach()
             self._ln(y, ca.norm, y2=st.npos, pos=qp)
-            k_linear_fwd(st.npos, w[:C], b[:C], st.q)
+            self._lin(st.npos, w[:C], b[:C], st.q)
             call("retr_attention_decode", dcode(cd), ptr(st.q), C, ptr(st.kx[li]), C,
                  ptr(st.vx[li]), C, ptr(st.o), C, R, H, S, S, hd, ptr(st.kpm), st.K, None, s)
-            k_linear_fwd(st.o, ops.WEIGHTS.get(sub.out_proj.weight, cd),
+            self._lin(st.o, ops.WEIGHTS.get(sub.out_proj.weight, cd),
                          sub.out_proj.bias.detach(), y2, res=y)
             y, y2 = y2, y
             ff = layer.ff
             self._ln(y, ff.norm, y=st.n)
             f0, f2 = ff.sublayer[0], ff.sublayer[2]
-            k_linear_fwd(st.n, ops.WEIGHTS.get(f0.weight, cd), f0.bias.detach(), st.ffh, relu=1)
-            k_linear_fwd(st.ffh, ops.WEIGHTS.get(f2.weight, cd), f2.bias.detach(), y2, res=y)
+            self._lin(st.n, ops.WEIGHTS.get(f0.weight, cd), f0.bias.detach(), st.ffh, relu=1)
+            self._lin(st.ffh, ops.WEIGHTS.get(f2.weight, cd), f2.bias.detach(), y2, res=y)
             y, y2 = y2, y
         l1, l2, l3 = model.mlp.layers
         V = l3.weight.shape[0]
         self._ln(y, tr.decoder.norm, y=st.n)
-        k_linear_fwd(st.n, ops.WEIGHTS.get(l1.weight, cd), l1.bias.detach(), st.h1, relu=1)
-        k_linear_fwd(st.h1, ops.WEIGHTS.get(l2.weight, cd), l2.bias.detach(), st.h2, relu=1)
-        k_linear_fwd(st.h2, ops.WEIGHTS.get(l3.weight, cd, rows=st.Vp),
+        self._lin(st.n, ops.WEIGHTS.get(l1.weight, cd), l1.bias.detach(), st.h1, relu=1)
+        self._lin(st.h1, ops.WEIGHTS.get(l2.weight, cd), l2.bias.detach(), st.h2, relu=1)
+        self._lin(st.h2, ops.WEIGHTS.get(l3.weight, cd, rows=st.Vp),
                      st.head_bias, st.logits)
         self._select(st, i, V, eos_token, s)
 

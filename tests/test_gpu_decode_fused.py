@@ -695,3 +695,27 @@ def test_dec_ffn_ln_hidden_block_widths_agree(R):
         torch.cuda.synchronize()
         assert torch.equal(xo, xo0), name
         assert _rel(sl.sum(0), ref) < 1e-2, name
+
+
+@pytest.mark.parametrize("M,N,K,relu,res", [(64, 256, 256, 0, True), (37, 2048, 256, 1, False),
+                                            (64, 256, 2048, 0, True), (2, 30528, 512, 0, False),
+                                            (16, 512, 512, 1, False)])
+def test_dec_linear_f32_matches_torch(M, N, K, relu, res):
+    """retr_dec_linear_f32 (the fp32 parity-mode decode linears) against fp32 torch: within fp32
+    reassociation; strided output rows (the cache append) and the residual."""
+    g = _g(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    r = torch.randn(M, N, generator=g).to(DEV) if res else None
+    big = torch.full((M, 2 * N), float("nan"), device=DEV)
+    y = big[:, 3:3 + N] if N % 4 else big[:, N:]
+    call("retr_dec_linear_f32", ptr(x), K, ptr(w), K, ptr(b), ptr(y), y.stride(0), M, N, K, relu,
+         ptr(r), N if res else 0, ops._st())
+    torch.cuda.synchronize()
+    ref = x.double() @ w.double().t() + b.double()
+    if relu:
+        ref = ref.clamp_min(0)
+    if res:
+        ref = ref + r.double()
+    assert _rel(y, ref) < 1e-6
