@@ -688,6 +688,14 @@ int retr_dec_ffn(const void* n3, int R, int C, const void* w1, const float* b1, 
 int retr_dec_linear_f32(const float* x, long ldx, const float* w, long ldw, const float* bias,
                         float* y, long ldy, int M, int N, int K, int relu, const float* res,
                         long ldr, void* stream);
+/* up to three such linears with the same M and K in one launch (the q | k | v projections) */
+int retr_dec_linear3_f32(int n, const float* x0, long ldx0, const float* w0, long ldw0,
+                         const float* b0, float* y0, long ldy0, int N0, int relu0,
+                         const float* r0, long ldr0, const float* x1, long ldx1, const float* w1,
+                         long ldw1, const float* b1, float* y1, long ldy1, int N1, int relu1,
+                         const float* r1, long ldr1, const float* x2, long ldx2, const float* w2,
+                         long ldw2, const float* b2, float* y2, long ldy2, int N2, int relu2,
+                         const float* r2, long ldr2, int M, int K, void* stream);
 /* retr_dec_ffn with its input LayerNorm in the prologue: per row x = xin + (sum_j hslab[j] + bo)
  * (slabs [nslab][R][C] in order), written to xout, FFN input = bf16(LN(x; gamma, beta, eps)) --
  * the retr_dec_rows launch between the per-head cross-attention partials and the FFN folded in. */

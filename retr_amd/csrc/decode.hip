@@ -115,13 +115,33 @@ dec_gemm_kernel(const bf16* a_plain, const bf16* a_pos, int R, const bf16* w, co
 // k0 + 4 g .. + 3 to the four MFMA steps (each step covers four distinct k, every k once), from
 // one 16-byte load of x and of w per lane.  The waves' partial tiles are added in wave order.
 // The generic GEMM ran these as 8-block grids (12.7 us per call, 50 calls per step).
+struct LinF32Seg {          // one linear of a grouped launch (blockIdx.z)
+  const float* x;
+  const float* w;
+  const float* bias;
+  float* y;
+  const float* res;
+  long ldx, ldw, ldy, ldr;
+  int N, relu;
+};
+struct LinF32Group {
+  LinF32Seg s[3];
+};
+
 __global__ void __launch_bounds__(256)
-dec_linear_f32_kernel(const float* x, long ldx, const float* w, long ldw, const float* bias,
-                      float* y, long ldy, int M, int N, int K, int relu, const float* res,
-                      long ldr) {
+dec_linear_f32_kernel(LinF32Group grp, int M, int K) {
+  const LinF32Seg& sg = grp.s[blockIdx.z];
+  const float* x = sg.x;
+  const float* w = sg.w;
+  const float* bias = sg.bias;
+  float* y = sg.y;
+  const float* res = sg.res;
+  const long ldx = sg.ldx, ldw = sg.ldw, ldy = sg.ldy, ldr = sg.ldr;
+  const int N = sg.N, relu = sg.relu;
   __shared__ f4 red[4][64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int n0 = 16 * blockIdx.x, m0 = 16 * blockIdx.y;
+  if (n0 >= N) return;
   const int rr = lane & 15, g = lane >> 4;
   const int m = m0 + rr, n = n0 + rr;
   const float* xr = x + (long)(m < M ? m : M - 1) * ldx + 4 * g;
@@ -1175,12 +1195,34 @@ int retr_dec_ffn_ln128(const float* xin, const float* hslab, int nslab, const fl
 int retr_dec_linear_f32(const float* x, long ldx, const float* w, long ldw, const float* bias,
                         float* y, long ldy, int M, int N, int K, int relu, const float* res,
                         long ldr, void* stream) {
-  RETR_REQUIRE(M >= 0 && M <= 64 && N > 0 && K > 0 && K % 16 == 0 && ldx % 4 == 0 &&
-                   ldw % 4 == 0 && (((uintptr_t)x | (uintptr_t)w) & 15) == 0,
-               "dec_linear_f32: M=%d N=%d K=%d (M <= 64, K %% 16, 16-byte rows)", M, N, K);
+  return retr_dec_linear3_f32(1, x, ldx, w, ldw, bias, y, ldy, N, relu, res, ldr, nullptr, 0,
+                              nullptr, 0, nullptr, nullptr, 0, 0, 0, nullptr, 0, nullptr, 0,
+                              nullptr, 0, nullptr, nullptr, 0, 0, 0, nullptr, 0, M, K, stream);
+}
+
+int retr_dec_linear3_f32(int n, const float* x0, long ldx0, const float* w0, long ldw0,
+                         const float* b0, float* y0, long ldy0, int N0, int relu0,
+                         const float* r0, long ldr0, const float* x1, long ldx1, const float* w1,
+                         long ldw1, const float* b1, float* y1, long ldy1, int N1, int relu1,
+                         const float* r1, long ldr1, const float* x2, long ldx2, const float* w2,
+                         long ldw2, const float* b2, float* y2, long ldy2, int N2, int relu2,
+                         const float* r2, long ldr2, int M, int K, void* stream) {
+  RETR_REQUIRE(n >= 1 && n <= 3 && M >= 0 && M <= 64 && K > 0 && K % 16 == 0,
+               "dec_linear3_f32: n=%d M=%d K=%d (M <= 64, K %% 16)", n, M, K);
+  LinF32Group g{{{x0, w0, b0, y0, r0, ldx0, ldw0, ldy0, ldr0, N0, relu0},
+                 {x1, w1, b1, y1, r1, ldx1, ldw1, ldy1, ldr1, N1, relu1},
+                 {x2, w2, b2, y2, r2, ldx2, ldw2, ldy2, ldr2, N2, relu2}}};
+  int nmax = 0;
+  for (int q = 0; q < n; ++q) {
+    const LinF32Seg& sg = g.s[q];
+    RETR_REQUIRE(sg.N > 0 && sg.ldx % 4 == 0 && sg.ldw % 4 == 0 &&
+                     (((uintptr_t)sg.x | (uintptr_t)sg.w) & 15) == 0,
+                 "dec_linear3_f32[%d]: N=%d, 16-byte rows", q, sg.N);
+    nmax = sg.N > nmax ? sg.N : nmax;
+  }
   if (M == 0) return 0;
-  hipLaunchKernelGGL(dec_linear_f32_kernel, dim3(cdiv(N, 16), cdiv(M, 16)), dim3(256), 0,
-                     (hipStream_t)stream, x, ldx, w, ldw, bias, y, ldy, M, N, K, relu, res, ldr);
+  hipLaunchKernelGGL(dec_linear_f32_kernel, dim3(cdiv(nmax, 16), cdiv(M, 16), n), dim3(256), 0,
+                     (hipStream_t)stream, g, M, K);
   return retr_check_launch("dec_linear_f32");
 }
 

@@ -235,10 +235,19 @@ argmax_part_kernel(const T* x, long ld, int V, float* pv, int* pi) {
   float bv = -INFINITY;
   int bi = 0x7fffffff;
   for (int c = c0 + threadIdx.x; c < c1; c += 256) {
-    const bf16x8 x8 = *(const bf16x8*)(xr + 8 * c);
+    float x8[8];
+    if constexpr (sizeof(T) == 2) {
+      const bf16x8 t = *(const bf16x8*)(xr + 8 * c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x8[e] = (float)t[e];
+    } else {
+      const f32x4 a = *(const f32x4*)(xr + 8 * c), b = *(const f32x4*)(xr + 8 * c + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x8[e] = a[e], x8[e + 4] = b[e];
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e)
-      if (am_better((float)x8[e], 8 * c + e, bv, bi)) bv = (float)x8[e], bi = 8 * c + e;
+      if (am_better(x8[e], 8 * c + e, bv, bi)) bv = x8[e], bi = 8 * c + e;
   }
   if (seg == kArgSeg - 1)                             // the ragged tail
     for (int j = 8 * V8 + threadIdx.x; j < V; j += 256)
@@ -448,14 +457,19 @@ extern "C" int retr_greedy_select(int dtype, const void* logits, long ld, int B,
                                   long long* tok, void* stream) {
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype != RETR_BF16 || ld % 8 != 0 || V < 8 * kArgSeg * 256 / 4 || !workspace || B > 1024) {
+  if (ld % 8 != 0 || V < 8 * kArgSeg * 256 / 4 || !workspace || B > 1024 ||
+      ((uintptr_t)logits & 15) != 0) {
     if (int e = retr_argmax_rows(dtype, logits, ld, B, V, pred, stream)) return e;
     return retr_greedy_update(pred, B, T, i, eos, caption, finished, done, tok, stream);
   }
   float* pv = (float*)workspace;
   int* pi = (int*)(pv + (size_t)B * kArgSeg);
-  hipLaunchKernelGGL(argmax_part_kernel<bf16>, dim3(kArgSeg, B), dim3(256), 0, st,
-                     (const bf16*)logits, ld, V, pv, pi);
+  if (dtype == RETR_BF16)
+    hipLaunchKernelGGL(argmax_part_kernel<bf16>, dim3(kArgSeg, B), dim3(256), 0, st,
+                       (const bf16*)logits, ld, V, pv, pi);
+  else
+    hipLaunchKernelGGL(argmax_part_kernel<float>, dim3(kArgSeg, B), dim3(256), 0, st,
+                       (const float*)logits, ld, V, pv, pi);
   if (int e = retr_check_launch("argmax_part")) return e;
   hipLaunchKernelGGL(greedy_select_kernel, dim3(1), dim3(1024), 0, st, pv, pi, B, T, i, eos, pred,
                      caption, finished, done, tok);

@@ -179,6 +179,25 @@ class IncrementalGreedy:
             return
         k_linear_fwd(x, w, bias, y, relu=relu, res=res)
 
+    def _lin3(self, items):
+        """q | k | v projections (same rows and K) in one skinny fp32 launch when they qualify."""
+        x0, w0 = items[0][0], items[0][1]
+        M, K = x0.shape
+        ok = (DEC_F32_SKINNY and M <= 64 and K % 16 == 0 and all(
+            x.dtype == torch.float32 and y.dtype == torch.float32 and x.shape == (M, K)
+            and w.shape[1] == K and x.stride(1) == 1 and w.stride(1) == 1
+            and x.stride(0) % 4 == 0 and w.stride(0) % 4 == 0 for x, w, b, y in items))
+        if not ok:
+            for x, w, b, y in items:
+                self._lin(x, w, b, y)
+            return
+        args = []
+        for x, w, b, y in items:
+            args += [ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(b), ptr(y), y.stride(0),
+                     w.shape[0], 0, None, 0]
+        args += [None, 0, None, 0, None, None, 0, 0, 0, None, 0] * (3 - len(items))
+        call("retr_dec_linear3_f32", len(items), *args, M, K, _st())
+
     def _step(self, st, i, eos_token):
         """Kernels of decode step i (reads token i, writes caption column i+1)."""
         if self._fusable(st):
@@ -202,9 +221,9 @@ class IncrementalGreedy:
             w = ops.WEIGHTS.get(sub.in_proj_weight, cd)
             b = sub.in_proj_bias.detach()
             self._ln(y, sa.norm, y=st.n, y2=st.npos, pos=qp)
-            self._lin(st.npos, w[:C], b[:C], st.q)
-            self._lin(st.npos, w[C:2 * C], b[C:2 * C], st.kc[li][i::T])
-            self._lin(st.n, w[2 * C:], b[2 * C:], st.vc[li][i::T])
+            self._lin3([(st.npos, w[:C], b[:C], st.q),
+                        (st.npos, w[C:2 * C], b[C:2 * C], st.kc[li][i::T]),
+                        (st.n, w[2 * C:], b[2 * C:], st.vc[li][i::T])])
             call("retr_attention_decode", dcode(cd), ptr(st.q), C, ptr(st.kc[li]), C,
                  ptr(st.vc[li]), C, ptr(st.o), C, R, H, i + 1, T, hd, None, 1,
                  ptr(st.anc) if self.beam else None, s)
