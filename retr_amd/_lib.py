@@ -206,6 +206,7 @@ _SIGS = {
                           _P, _P, _P, _P, _P],
     "retr_dec_ffn": [_P, _I, _I, _P, _P, _P, _I, _P, _P],
     "retr_dec_ffn_ln": [_P, _P, _I, _P, _P, _P, _F, _P, _I, _I, _P, _P, _P, _I, _P, _P],
+    "retr_dec_linear_bf16": [_P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _P],
     "retr_dec_linear_f32": [_P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _P, _L, _P],
     "retr_dec_linear3_f32": [_I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _L, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _L, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _L, _I, _I, _P],
     "retr_dec_ffn_ln64": [_P, _P, _I, _P, _P, _P, _F, _P, _I, _I, _P, _P, _P, _I, _P, _P],

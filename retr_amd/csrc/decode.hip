@@ -181,6 +181,50 @@ dec_linear_f32_kernel(LinF32Group grp, int M, int K) {
   }
 }
 
+// ---- dec_linear_bf16: the greedy step's MLP-head linears (M <= 64 rows), same tiling -------
+// y = bf16(relu(x W^T + b)), bf16 operands, one 16 x 16 tile per block, the 32-column blocks of
+// K dealt to the four waves (16x16x32 bf16 MFMA), partial tiles added in wave order.
+__global__ void __launch_bounds__(256)
+dec_linear_bf16_kernel(const bf16* x, long ldx, const bf16* w, long ldw, const float* bias,
+                       bf16* y, long ldy, int M, int N, int K, int relu) {
+  __shared__ f4 red[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int n0 = 16 * blockIdx.x, m0 = 16 * blockIdx.y;
+  const int rr = lane & 15, g = lane >> 4;
+  const int m = m0 + rr, n = n0 + rr;
+  const bf16* xr = x + (long)(m < M ? m : M - 1) * ldx + 8 * g;
+  const bf16* wr = w + (long)(n < N ? n : N - 1) * ldw + 8 * g;
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  const int nb = K / 32;
+  constexpr int U = 4;
+  for (int b0 = wv; b0 < nb; b0 += 4 * U) {
+    u32x4 xa[U], wa[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int b = b0 + 4 * u;
+      xa[u] = b < nb ? *(const u32x4*)(xr + 32 * b) : u32x4{0u, 0u, 0u, 0u};
+      wa[u] = b < nb ? *(const u32x4*)(wr + 32 * b) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = mfma16(xa[u], wa[u], acc);
+  }
+  red[wv][lane] = acc;
+  __syncthreads();
+  if (wv != 0) return;
+  const f4 t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  const int col = n0 + (lane & 15);
+  if (col >= N) return;
+  const float bb = bias ? bias[col] : 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int row = m0 + 4 * (lane >> 4) + e;
+    if (row >= M) continue;
+    float v = t[e] + bb;
+    if (relu) v = fmaxf(v, 0.f);
+    y[(long)row * ldy + col] = (bf16)v;
+  }
+}
+
 // ---- dec_rows: residual update + LayerNorm, one block per row ---------------------------------
 // x = xin (+ b2 + sum_j slabs[j], slabs in order); xout = x (if given); n = LN(x) (bf16),
 // npos = LN(x) + pos (bf16, if given).
@@ -1190,6 +1234,18 @@ int retr_dec_ffn_ln128(const float* xin, const float* hslab, int nslab, const fl
                      (hipStream_t)stream, xin, hslab, nslab, bo, gamma, beta, eps, xout, R,
                      (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
   return retr_check_launch("dec_ffn_ln128");
+}
+
+int retr_dec_linear_bf16(const void* x, long ldx, const void* w, long ldw, const float* bias,
+                         void* y, long ldy, int M, int N, int K, int relu, void* stream) {
+  RETR_REQUIRE(M >= 0 && M <= 64 && N > 0 && K > 0 && K % 32 == 0 && ldx % 8 == 0 &&
+                   ldw % 8 == 0 && (((uintptr_t)x | (uintptr_t)w) & 15) == 0,
+               "dec_linear_bf16: M=%d N=%d K=%d (M <= 64, K %% 32, 16-byte rows)", M, N, K);
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(dec_linear_bf16_kernel, dim3(cdiv(N, 16), cdiv(M, 16)), dim3(256), 0,
+                     (hipStream_t)stream, (const bf16*)x, ldx, (const bf16*)w, ldw, bias,
+                     (bf16*)y, ldy, M, N, K, relu);
+  return retr_check_launch("dec_linear_bf16");
 }
 
 int retr_dec_linear_f32(const float* x, long ldx, const float* w, long ldw, const float* bias,

@@ -52,6 +52,8 @@ DEC_FFN_LN = True
 DEC_FOLD_ROWS = True
 # fp32 parity mode: the step's linears on the skinny exact-f32 kernel
 DEC_F32_SKINNY = True
+# the greedy step's MLP-head layers 1-2 on the skinny bf16 linear
+DEC_HEAD_SKINNY = True
 # rows up to which the folded (three-launch) layer is used (beyond: five launches per layer)
 DEC_FOLD_MAX_ROWS = 512
 # rows beyond which the folded FFN runs 128 hidden units per block
@@ -421,9 +423,17 @@ class IncrementalGreedy:
         l1, l2, l3 = model.mlp.layers
         V = l3.weight.shape[0]
         H1 = l1.weight.shape[0]
-        call("retr_dec_gemm", ptr(st.n), None, R, C, ptr(W(l1.weight)), ptr(l1.bias), H1,
-             ptr(st.h1), H1, 0, None, 0, 0, None, 0, 0, H1, 1, s)
-        k_linear_fwd(st.h1, W(l2.weight), l2.bias.detach(), st.h2, relu=1)
+        w1, w2 = W(l1.weight), W(l2.weight)
+        if DEC_HEAD_SKINNY and R <= 64 and C % 32 == 0 and H1 % 32 == 0:
+            # the head's first two layers on the 16 x 16-tile decode linear (128 blocks each)
+            call("retr_dec_linear_bf16", ptr(st.n), C, ptr(w1), C, ptr(l1.bias), ptr(st.h1),
+                 st.h1.stride(0), R, H1, C, 1, s)
+            call("retr_dec_linear_bf16", ptr(st.h1), st.h1.stride(0), ptr(w2), w2.stride(0),
+                 ptr(l2.bias), ptr(st.h2), st.h2.stride(0), R, w2.shape[0], H1, 1, s)
+        else:
+            call("retr_dec_gemm", ptr(st.n), None, R, C, ptr(w1), ptr(l1.bias), H1,
+                 ptr(st.h1), H1, 0, None, 0, 0, None, 0, 0, H1, 1, s)
+            k_linear_fwd(st.h1, w2, l2.bias.detach(), st.h2, relu=1)
         k_linear_fwd(st.h2, ops.WEIGHTS.get(l3.weight, cd, rows=st.Vp), st.head_bias, st.logits)
         self._select(st, i, V, eos_token, s)
 
