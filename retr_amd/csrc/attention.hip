@@ -491,8 +491,11 @@ attn_decode_kernel(const T* q, long ldq, const T* k, long ldk, const T* v, long 
   __syncthreads();
   const int nc = 256 / hd, d = tid % hd, c = tid / hd;
   float acc = 0.f;
-  if (c < nc)
+  if (c < nc) {
+    // (unrolled: the value loads of a stripe are independent, the sum stays in key order)
+#pragma unroll 8
     for (int j = c; j < Lk; j += nc) acc += sc[j] * to_f(vb[kvrow(j) * ldv + d]);
+  }
   red[tid] = acc;
   __syncthreads();
   if (tid < hd) {
