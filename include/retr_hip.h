@@ -683,7 +683,7 @@ int retr_dec_cross_heads_mr(const float* slab_in, const float* x, const float* b
 int retr_dec_ffn(const void* n3, int R, int C, const void* w1, const float* b1, const void* w2,
                  int F, float* slabs, void* stream);
 /* bf16 decode linear for few rows (the greedy step's MLP head): y = bf16(x W^T + bias) (ReLU),
- * the same 16 x 16 tiles with K split over 4 waves; M <= 64, K % 32 == 0, 16-byte aligned rows. */
+ * the same 16 x 16 tiles with K split over 4 waves; M <= 4096, K % 32 == 0, 16-byte aligned rows. */
 int retr_dec_linear_bf16(const void* x, long ldx, const void* w, long ldw, const float* bias,
                          void* y, long ldy, int M, int N, int K, int relu, void* stream);
 /* fp32 parity-mode decode linear for few rows: y = x W^T (+ bias) (ReLU) (+ res), exact-f32 MFMA,

@@ -1238,9 +1238,9 @@ int retr_dec_ffn_ln128(const float* xin, const float* hslab, int nslab, const fl
 
 int retr_dec_linear_bf16(const void* x, long ldx, const void* w, long ldw, const float* bias,
                          void* y, long ldy, int M, int N, int K, int relu, void* stream) {
-  RETR_REQUIRE(M >= 0 && M <= 64 && N > 0 && K > 0 && K % 32 == 0 && ldx % 8 == 0 &&
+  RETR_REQUIRE(M >= 0 && M <= 4096 && N > 0 && K > 0 && K % 32 == 0 && ldx % 8 == 0 &&
                    ldw % 8 == 0 && (((uintptr_t)x | (uintptr_t)w) & 15) == 0,
-               "dec_linear_bf16: M=%d N=%d K=%d (M <= 64, K %% 32, 16-byte rows)", M, N, K);
+               "dec_linear_bf16: M=%d N=%d K=%d (M <= 4096, K %% 32, 16-byte rows)", M, N, K);
   if (M == 0) return 0;
   hipLaunchKernelGGL(dec_linear_bf16_kernel, dim3(cdiv(N, 16), cdiv(M, 16)), dim3(256), 0,
                      (hipStream_t)stream, (const bf16*)x, ldx, (const bf16*)w, ldw, bias,

@@ -424,7 +424,7 @@ class IncrementalGreedy:
         V = l3.weight.shape[0]
         H1 = l1.weight.shape[0]
         w1, w2 = W(l1.weight), W(l2.weight)
-        if DEC_HEAD_SKINNY and R <= 64 and C % 32 == 0 and H1 % 32 == 0:
+        if DEC_HEAD_SKINNY and R <= 512 and C % 32 == 0 and H1 % 32 == 0:
             # the head's first two layers on the 16 x 16-tile decode linear (128 blocks each)
             call("retr_dec_linear_bf16", ptr(st.n), C, ptr(w1), C, ptr(l1.bias), ptr(st.h1),
                  st.h1.stride(0), R, H1, C, 1, s)
