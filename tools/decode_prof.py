@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--fold-max-rows", type=int, default=None,
                     help="eval_utils.decode.DEC_FOLD_MAX_ROWS (default: the module's)")
     ap.add_argument("--fp32", action="store_true", help="cfg5 in fp32 parity mode")
+    ap.add_argument("--select-embed", type=int, default=None,
+                    help="1 / 0: eval_utils.decode.DEC_SELECT_EMBED (default: the module's)")
     ap.add_argument("--head-skinny", type=int, default=0,
                     help="1 / 2: eval_utils.decode.DEC_HEAD_SKINNY on / off (0: the module's)")
     ap.add_argument("--rows-per-block", type=int, default=None,
@@ -43,6 +45,8 @@ def main():
     if a.fold is not None:
         dec.DEC_FOLD_ROWS = bool(a.fold)
     dec.DEC_ROWS_PER_BLOCK = a.rows_per_block
+    if a.select_embed is not None:
+        dec.DEC_SELECT_EMBED = bool(a.select_embed)
     if a.head_skinny:
         dec.DEC_HEAD_SKINNY = a.head_skinny == 1
     if a.fold_max_rows is not None:
