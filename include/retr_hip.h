@@ -545,16 +545,6 @@ int retr_greedy_select(int dtype, const void* logits, long ld, int B, int V, voi
                        int T, int i, long long eos, long long* pred, long long* caption,
                        unsigned char* finished, int* done, long long* tok, void* stream);
 
-/* retr_greedy_select that also prepares the next decode step's input for the chosen tokens:
- * x = LN(word[tok] + pos; ge, be, epse), n = bf16(LN(x; g1, b1, eps1)), npos = bf16(that + pos)
- * -- retr_dec_embed_rows' arithmetic, bitwise, in the selection launch.  bf16 logits, C = 256. */
-int retr_greedy_select_embed(const void* logits, long ld, int B, int V, void* workspace, int T,
-                             int i, long long eos, long long* pred, long long* caption,
-                             unsigned char* finished, int* done, long long* tok, int C,
-                             const float* word, const float* pos, const float* ge,
-                             const float* be, float epse, const float* g1, const float* b1,
-                             float eps1, float* x, void* n, void* npos, void* stream);
-
 /* ---- elementwise helpers --------------------------------------------------------------- */
 /* Encoder output without a final LayerNorm (pre_norm=False; models/ConcatTransformer.py:24,
  * 105-106): y = cast(x), y2 = cast(x + pos[row % period]) (either output may be NULL) */

@@ -209,8 +209,6 @@ _SIGS = {
     "retr_dec_linear_bf16": [_P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _P],
     "retr_dec_linear_f32": [_P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _P, _L, _P],
     "retr_dec_linear3_f32": [_I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _L, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _L, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _L, _I, _I, _P],
-    "retr_greedy_select_embed": [_P, _L, _I, _I, _P, _I, _I, _L, _P, _P, _P, _P, _P, _I, _P, _P,
-                                 _P, _P, _F, _P, _P, _F, _P, _P, _P, _P],
     "retr_dec_ffn_ln64": [_P, _P, _I, _P, _P, _P, _F, _P, _I, _I, _P, _P, _P, _I, _P, _P],
     "retr_dec_ffn_ln128": [_P, _P, _I, _P, _P, _P, _F, _P, _I, _I, _P, _P, _P, _I, _P, _P],
     "retr_dec_self_heads_ln": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _I,

@@ -451,134 +451,6 @@ greedy_select_kernel(const float* pv, const int* pi, int B, int T, int i, long l
   if (threadIdx.x == 0 && prev_done < 0 && all_fin) *done = i;
 }
 
-// greedy_select_kernel that also prepares the next step's decoder input for its token: x =
-// LN_e(word[tok] + pos) (DecoderEmbeddings) and the first layer's n = bf16(LN1(x)), npos =
-// bf16(LN1(x) + pos) -- retr_dec_embed_rows' arithmetic (LN_e: one wave, lane l owning columns
-// l + 64 i; LN1: four 64-column wave sums added in order), without its launch.  C = 256.
-struct NextEmbed {
-  const float* word;
-  const float* pos;       // position row of the next step
-  const float* ge;
-  const float* be;
-  float epse;
-  const float* g1;
-  const float* b1;
-  float eps1;
-  float* x;
-  bf16* n;
-  bf16* npos;
-};
-
-__global__ void __launch_bounds__(1024)
-greedy_select_embed_kernel(const float* pv, const int* pi, int B, int T, int i, long long eos,
-                           long long* pred, long long* caption, unsigned char* finished,
-                           int* done, long long* tok, NextEmbed ne) {
-  constexpr int C = 256;
-  __shared__ int all_fin;
-  __shared__ long long sp[1024];
-  if (threadIdx.x == 0) all_fin = 1;
-  const int s = threadIdx.x % kArgSeg;
-  for (int r0 = 0; r0 < B; r0 += 1024 / kArgSeg) {
-    const int row = r0 + threadIdx.x / kArgSeg;
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    if (row < B) bv = pv[row * kArgSeg + s], bi = pi[row * kArgSeg + s];
-    for (int o = kArgSeg / 2; o > 0; o >>= 1) {
-      const float v2 = __shfl_xor(bv, o, 64);
-      const int i2 = __shfl_xor(bi, o, 64);
-      if (am_better(v2, i2, bv, bi)) bv = v2, bi = i2;
-    }
-    if (row < B && s == 0) {
-      pred[row] = bi;
-      if (row < 1024) sp[row] = bi;
-    }
-  }
-  __syncthreads();
-  const int prev_done = *done;
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    const long long pb = b < 1024 ? sp[b] : pred[b];
-    unsigned char f = finished[b] | (pb == eos ? 1 : 0);
-    finished[b] = f;
-    if (!f) atomicAnd(&all_fin, 0);
-  }
-  __syncthreads();
-  const bool stop = prev_done >= 0 || all_fin;
-  for (int b = threadIdx.x; b < B; b += blockDim.x) {
-    const long long pb = b < 1024 ? sp[b] : pred[b];
-    if (!stop) caption[(long)b * T + i + 1] = pb;
-    tok[b] = pb;
-  }
-  if (threadIdx.x == 0 && prev_done < 0 && all_fin) *done = i;
-  // the next step's embeddings + LN1, one wave per row
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int r = wv; r < B; r += blockDim.x / 64) {
-    const long t = r < 1024 ? sp[r] : pred[r];
-    float v[4], su = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = lane + 64 * q;
-      v[q] = ne.word[t * C + c] + ne.pos[c];
-      su += v[q];
-    }
-    const float me = wave_sum(su) / C;
-    float qe = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float d = v[q] - me;
-      qe += d * d;
-    }
-    const float re = 1.0f / sqrtf(wave_sum(qe) / C + ne.epse);
-    float ws[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = lane + 64 * q;
-      v[q] = (v[q] - me) * re * ne.ge[c] + ne.be[c];
-      ne.x[(long)r * C + c] = v[q];
-      ws[q] = wave_sum(v[q]);                      // retr_dec_embed_rows: one sum per wave
-    }
-    const float mean = (ws[0] + ws[1] + ws[2] + ws[3]) / C;
-    float wq[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float d = v[q] - mean;
-      wq[q] = wave_sum(d * d);
-    }
-    const float rstd = 1.0f / sqrtf((wq[0] + wq[1] + wq[2] + wq[3]) / C + ne.eps1);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int c = lane + 64 * q;
-      const float o = (v[q] - mean) * rstd * ne.g1[c] + ne.b1[c];
-      ne.n[(long)r * C + c] = (bf16)o;
-      ne.npos[(long)r * C + c] = (bf16)(o + ne.pos[c]);
-    }
-  }
-}
-
-extern "C" int retr_greedy_select_embed(const void* logits, long ld, int B, int V,
-                                        void* workspace, int T, int i, long long eos,
-                                        long long* pred, long long* caption,
-                                        unsigned char* finished, int* done, long long* tok,
-                                        int C, const float* word, const float* pos,
-                                        const float* ge, const float* be, float epse,
-                                        const float* g1, const float* b1, float eps1, float* x,
-                                        void* n, void* npos, void* stream) {
-  RETR_REQUIRE(C == 256 && ld % 8 == 0 && V >= 8 * kArgSeg * 256 / 4 && workspace && B <= 1024 &&
-                   ((uintptr_t)logits & 15) == 0 && word && pos && ge && be && g1 && b1 && x &&
-                   n && npos,
-               "greedy_select_embed: C=%d B=%d V=%d (C 256, bf16 logits, B <= 1024)", C, B, V);
-  if (B == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  float* pv = (float*)workspace;
-  int* pi = (int*)(pv + (size_t)B * kArgSeg);
-  hipLaunchKernelGGL(argmax_part_kernel<bf16>, dim3(kArgSeg, B), dim3(256), 0, st,
-                     (const bf16*)logits, ld, V, pv, pi);
-  if (int e = retr_check_launch("argmax_part")) return e;
-  NextEmbed ne{word, pos, ge, be, epse, g1, b1, eps1, x, (bf16*)n, (bf16*)npos};
-  hipLaunchKernelGGL(greedy_select_embed_kernel, dim3(1), dim3(1024), 0, st, pv, pi, B, T, i, eos,
-                     pred, caption, finished, done, tok, ne);
-  return retr_check_launch("greedy_select_embed");
-}
-
 extern "C" int retr_greedy_select(int dtype, const void* logits, long ld, int B, int V,
                                   void* workspace, int T, int i, long long eos, long long* pred,
                                   long long* caption, unsigned char* finished, int* done,

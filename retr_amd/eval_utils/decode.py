@@ -54,8 +54,6 @@ DEC_FOLD_ROWS = True
 DEC_F32_SKINNY = True
 # the greedy step's MLP-head layers 1-2 on the skinny bf16 linear
 DEC_HEAD_SKINNY = True
-# greedy: the next step's embeddings + first LN1 in the selection launch
-DEC_SELECT_EMBED = False
 # rows up to which the folded (three-launch) layer is used (beyond: five launches per layer)
 DEC_FOLD_MAX_ROWS = 512
 # rows beyond which the folded FFN runs 128 hidden units per block
@@ -343,9 +341,6 @@ class IncrementalGreedy:
         x, xa = st.y, st.y2
         n0 = layers[0].tgt_self_attn.norm
         anc = ptr(st.anc) if self.beam else None
-        # greedy: the selection launch of step i - 1 already wrote this step's x / n / npos
-        sel_embed = (DEC_SELECT_EMBED and not self.beam and C == 256 and cd == torch.bfloat16
-                     and st.Vp % 8 == 0)
         nslab = F // 32
         # three launches per layer (up to 64 rows): the FFN residual + next LN1 in the next
         # layer's self-attention prologue, the cross residual + LN3 in the FFN prologue
@@ -356,7 +351,7 @@ class IncrementalGreedy:
         hb = 128 if (R > DEC_FFN_HB128_ROWS and C == 256 and F % 128 == 0 and H <= 8) else 64
         # the embeddings + first LN1 in the first self-attention launch (per-row blocks)
         embed = fold and DEC_EMBED_FOLD and rbs == 1 and C // H == 32 and i < 128
-        if not embed and not (sel_embed and i > 0):
+        if not embed:
             call("retr_dec_embed_rows", ptr(st.tok), R, C, ptr(emb.word_embeddings.weight),
                  ptr(qp), ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias),
                  float(emb.LayerNorm.eps), ptr(x), ptr(n0.weight), ptr(n0.bias), float(n0.eps),
@@ -440,16 +435,6 @@ class IncrementalGreedy:
                  ptr(st.h1), H1, 0, None, 0, 0, None, 0, 0, H1, 1, s)
             k_linear_fwd(st.h1, w2, l2.bias.detach(), st.h2, relu=1)
         k_linear_fwd(st.h2, ops.WEIGHTS.get(l3.weight, cd, rows=st.Vp), st.head_bias, st.logits)
-        if sel_embed:
-            pe = emb.position_embeddings.weight.detach()
-            qn = pe[min(i + 1, pe.shape[0] - 1)]
-            call("retr_greedy_select_embed", ptr(st.logits), st.Vp, st.B, V, ptr(st.am_ws), st.T,
-                 i, int(eos_token), ptr(st.pred), ptr(st.caption), ptr(st.finished),
-                 ptr(st.done), ptr(st.tok), C, ptr(emb.word_embeddings.weight), ptr(qn),
-                 ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias), float(emb.LayerNorm.eps),
-                 ptr(n0.weight), ptr(n0.bias), float(n0.eps), ptr(st.y), ptr(st.n),
-                 ptr(st.npos), s)
-            return
         self._select(st, i, V, eos_token, s)
 
     def _select(self, st, i, V, eos_token, s):

@@ -719,41 +719,3 @@ def test_dec_linear_f32_matches_torch(M, N, K, relu, res):
     if res:
         ref = ref + r.double()
     assert _rel(y, ref) < 1e-6
-
-
-def test_dec_select_embed_step_matches():
-    """Greedy decode with the next step's embeddings + LN1 computed in the selection launch
-    (DEC_SELECT_EMBED, retr_greedy_select_embed) against the separate retr_dec_embed_rows launch
-    on the cfg5 model: the same arithmetic, so ids and the logits of a middle step are bitwise
-    equal; graphs == eager."""
-    from bench import build, cfg5
-    from retr_amd.eval_utils import decode as dec
-    from retr_amd.synthetic import synthetic_images
-    model, _ = build(cfg5(), DEV)
-    model.eval()
-    B, T = 16, 128
-    img, mask = synthetic_images(B, 224, seed=29, pad_band=True)
-    s = NestedTensor(img.to(DEV), mask.to(DEV))
-    old = dec.DEC_SELECT_EMBED
-    res = []
-    try:
-        for f in (True, False):
-            dec.DEC_SELECT_EMBED = f
-            model._retr_decode_states = {}
-            gr = dec.IncrementalGreedy(model)
-            ids = gr(s, T, 101, 102)
-            st = next(v for k, v in model._retr_decode_states.items() if k[0] == "IncrementalGreedy")
-            with torch.no_grad():
-                gr._reset(st, 101)
-                for i in range(3):
-                    gr._step(st, i, 102)
-                torch.cuda.synchronize()
-            res.append((ids, st.logits.float().clone()))
-            if f:
-                ids_e = dec.IncrementalGreedy(model, use_graphs=False)(s, T, 101, 102)
-                assert torch.equal(ids, ids_e)
-    finally:
-        dec.DEC_SELECT_EMBED = old
-        model._retr_decode_states = {}
-    assert torch.equal(res[0][0], res[1][0])
-    assert torch.equal(res[0][1], res[1][1])
