@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--fold-max-rows", type=int, default=None,
                     help="eval_utils.decode.DEC_FOLD_MAX_ROWS (default: the module's)")
     ap.add_argument("--fp32", action="store_true", help="cfg5 in fp32 parity mode")
+    ap.add_argument("--hb128-rows", type=int, default=None,
+                    help="eval_utils.decode.DEC_FFN_HB128_ROWS (default: the module's)")
     ap.add_argument("--select-embed", type=int, default=None,
                     help="1 / 0: eval_utils.decode.DEC_SELECT_EMBED (default: the module's)")
     ap.add_argument("--head-skinny", type=int, default=0,
@@ -45,6 +47,8 @@ def main():
     if a.fold is not None:
         dec.DEC_FOLD_ROWS = bool(a.fold)
     dec.DEC_ROWS_PER_BLOCK = a.rows_per_block
+    if a.hb128_rows is not None:
+        dec.DEC_FFN_HB128_ROWS = a.hb128_rows
     if a.select_embed is not None:
         dec.DEC_SELECT_EMBED = bool(a.select_embed)
     if a.head_skinny:
