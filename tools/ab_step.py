@@ -80,8 +80,8 @@ VARIANTS = {
     "pos_off": {("ATTR", "POS_DEFER"): False},
     "up2k": {("TUNE", 28): 2048},
     "up8k": {("TUNE", 28): 8192},
-    # round 5: slice-affine conv wgrad / problem-affine linear wgrad orders are the defaults;
-    # these restore the round-4 runs of 4 logical blocks per XCD turn
+    # round 5 (opt-in, measured slower: profiles/r5_ab_wgrad_orders.txt): slice-affine conv
+    # wgrad / problem-affine linear wgrad block orders instead of runs of 4 blocks per XCD turn
     "cw_aff": {("TUNE", 20): -1},
     "wb_aff": {("TUNE", 19): -1},
     "orders_aff": {("TUNE", 19): -1, ("TUNE", 20): -1},
