@@ -181,9 +181,10 @@ enum {
                                    group's) head blocks on one XCD (its L2 holds the row's partial
                                    slabs and whole K / V cache lines), 1 block b = (b / H, b % H) */
   RETR_TUNE_DEC_WAVES = 31,     /* decode wave layouts (C 256): 0 four waves per (row, head)
-                                   attention block (hd 32, <= 128 self / 256 memory keys; greedy
-                                   0.250 -> 0.244 ms/step) and eight per FFN block; 1 two / four
-                                   (round-5 kernels as first built); 2 four / four */
+                                   attention block (hd 32, <= 128 self / 256 memory keys), 16 per
+                                   64-unit FFN block, 8 per 128-unit block; 1 two / four (round-5
+                                   kernels as first built); 2 four / four; 3 16-wave FFN blocks
+                                   of both widths; 4 eight-wave 64-unit FFN blocks */
   RETR_TUNE_COUNT = 32
 };
 int retr_tune(int knob, int value);

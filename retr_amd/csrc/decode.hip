@@ -1203,7 +1203,9 @@ int retr_dec_ffn_ln64(const float* xin, const float* hslab, int nslab, const flo
   // 8 waves (2 LayerNorm rows, 2 FFN2 column tiles each) unless RETR_TUNE_DEC_WAVES asks for 4
   const int kn = retr_tune_get(RETR_TUNE_DEC_WAVES);
   const bool w8 = C == 256 && nslab <= 8 && kn != 1 && kn != 2;
-  if (w8 && kn == 3) {                     // sweeps: 16 waves (one LayerNorm row, one FFN2 tile)
+  // 16 waves (one LayerNorm row, one FFN2 column tile each) by default: greedy 0.227 -> 0.223
+  // ms/step; RETR_TUNE_DEC_WAVES 4 keeps 8
+  if (w8 && kn != 4) {
     hipLaunchKernelGGL((dec_ffn_ln_kernel<4, 8, 64, 16>), grid, dim3(1024), 0, st, xin, hslab,
                        nslab, bo, gamma, beta, eps, xout, R, (const bf16*)w1, b1,
                        (const bf16*)w2, F, slabs);
@@ -1230,9 +1232,15 @@ int retr_dec_ffn_ln128(const float* xin, const float* hslab, int nslab, const fl
                "dec_ffn_ln128: C=%d F=%d nslab=%d (C 256, nslab <= 8)", C, F, nslab);
   if (R == 0) return 0;
   // 8 waves: FFN1 column tile w (16 hidden units) each, 2 FFN2 column tiles x 4 K-steps each
-  hipLaunchKernelGGL((dec_ffn_ln_kernel<4, 8, 128, 8>), dim3(F / 128, cdiv(R, 16)), dim3(512), 0,
-                     (hipStream_t)stream, xin, hslab, nslab, bo, gamma, beta, eps, xout, R,
-                     (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
+  // (RETR_TUNE_DEC_WAVES 3, sweeps: 16 waves, one LayerNorm row / FFN2 tile each)
+  if (retr_tune_get(RETR_TUNE_DEC_WAVES) == 3)
+    hipLaunchKernelGGL((dec_ffn_ln_kernel<4, 8, 128, 16>), dim3(F / 128, cdiv(R, 16)), dim3(1024),
+                       0, (hipStream_t)stream, xin, hslab, nslab, bo, gamma, beta, eps, xout, R,
+                       (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
+  else
+    hipLaunchKernelGGL((dec_ffn_ln_kernel<4, 8, 128, 8>), dim3(F / 128, cdiv(R, 16)), dim3(512), 0,
+                       (hipStream_t)stream, xin, hslab, nslab, bo, gamma, beta, eps, xout, R,
+                       (const bf16*)w1, b1, (const bf16*)w2, F, slabs);
   return retr_check_launch("dec_ffn_ln128");
 }
 
