@@ -14,6 +14,7 @@ host's cores (training step and the reference decode algorithm).
 Rank 0 prints one JSON line.
 """
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -31,6 +32,12 @@ from retr_amd.models.utils import NestedTensor  # noqa: E402
 from retr_amd.synthetic import (synthetic_captions, synthetic_images,  # noqa: E402
                                 synthetic_state_dict)
 from retr_amd import probe as probe_mod  # noqa: E402
+
+# Collective timeout of the bench's process group: every rank runs the same build / capture /
+# timed loop, so no collective legitimately waits long; a deadlocked multi-rank run (a schedule
+# disagreement the pre-flight missed, a lost rank) then fails within minutes instead of holding
+# the node for NCCL's default 10 minutes per collective.
+DIST_TIMEOUT = datetime.timedelta(minutes=2)
 
 METRIC = "RefCOCO images/sec (train fwd+bwd) at 1/2/4/8 GPUs; greedy-decode refs/sec"
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
@@ -345,11 +352,18 @@ def cpu_baseline(args, cores):
                       f"after 1 warm-up, fp32 oracle/model.py, {cores} threads"}
 
 
-def _traffic(family):
-    """Per-launch HBM bytes of ``family`` from the committed rocprofv3 --pmc pass
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py with the gfx950 FETCH_SIZE x2
-    correction), or None when no counter pass covers it."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def _pmc_path(kind, workload):
+    """The committed rocprofv3 --pmc summary of ``kind`` ("traffic" / "mfma") for ``workload``:
+    profiles/pmc_<kind>_<workload>.json.  Counters are only ever reported for the workload they
+    were collected on: no file, no counter fields."""
+    return os.path.join(ROOT, "profiles", f"pmc_{kind}_{workload}.json")
+
+
+def _traffic(family, workload):
+    """Per-launch HBM bytes of ``family`` from the workload's committed rocprofv3 --pmc pass
+    (profiles/pmc_traffic_<workload>.json, written by tools/pmc_traffic.py with the gfx950
+    FETCH_SIZE x2 correction), or None when no counter pass covers it."""
+    path = _pmc_path("traffic", workload)
     try:
         with open(path) as f:
             d = json.load(f)
@@ -361,11 +375,11 @@ def _traffic(family):
     return ent, d.get("source")
 
 
-def _traffic_fields(family, calls_per_step, bytes_per_call):
+def _traffic_fields(family, calls_per_step, bytes_per_call, workload):
     """Counted HBM traffic of ``family`` in both units: per kernel DISPATCH (what the --pmc pass
     measures) and per retr_* API CALL (what the probe times; one call can dispatch several
     kernels), with the counted / algorithmic ratio per call."""
-    ent, src = _traffic(family)
+    ent, src = _traffic(family, workload)
     if not ent:
         return {"traffic": None, "traffic_source": None}
     out = {"traffic": ent.get("bytes_per_launch"), "traffic_unit": "bytes per dispatch",
@@ -380,7 +394,7 @@ def _traffic_fields(family, calls_per_step, bytes_per_call):
     return out
 
 
-def _roofline(fam, psteps):
+def _roofline(fam, psteps, workload):
     """Roofline object of the dominant kernel family (most device time per step).  Its bound is
     set by its arithmetic intensity (algorithmic FLOP / algorithmic HBM bytes, summed over its
     launches) against the ridge point 2.5 PF / 8 TB/s = 312.5 FLOP/B: below it the family is
@@ -397,7 +411,7 @@ def _roofline(fam, psteps):
     else:
         achieved, peak, unit = d["tflops"], PEAK_BF16_TFLOPS, "TFLOP/s"
     n = max(1, d["launches"])
-    tf = _traffic_fields(dom_key, d["launches"] / psteps, d["bytes"] / n)
+    tf = _traffic_fields(dom_key, d["launches"] / psteps, d["bytes"] / n, workload)
     return {"bound": "hbm" if hbm else "mfma", "kernel": dom_key,
             "kernel_symbol": probe_mod.FAMILY_SYMBOL.get(dom_key, dom_key),
             "achieved": round(achieved, 2), "peak": peak, "unit": unit,
@@ -407,7 +421,7 @@ def _roofline(fam, psteps):
             "tflops": round(d["tflops"], 2), "mfma_frac": round(d["tflops"] / PEAK_BF16_TFLOPS, 4),
             "gbs": round(d["gbs"], 1), "hbm_frac": round(d["gbs"] / PEAK_HBM_GBS, 4),
             "attainable_frac": round(d["attainable_frac"], 4),
-            "mfma_busy": _mfma_busy(dom_key),
+            "mfma_busy": _mfma_busy(dom_key, workload),
             "api_calls_per_step": d["launches"] // psteps,
             "avg_launch_us": round(d["ms_avg"] * 1e3, 2),
             "flops_per_launch": round(d["flops"] / n, 1),
@@ -418,17 +432,29 @@ def _roofline(fam, psteps):
                       "device time only; eager re-run of the step"}
 
 
-def _mfma_busy(family):
-    """MFMA-busy fraction of ``family`` from the committed rocprofv3 --pmc pass
-    (profiles/pmc_mfma.json, tools/pmc_mfma.py): SQ_VALU_MFMA_BUSY_CYCLES over
+def _mfma_busy(family, workload):
+    """MFMA-busy fraction of ``family`` from the workload's committed rocprofv3 --pmc pass
+    (profiles/pmc_mfma_<workload>.json, tools/pmc_mfma.py): SQ_VALU_MFMA_BUSY_CYCLES over
     (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), i.e. rocprof's MfmaUtil per launch."""
     try:
-        with open(os.path.join(ROOT, "profiles", "pmc_mfma.json")) as f:
+        with open(_pmc_path("mfma", workload)) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
     ent = d.get("families", {}).get(family)
     return None if not ent else ent.get("mfma_busy")
+
+
+def init_dist(local, backend="nccl"):
+    """One process per GPU from the torchrun environment (RANK / WORLD_SIZE / MASTER_*), RCCL
+    ("nccl") over xGMI, with the bench's short collective timeout (DIST_TIMEOUT)."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=DIST_TIMEOUT)
+    else:
+        dist.init_process_group(backend, timeout=DIST_TIMEOUT)
 
 
 def main():
@@ -469,23 +495,22 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        init_dist(local)
     device = torch.device("cuda", local)
     torch.manual_seed(42 + rank)
 
     dt, loss, fam, psteps, sched = train_bench(args, rank, world, device)
     imgs = world * args.batch * args.steps
     value = imgs / dt
-    roof = _roofline(fam, psteps)
+    roof = _roofline(fam, psteps, args.workload)
     families = {k: {"ms_per_step": round(v["ms_total"] / psteps, 3),
                     "tflops": round(v["tflops"], 1), "gbs": round(v["gbs"], 1),
                     "bound": "hbm" if v["intensity"] < probe_mod.RIDGE else "mfma",
                     "attainable_frac": round(v["attainable_frac"], 4),
                     "api_calls_per_step": v["launches"] // psteps,
                     **{f: t for f, t in _traffic_fields(
-                        k, v["launches"] / psteps, v["bytes"] / max(1, v["launches"])).items()
+                        k, v["launches"] / psteps, v["bytes"] / max(1, v["launches"]),
+                        args.workload).items()
                        if f in ("dispatches_per_step", "traffic", "traffic_per_call",
                                 "traffic_over_algorithmic")}}
                 for k, v in sorted(fam.items(), key=lambda kv: -kv[1]["ms_total"])}

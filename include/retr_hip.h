@@ -720,6 +720,40 @@ int retr_dec_ffn_ln128(const float* xin, const float* hslab, int nslab, const fl
                        int C, const void* w1, const float* b1, const void* w2, int F,
                        float* slabs, void* stream);
 
+/* ---- fused decode step of the fp32 parity mode (csrc/decode_f32.hip, round 6): the same
+ * three launches per decoder layer as the bf16 step, every value fp32 (eval_utils/decode.py:53-81
+ * greedy / beam steps; models/transformer_modules.py:22-97, ConcatTransformer.py:187-214,
+ * 224-243).  d_model 256, 8 heads; all row / weight operands 16-byte aligned. */
+/* block (row, head): prologue x = xin + (sum_j slabs[j] + b2) (slabs [nslab][R][C]) or, with
+ * tok != NULL (layer 0), x = LN_e(word[tok] + qpos); x -> xout (h = 0 blocks); LN1(x) (+qpos)
+ * -> the head's q | k | v (win [3C][C], bin [3C]), k / v -> cache row r * Lmax + i (fp32
+ * caches), attention over keys 0..i (anc: beam ancestry [R][Lmax] or NULL), the head's partial
+ * out-projection -> slab [H][R][C] */
+int retr_dec_self_f32(int R, int C, int H, const float* win, const float* bin, float* kc,
+                      float* vc, int i, int Lmax, const int* anc, const float* wo, float* slab,
+                      const float* xin, const float* slabs, int nslab, const float* b2,
+                      const long long* tok, const float* word, const float* ge, const float* be,
+                      float epse, const float* gamma, const float* beta, float eps,
+                      const float* qpos, float* xout, void* stream);
+/* block (row, head): x' = x + (sum_h slab_in[h] + bo_in) -> xo; LN2(x') + pos -> the head's cross
+ * query (wq rows 0..C, bq), attention over Lk memory rows (r / kv_group) * Lk + j (kpm
+ * [R / kv_group][Lk] or NULL), the head's partial out-projection -> slab_out [H][R][C] */
+int retr_dec_cross_f32(int R, int C, int H, const float* slab_in, const float* x,
+                       const float* bo_in, float* xo, const float* gamma, const float* beta,
+                       float eps, const float* pos, const float* wq, const float* bq,
+                       const float* k, const float* v, int Lk, int kv_group,
+                       const unsigned char* kpm, const float* wo, float* slab_out, void* stream);
+/* x'' = xin + (sum_j hslab[j] + bo) -> xout; FFN partials of LN3(x'') over 64 hidden units per
+ * block (exact-f32 MFMA) -> slabs [F / 64][R][C] */
+int retr_dec_ffn_f32(const float* xin, const float* hslab, int nslab, const float* bo,
+                     const float* gamma, const float* beta, float eps, float* xout, int R, int C,
+                     const float* w1, const float* b1, const float* w2, int F, float* slabs,
+                     void* stream);
+/* x = xin + (sum_j slabs[j] + b2) -> xout (optional); n = LN(x) (fp32) */
+int retr_dec_rows_f32(const float* xin, const float* slabs, int nslab, const float* b2, int R,
+                      int C, float* xout, const float* gamma, const float* beta, float eps,
+                      float* n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,6 +5,7 @@ every op raises.  Build the library with ``make`` (or ``__graft_entry__.build()`
 """
 import ctypes
 import os
+import warnings
 
 import torch
 
@@ -209,6 +210,12 @@ _SIGS = {
     "retr_dec_linear_bf16": [_P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _P],
     "retr_dec_linear_f32": [_P, _L, _P, _L, _P, _P, _L, _I, _I, _I, _I, _P, _L, _P],
     "retr_dec_linear3_f32": [_I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _L, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _L, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _L, _I, _I, _P],
+    "retr_dec_self_f32": [_I, _I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P,
+                          _P, _P, _F, _P, _P, _F, _P, _P, _P],
+    "retr_dec_cross_f32": [_I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I, _P,
+                           _P, _P, _P],
+    "retr_dec_ffn_f32": [_P, _P, _I, _P, _P, _P, _F, _P, _I, _I, _P, _P, _P, _I, _P, _P],
+    "retr_dec_rows_f32": [_P, _P, _I, _P, _I, _I, _P, _P, _P, _F, _P, _P],
     "retr_dec_ffn_ln64": [_P, _P, _I, _P, _P, _P, _F, _P, _I, _I, _P, _P, _P, _I, _P, _P],
     "retr_dec_ffn_ln128": [_P, _P, _I, _P, _P, _P, _F, _P, _I, _I, _P, _P, _P, _I, _P, _P],
     "retr_dec_self_heads_ln": [_P, _P, _I, _I, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _I,
@@ -250,9 +257,17 @@ def load():
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, ctypes.c_int)
         # RETR_TUNE_<knob>=<value> in the environment presets a tuning knob (A/B runs)
+        # (a malformed value or an unknown knob number is reported and skipped: it must not
+        # break every import of the package)
         for k, v in os.environ.items():
             if k.startswith("RETR_TUNE_") and k[10:].isdigit():
-                lib.retr_tune(int(k[10:]), int(v))
+                try:
+                    val = int(v)
+                except ValueError:
+                    warnings.warn(f"retr_amd: ignoring {k}={v!r} (not an integer)")
+                    continue
+                if lib.retr_tune(int(k[10:]), val) != 0:
+                    warnings.warn(f"retr_amd: ignoring {k}={v!r} (no tuning knob {k[10:]})")
         _lib = lib
     return _lib
 

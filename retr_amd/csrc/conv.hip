@@ -1207,12 +1207,8 @@ Geom make_geom(int Nb, int H, int W, int C, int Co, int KH, int KW, int s, int p
 // stream order); logical blocks go to the XCDs in runs of kCWChunk, the XCDs taking turns, with
 // the longest blocks first.
 //
-// Slice-affine order (round 5, opt-in: RETR_TUNE_CW_CHUNK = -1; measured slower): every tile of one K-slice (one pixel range of one
-// conv) runs on ONE XCD, the slices dealt to the XCDs round-robin (longest blocks first).  The
-// tiles of a slice all read the same dY rows and X rows, so that XCD's L2 fetches them from HBM
-// once; in runs of 4 tiles per XCD turn (the round-4 order, still selectable with a positive
-// RETR_TUNE_CW_CHUNK) the 36 tiles of a 3x3 / 256-channel slice were spread over 9 runs on
-// different XCDs and dY came from HBM ~4.5 times (1.89x the algorithmic bytes per step).
+// (Round 5's slice-affine order -- every tile of one K-slice on one XCD, from a host-built piece
+// table -- was measured 0.17 ms/step slower and has been removed: DESIGN.md §4.)
 struct CWProb {
   const bf16* dy;
   const bf16* x;
@@ -1220,52 +1216,32 @@ struct CWProb {
   Geom g;
   int splits, kchunk, tiles_n, tiles, blk0, vec;
 };
-struct CWPiece {    // slice-affine order: one K-slice of one problem, all its tiles on one XCD
-  int prob, split, pre, pad;   // pre: position of the slice's first block in its XCD's queue
-};
 struct CWHead {
-  int nprob, total, npiece, pad1;
-  int xpiece[8];    // first piece of each XCD (pieces stored XCD by XCD)
-  int xtot[8];      // blocks in each XCD's queue
+  int nprob, total, pad0, pad1;
 };
-static_assert(sizeof(CWProb) == 96 && sizeof(CWHead) == 80 && sizeof(CWPiece) == 16,
-              "conv wgrad table");
+static_assert(sizeof(CWProb) == 96 && sizeof(CWHead) == 16, "conv wgrad table");
 constexpr int kCWChunk = 4;
-constexpr int kCWMaxSlices = 128;   // per problem (the plan caps the split count at 128)
 
 template <int KIND, int NW, int BN = 128>
 __global__ void __launch_bounds__(NW * 64) conv_wgrad_group_kernel(const char* __restrict__ table,
                                                                    int chunk) {
   const CWHead& h = *(const CWHead*)table;
   const CWProb* P = (const CWProb*)(table + sizeof(CWHead));
-  const CWPiece* Q = (const CWPiece*)(table + sizeof(CWHead) + (size_t)h.nprob * sizeof(CWProb));
   const int hw = blockIdx.x, xc = hw & 7, q = hw >> 3;
   const int nprob = h.nprob;
   int lo = 0, split, tile;
-  if (chunk > 0) {                       // runs of `chunk` logical blocks per XCD turn
-    const int L = (q / chunk) * (8 * chunk) + xc * chunk + q % chunk;
-    if (L >= h.total) return;
-    int hi = nprob - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (P[mid].blk0 <= L) lo = mid;
-      else hi = mid - 1;
-    }
-    const int local = L - P[lo].blk0;
-    split = local / P[lo].tiles;
-    tile = local - split * P[lo].tiles;
-  } else {                               // slice-affine: this XCD's slices in queue order
-    if (q >= h.xtot[xc]) return;
-    int a = h.xpiece[xc], b = (xc < 7 ? h.xpiece[xc + 1] : h.npiece) - 1;
-    while (a < b) {
-      const int mid = (a + b + 1) >> 1;
-      if (Q[mid].pre <= q) a = mid;
-      else b = mid - 1;
-    }
-    lo = Q[a].prob;
-    split = Q[a].split;
-    tile = q - Q[a].pre;
+  // runs of `chunk` logical blocks per XCD turn
+  const int L = (q / chunk) * (8 * chunk) + xc * chunk + q % chunk;
+  if (L >= h.total) return;
+  int hi = nprob - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (P[mid].blk0 <= L) lo = mid;
+    else hi = mid - 1;
   }
+  const int local = L - P[lo].blk0;
+  split = local / P[lo].tiles;
+  tile = local - split * P[lo].tiles;
   if (lo >= nprob || split >= P[lo].splits || tile >= P[lo].tiles) return;   // table guard
   const CWProb d = P[lo];
   const Geom& g = d.g;
@@ -1503,14 +1479,17 @@ int pack_class(const retr_conv_pack_desc* const* d, int n, hipStream_t st) {
 
 template <typename T>
 int pack_all(int n, const retr_conv_pack_desc* d, hipStream_t st) {
-  // classes: 3x3 / 1x1 tiled (Ci == Cp, 64 | Co, 64 | Cp), everything else elementwise
+  // classes: 3x3 / 1x1 tiled (Ci == Cp, 64 | Co, 64 | Cp, 16-byte aligned w / w_out / wt_out:
+  // the tiled kernel moves float4 / 16-byte chunks), everything else elementwise
   const retr_conv_pack_desc* c9[256];
   const retr_conv_pack_desc* c1[256];
   const retr_conv_pack_desc* ce[256];
   int n9 = 0, n1 = 0, ne = 0;
   for (int i = 0; i < n; ++i) {
     const retr_conv_pack_desc& q = d[i];
-    const bool tiled = q.Ci == q.Cp && q.Co % 64 == 0 && q.Cp % 64 == 0;
+    const bool aligned =
+        (((uintptr_t)q.w | (uintptr_t)q.w_out | (uintptr_t)q.wt_out) & 15) == 0;
+    const bool tiled = q.Ci == q.Cp && q.Co % 64 == 0 && q.Cp % 64 == 0 && aligned;
     if (tiled && q.KH * q.KW == 9) c9[n9++] = &q;
     else if (tiled && q.KH * q.KW == 1) c1[n1++] = &q;
     else ce[ne++] = &q;
@@ -1585,8 +1564,8 @@ int retr_conv2d_wgrad_splits(int dtype, int Nb, int H, int W, int C, int Co, int
 }
 
 size_t retr_conv2d_wgrad_group_table_bytes(int n) {
-  // two kinds, each header + problems + slices, each start 256-byte aligned
-  return n < 0 ? 0 : 2 * (sizeof(CWHead) + 256) + (size_t)n * (sizeof(CWProb) + kCWMaxSlices * sizeof(CWPiece));
+  // two kinds, each header + problems, each start 256-byte aligned
+  return n < 0 ? 0 : 2 * (sizeof(CWHead) + 256) + (size_t)n * sizeof(CWProb);
 }
 
 int retr_conv2d_wgrad_group_plan(int dtype, int n, retr_conv_wgrad_desc* d) {
@@ -1648,7 +1627,7 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
       return cdiv(g.Nb * g.OH * g.OW, d[i].splits);
     };
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return blk_len(a) > blk_len(b); });
-    std::vector<char> buf(sizeof(CWHead) + ord.size() * (sizeof(CWProb) + kCWMaxSlices * sizeof(CWPiece)) + 16, 0);
+    std::vector<char> buf(sizeof(CWHead) + ord.size() * sizeof(CWProb) + 16, 0);
     CWHead* h = (CWHead*)buf.data();
     CWProb* P = (CWProb*)(buf.data() + sizeof(CWHead));
     int blocks = 0;
@@ -1674,30 +1653,7 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
     }
     h->nprob = (int)ord.size();
     h->total = blocks;
-    // slice-affine pieces: every K-slice to the least-loaded XCD (load = tiles x K-steps), in
-    // order (longest blocks first)
-    std::vector<CWPiece> per[8];
-    long load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (size_t j = 0; j < ord.size(); ++j) {
-      for (int sp = 0; sp < P[j].splits; ++sp) {
-        int best = 0;
-        for (int x = 1; x < 8; ++x)
-          if (load[x] < load[best]) best = x;
-        const int pre = per[best].empty() ? 0 : per[best].back().pre + P[per[best].back().prob].tiles;
-        per[best].push_back(CWPiece{(int)j, sp, pre, 0});
-        load[best] += (long)P[j].tiles * (P[j].kchunk / 64);
-      }
-    }
-    CWPiece* Qd = (CWPiece*)(buf.data() + sizeof(CWHead) + ord.size() * sizeof(CWProb));
-    int npc = 0, xmax = 0;
-    for (int x = 0; x < 8; ++x) {
-      h->xpiece[x] = npc;
-      for (const CWPiece& w : per[x]) Qd[npc++] = w;
-      h->xtot[x] = per[x].empty() ? 0 : per[x].back().pre + P[per[x].back().prob].tiles;
-      xmax = h->xtot[x] > xmax ? h->xtot[x] : xmax;
-    }
-    h->npiece = npc;
-    const size_t used = sizeof(CWHead) + ord.size() * sizeof(CWProb) + (size_t)npc * sizeof(CWPiece);
+    const size_t used = sizeof(CWHead) + ord.size() * sizeof(CWProb);
     const int words = (int)((used + 3) / 4);
     const unsigned* src = (const unsigned*)buf.data();
     for (int off = 0; off < words; off += 640) {
@@ -1708,11 +1664,10 @@ int retr_conv2d_wgrad_group(int dtype, int n, const retr_conv_wgrad_desc* d, voi
       hipLaunchKernelGGL(cw_table_put_kernel, dim3(1), dim3(256), 0, st, c, (unsigned*)table);
       if (int e = retr_check_launch("conv2d_wgrad_group table")) return e;
     }
-    // RETR_TUNE_CW_CHUNK: 0 (default) runs of kCWChunk logical blocks per XCD turn, n > 0 runs
-    // of n, -1 slice-affine (0.17 ms/step slower: profiles/r5_ab_wgrad_orders.txt)
+    // RETR_TUNE_CW_CHUNK > 0: runs of that many logical blocks per XCD turn (sweeps); else kCWChunk
     int chunk = retr_tune_get(RETR_TUNE_CW_CHUNK);
-    chunk = chunk > 0 ? chunk : (chunk < 0 ? 0 : kCWChunk);
-    const int grid = chunk > 0 ? cdiv(blocks, 8 * chunk) * 8 * chunk : 8 * xmax;
+    chunk = chunk > 0 ? chunk : kCWChunk;
+    const int grid = cdiv(blocks, 8 * chunk) * 8 * chunk;
     const int nw = wl == 1 ? 4 : wl == 2 ? 8 : (kind == 0 ? 4 : 8);
     auto launch = [&](auto kern, int threads, size_t lds) {
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -979,33 +979,49 @@ dec_ffn_ln_kernel(const float* xin, const float* hslab, int nslab, const float* 
     *(f4v*)(gm + e) = *(const f4v*)(gamma + c0 + e);
     *(f4v*)(bt + e) = *(const f4v*)(beta + c0 + e);
   }
-  // the wave's RPW rows: every slab / residual load in flight at once
-  float t[RPW][MAXS][CPL], xv[RPW][CPL];
+  // the wave's RPW rows: slab loads in flight SCH slabs at a time (every one of them when the
+  // registers allow: 64 floats per lane), summed per column in slab order
+  constexpr int SCH0 = 64 / (RPW * CPL) < 1 ? 1 : 64 / (RPW * CPL);
+  constexpr int SCH = SCH0 < MAXS ? SCH0 : MAXS;
+  float sacc[RPW][CPL], xv[RPW][CPL];
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     const int r = r0 + RPW * w + q;
     const int rr = r < R ? r : R - 1;
 #pragma unroll
-    for (int j = 0; j < MAXS; ++j)
-#pragma unroll
-      for (int e = 0; e < CPL; e += 4)
-        *(f4v*)(&t[q][j][e]) = j < nslab ? *(const f4v*)(hslab + j * RC + (long)rr * C + c0 + e)
-                                         : f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
     for (int e = 0; e < CPL; e += 4) *(f4v*)(&xv[q][e]) = *(const f4v*)(xin + (long)rr * C + c0 + e);
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) sacc[q][e] = 0.f;
+  }
+#pragma unroll
+  for (int j0 = 0; j0 < MAXS; j0 += SCH) {
+    float t[RPW][SCH][CPL];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int r = r0 + RPW * w + q;
+      const int rr = r < R ? r : R - 1;
+#pragma unroll
+      for (int j = 0; j < SCH; ++j)
+#pragma unroll
+        for (int e = 0; e < CPL; e += 4)
+          *(f4v*)(&t[q][j][e]) = j0 + j < nslab
+                                     ? *(const f4v*)(hslab + (j0 + j) * RC + (long)rr * C + c0 + e)
+                                     : f4v{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q)
+#pragma unroll
+      for (int e = 0; e < CPL; ++e)
+#pragma unroll
+        for (int j = 0; j < SCH; ++j)
+          if (j0 + j < nslab) sacc[q][e] += t[q][j][e];
   }
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     const int r = r0 + RPW * w + q;
     float v[CPL];
 #pragma unroll
-    for (int e = 0; e < CPL; ++e) {
-      float s = 0.f;
-#pragma unroll
-      for (int j = 0; j < MAXS; ++j)
-        if (j < nslab) s += t[q][j][e];
-      v[e] = xv[q][e] + (s + bb[e]);
-    }
+    for (int e = 0; e < CPL; ++e) v[e] = xv[q][e] + (sacc[q][e] + bb[e]);
     float sm = 0.f;
 #pragma unroll
     for (int e = 0; e < CPL; ++e) sm += v[e];

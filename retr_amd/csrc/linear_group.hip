@@ -592,33 +592,19 @@ struct WBRow {                // dst[c] (=|+=) sum_s parts[s * stride + c]
   float* dst;
   int stride, nparts, cols, accumulate, blk0, pad;
 };
-// Problem-affine block order (round 5, opt-in: RETR_TUNE_WB_CHUNK = -1): the tiles of one problem -- or, for a
-// problem with more than kWBPieceTiles tiles (the vocabulary head), of one run of whole row
-// tiles -- form a PIECE that runs on ONE XCD; pieces go to the XCDs longest-problem first, each
-// to the XCD with the least work so far.  All tiles of a piece read the same X panels (and a row
-// tile's column tiles the same dY panel), so that XCD's L2 fetches them from HBM once; dealt in
-// runs of 4 tiles per XCD turn (round 4, still selectable with RETR_TUNE_WB_CHUNK > 0) the
-// 32-tile FFN problems were spread over 8 L2s and each fetched the shared panel itself
-// (1.54x the algorithmic bytes per step).
-struct WBPiece {
-  int prob, tile0, ntiles, pre;   // pre: position of the piece's first block in its XCD queue
-};
+// Block order: logical blocks (problems longest-reduction first, then the partial-row sums) go
+// to the XCDs in runs of kWBChunk (RETR_TUNE_WB_CHUNK > 0: runs of that many), the XCDs taking
+// turns.  (Round 5's problem-affine order -- every tile of a problem on one XCD, from a host-built
+// piece table -- was measured 0.05 ms/step slower and has been removed: DESIGN.md §4.)
 struct WBHead {
   int nprob, nrow, gemm_blocks, total;
-  int npiece, rblocks, pad0, pad1;
-  int xpiece[8];                  // first piece of each XCD (pieces stored XCD by XCD)
-  int xtot[8];                    // GEMM blocks in each XCD's queue
 };
-static_assert(sizeof(WBProb) == 64 && sizeof(WBRow) == 40 && sizeof(WBHead) == 96 &&
-                  sizeof(WBPiece) == 16, "table");
+static_assert(sizeof(WBProb) == 64 && sizeof(WBRow) == 40 && sizeof(WBHead) == 16, "table");
 
-constexpr int kWBChunk = 4;        // default order: consecutive logical blocks per XCD turn
-constexpr int kWBPieceTiles = 64;  // one XCD's block slots (32 CUs x 2)
-constexpr int kWBMaxPieces = 16;   // per problem (table bound)
+constexpr int kWBChunk = 4;        // consecutive logical blocks per XCD turn
 
 size_t wb_table_bytes(int n, int nx) {
-  return sizeof(WBHead) + (size_t)n * sizeof(WBProb) + (size_t)nx * sizeof(WBRow) +
-         (size_t)n * kWBMaxPieces * sizeof(WBPiece);
+  return sizeof(WBHead) + (size_t)n * sizeof(WBProb) + (size_t)nx * sizeof(WBRow);
 }
 
 template <int BM, int S>
@@ -628,39 +614,21 @@ __global__ void __launch_bounds__(256) wgrad_batch_kernel(const char* __restrict
   const WBHead& h = *(const WBHead*)table;
   const WBProb* P = (const WBProb*)(table + sizeof(WBHead));
   const WBRow* R = (const WBRow*)(table + sizeof(WBHead) + (size_t)h.nprob * sizeof(WBProb));
-  const WBPiece* Q = (const WBPiece*)((const char*)R + (size_t)h.nrow * sizeof(WBRow));
-  // hardware block b runs on XCD b % 8
+  // hardware block b runs on XCD b % 8: logical blocks in `chunk` runs, the XCDs taking turns
   const int hw = blockIdx.x, x = hw & 7, q = hw >> 3;
+  const int L = (q / chunk) * (8 * chunk) + x * chunk + q % chunk;
+  if (L >= h.total) return;
   int lo = 0, tile = 0, rb = -1;
-  if (chunk > 0) {
-    // round-4 order: logical blocks in `chunk` runs, the XCDs taking turns
-    const int L = (q / chunk) * (8 * chunk) + x * chunk + q % chunk;
-    if (L >= h.total) return;
-    if (L >= h.gemm_blocks) {
-      rb = L - h.gemm_blocks;
-    } else {
-      int hi = h.nprob - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (P[mid].blk0 <= L) lo = mid;
-        else hi = mid - 1;
-      }
-      tile = L - P[lo].blk0;
-    }
-  } else if (q < h.xtot[x]) {
-    // problem-affine: this XCD's pieces in queue order
-    int a = h.xpiece[x], b = (x < 7 ? h.xpiece[x + 1] : h.npiece) - 1;
-    while (a < b) {
-      const int mid = (a + b + 1) >> 1;
-      if (Q[mid].pre <= q) a = mid;
-      else b = mid - 1;
-    }
-    lo = Q[a].prob;
-    tile = Q[a].tile0 + (q - Q[a].pre);
+  if (L >= h.gemm_blocks) {
+    rb = L - h.gemm_blocks;
   } else {
-    // the partial-row sums after the XCD's GEMM blocks, dealt round-robin
-    rb = (q - h.xtot[x]) * 8 + x;
-    if (rb >= h.rblocks) return;
+    int hi = h.nprob - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (P[mid].blk0 <= L) lo = mid;
+      else hi = mid - 1;
+    }
+    tile = L - P[lo].blk0;
   }
   if (rb >= 0) {
     int j = 0;
@@ -725,7 +693,7 @@ __global__ void __launch_bounds__(256) table_put_kernel(PutChunk c, unsigned* ds
 }
 
 template <int BM, int S>
-int wgrad_batch_launch(const char* table, int total, int grid_affine, hipStream_t st) {
+int wgrad_batch_launch(const char* table, int total, hipStream_t st) {
   constexpr size_t lds = gemm2_lds_bytes<BM, BM, S, 0>();
   auto kern = wgrad_batch_kernel<BM, S>;
   if constexpr (lds > 65536) {
@@ -736,11 +704,10 @@ int wgrad_batch_launch(const char* table, int total, int grid_affine, hipStream_
       attr_set = true;
     }
   }
-  // RETR_TUNE_WB_CHUNK: 0 runs of kWBChunk blocks per XCD turn (default), n > 0 runs of n,
-  // -1 problem-affine pieces (measured 0.05 ms/step slower: profiles/r5_ab_wgrad_orders.txt)
+  // RETR_TUNE_WB_CHUNK > 0: runs of that many blocks per XCD turn (sweeps); else kWBChunk
   const int knob = retr_tune_get(RETR_TUNE_WB_CHUNK);
-  const int chunk = knob > 0 ? knob : (knob < 0 ? 0 : kWBChunk);
-  const int grid = chunk > 0 ? cdiv(total, 8 * chunk) * 8 * chunk : grid_affine;
+  const int chunk = knob > 0 ? knob : kWBChunk;
+  const int grid = cdiv(total, 8 * chunk) * 8 * chunk;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, table, chunk);
   return retr_check_launch("linear_wgrad_batch");
 }
@@ -988,41 +955,9 @@ int retr_linear_wgrad_batch(int n, const retr_linear_wgrad_desc* d, int nx,
   h->nrow = nr;
   h->gemm_blocks = blocks;
   h->total = blocks + rblocks;
-  h->rblocks = rblocks;
   if (h->total == 0) return 0;
-  // problem-affine pieces (see WBPiece): whole problems, or runs of whole row tiles of at most
-  // kWBPieceTiles tiles, each to the least-loaded XCD (load = tiles x K-steps), longest first
-  std::vector<WBPiece> per[8];
-  long load[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int j = 0; j < np; ++j) {
-    const WBProb& p = P[j];
-    const int tn = p.flags >> 2, tm = cdiv(p.N, bm), tiles = tm * tn;
-    int rows = tiles <= kWBPieceTiles ? tm : (kWBPieceTiles / tn > 0 ? kWBPieceTiles / tn : 1);
-    if (cdiv(tm, rows) > kWBMaxPieces) rows = cdiv(tm, kWBMaxPieces);
-    for (int r0 = 0; r0 < tm; r0 += rows) {
-      const int nt = (r0 + rows <= tm ? rows : tm - r0) * tn;
-      int best = 0;
-      for (int xx = 1; xx < 8; ++xx)
-        if (load[xx] < load[best]) best = xx;
-      const int pre = per[best].empty() ? 0 : per[best].back().pre + per[best].back().ntiles;
-      per[best].push_back(WBPiece{j, r0 * tn, nt, pre});
-      load[best] += (long)nt * cdiv(p.M, 64);
-    }
-  }
-  WBPiece* Qd = (WBPiece*)((char*)R + (size_t)nr * sizeof(WBRow));
-  int npc = 0, gmax = 0;
-  for (int xx = 0; xx < 8; ++xx) {
-    h->xpiece[xx] = npc;
-    for (const WBPiece& w : per[xx]) Qd[npc++] = w;
-    h->xtot[xx] = per[xx].empty() ? 0 : per[xx].back().pre + per[xx].back().ntiles;
-    const int q = h->xtot[xx] + (rblocks > xx ? (rblocks - xx + 7) / 8 : 0);
-    gmax = q > gmax ? q : gmax;
-  }
-  h->npiece = npc;
-  RETR_REQUIRE(npc <= np * kWBMaxPieces, "linear_wgrad_batch: %d pieces", npc);
   // the table into device memory, in stream order before the GEMM launch
-  const size_t used = sizeof(WBHead) + (size_t)np * sizeof(WBProb) + (size_t)nr * sizeof(WBRow) +
-                      (size_t)npc * sizeof(WBPiece);
+  const size_t used = sizeof(WBHead) + (size_t)np * sizeof(WBProb) + (size_t)nr * sizeof(WBRow);
   const int words = (int)((used + 3) / 4);
   const unsigned* src = (const unsigned*)buf.data();
   for (int off = 0; off < words; off += 640) {
@@ -1034,8 +969,8 @@ int retr_linear_wgrad_batch(int n, const retr_linear_wgrad_desc* d, int nx,
     if (int e = retr_check_launch("linear_wgrad_batch table")) return e;
   }
   const char* tb = (const char*)table;
-  return bm == 128 ? wgrad_batch_launch<128, 2>(tb, h->total, 8 * gmax, st)
-                   : wgrad_batch_launch<64, 2>(tb, h->total, 8 * gmax, st);
+  return bm == 128 ? wgrad_batch_launch<128, 2>(tb, h->total, st)
+                   : wgrad_batch_launch<64, 2>(tb, h->total, st);
 }
 
 }  // extern "C"

@@ -52,6 +52,9 @@ DEC_FFN_LN = True
 DEC_FOLD_ROWS = True
 # fp32 parity mode: the step's linears on the skinny exact-f32 kernel
 DEC_F32_SKINNY = True
+# fp32 parity mode: three fused launches per decoder layer (csrc/decode_f32.hip, round 6)
+# instead of the per-op step
+DEC_F32_FUSED = False   # (enabled once measured, below)
 # the greedy step's MLP-head layers 1-2 on the skinny bf16 linear
 DEC_HEAD_SKINNY = True
 # rows up to which the folded (three-launch) layer is used (beyond: five launches per layer)
@@ -168,6 +171,26 @@ class IncrementalGreedy:
                 and C // H in (32, 64) and H % 4 == 0 and F % 32 == 0 and st.S <= 512
                 and st.T <= 512 and self.model.mlp.layers[0].weight.shape[0] % 32 == 0)
 
+    def _fusable_f32(self, st):
+        """The fused fp32 parity-mode step (csrc/decode_f32.hip): d_model 256 in 8 heads, FFN
+        width a multiple of 64, at most 512 self / memory keys; other shapes take the per-op
+        step."""
+        layers = list(self.tr.decoder.layers)
+        C = st.n.shape[1]
+        H = layers[0].tgt_self_attn.sublayer.num_heads
+        F = layers[0].ff.sublayer[0].weight.shape[0]
+        return (self.fused and DEC_F32_FUSED and self.cdtype == torch.float32 and C == 256
+                and H == 8 and F % 64 == 0 and st.S <= 512 and st.T <= 512)
+
+    def _heads_ok(self, st):
+        """The per-(row, head) kernels (csrc/decode_heads.hip) hold at most 4 key chunks per wave:
+        512 self / memory keys at head dim 32, 256 at head dim 64 (retr_dec_self_heads_ln /
+        retr_dec_cross_heads); longer memories or captions take the block-per-row step (up to
+        512 keys, retr_dec_attn_row)."""
+        layers = list(self.tr.decoder.layers)
+        hd = st.n.shape[1] // layers[0].tgt_self_attn.sublayer.num_heads
+        return hd == 32 or (st.S <= 256 and st.T <= 256)
+
     def _lin(self, x, w, bias, y, relu=0, res=None):
         """The unfused step's linears; the fp32 parity mode's (few rows) on the skinny exact-f32
         kernel (csrc/decode.hip dec_linear_f32), everything else on the generic GEMM."""
@@ -204,6 +227,8 @@ class IncrementalGreedy:
         """Kernels of decode step i (reads token i, writes caption column i+1)."""
         if self._fusable(st):
             return self._step_fused(st, i, eos_token)
+        if self._fusable_f32(st):
+            return self._step_f32(st, i, eos_token)
         model, tr, cd = self.model, self.tr, self.cdtype
         B, S, T, R = st.B, st.S, st.T, st.R
         C = st.n.shape[1]
@@ -258,6 +283,68 @@ class IncrementalGreedy:
                      st.head_bias, st.logits)
         self._select(st, i, V, eos_token, s)
 
+    def _step_f32(self, st, i, eos_token):
+        """Decode step i of the fp32 parity mode as three fused launches per decoder layer
+        (csrc/decode_f32.hip): retr_dec_self_f32 (previous FFN partials + residual -- or, at
+        layer 0, the token embedding -- + LN1, the head's q | k | v, cache append, attention,
+        partial out-projection), retr_dec_cross_f32 (head-partial sum + residual + LN2, cross
+        query, attention over the memory, partial out-projection), retr_dec_ffn_f32 (head-partial
+        sum + residual + LN3, FFN partials over 64 hidden units per block); then the final
+        residual + decoder LN (retr_dec_rows_f32), the MLP head on the skinny exact-f32 linear and
+        the selection.  Every value fp32."""
+        model, tr = self.model, self.tr
+        S, T, R = st.S, st.T, st.R
+        C = st.n.shape[1]
+        layers = list(tr.decoder.layers)
+        H = layers[0].tgt_self_attn.sublayer.num_heads
+        F = layers[0].ff.sublayer[0].weight.shape[0]
+        W = lambda p: ops.WEIGHTS.get(p, torch.float32)        # noqa: E731
+        if st.hslab is None:
+            st.hslab = torch.empty(H, R, C, dtype=torch.float32, device=st.n.device)
+            st.hslab2 = torch.empty_like(st.hslab)
+        emb = tr.embeddings
+        qp = emb.position_embeddings.weight.detach()[i]
+        s = _st()
+        x, xa = st.y, st.y2
+        anc = ptr(st.anc) if self.beam else None
+        nslab = F // 64
+        for li, layer in enumerate(layers):
+            sa, ca, ff = layer.tgt_self_attn, layer.tgt_src_cross_attn, layer.ff
+            sub, csub = sa.sublayer, ca.sublayer
+            f0, f2 = ff.sublayer[0], ff.sublayer[2]
+            if li == 0:
+                pro = (None, None, 0, None, ptr(st.tok), ptr(emb.word_embeddings.weight),
+                       ptr(emb.LayerNorm.weight), ptr(emb.LayerNorm.bias),
+                       float(emb.LayerNorm.eps))
+            else:
+                pf2 = layers[li - 1].ff.sublayer[2]
+                pro = (ptr(x), ptr(st.slabs), nslab, ptr(pf2.bias), None, None, None, None, 0.0)
+            call("retr_dec_self_f32", R, C, H, ptr(W(sub.in_proj_weight)), ptr(sub.in_proj_bias),
+                 ptr(st.kc[li]), ptr(st.vc[li]), i, T, anc, ptr(W(sub.out_proj.weight)),
+                 ptr(st.hslab), *pro, ptr(sa.norm.weight), ptr(sa.norm.bias), float(sa.norm.eps),
+                 ptr(qp), ptr(xa), s)
+            x, xa = xa, x
+            call("retr_dec_cross_f32", R, C, H, ptr(st.hslab), ptr(x), ptr(sub.out_proj.bias),
+                 ptr(xa), ptr(ca.norm.weight), ptr(ca.norm.bias), float(ca.norm.eps), ptr(qp),
+                 ptr(W(csub.in_proj_weight)), ptr(csub.in_proj_bias), ptr(st.kx[li]),
+                 ptr(st.vx[li]), S, st.K, ptr(st.kpm), ptr(W(csub.out_proj.weight)),
+                 ptr(st.hslab2), s)
+            x, xa = xa, x
+            call("retr_dec_ffn_f32", ptr(x), ptr(st.hslab2), H, ptr(csub.out_proj.bias),
+                 ptr(ff.norm.weight), ptr(ff.norm.bias), float(ff.norm.eps), ptr(xa), R, C,
+                 ptr(W(f0.weight)), ptr(f0.bias), ptr(W(f2.weight)), F, ptr(st.slabs), s)
+            x, xa = xa, x
+        nx, f2 = tr.decoder.norm, layers[-1].ff.sublayer[2]
+        call("retr_dec_rows_f32", ptr(x), ptr(st.slabs), nslab, ptr(f2.bias), R, C, ptr(xa),
+             ptr(nx.weight), ptr(nx.bias), float(nx.eps), ptr(st.n), s)
+        l1, l2, l3 = model.mlp.layers
+        V = l3.weight.shape[0]
+        self._lin(st.n, W(l1.weight), l1.bias.detach(), st.h1, relu=1)
+        self._lin(st.h1, W(l2.weight), l2.bias.detach(), st.h2, relu=1)
+        self._lin(st.h2, ops.WEIGHTS.get(l3.weight, torch.float32, rows=st.Vp), st.head_bias,
+                  st.logits)
+        self._select(st, i, V, eos_token, s)
+
     def _step_fused(self, st, i, eos_token):
         """Decode step i as five fused launches per decoder layer (csrc/decode.hip):
         [q|k|v] GEMM (+cache append); self-attention + out-proj + residual + LN2 + cross query;
@@ -267,7 +354,7 @@ class IncrementalGreedy:
         append + self-attention + partial out-projection; the self-attention residual + LN2 +
         the head's cross query + cross-attention + partial out-projection; then the head
         partials' ordered sum + residual + LN3 by retr_dec_rows."""
-        if DEC_HEADS:
+        if DEC_HEADS and self._heads_ok(st):
             return self._step_heads(st, i, eos_token)
         model, tr, cd = self.model, self.tr, self.cdtype
         S, T, R = st.S, st.T, st.R

@@ -67,3 +67,33 @@ def test_gradsync_equals_concatenated_batch():
     for rank, worst, nb in res:
         assert nb > 1                  # exercised multiple buckets
         assert worst < 1e-5, (rank, worst)
+
+
+def _timeout_worker(rank, world, port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    import bench
+    bench.init_dist(rank, backend="gloo")
+    t = torch.ones(1) * (rank + 1)
+    dist.all_reduce(t)                          # the group works
+    pg = dist.group.WORLD._get_backend(torch.device("cpu"))
+    q.put((rank, pg.options._timeout.total_seconds(), t.item()))
+    dist.destroy_process_group()
+
+
+def test_bench_process_group_has_short_timeout():
+    """bench.py's multi-rank process group (the driver's SCALE run) is created with the 2-minute
+    collective timeout (bench.DIST_TIMEOUT), not the 10-minute default: a first 8-rank run that
+    deadlocks fails fast.  gloo world 2 through the same init_dist the nccl path uses."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timeout_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, secs, tot in res:
+        assert secs == 120.0, (rank, secs)
+        assert tot == 3.0

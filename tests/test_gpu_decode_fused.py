@@ -719,3 +719,37 @@ def test_dec_linear_f32_matches_torch(M, N, K, relu, res):
     if res:
         ref = ref + r.double()
     assert _rel(y, ref) < 1e-6
+
+
+def test_fused_decode_head_dim64_long_memory_takes_block_per_row_step():
+    """Head dim 64 with 289 memory keys (> 256, the per-(row, head) kernels' limit at that head
+    dim): the fused greedy step must route to the block-per-row kernels (up to 512 keys) instead
+    of failing partway through decoding, and agree with the per-op step (bf16 rounding)."""
+    from tests.helpers import make_config
+    from retr_amd.eval_utils import decode as dec
+    from retr_amd.models.caption import build_model
+    from retr_amd.synthetic import synthetic_images, synthetic_state_dict
+    cfg = make_config(backbone="ResNet18", hidden=256, layers=(1, 2), vocab=1000, max_pos=16,
+                      nheads=4, ffn=512, dtype="bf16")
+    model, _ = build_model(cfg)
+    model.load_state_dict(synthetic_state_dict(model, seed=5))
+    model.to(DEV).eval()
+    B, T = 4, 16
+    img, mask = synthetic_images(B, 544, seed=13, pad_band=True)
+    s = NestedTensor(img.to(DEV), mask.to(DEV))
+    fused = dec.IncrementalGreedy(model, fused=True)
+    ids_f = fused(s, T, 101, 102)
+    st = next(v for k, v in model._retr_decode_states.items() if k[0] == "IncrementalGreedy" and k[-1])
+    assert st.S == 289 and fused._fusable(st) and not fused._heads_ok(st)
+    assert st.hslab is None                       # the per-(row, head) kernels never ran
+    plain = dec.IncrementalGreedy(model, fused=False)
+    ids_p = plain(s, T, 101, 102)
+    assert (ids_f == ids_p).float().mean().item() > 0.3
+    with torch.no_grad():
+        fused._reset(st, 101)
+        fused._step(st, 0, 102)
+        lf = st.logits.float().clone()
+        fused._reset(st, 101)
+        plain._step(st, 0, 102)
+        lp = st.logits.float().clone()
+    assert _rel(lf, lp) < 2e-2
