@@ -148,12 +148,12 @@ enum {
   RETR_TUNE_SPLITK_FUSED = 18,  /* split-K forward / data-gradient linears: 0 slabs + a separate
                                    slab-epilogue launch, 1 slice sum + epilogue by each tile's
                                    last-arriving block (csrc/splitk_fused.hpp) */
-  RETR_TUNE_WB_CHUNK = 19,      /* retr_linear_wgrad_batch block order: 0 runs of 4 logical
-                                   blocks per XCD turn, n > 0 runs of n, -1 problem-affine pieces
-                                   (one XCD per problem / row-tile run; 0.05 ms/step slower) */
-  RETR_TUNE_CW_CHUNK = 20,      /* retr_conv2d_wgrad_group block order: 0 runs of 4 logical blocks
-                                   per XCD turn, n > 0 runs of n, -1 slice-affine (every tile of
-                                   a K-slice on one XCD, slices to the least-loaded XCD; slower) */
+  RETR_TUNE_WB_CHUNK = 19,      /* retr_linear_wgrad_batch block order: runs of n > 0 logical
+                                   blocks per XCD turn (0: 4).  (Round 5's problem-affine order was
+                                   removed in round 6: DESIGN.md section 4) */
+  RETR_TUNE_CW_CHUNK = 20,      /* retr_conv2d_wgrad_group block order: runs of n > 0 logical
+                                   blocks per XCD turn (0: 4).  (The slice-affine order was
+                                   removed in round 6) */
   RETR_TUNE_CONV3X3 = 21,       /* bf16 3x3 stride-1 convs (fwd / dgrad): 0 the direct kernel with
                                    the input halo in LDS on maps >= 32 wide (csrc/conv3x3.hip),
                                    1 the implicit GEMM, 2 the direct kernel on every map >= 16 */
@@ -185,7 +185,11 @@ enum {
                                    64-unit FFN block, 8 per 128-unit block; 1 two / four (round-5
                                    kernels as first built); 2 four / four; 3 16-wave FFN blocks
                                    of both widths; 4 eight-wave 64-unit FFN blocks */
-  RETR_TUNE_COUNT = 32
+  RETR_TUNE_ROWLN = 32,         /* retr_linear_fwd_splitk_ln at N = 256: 0 auto, 1 the split-K
+                                   slabs + slab_epilogue_ln path, 2 / 3 / 4 the row-complete
+                                   32 x 256 tile with the LayerNorm in its epilogue (2 / 3 / 4
+                                   stage ring), 5 its 64 x 256 8-wave variant (csrc/linear.hip) */
+  RETR_TUNE_COUNT = 40
 };
 int retr_tune(int knob, int value);
 

@@ -20,6 +20,7 @@ if os.environ.get("RETR_AB_LIB"):
           f"in-tree libretr_hip.so (A/B tooling only)", file=_sys.stderr)
 
 F32, BF16 = 0, 1
+TUNE_COUNT = 40          # include/retr_hip.h RETR_TUNE_COUNT
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -266,8 +267,10 @@ def load():
                 except ValueError:
                     warnings.warn(f"retr_amd: ignoring {k}={v!r} (not an integer)")
                     continue
-                if lib.retr_tune(int(k[10:]), val) != 0:
+                if not 0 <= int(k[10:]) < TUNE_COUNT:
                     warnings.warn(f"retr_amd: ignoring {k}={v!r} (no tuning knob {k[10:]})")
+                    continue
+                lib.retr_tune(int(k[10:]), val)     # (returns the knob's previous value)
         _lib = lib
     return _lib
 

@@ -340,14 +340,25 @@ bottleneck_s1_kernel(const bf16* __restrict__ x, int H, int W, const bf16* __res
 #pragma unroll
   for (int j = 0; j < 4; ++j) bj[j] = *(const f32x4*)(bias_s + 128 + co0 + 16 * j + 4 * kq);
   const int pp0 = lane >> 3, c8 = (lane & 7) * 8;
+  // the residual rows of all four output rows in flight at once (one exposed memory latency
+  // instead of one per row: the MFMA registers of conv3 are dead here)
+  u32x4 resv[4][2];
+  if constexpr (!DS && BN_DIAG != 2) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long pix0 = ((long)n * H + y0 + 4 * pr + i) * W + x0;
+#pragma unroll
+      for (int it = 0; it < 2; ++it)
+        resv[i][it] = *(const u32x4*)(x + (pix0 + pp0 + 8 * it) * CIN + co0 + c8);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const long pix0 = ((long)n * H + y0 + 4 * pr + i) * W + x0;
     u32x4 res[2];
     if constexpr (!DS && BN_DIAG != 2) {
-#pragma unroll
-      for (int it = 0; it < 2; ++it)
-        res[it] = *(const u32x4*)(x + (pix0 + pp0 + 8 * it) * CIN + co0 + c8);
+      res[0] = resv[i][0];
+      res[1] = resv[i][1];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

@@ -110,11 +110,15 @@ dec_gemm_kernel(const bf16* a_plain, const bf16* a_pos, int R, const bf16* w, co
 
 // ---- dec_linear_f32: the fp32 parity-mode decode step's linears (M <= 64 rows) ---------------
 // y[m][n] = x[m][:] . w[n][:] (+ b[n]) (ReLU) (+ res[m][n]) in exact fp32 (16x16x4 f32 MFMA).
-// Block = one 16 x 16 output tile, its four waves split K in quarters (wave w: the 16-column
-// blocks of K numbered w mod 4); within a 16-column block lane group g feeds columns
-// k0 + 4 g .. + 3 to the four MFMA steps (each step covers four distinct k, every k once), from
-// one 16-byte load of x and of w per lane.  The waves' partial tiles are added in wave order.
-// The generic GEMM ran these as 8-block grids (12.7 us per call, 50 calls per step).
+// Block = one 16-column tile x ALL (up to four) 16-row tiles: its four waves split K in quarters
+// (wave w: the 16-column blocks of K numbered w mod 4) and each wave runs the four row tiles off
+// one weight load, so every weight byte is read once per launch (round 5's one-row-tile blocks
+// re-read the 62.5 MB vocabulary projection from HBM once per row tile: 57 us of the 0.45 ms
+// fused fp32 step).  Within a 16-column block lane group g feeds columns k0 + 4 g .. + 3 to the
+// four MFMA steps (each step covers four distinct k, every k once), from one 16-byte load of x
+// and of w per lane.  Each tile's wave partials are added in wave order (the same sums as the
+// per-tile blocks).  The generic GEMM ran these as 8-block grids (12.7 us per call, 50 calls
+// per step).
 struct LinF32Seg {          // one linear of a grouped launch (blockIdx.z)
   const float* x;
   const float* w;
@@ -138,43 +142,58 @@ dec_linear_f32_kernel(LinF32Group grp, int M, int K) {
   const float* res = sg.res;
   const long ldx = sg.ldx, ldw = sg.ldw, ldy = sg.ldy, ldr = sg.ldr;
   const int N = sg.N, relu = sg.relu;
-  __shared__ f4 red[4][64];
+  __shared__ f4 red[4][4][64];                    // [wave][row tile][lane]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int n0 = 16 * blockIdx.x, m0 = 16 * blockIdx.y;
+  const int n0 = 16 * blockIdx.x;
   if (n0 >= N) return;
   const int rr = lane & 15, g = lane >> 4;
-  const int m = m0 + rr, n = n0 + rr;
-  const float* xr = x + (long)(m < M ? m : M - 1) * ldx + 4 * g;
+  const int n = n0 + rr;
+  const int MT = (M + 15) / 16;                   // row tiles (<= 4)
+  const float* xr[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int m = 16 * t + rr;
+    xr[t] = x + (long)(m < M ? m : M - 1) * ldx + 4 * g;
+  }
   const float* wr = w + (long)(n < N ? n : N - 1) * ldw + 4 * g;
-  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  f4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
   const int nb = K / 16;                          // 16-column blocks of K
   constexpr int U = 4;                            // blocks per wave in flight
   for (int b0 = wv; b0 < nb; b0 += 4 * U) {
-    f4 xa[U], wa[U];
+    f4 wa[U], xa[U][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int b = b0 + 4 * u;
-      xa[u] = b < nb ? *(const f4*)(xr + 16 * b) : f4{0.f, 0.f, 0.f, 0.f};
       wa[u] = b < nb ? *(const f4*)(wr + 16 * b) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        xa[u][t] = b < nb && t < MT ? *(const f4*)(xr[t] + 16 * b) : f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[u][s], wa[u][s], acc, 0, 0, 0);
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[u][t][s], wa[u][s], acc[t], 0, 0, 0);
   }
-  red[wv][lane] = acc;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) red[wv][t][lane] = acc[t];
   __syncthreads();
-  if (wv != 0) return;
-  const f4 t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  // wave t finalises row tile t
+  const int t = wv;
+  if (t >= MT) return;
+  const f4 v4 = ((red[0][t][lane] + red[1][t][lane]) + red[2][t][lane]) + red[3][t][lane];
   const int col = n0 + (lane & 15);
   if (col >= N) return;
   const float bb = bias ? bias[col] : 0.f;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const int row = m0 + 4 * (lane >> 4) + e;
+    const int row = 16 * t + 4 * (lane >> 4) + e;
     if (row >= M) continue;
-    float v = t[e] + bb;
+    float v = v4[e] + bb;
     if (relu) v = fmaxf(v, 0.f);
     if (res) v += res[(long)row * ldr + col];
     y[(long)row * ldy + col] = v;
@@ -1301,7 +1320,7 @@ int retr_dec_linear3_f32(int n, const float* x0, long ldx0, const float* w0, lon
     nmax = sg.N > nmax ? sg.N : nmax;
   }
   if (M == 0) return 0;
-  hipLaunchKernelGGL(dec_linear_f32_kernel, dim3(cdiv(nmax, 16), cdiv(M, 16), n), dim3(256), 0,
+  hipLaunchKernelGGL(dec_linear_f32_kernel, dim3(cdiv(nmax, 16), 1, n), dim3(256), 0,
                      (hipStream_t)stream, g, M, K);
   return retr_check_launch("dec_linear_f32");
 }

@@ -181,6 +181,14 @@ template <class E>
 struct has_ones_bias<E, std::void_t<decltype(E::kOnesBias)>>
     : std::integral_constant<bool, E::kOnesBias> {};
 
+// Epilogues with kRows = true take whole output ROWS: the fp32 tile goes to LDS once and
+// ep.rows(ct, ld, m0, rows, tid, nthreads) runs per row (a LayerNorm over a row the tile holds
+// completely: BN = N).
+template <class E, class = void>
+struct has_rows_epi : std::false_type {};
+template <class E>
+struct has_rows_epi<E, std::void_t<decltype(E::kRows)>> : std::integral_constant<bool, E::kRows> {};
+
 // One BM x BN output tile (index `tile` in row-major tile order), K range
 // [split * kchunk, (split + 1) * kchunk).
 template <int FAM, int BM, int BN, int WM, int WN, int S, int EPB, class LA, class LB, class EP>
@@ -295,6 +303,21 @@ RETR_DEVICE __attribute__((always_inline)) void gemm2_tile(const LA& la, const L
   }
   (void)ones;
   __syncthreads();
+  if constexpr (has_rows_epi<EP>::value) {
+    static_assert(epi_bands<BM, BN, EPB>() == 1, "row epilogue: the fp32 tile must fit in LDS");
+    float* ct = (float*)smem;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          ct[(wm * WTM + 16 * i + 4 * (lane >> 4) + e) * (BN + 4) + wn * WTN + 16 * j +
+             (lane & 15)] = acc[i][j][e];
+    __syncthreads();
+    ep.rows(ct, BN + 4, m0, min(BM, M - m0), tid, NT);
+    return;
+  }
 
   // ---- epilogue through LDS (see gemm.hpp), in EP_PASSES row bands when the fp32 tile does
   // not fit in LDS (wave rows wm belong to band wm / (WM / EP_PASSES))

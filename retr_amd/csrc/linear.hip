@@ -267,6 +267,94 @@ slab_epilogue_ln_kernel(const float* ws, int splits, int M, EpiFwd<float, float>
   }
 }
 
+// Row-complete forward linear with the next LayerNorm in its epilogue (round 6): the GEMM tile
+// spans all N = 256 output columns (gemm2_tile BM x 256, the whole K in one pass), so its
+// epilogue owns complete rows -- EpiFwd's bias / dropout / residual arithmetic and the
+// LayerNorm outputs of slab_epilogue_ln_kernel, from the fp32 tile in LDS instead of summed
+// split-K slabs: no slab round trip through HBM, no second launch.  (One fp32 MFMA chain over K
+// per output instead of four slab chains summed: the same values to fp32 reassociation.)
+struct EpiRowLN {
+  static constexpr bool kRows = true;
+  EpiFwd<float, float> ep;
+  retr_ln_out ln;
+  RETR_DEVICE void rows(const float* ct, int ld, int m0, int nrows, int tid, int nthreads) const {
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    constexpr int N = 256;
+    const int lane = tid & 63, nw = nthreads >> 6;
+    const int c = 4 * lane;
+    const uint32_t th = drop_th16(ep.dp.thresh);
+    for (int r = tid >> 6; r < nrows; r += nw) {
+      const int row = m0 + r;
+      f32x4 v = *(const f32x4*)(ct + r * ld + c);
+      const uint32_t rk = ep.dp.thresh ? drop_row_key(dp_seed(ep.dp), (uint32_t)row) : 0u;
+      if (ep.bias) {
+        const f32x4 b = *(const f32x4*)(ep.bias + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += b[e];
+      }
+      if (ep.relu == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (ep.dp.thresh) {
+        const uint32_t km = drop_keep4(rk, (uint32_t)c, th);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = ((km >> e) & 1u) ? v[e] * ep.dp.scale : 0.f;
+      }
+      if (ep.res) {
+        const f32x4 rr = *(const f32x4*)(ep.res + (long)row * ep.ldr + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += rr[e];
+      }
+      if (ep.relu == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      *(f32x4*)(ep.out + (long)row * ep.ldo + c) = v;
+      const float mean = wave_sum((v[0] + v[1]) + (v[2] + v[3])) / N;
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = v[e] - mean;
+        q += d * d;
+      }
+      const float rstd = 1.0f / sqrtf(wave_sum(q) / N + ln.eps);
+      const f32x4 g = *(const f32x4*)(ln.gamma + c), b = *(const f32x4*)(ln.beta + c);
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (v[e] - mean) * rstd * g[e] + b[e];
+      if (ln.y)
+        *(bf16x4*)((bf16*)ln.y + (long)row * ln.ldy + c) =
+            bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+      if (ln.y2) {
+        const f32x4 o2 = o + *(const f32x4*)(ln.pos + (long)(row % ln.period) * N + c);
+        *(bf16x4*)((bf16*)ln.y2 + (long)row * ln.ldy + c) =
+            bf16x4{(bf16)o2[0], (bf16)o2[1], (bf16)o2[2], (bf16)o2[3]};
+      }
+      if (lane == 0) {
+        if (ln.mean) ln.mean[row] = mean;
+        if (ln.rstd) ln.rstd[row] = rstd;
+      }
+    }
+  }
+  // (the per-chunk epilogue interface gemm2_tile instantiates but never calls with kRows)
+  RETR_DEVICE bool lane_contiguous() const { return false; }
+  RETR_DEVICE void apply(int, int, float) const {}
+  RETR_DEVICE void apply8(int, int, float (&)[8]) const {}
+  RETR_DEVICE void empty_split(int, int) const {}
+};
+
+int launch_rowln(int variant, const DenseK<bf16>& la, const DenseK<bf16>& lb, const EpiRowLN& ep,
+                 int M, int K, hipStream_t st) {
+  constexpr const char* what = "linear_fwd_rowln";
+  switch (variant) {
+    case 2: return launch_gemm2<kFamLinearFwd, 32, 256, 1, 4, 2, 1>(la, lb, ep, M, 256, K, 1, st, what);
+    case 4: return launch_gemm2<kFamLinearFwd, 32, 256, 1, 4, 4, 1>(la, lb, ep, M, 256, K, 1, st, what);
+    case 5: return launch_gemm2<kFamLinearFwd, 64, 256, 2, 4, 3, 1>(la, lb, ep, M, 256, K, 1, st, what);
+    default: return launch_gemm2<kFamLinearFwd, 32, 256, 1, 4, 3, 1>(la, lb, ep, M, 256, K, 1, st, what);
+  }
+}
+
 template <typename T, class LA, class LB, class EP>
 int splitk_run(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, float* ws,
                int splits, int fam_dgrad, hipStream_t st, const char* what) {
@@ -521,6 +609,14 @@ int retr_linear_fwd_splitk_ln(int dtype, const void* x, long ldx, const void* w,
   }
   DenseK<bf16> la{(const bf16*)x, ldx, M, K};
   DenseK<bf16> lb{(const bf16*)w, ldw, N, K};
+  // RETR_TUNE_ROWLN: the row-complete tile with the LayerNorm in its epilogue (N = 256)
+  const int rv = retr_tune_get(RETR_TUNE_ROWLN);
+  if (N == 256 && rv >= 2 && (ln->pos == nullptr || ln->y2 != nullptr)) {
+    EpiRowLN ep{EpiFwd<float, float>{y, ldy, bias, residual, ldr, relu, make_dp(drop_p, seed),
+                                     (long)N},
+                *ln};
+    return launch_rowln(rv, la, lb, ep, M, K, st);
+  }
   splits = norm_splits_k(K, Elem<bf16>::BK, splits);
   if (int e = splitk_slabs<bf16>(la, lb, M, N, K, ws, splits, 0, st, "linear_fwd_splitk_ln"))
     return e;

@@ -52,9 +52,12 @@ DEC_FFN_LN = True
 DEC_FOLD_ROWS = True
 # fp32 parity mode: the step's linears on the skinny exact-f32 kernel
 DEC_F32_SKINNY = True
+# decode steps per captured hipGraph (the host polls the early-exit flag between graphs):
+# one replay launch per 8 steps instead of per step
+DEC_GRAPH_STEPS = 8
 # fp32 parity mode: three fused launches per decoder layer (csrc/decode_f32.hip, round 6)
 # instead of the per-op step
-DEC_F32_FUSED = False   # (enabled once measured, below)
+DEC_F32_FUSED = True
 # the greedy step's MLP-head layers 1-2 on the skinny bf16 linear
 DEC_HEAD_SKINNY = True
 # rows up to which the folded (three-launch) layer is used (beyond: five launches per layer)
@@ -587,25 +590,31 @@ class IncrementalGreedy:
             self._step(st, 0, eos_token)
             torch.cuda.synchronize()
             self._reset(st, bos_token)
+            # DEC_GRAPH_STEPS consecutive steps per graph (one replay launch each, the host
+            # polls `done` between graphs)
             graphs = []
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
-                for i in range(T - 1):
+                for i0 in range(0, T - 1, DEC_GRAPH_STEPS):
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, stream=side):
-                        self._step(st, i, eos_token)
+                        for i in range(i0, min(i0 + DEC_GRAPH_STEPS, T - 1)):
+                            self._step(st, i, eos_token)
                     graphs.append(g)
             torch.cuda.current_stream().wait_stream(side)
             st.graphs = graphs
         st.signature = sig
-        for i in range(T - 1):
-            if self.use_graphs:
-                st.graphs[i].replay()
-            else:
+        if self.use_graphs:
+            for g in st.graphs:
+                g.replay()
+                if int(st.done.item()) >= 0:
+                    break
+        else:
+            for i in range(T - 1):
                 self._step(st, i, eos_token)
-            if (i + 1) % poll == 0 and int(st.done.item()) >= 0:
-                break
+                if (i + 1) % poll == 0 and int(st.done.item()) >= 0:
+                    break
         return self._result(st)
 
 

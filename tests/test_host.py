@@ -132,3 +132,23 @@ def test_prune_cap_ids_product_matches_oracle():
     for clean in (True, False):
         assert prune_cap_ids(seqs, clean, 0, 101, 102) == \
             orc.prune_cap_ids(seqs, clean, 0, 101, 102)
+
+
+def test_tune_knob_table_matches_header_and_bad_env_is_skipped():
+    """retr_amd._lib.TUNE_COUNT is the header's RETR_TUNE_COUNT, and a malformed or unknown
+    RETR_TUNE_<n> environment preset is reported and skipped instead of breaking the import
+    (ADVICE r5)."""
+    import re
+    import subprocess
+    import sys
+    from retr_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "retr_hip.h")).read()
+    assert int(re.search(r"RETR_TUNE_COUNT = (\d+)", hdr).group(1)) == _lib.TUNE_COUNT
+    code = ("import warnings; warnings.simplefilter('always'); "
+            "from retr_amd import _lib; _lib.load(); print('loaded')")
+    env = dict(os.environ, RETR_TUNE_7="abc", RETR_TUNE_99="1", RETR_TUNE_3="")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "loaded" in r.stdout
+    assert "RETR_TUNE_7" in r.stderr and "RETR_TUNE_99" in r.stderr and "RETR_TUNE_3" in r.stderr

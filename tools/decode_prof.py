@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--fold-max-rows", type=int, default=None,
                     help="eval_utils.decode.DEC_FOLD_MAX_ROWS (default: the module's)")
     ap.add_argument("--fp32", action="store_true", help="cfg5 in fp32 parity mode")
+    ap.add_argument("--f32-fused", type=int, default=None,
+                    help="1 / 0: eval_utils.decode.DEC_F32_FUSED (default: the module's)")
     ap.add_argument("--hb128-rows", type=int, default=None,
                     help="eval_utils.decode.DEC_FFN_HB128_ROWS (default: the module's)")
     ap.add_argument("--select-embed", type=int, default=None,
@@ -53,6 +55,8 @@ def main():
         dec.DEC_SELECT_EMBED = bool(a.select_embed)
     if a.head_skinny:
         dec.DEC_HEAD_SKINNY = a.head_skinny == 1
+    if a.f32_fused is not None:
+        dec.DEC_F32_FUSED = bool(a.f32_fused)
     if a.fold_max_rows is not None:
         dec.DEC_FOLD_MAX_ROWS = a.fold_max_rows
     model, _ = build(cfg5("fp32") if a.fp32 else cfg5(), "cuda")
