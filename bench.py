@@ -538,9 +538,12 @@ def main():
                                  "guaranteed equal to the reference's (bf16 rounding flips "
                                  "near-tie argmaxes; tests/test_gpu_configs.py)")
             else:
-                ent["config"] = ("cfg5 in fp32 parity mode (exact-f32 MFMA): token ids equal "
-                                 "to the reference algorithm (tests/test_gpu_configs.py: B=64 "
-                                 "vs the full-recompute algorithm, B=2 vs the CPU oracle)")
+                ent["config"] = ("cfg5 in fp32 parity mode (every value fp32; the step as "
+                                 "three fused launches per decoder layer, csrc/decode_f32.hip, "
+                                 "exact-f32 MFMA / FMA chains): token ids equal to the reference "
+                                 "algorithm (tests/test_gpu_configs.py: B=64 vs the "
+                                 "full-recompute algorithm, B=2 and 4 rows of B=64 vs the CPU "
+                                 "oracle)")
             decode[dtype] = ent
         decode["value"] = decode["bf16"]["value"]
         decode["unit"] = "refs/s"

@@ -549,6 +549,13 @@ int retr_greedy_update(const long long* pred, int B, int T, int i, long long eos
 int retr_greedy_select(int dtype, const void* logits, long ld, int B, int V, void* workspace,
                        int T, int i, long long eos, long long* pred, long long* caption,
                        unsigned char* finished, int* done, long long* tok, void* stream);
+/* retr_greedy_select for one row group of a batch decoded as independent groups (write_all = 1:
+ * every column written, done = the group's first all-finished step; eval_utils/decode.py
+ * DEC_SPLIT clears the columns after the last group's) */
+int retr_greedy_select2(int dtype, const void* logits, long ld, int B, int V, void* workspace,
+                        int T, int i, long long eos, long long* pred, long long* caption,
+                        unsigned char* finished, int* done, long long* tok, int write_all,
+                        void* stream);
 
 /* ---- elementwise helpers --------------------------------------------------------------- */
 /* Encoder output without a final LayerNorm (pre_norm=False; models/ConcatTransformer.py:24,

@@ -204,6 +204,8 @@ _SIGS = {
     "retr_dec_embed_rows": [_P, _I, _I, _P, _P, _P, _P, _F, _P, _P, _P, _F, _P, _P, _P],
     "retr_greedy_select": [_I, _P, _L, _I, _I, _P, _I, _I, ctypes.c_longlong, _P, _P, _P, _P, _P,
                            _P],
+    "retr_greedy_select2": [_I, _P, _L, _I, _I, _P, _I, _I, ctypes.c_longlong, _P, _P, _P, _P, _P,
+                            _I, _P],
     "retr_dec_attn_row": [_P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F,
                           _P, _P, _P, _P, _P],
     "retr_dec_ffn": [_P, _I, _I, _P, _P, _P, _I, _P, _P],

@@ -63,9 +63,11 @@ RETR_DEVICE f32x4 mfma(const u32x4& w, const u32x4& x, f32x4 acc) {
                                                  __builtin_bit_cast(bf16x8, x), acc, 0, 0, 0);
 }
 
-// [rows][64] bf16 image with 144-byte rows (16 bytes of padding): the 16 rows x 16 bytes of a
-// fragment read land on distinct banks, and a row offset is a compile-time constant times the
-// stride, so the conv2 tap walk reads LDS at immediate offsets from one per-lane base
+// [rows][64] bf16 image with 144-byte rows (16 bytes of padding): a row offset is a compile-time
+// constant times the stride, so the conv2 tap walk reads LDS at immediate offsets from one
+// per-lane base.  (A ds_read_b128 lane group mixes two k chunks of 8 rows, which 144-byte rows
+// put 2-way on some bank slots; 160-byte rows remove that and measured no faster -- phases B / C
+// are not LDS-bound: profiles/r6_ab_bn_rs160_rejected.txt.)
 constexpr int RS = 144;
 constexpr int SST = 68;                           // phase C stage: [8 waves][16 px][64 + 4] fp32
 constexpr int H2OFF = 8 * 16 * SST * 4;           // 34816 >= the 192 x 144 of h1s

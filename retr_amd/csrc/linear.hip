@@ -589,8 +589,7 @@ int retr_linear_fwd_splitk_ln(int dtype, const void* x, long ldx, const void* w,
                               const retr_ln_out* ln, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) return 0;
-  RETR_REQUIRE(splits >= 1 && ws != nullptr && ln != nullptr, "linear_fwd_splitk_ln: splits=%d",
-               splits);
+  RETR_REQUIRE(splits >= 1 && ln != nullptr, "linear_fwd_splitk_ln: splits=%d", splits);
   auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   auto a8 = [](const void* q) { return ((uintptr_t)q & 7) == 0; };
   const bool fused = dtype == RETR_BF16 && ln->y_bf16 && N % 256 == 0 && N <= 512 &&
@@ -599,9 +598,11 @@ int retr_linear_fwd_splitk_ln(int dtype, const void* x, long ldx, const void* w,
                      a16(ws) && a16(ln->gamma) && a16(ln->beta) && a16(ln->pos) && a8(ln->y) &&
                      a8(ln->y2) && (ln->pos == nullptr || ln->period > 0);
   if (!fused) {
-    // two launches with the same results: the split-K linear, then the LayerNorm
-    if (int e = retr_linear_fwd_splitk(dtype, x, ldx, w, ldw, bias, y, ldy, 1, M, N, K, relu,
-                                       residual, ldr, drop_p, seed, ws, splits, stream))
+    // two launches with the same results: the (split-K) linear, then the LayerNorm
+    if (int e = ws ? retr_linear_fwd_splitk(dtype, x, ldx, w, ldw, bias, y, ldy, 1, M, N, K,
+                                            relu, residual, ldr, drop_p, seed, ws, splits, stream)
+                   : retr_linear_fwd(dtype, x, ldx, w, ldw, bias, y, ldy, 1, M, N, K, relu,
+                                     residual, ldr, drop_p, seed, stream))
       return e;
     return retr_layernorm_fwd(ln->y_bf16 ? RETR_BF16 : RETR_F32, y, ldy, ln->gamma, ln->beta,
                               ln->eps, M, N, ln->y, ln->ldy, ln->y2, ln->pos, ln->period,
@@ -609,14 +610,19 @@ int retr_linear_fwd_splitk_ln(int dtype, const void* x, long ldx, const void* w,
   }
   DenseK<bf16> la{(const bf16*)x, ldx, M, K};
   DenseK<bf16> lb{(const bf16*)w, ldw, N, K};
-  // RETR_TUNE_ROWLN: the row-complete tile with the LayerNorm in its epilogue (N = 256)
-  const int rv = retr_tune_get(RETR_TUNE_ROWLN);
-  if (N == 256 && rv >= 2 && (ln->pos == nullptr || ln->y2 != nullptr)) {
+  // the row-complete tile with the LayerNorm in its epilogue (N = 256): by default for short
+  // reductions (K <= 512: the attention out-projections, 4-8 K-steps), where the whole-K tile
+  // costs no latency; long ones keep the split-K slabs (profiles/r6_ab_rowln_rejected.txt).
+  // RETR_TUNE_ROWLN: 1 slabs always, 2-5 a row-complete variant always
+  int rv = retr_tune_get(RETR_TUNE_ROWLN);
+  if (rv == 0) rv = K <= 512 ? 2 : 1;
+  if (N == 256 && rv >= 2) {
     EpiRowLN ep{EpiFwd<float, float>{y, ldy, bias, residual, ldr, relu, make_dp(drop_p, seed),
                                      (long)N},
                 *ln};
     return launch_rowln(rv, la, lb, ep, M, K, st);
   }
+  RETR_REQUIRE(ws != nullptr, "linear_fwd_splitk_ln: the split-K path needs a workspace");
   splits = norm_splits_k(K, Elem<bf16>::BK, splits);
   if (int e = splitk_slabs<bf16>(la, lb, M, N, K, ws, splits, 0, st, "linear_fwd_splitk_ln"))
     return e;

@@ -386,9 +386,12 @@ int retr_argmax_rows(int dtype, const void* x, long ld, int M, int V, long long*
 // Greedy bookkeeping of eval_utils/decode.py:72-79 for step i, on device (no host sync):
 //   finished |= pred == eos; if all finished -> done = i (the reference returns here, so column
 //   i+1 is never written); else caption[:, i+1] = pred.  tok <- pred feeds step i+1.
+//   write_all (a batch decoded in independent row groups, eval_utils/decode.py DEC_SPLIT): every
+//   column is written and `done` only records the group's first all-finished step -- the
+//   caller ends the batch at the LAST group's and clears the columns after it.
 __global__ void greedy_update_kernel(const long long* pred, int B, int T, int i, long long eos,
                                      long long* caption, unsigned char* finished, int* done,
-                                     long long* tok) {
+                                     long long* tok, int write_all) {
   __shared__ int all_fin;
   if (threadIdx.x == 0) all_fin = 1;
   __syncthreads();
@@ -399,7 +402,7 @@ __global__ void greedy_update_kernel(const long long* pred, int B, int T, int i,
     if (!f) atomicAnd(&all_fin, 0);
   }
   __syncthreads();
-  const bool stop = prev_done >= 0 || all_fin;
+  const bool stop = !write_all && (prev_done >= 0 || all_fin);
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     if (!stop) caption[(long)b * T + i + 1] = pred[b];
     tok[b] = pred[b];
@@ -413,7 +416,7 @@ __global__ void greedy_update_kernel(const long long* pred, int B, int T, int i,
 __global__ void __launch_bounds__(1024)
 greedy_select_kernel(const float* pv, const int* pi, int B, int T, int i, long long eos,
                      long long* pred, long long* caption, unsigned char* finished, int* done,
-                     long long* tok) {
+                     long long* tok, int write_all) {
   __shared__ int all_fin;
   __shared__ long long sp[1024];
   if (threadIdx.x == 0) all_fin = 1;
@@ -442,7 +445,7 @@ greedy_select_kernel(const float* pv, const int* pi, int B, int T, int i, long l
     if (!f) atomicAnd(&all_fin, 0);
   }
   __syncthreads();
-  const bool stop = prev_done >= 0 || all_fin;
+  const bool stop = !write_all && (prev_done >= 0 || all_fin);
   for (int b = threadIdx.x; b < B; b += blockDim.x) {
     const long long pb = b < 1024 ? sp[b] : pred[b];
     if (!stop) caption[(long)b * T + i + 1] = pb;
@@ -455,12 +458,22 @@ extern "C" int retr_greedy_select(int dtype, const void* logits, long ld, int B,
                                   void* workspace, int T, int i, long long eos, long long* pred,
                                   long long* caption, unsigned char* finished, int* done,
                                   long long* tok, void* stream) {
+  return retr_greedy_select2(dtype, logits, ld, B, V, workspace, T, i, eos, pred, caption,
+                             finished, done, tok, 0, stream);
+}
+
+extern "C" int retr_greedy_select2(int dtype, const void* logits, long ld, int B, int V,
+                                   void* workspace, int T, int i, long long eos, long long* pred,
+                                   long long* caption, unsigned char* finished, int* done,
+                                   long long* tok, int write_all, void* stream) {
   if (B == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (ld % 8 != 0 || V < 8 * kArgSeg * 256 / 4 || !workspace || B > 1024 ||
       ((uintptr_t)logits & 15) != 0) {
     if (int e = retr_argmax_rows(dtype, logits, ld, B, V, pred, stream)) return e;
-    return retr_greedy_update(pred, B, T, i, eos, caption, finished, done, tok, stream);
+    hipLaunchKernelGGL(greedy_update_kernel, dim3(1), dim3(256), 0, st, pred, B, T, i, eos,
+                       caption, finished, done, tok, write_all);
+    return retr_check_launch("greedy_update");
   }
   float* pv = (float*)workspace;
   int* pi = (int*)(pv + (size_t)B * kArgSeg);
@@ -472,7 +485,7 @@ extern "C" int retr_greedy_select(int dtype, const void* logits, long ld, int B,
                        (const float*)logits, ld, V, pv, pi);
   if (int e = retr_check_launch("argmax_part")) return e;
   hipLaunchKernelGGL(greedy_select_kernel, dim3(1), dim3(1024), 0, st, pv, pi, B, T, i, eos, pred,
-                     caption, finished, done, tok);
+                     caption, finished, done, tok, write_all);
   return retr_check_launch("greedy_select");
 }
 
@@ -480,6 +493,6 @@ extern "C" int retr_greedy_update(const long long* pred, int B, int T, int i, lo
                                   long long* caption, unsigned char* finished, int* done,
                                   long long* tok, void* stream) {
   hipLaunchKernelGGL(greedy_update_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, pred, B, T,
-                     i, eos, caption, finished, done, tok);
+                     i, eos, caption, finished, done, tok, 0);
   return retr_check_launch("greedy_update");
 }

@@ -55,6 +55,10 @@ DEC_F32_SKINNY = True
 # decode steps per captured hipGraph (the host polls the early-exit flag between graphs):
 # one replay launch per 8 steps instead of per step
 DEC_GRAPH_STEPS = 8
+# greedy batches decoded as DEC_SPLIT independent row groups on concurrent streams of one graph
+# (each group at least DEC_SPLIT_MIN_ROWS rows); 1 = one group
+DEC_SPLIT = 1   # 2 measured SLOWER (bf16 2290 -> 1486, fp32 1217 -> ~1000 refs/s: profiles/r6_ab_dec_split_rejected.txt)
+DEC_SPLIT_MIN_ROWS = 16
 # fp32 parity mode: three fused launches per decoder layer (csrc/decode_f32.hip, round 6)
 # instead of the per-op step
 DEC_F32_FUSED = True
@@ -127,6 +131,7 @@ class _DecodeState:
         self.head_bias = None
         self.graphs = None
         self.signature = None
+        self.write_all = False    # a row group of a split batch (IncrementalGreedy._call_split)
 
     def init_beam(self, dev):
         R, K, T = self.R, self.K, self.T
@@ -528,11 +533,12 @@ class IncrementalGreedy:
         self._select(st, i, V, eos_token, s)
 
     def _select(self, st, i, V, eos_token, s):
-        """Greedy: first-index argmax + the reference's finished/early-exit bookkeeping."""
+        """Greedy: first-index argmax + the reference's finished/early-exit bookkeeping (a row
+        group of a split batch writes every column: _call_split ends the batch)."""
         cd = self.cdtype
-        call("retr_greedy_select", dcode(cd), ptr(st.logits), st.Vp, st.B, V, ptr(st.am_ws),
+        call("retr_greedy_select2", dcode(cd), ptr(st.logits), st.Vp, st.B, V, ptr(st.am_ws),
              st.T, i, int(eos_token), ptr(st.pred), ptr(st.caption), ptr(st.finished),
-             ptr(st.done), ptr(st.tok), s)
+             ptr(st.done), ptr(st.tok), int(st.write_all), s)
 
     # -- state handling (overridden by IncrementalBeam) --------------------------------------
     def _new_state(self, B, S, T, C, F, L, V, cd, dev):
@@ -547,6 +553,36 @@ class IncrementalGreedy:
 
     def _result(self, st):
         return st.caption.clone()
+
+    def _state(self, key, B, S, T, C, dev):
+        st = self.states.get(key)
+        if st is None:
+            layers = list(self.tr.decoder.layers)
+            st = self._new_state(B, S, T, C, layers[0].ff.sublayer[0].weight.shape[0],
+                                 len(layers), self.model.mlp.layers[2].weight.shape[0],
+                                 self.cdtype, dev)
+            self.states[key] = st
+        return st
+
+    def _memory_kv(self, st, mem, mem_pos, kpm):
+        """The cross-attention K/V of every decoder layer, once per batch, into the static
+        buffers of ``st`` (mem / mem_pos: its rows' memory tokens)."""
+        cd = self.cdtype
+        C = mem.shape[1]
+        for li, layer in enumerate(self.tr.decoder.layers):
+            sub = layer.tgt_src_cross_attn.sublayer
+            w = ops.WEIGHTS.get(sub.in_proj_weight, cd)
+            b = sub.in_proj_bias.detach()
+            k_linear_fwd(mem_pos, w[C:2 * C], b[C:2 * C], st.kx[li])
+            k_linear_fwd(mem, w[2 * C:], b[2 * C:], st.vx[li])
+        st.kpm.copy_(kpm)
+
+    def _split(self, B):
+        """Row groups of a batch decoded concurrently (DEC_SPLIT)."""
+        n = DEC_SPLIT
+        if self.beam or not self.use_graphs or n < 2 or B % n or B // n < DEC_SPLIT_MIN_ROWS:
+            return 1
+        return n
 
     @torch.no_grad()
     def __call__(self, samples, max_len, bos_token, eos_token, poll=8):
@@ -564,22 +600,12 @@ class IncrementalGreedy:
             raise RuntimeError(f"The size of tensor a ({T}) must match the size of tensor b "
                                f"({qpos_w.shape[0]}) at non-singleton dimension 0")
         C = mem.shape[1]
-        layers = list(tr.decoder.layers)
+        n = self._split(B)
+        if n > 1:
+            return self._call_split(n, mem, mem_pos, kpm, B, S, T, C, bos_token, eos_token)
         key = (type(self).__name__, self.K, B, S, T, cd, int(eos_token), bool(self.fused))
-        st = self.states.get(key)
-        if st is None:
-            st = self._new_state(B, S, T, C, layers[0].ff.sublayer[0].weight.shape[0],
-                                 len(layers), model.mlp.layers[2].weight.shape[0], cd,
-                                 mem.device)
-            self.states[key] = st
-        # cross-attention K/V of every decoder layer, once per batch, into the static buffers
-        for li, layer in enumerate(layers):
-            sub = layer.tgt_src_cross_attn.sublayer
-            w = ops.WEIGHTS.get(sub.in_proj_weight, cd)
-            b = sub.in_proj_bias.detach()
-            k_linear_fwd(mem_pos, w[C:2 * C], b[C:2 * C], st.kx[li])
-            k_linear_fwd(mem, w[2 * C:], b[2 * C:], st.vx[li])
-        st.kpm.copy_(kpm)
+        st = self._state(key, B, S, T, C, mem.device)
+        self._memory_kv(st, mem, mem_pos, kpm)
         self._reset(st, bos_token)
         sig = self._signature()
         if st.signature != sig:
@@ -616,6 +642,66 @@ class IncrementalGreedy:
                 if (i + 1) % poll == 0 and int(st.done.item()) >= 0:
                     break
         return self._result(st)
+
+    def _call_split(self, n, mem, mem_pos, kpm, B, S, T, C, bos_token, eos_token):
+        """The batch as n independent row groups (their own state, captured on n streams of
+        ONE graph per DEC_GRAPH_STEPS steps, so the groups' latency-bound step kernels overlap
+        on the GPU).  Rows never interact in a step, so every id is the unsplit decoder's: each
+        group writes every column (retr_greedy_select2 write_all) and records its first
+        all-finished step; the batch ends at the last group's -- the reference's exit
+        (decode.py:77-79: all rows finished) -- and the columns after it are cleared, as the
+        unsplit step leaves them."""
+        cd = self.cdtype
+        Bh = B // n
+        base = (type(self).__name__, self.K, Bh, S, T, cd, int(eos_token), bool(self.fused))
+        sts = [self._state(base + ("split", h, n), Bh, S, T, C, mem.device) for h in range(n)]
+        for h, st in enumerate(sts):
+            st.write_all = True
+            rows = slice(h * Bh * S, (h + 1) * Bh * S)
+            self._memory_kv(st, mem[rows], mem_pos[rows], kpm[h * Bh:(h + 1) * Bh])
+            self._reset(st, bos_token)
+        sig = self._signature()
+        st0 = sts[0]
+        if st0.signature != sig:
+            for st in sts:
+                st.head_bias = ops._pad_vec(self.model.mlp.layers[2].bias, st.Vp)
+            st0.graphs = None
+        if st0.graphs is None:
+            for st in sts:                  # warm once eagerly (attributes, weight copies)
+                self._step(st, 0, eos_token)
+            torch.cuda.synchronize()
+            for st in sts:
+                self._reset(st, bos_token)
+            graphs = []
+            side = torch.cuda.Stream()
+            lanes = [torch.cuda.Stream() for _ in range(n - 1)]
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for i0 in range(0, T - 1, DEC_GRAPH_STEPS):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=side):
+                        for ln in lanes:
+                            ln.wait_stream(side)
+                        for h, st in enumerate(sts):
+                            with torch.cuda.stream(side if h == 0 else lanes[h - 1]):
+                                for i in range(i0, min(i0 + DEC_GRAPH_STEPS, T - 1)):
+                                    self._step(st, i, eos_token)
+                        for ln in lanes:
+                            side.wait_stream(ln)
+                    graphs.append(g)
+            torch.cuda.current_stream().wait_stream(side)
+            st0.graphs = graphs
+        st0.signature = sig
+        dones = torch.stack([st.done for st in sts])
+        for g in st0.graphs:
+            g.replay()
+            torch.stack([st.done for st in sts], out=dones)
+            if int(dones.min().item()) >= 0:
+                break
+        ids = torch.cat([self._result(st) for st in sts])
+        if int(dones.min().item()) >= 0:
+            ids[:, int(dones.max().item()) + 1:] = 0
+        return ids
 
 
 class IncrementalBeam(IncrementalGreedy):

@@ -211,3 +211,39 @@ def test_fused_f32_step_matches_per_op_step_cfg5():
     # beams legitimately diverge -- most images must still agree token for token
     agree = (ids_bf == ids_bp).all(1).float().mean().item()
     assert agree >= 0.5, agree
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_split_batch_decode_equals_one_group(dtype):
+    """DEC_SPLIT: the batch decoded as two independent row groups on concurrent streams of one
+    graph gives the one-group decoder's ids token for token -- with an EOS that ends rows at
+    different steps (each group writes every column, the batch ends at the last group's
+    all-finished step and the later columns are cleared) and with one no row emits."""
+    from bench import build, cfg5
+    from retr_amd.eval_utils import decode as dec
+    from retr_amd.synthetic import synthetic_images
+    model, _ = build(cfg5(dtype), DEV)
+    model.eval()
+    B, T = 32, 128
+    img, mask = synthetic_images(B, 224, seed=31, pad_band=True)
+    s = NestedTensor(img.to(DEV), mask.to(DEV))
+    old = dec.DEC_SPLIT
+    try:
+        dec.DEC_SPLIT = 1
+        probe = dec.IncrementalGreedy(model)(s, T, 101, 102)
+        # an EOS that some rows emit early and others late / never
+        vals, counts = torch.unique(probe[:, 2:12], return_counts=True)
+        eos = int(vals[counts.argmax()])
+        for e in (eos, 102):
+            dec.DEC_SPLIT = 1
+            ids1 = dec.IncrementalGreedy(model)(s, T, 101, e)
+            dec.DEC_SPLIT = 2
+            g2 = dec.IncrementalGreedy(model)
+            assert g2._split(B) == 2
+            ids2 = g2(s, T, 101, e)
+            assert torch.equal(ids1, ids2), (e, (ids1 != ids2).nonzero()[:5].tolist())
+            ids2b = g2(s, T, 101, e)                 # replayed graphs
+            assert torch.equal(ids1, ids2b)
+    finally:
+        dec.DEC_SPLIT = old
+        model._retr_decode_states = {}

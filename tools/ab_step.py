@@ -80,11 +80,10 @@ VARIANTS = {
     "pos_off": {("ATTR", "POS_DEFER"): False},
     "up2k": {("TUNE", 28): 2048},
     "up8k": {("TUNE", 28): 8192},
-    # round 5 (opt-in, measured slower: profiles/r5_ab_wgrad_orders.txt): slice-affine conv
-    # wgrad / problem-affine linear wgrad block orders instead of runs of 4 blocks per XCD turn
-    "cw_aff": {("TUNE", 20): -1},
-    "wb_aff": {("TUNE", 19): -1},
-    "orders_aff": {("TUNE", 19): -1, ("TUNE", 20): -1},
+    # round 6: the attention out-projections' next LayerNorm in their epilogue (row-complete
+    # tile) on / off
+    "rowln_off": {("ATTR", "ROWLN_SHORT"): False},
+    "rowln_s3": {("TUNE", 32): 3},
     "cw_w4": {("TUNE", 29): 1},
     "cw_w8": {("TUNE", 29): 2},
     "cw_256": {("TUNE", 29): 3},
@@ -103,12 +102,13 @@ def apply(v):
     ops.FUSE_LN_NEXT = True
     ops.HEAD_WGRAD_DEFER = True
     ops.POS_DEFER = True
+    ops.ROWLN_SHORT = True
     resnet.CONV_WGRAD_GROUP = True
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29):
+    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 32):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
