@@ -7,7 +7,7 @@
 // nine times, and a 128x128 tile at 64 channels per K-step needs 32 KB per step, the CU's whole
 // fabric bandwidth at full MFMA rate.  Here a block owns a TH x TW output
 // tile x BN output channels; per 64-channel input chunk it stages the (TH+2) x (TW+2) halo ONCE
-// (global loads -> VGPRs -> LDS, 144-byte padded pixel rows) and runs the chunk's nine taps as
+// (global loads -> VGPRs -> LDS, 160-byte padded pixel rows) and runs the chunk's nine taps as
 // nine K-steps whose A fragments are LDS reads of the halo at a compile-time offset per tap.
 // Only the weights stream per K-step (BN x 64 channels by LDS-DMA, the gemm2.hpp stager and
 // swizzle): 16 KB + 1/9 of a halo per step instead of 32 KB.
@@ -59,21 +59,27 @@ struct TapW {
   }
 };
 
-constexpr int kHaloRB = 144;     // padded pixel row: 64 bf16 channels + 16 bytes
-
-template <int TH, int TW, int BN>
+// Halo pixel rows are RB bytes: 64 bf16 channels + padding.  A fragment read (ds_read_b128) is
+// serviced in four 16-lane groups, each mixing two 16-byte k chunks of 8 pixels; with 144-byte
+// rows (36 dwords, 9 x 4) pixel r of chunk 1 and pixel r + 7 of chunk 0 share a bank slot -- every
+// read of a whole 16-pixel line is a 2-way conflict.  160-byte rows (40 dwords) put a group's 16
+// slots on 16 distinct bank slots (the 20-pixel tiles' wrapped lines: 6.4 instead of 10.4 LDS
+// cycles per read).  The 4 x 20 four-wave tile keeps 144: at 160 its LDS no longer fits three
+// blocks per CU, which costs more than the conflicts (tools/c3_micro.py, profiles/r6_c3_rb.txt);
+// the default tiles no longer use it.
+template <int TH, int TW, int BN, int RB>
 constexpr size_t c3_main_lds() {
-  return ((size_t)(TH + 2) * (TW + 2) * kHaloRB + 255) / 256 * 256 + 2 * (size_t)BN * kBKBytes;
+  return ((size_t)(TH + 2) * (TW + 2) * RB + 255) / 256 * 256 + 2 * (size_t)BN * kBKBytes;
 }
 // epilogue bands: as few as keep the fp32 staging tile within the main loop's LDS footprint
-template <int TH, int TW, int BN, int WM>
+template <int TH, int TW, int BN, int WM, int RB>
 constexpr int epi_passes() {
   int p = 1;
-  while (p < WM && (size_t)TH * TW * (BN + 4) * 4 / p > c3_main_lds<TH, TW, BN>()) p *= 2;
+  while (p < WM && (size_t)TH * TW * (BN + 4) * 4 / p > c3_main_lds<TH, TW, BN, RB>()) p *= 2;
   return p;
 }
 
-template <int TH, int TW, int BN, int WM, int WN, bool DGRAD, class EP>
+template <int TH, int TW, int BN, int WM, int WN, int RB, bool DGRAD, class EP>
 __global__ void __launch_bounds__(WM * WN * 64, 2)
 conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, int H, int W,
                int CI, int CO, int tiles_x, int tiles_y, int tiles_n) {
@@ -83,7 +89,8 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
-  constexpr int HALO_BYTES = (HP * kHaloRB + 255) / 256 * 256;
+  constexpr int HALO_BYTES = (HP * RB + 255) / 256 * 256;
+  static_assert(RB % 16 == 0 && RB >= 128, "halo row");
   constexpr int WST = BN * kBKBytes;            // one weight stage
   constexpr int S = 2;
   constexpr int HCH = (HP * 8 + NT - 1) / NT;   // 16-byte halo chunks per thread per channel chunk
@@ -112,23 +119,29 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
 
   // halo chunk loader: thread q-slots (pixel hp, 16-byte piece j)
   const bf16* xin = x + (long)img * H * W * CI;
+  // Every thread issues exactly HCH loads: slots past the halo and pixels outside the image read
+  // the zero page.  (The wait at t == 1 below counts HCH halo loads behind the step-1 weight
+  // DMA; a predicated load became a branch the compiler skips when a whole wave is masked --
+  // waves past the halo's last slots always were -- and vmcnt(HCH) then let that wave's weight
+  // chunks still be in flight at the barrier: other waves could read the previous step's
+  // weights.  Seen as a rare 1-ulp-scale loss difference in test_gpu_ddp's bitwise check.)
   auto halo_load = [&](int c, u32x4 (&r)[HCH]) {
 #pragma unroll
     for (int i = 0; i < HCH; ++i) {
       const int q = tid + NT * i;
       const int hp = q >> 3, j = q & 7;
       const int gy = y0 + hp / HW - 1, gx = x0 + hp % HW - 1;
-      u32x4 v = u32x4{0u, 0u, 0u, 0u};
-      if (q < HP * 8 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-        v = *(const u32x4*)(xin + ((long)gy * W + gx) * CI + c * 64 + j * 8);
-      r[i] = v;
+      const bool ok = q < HP * 8 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W;
+      const bf16* src = ok ? xin + ((long)gy * W + gx) * CI + c * 64 + j * 8
+                           : (const bf16*)g_zero_page;
+      r[i] = *(const u32x4*)src;
     }
   };
   auto halo_store = [&](const u32x4 (&r)[HCH]) {
 #pragma unroll
     for (int i = 0; i < HCH; ++i) {
       const int q = tid + NT * i;
-      if (q < HP * 8) *(u32x4*)(halo + (q >> 3) * kHaloRB + (q & 7) * 16) = r[i];
+      if (q < HP * 8) *(u32x4*)(halo + (q >> 3) * RB + (q & 7) * 16) = r[i];
     }
   };
 
@@ -137,7 +150,7 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int p = wm * WTM + 16 * i + (lane & 15);
-    abase[i] = ((p / TW) * HW + p % TW) * kHaloRB + (lane >> 4) * 16;
+    abase[i] = ((p / TW) * HW + p % TW) * RB + (lane >> 4) * 16;
   }
 
   SB sb;
@@ -173,7 +186,7 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
       if (s + 1 < nsteps) sb.issue(lb, wst + ((s + 1) % S) * WST, wave);
       if (t == 0 && more) halo_load(c + 1, hr);
       const char* B = wst + (s % S) * WST;
-      const int tapoff = ((t / 3) * HW + t % 3) * kHaloRB;
+      const int tapoff = ((t / 3) * HW + t % 3) * RB;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         u32x4 af[TM], bfr[TN];
@@ -195,7 +208,7 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
   // epilogue through LDS: fp32 tile [BM][BN + 4], 8 consecutive channels per thread, in EPB
   // bands of wave rows when the whole tile does not fit under the main-loop footprint
   constexpr int CS = BN + 4;
-  constexpr int EPB = epi_passes<TH, TW, BN, WM>();
+  constexpr int EPB = epi_passes<TH, TW, BN, WM, RB>();
   constexpr int BAND = BM / EPB;
   constexpr int CH = BN / 8;
   float* ct = (float*)smem;
@@ -227,20 +240,20 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
   }
 }
 
-template <int TH, int TW, int BN, int WM, int WN>
+template <int TH, int TW, int BN, int WM, int WN, int RB>
 constexpr size_t c3_lds() {
-  constexpr size_t main = c3_main_lds<TH, TW, BN>();
-  constexpr size_t epi = (size_t)TH * TW * (BN + 4) * 4 / epi_passes<TH, TW, BN, WM>();
+  constexpr size_t main = c3_main_lds<TH, TW, BN, RB>();
+  constexpr size_t epi = (size_t)TH * TW * (BN + 4) * 4 / epi_passes<TH, TW, BN, WM, RB>();
   return main > epi ? main : epi;
 }
 
-template <int TH, int TW, int BN, int WM, int WN, bool DGRAD, class EP>
+template <int TH, int TW, int BN, int WM, int WN, int RB, bool DGRAD, class EP>
 int launch_c3(const bf16* x, const bf16* w, const EP& ep, int Nb, int H, int W, int CI, int CO,
               hipStream_t st, const char* what) {
   const int tiles_x = cdiv(W, TW), tiles_y = cdiv(H, TH), tiles_n = cdiv(CO, BN);
   const long blocks = (long)Nb * tiles_x * tiles_y * tiles_n;
-  constexpr size_t lds = c3_lds<TH, TW, BN, WM, WN>();
-  auto kern = conv3x3_kernel<TH, TW, BN, WM, WN, DGRAD, EP>;
+  constexpr size_t lds = c3_lds<TH, TW, BN, WM, WN, RB>();
+  auto kern = conv3x3_kernel<TH, TW, BN, WM, WN, RB, DGRAD, EP>;
   if constexpr (lds > 65536) {
     static bool attr_set = false;
     if (!attr_set) {
@@ -261,25 +274,30 @@ template <bool DGRAD, class EP>
 int run_c3(const bf16* x, const bf16* w, const EP& ep, int Nb, int H, int W, int CI, int CO,
            hipStream_t st, const char* what) {
   switch (retr_tune_get(RETR_TUNE_C3_TILE)) {
-    case 1: return launch_c3<8, 16, 128, 4, 2, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
-    case 2: return launch_c3<8, 20, 128, 2, 4, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
-    case 3: return launch_c3<4, 16, 128, 2, 4, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
-    case 4: return launch_c3<8, 16, 64, 4, 2, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
-    case 5: return launch_c3<16, 16, 128, 4, 2, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    case 1: return launch_c3<8, 16, 128, 4, 2, 160, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    case 2: return launch_c3<8, 20, 128, 2, 4, 160, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    case 3: return launch_c3<4, 16, 128, 2, 4, 160, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    case 4: return launch_c3<8, 16, 64, 4, 2, 160, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    case 5: return launch_c3<16, 16, 128, 4, 2, 160, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
     case 6:
-      if (CO % 256 == 0) return launch_c3<8, 20, 256, 2, 4, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+      if (CO % 256 == 0) return launch_c3<8, 20, 256, 2, 4, 160, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
       break;
-    case 7: return launch_c3<4, 20, 128, 1, 4, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
-    case 8: return launch_c3<8, 16, 128, 2, 2, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    case 7: return launch_c3<4, 20, 128, 1, 4, 160, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    case 8: return launch_c3<8, 16, 128, 2, 2, 160, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    // the 144-byte-row layout of rounds 3-5 (A/B)
+    case 9: return launch_c3<4, 20, 128, 1, 4, 144, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    case 10: return launch_c3<8, 16, 128, 4, 2, 144, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    case 11: return launch_c3<8, 20, 128, 2, 4, 144, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
     default: break;
   }
-  // tools/c3_micro.py (profiles/r4_c3_micro.txt): 80x80x128 -> 4 x 20 tiles over four waves
-  // (fwd 50.7 -> 39.4 us, dgrad 46.8 -> 40.5 vs the implicit GEMM), 40x40x256 -> 8 x 16 over
-  // eight (40.7 -> 36.7, 39.0 -> 36.9); the 20x20x512 maps stay on the implicit GEMM
-  // (conv3x3_direct_ok), where no variant won
-  if (W % 20 == 0 && W >= 60)
-    return launch_c3<4, 20, 128, 1, 4, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
-  return launch_c3<8, 16, 128, 4, 2, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+  // tools/c3_micro.py --rounds 3 (profiles/r6_c3_rb.txt, interleaved in one process): with
+  // 160-byte halo rows the 8 x 16 eight-wave tile is the fastest on the 80- and 40-wide maps
+  // (80x80x128 fwd 38.4 / dgrad 39.3 us vs 38.7 / 40.0 for round 5's 4 x 20 tile; 40x40x256
+  // 35.5 / 36.1 vs 36.0 / 36.8 at 144-byte rows), and the 8 x 20 tile now beats the implicit GEMM
+  // on the 20x20x512 maps of layer 4 (48.2 / 49.1 vs 51.6 / 52.0 us; at 144-byte rows it lost:
+  // 54.4 / 54.7)
+  if (W == 20) return launch_c3<8, 20, 128, 2, 4, 160, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+  return launch_c3<8, 16, 128, 4, 2, 160, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
 }
 
 }  // namespace
@@ -291,7 +309,7 @@ bool conv3x3_direct_ok(int H, int W, int CI, int CO) {
   const int mode = retr_tune_get(RETR_TUNE_CONV3X3);
   if (mode == 1) return false;
   if (mode == 2) return CI % 64 == 0 && CO % 128 == 0 && H >= 8 && W >= 16;   // sweeps
-  return CI % 64 == 0 && CO % 128 == 0 && H >= 8 && W >= 32;
+  return CI % 64 == 0 && CO % 128 == 0 && H >= 8 && (W >= 32 || W == 20);
 }
 
 int conv3x3_fwd_direct(const bf16* x, const bf16* w, const float* bias, bf16* y, int relu, int Nb,
