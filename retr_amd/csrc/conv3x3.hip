@@ -67,19 +67,20 @@ struct TapW {
 // cycles per read).  The 4 x 20 four-wave tile keeps 144: at 160 its LDS no longer fits three
 // blocks per CU, which costs more than the conflicts (tools/c3_micro.py, profiles/r6_c3_rb.txt);
 // the default tiles no longer use it.
-template <int TH, int TW, int BN, int RB>
+template <int TH, int TW, int BN, int RB, int S>
 constexpr size_t c3_main_lds() {
-  return ((size_t)(TH + 2) * (TW + 2) * RB + 255) / 256 * 256 + 2 * (size_t)BN * kBKBytes;
+  return ((size_t)(TH + 2) * (TW + 2) * RB + 255) / 256 * 256 + (size_t)S * BN * kBKBytes;
 }
 // epilogue bands: as few as keep the fp32 staging tile within the main loop's LDS footprint
-template <int TH, int TW, int BN, int WM, int RB>
+template <int TH, int TW, int BN, int WM, int RB, int S>
 constexpr int epi_passes() {
   int p = 1;
-  while (p < WM && (size_t)TH * TW * (BN + 4) * 4 / p > c3_main_lds<TH, TW, BN, RB>()) p *= 2;
+  while (p < WM && (size_t)TH * TW * (BN + 4) * 4 / p > c3_main_lds<TH, TW, BN, RB, S>()) p *= 2;
   return p;
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int RB, bool DGRAD, class EP>
+// S: weight stages in the ring (2: one step of look-ahead; 3: two, counted waits)
+template <int TH, int TW, int BN, int WM, int WN, int RB, int S, bool DGRAD, class EP>
 __global__ void __launch_bounds__(WM * WN * 64, 2)
 conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, int H, int W,
                int CI, int CO, int tiles_x, int tiles_y, int tiles_n) {
@@ -92,7 +93,7 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
   constexpr int HALO_BYTES = (HP * RB + 255) / 256 * 256;
   static_assert(RB % 16 == 0 && RB >= 128, "halo row");
   constexpr int WST = BN * kBKBytes;            // one weight stage
-  constexpr int S = 2;
+  static_assert(S == 2 || S == 3, "weight ring");
   constexpr int HCH = (HP * 8 + NT - 1) / NT;   // 16-byte halo chunks per thread per channel chunk
   using LB = TapW<DGRAD>;
   using SB = GStager<BN, NT, LB>;
@@ -165,7 +166,8 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
 
   u32x4 hr[HCH];
   halo_load(0, hr);
-  sb.issue(lb, wst, wave);                      // weights of step 0
+  sb.issue(lb, wst, wave);                      // weights of step 0 (and 1)
+  if (S == 3 && nsteps > 1) sb.issue(lb, wst + WST, wave);
   halo_store(hr);
 
   int s = 0;
@@ -178,12 +180,17 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
     const bool more = c + 1 < nchunks;
 #pragma unroll
     for (int t = 0; t < 9; ++t, ++s) {
-      // weights of step s landed (the halo loads of chunk c + 1, issued at t = 0 after the
-      // weights of step 1, may still be in flight behind them at t = 1)
-      if (t == 1 && more) wait_vmcnt_lgkm0<HCH>();
+      // weights of step s landed.  In flight behind them may be: the halo loads of chunk
+      // c + 1 (issued at t = 0 after the weights of step s0 + S - 1: still allowed at t = 1, and
+      // at t = 2 with three stages) and, with three stages, the weights of step s + 1
+      const bool nx = S == 3 && s + 1 < nsteps;
+      const bool hh = more && (t == 1 || (S == 3 && t == 2));
+      if (nx && hh) wait_vmcnt_lgkm0<LPT + HCH>();
+      else if (nx) wait_vmcnt_lgkm0<LPT>();
+      else if (hh) wait_vmcnt_lgkm0<HCH>();
       else wait_vmcnt_lgkm0<0>();
       raw_barrier();
-      if (s + 1 < nsteps) sb.issue(lb, wst + ((s + 1) % S) * WST, wave);
+      if (s + S - 1 < nsteps) sb.issue(lb, wst + ((s + S - 1) % S) * WST, wave);
       if (t == 0 && more) halo_load(c + 1, hr);
       const char* B = wst + (s % S) * WST;
       const int tapoff = ((t / 3) * HW + t % 3) * RB;
@@ -208,7 +215,7 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
   // epilogue through LDS: fp32 tile [BM][BN + 4], 8 consecutive channels per thread, in EPB
   // bands of wave rows when the whole tile does not fit under the main-loop footprint
   constexpr int CS = BN + 4;
-  constexpr int EPB = epi_passes<TH, TW, BN, WM, RB>();
+  constexpr int EPB = epi_passes<TH, TW, BN, WM, RB, S>();
   constexpr int BAND = BM / EPB;
   constexpr int CH = BN / 8;
   float* ct = (float*)smem;
@@ -240,20 +247,20 @@ conv3x3_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, EP ep, in
   }
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int RB>
+template <int TH, int TW, int BN, int WM, int WN, int RB, int S>
 constexpr size_t c3_lds() {
-  constexpr size_t main = c3_main_lds<TH, TW, BN, RB>();
-  constexpr size_t epi = (size_t)TH * TW * (BN + 4) * 4 / epi_passes<TH, TW, BN, WM, RB>();
+  constexpr size_t main = c3_main_lds<TH, TW, BN, RB, S>();
+  constexpr size_t epi = (size_t)TH * TW * (BN + 4) * 4 / epi_passes<TH, TW, BN, WM, RB, S>();
   return main > epi ? main : epi;
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int RB, bool DGRAD, class EP>
+template <int TH, int TW, int BN, int WM, int WN, int RB, bool DGRAD, int S = 2, class EP>
 int launch_c3(const bf16* x, const bf16* w, const EP& ep, int Nb, int H, int W, int CI, int CO,
               hipStream_t st, const char* what) {
   const int tiles_x = cdiv(W, TW), tiles_y = cdiv(H, TH), tiles_n = cdiv(CO, BN);
   const long blocks = (long)Nb * tiles_x * tiles_y * tiles_n;
-  constexpr size_t lds = c3_lds<TH, TW, BN, WM, WN, RB>();
-  auto kern = conv3x3_kernel<TH, TW, BN, WM, WN, RB, DGRAD, EP>;
+  constexpr size_t lds = c3_lds<TH, TW, BN, WM, WN, RB, S>();
+  auto kern = conv3x3_kernel<TH, TW, BN, WM, WN, RB, S, DGRAD, EP>;
   if constexpr (lds > 65536) {
     static bool attr_set = false;
     if (!attr_set) {
@@ -288,6 +295,10 @@ int run_c3(const bf16* x, const bf16* w, const EP& ep, int Nb, int H, int W, int
     case 9: return launch_c3<4, 20, 128, 1, 4, 144, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
     case 10: return launch_c3<8, 16, 128, 4, 2, 144, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
     case 11: return launch_c3<8, 20, 128, 2, 4, 144, DGRAD>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    // three weight stages (two steps of look-ahead): within 1-3 % of two, either way
+    // (profiles/r6_c3_rb.txt) -- the weight DMA latency is hidden by the second block per CU
+    case 12: return launch_c3<8, 16, 128, 4, 2, 160, DGRAD, 3>(x, w, ep, Nb, H, W, CI, CO, st, what);
+    case 13: return launch_c3<8, 20, 128, 2, 4, 160, DGRAD, 3>(x, w, ep, Nb, H, W, CI, CO, st, what);
     default: break;
   }
   // tools/c3_micro.py --rounds 3 (profiles/r6_c3_rb.txt, interleaved in one process): with
