@@ -263,8 +263,8 @@ def family_of_symbol(name):
     if m:
         return ("linear_fwd", "linear_dgrad", "linear_wgrad", "conv_fwd", "conv_dgrad",
                 "conv_wgrad")[int(m.group(1))]
-    m = re.search(r"conv3x3_kernelI(?:Li\d+E){5}Lb([01])E", name) or \
-        re.search(r"conv3x3_kernel<(?:\d+, ){5}(false|true)", name)
+    m = re.search(r"conv3x3_kernelI(?:Li\d+E){5,7}Lb([01])E", name) or \
+        re.search(r"conv3x3_kernel<(?:\d+, ){5,7}(false|true)", name)
     if m:                                         # direct 3x3 conv (csrc/conv3x3.hip)
         return "conv_dgrad" if m.group(1) in ("1", "true") else "conv_fwd"
     if "wgrad_batch_kernel" in name:

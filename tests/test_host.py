@@ -152,3 +152,19 @@ def test_tune_knob_table_matches_header_and_bad_env_is_skipped():
     assert r.returncode == 0, r.stderr
     assert "loaded" in r.stdout
     assert "RETR_TUNE_7" in r.stderr and "RETR_TUNE_99" in r.stderr and "RETR_TUNE_3" in r.stderr
+
+
+def test_kernel_family_classifier_covers_current_kernel_names():
+    """bench.py / tools/pmc_*.py / tools/rocprof_families.py put every rocprof kernel name into a
+    family with retr_amd.probe.family_of_symbol: the direct 3x3 conv's template (tile, row
+    bytes, weight stages, direction) in both the mangled and the demangled spelling."""
+    from retr_amd.probe import family_of_symbol
+    mangled = ("_ZN12_GLOBAL__N_114conv3x3_kernelILi8ELi16ELi128ELi4ELi2ELi160ELi2ELb{}EN4retr6"
+               "EpiFwdIDF16bDF16bEEEEvPKDF16bS5_T7_iiiiiii")
+    assert family_of_symbol(mangled.format(0)) == "conv_fwd"
+    assert family_of_symbol(mangled.format(1)) == "conv_dgrad"
+    assert family_of_symbol("void (anonymous namespace)::conv3x3_kernel<8, 20, 128, 2, 4, 160, 3, "
+                            "true, retr::EpiDgrad<bf16, bf16, bf16> >(...)") == "conv_dgrad"
+    assert family_of_symbol("_ZN4retr12gemm2_kernelILi3ELi64ELi64E") == "conv_fwd"
+    assert family_of_symbol("conv_wgrad_group_kernel<1, 8, 128>") == "conv_wgrad"
+    assert family_of_symbol("adamw_update_kernel<true>") is None

@@ -9,9 +9,10 @@
 #   4. a rocprofv3 kernel trace of a short graphed cfg2 bench (step breakdown + families) and
 #      decode traces (bf16 greedy, fp32 parity greedy, bf16 beam 5).
 # Every GPU step has its own limit; the first failure stops the script.
-#   usage: bash tools/gpu_profile_r6.sh <tag>
+#   usage: bash tools/gpu_profile_r6.sh <tag> [pmc|run|all]   (two gpurun calls: pmc, then run)
 set -o pipefail
 TAG=${1:-r6}
+PHASE=${2:-all}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -45,8 +46,11 @@ pmc() {  # workload
   rm -f $F $W $M
   echo "pmc $wl done"
 }
-pmc cfg2
-pmc cfg4
+if [ "$PHASE" != run ]; then
+  pmc cfg2
+  pmc cfg4
+fi
+[ "$PHASE" = pmc ] && exit 0
 step bench 420 python bench.py --steps 20 --warmup 5 --probe-detail $OUT/probe_shapes.txt
 cp $OUT/bench.log $OUT/bench.json
 echo "bench done"; grep -o '"value": [0-9.]*' $OUT/bench.json | head -3
