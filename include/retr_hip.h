@@ -172,8 +172,9 @@ enum {
   RETR_TUNE_LN_BWD = 27,        /* LayerNorm backward (C 256 / 512) rows / waves per block: 0 auto
                                    (32 / 16 at >= 4096 rows, else 8 / 4), 1 32/16, 2 16/8, 3 8/4,
                                    4 16/16, 5 64/16, 6 8/8 (tools/ln_micro.py) */
-  RETR_TUNE_UNPACK_GRID = 28,   /* retr_conv_wgrad_unpack_group grid cap (blocks walk the
-                                   64-chunk groups): 0 one block per group */
+  RETR_TUNE_UNPACK_GRID = 28,   /* retr_conv_wgrad_unpack_group: 0 one block per output-channel
+                                   row; -1 round 5's block per 64 chunks, > 0 that kernel with
+                                   its grid capped (A/B) */
   RETR_TUNE_CW_WAVES = 29,      /* retr_conv2d_wgrad_group wave layout of the 128x128 tile (sweeps):
                                    0 kind 0 (1x1) 4 waves / kind 1 (3x3, strided) 8 waves, 1 both
                                    4 waves (64x64 per wave), 2 both 8 waves (32x64 per wave) */

@@ -1285,7 +1285,7 @@ struct UPJob {
   const float* ws;
   const float* scale;
   float* grad;
-  int Co, Ci, Cp, KHW, splits, accumulate, blk0, pad;
+  int Co, Ci, Cp, KHW, splits, accumulate, blk0, pad;   // pad: grad 16-byte aligned
 };
 static_assert(sizeof(UPJob) == 56, "unpack table");
 
@@ -1339,6 +1339,84 @@ __global__ void __launch_bounds__(256) wgrad_unpack_group_kernel(const char* __r
       }
     }
     __syncthreads();                             // red[] is rewritten by the next group
+  }
+}
+
+// Round 6: one block per output-channel row (co) of one problem instead of one per 64 chunks.
+// A thread owns a 16-byte chunk (4 input channels at one tap) and forms the same four partial
+// sums as wgrad_unpack_group_kernel's four waves (slices s = w mod 4, ascending) in registers,
+// eight slices in flight, then ((p0 + p1) + p2) + p3 -- bitwise the same values, without the LDS
+// reduction and its two barriers per group.  The row's KHW x Ci outputs go through LDS in OIHW
+// order, so the gradient is written in contiguous runs (the 64-chunk kernel wrote each 3x3
+// value as a 4-byte store KHW floats from its neighbour).  ~92 k tiny blocks -> ~20 k rows.
+constexpr int kUnpackRowMax = 9 * 1024;           // floats of LDS: KHW x Ci of one row
+
+__global__ void __launch_bounds__(256) wgrad_unpack_rows_kernel(const char* __restrict__ table) {
+  extern __shared__ __attribute__((aligned(16))) float rowbuf[];
+  const CWHead h = *(const CWHead*)table;
+  const UPJob* J = (const UPJob*)(table + sizeof(CWHead));
+  const int bid = blockIdx.x;
+  int lo = 0, hi = h.nprob - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (J[mid].blk0 <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const UPJob d = J[lo];
+  const int co = bid - d.blk0;
+  if (co >= d.Co) return;                          // table guard
+  const int c4 = d.Ci / 4, nch = d.KHW * c4;
+  const long slab = (long)d.Co * d.KHW * d.Cp;
+  const float sc = d.scale ? d.scale[co] : 1.f;
+  const float* rowp = d.ws + (long)co * d.KHW * d.Cp;
+  float* grow = d.grad + (long)co * d.Ci * d.KHW;
+  const bool staged = d.KHW > 1 && d.KHW * d.Ci <= kUnpackRowMax;
+  for (int q = threadIdx.x; q < nch; q += 256) {
+    const int tap = q / c4, ci = (q - tap * c4) * 4;
+    const float* src = rowp + (long)tap * d.Cp + ci;
+    f32x4 p[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) p[w] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int s = 0;
+    for (; s + 8 <= d.splits; s += 8) {
+      f32x4 u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) u[k] = *(const f32x4*)(src + (long)(s + k) * slab);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) p[k & 3] += u[k];
+    }
+    {
+      f32x4 u[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (s + k < d.splits) u[k] = *(const f32x4*)(src + (long)(s + k) * slab);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (s + k < d.splits) p[k & 3] += u[k];
+    }
+    const f32x4 v = ((p[0] + p[1]) + p[2]) + p[3];
+    if (staged) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rowbuf[(ci + e) * d.KHW + tap] = v[e] * sc;
+    } else if (d.KHW == 1 && d.pad) {
+      f32x4 x = v * sc;
+      if (d.accumulate) x += *(const f32x4*)(grow + ci);
+      *(f32x4*)(grow + ci) = x;
+    } else {
+      float* dst = grow + (long)ci * d.KHW + tap;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = v[e] * sc;
+        dst[(long)e * d.KHW] = d.accumulate ? dst[(long)e * d.KHW] + x : x;
+      }
+    }
+  }
+  if (!staged) return;
+  __syncthreads();
+  const int n = d.KHW * d.Ci;
+  for (int t = threadIdx.x; t < n; t += 256) {
+    const float x = rowbuf[t];
+    grow[t] = d.accumulate ? grow[t] + x : x;
   }
 }
 
@@ -1711,7 +1789,12 @@ int retr_conv_wgrad_unpack_group(int n, const retr_conv_unpack_desc* d, void* ta
   std::vector<char> buf(retr_conv_wgrad_unpack_group_table_bytes(n) + 16, 0);
   CWHead* h = (CWHead*)buf.data();
   UPJob* J = (UPJob*)(buf.data() + sizeof(CWHead));
+  // RETR_TUNE_UNPACK_GRID: 0 = one block per output-channel row (wgrad_unpack_rows_kernel);
+  // -1 = round 5's block per 64 chunks, > 0 = that kernel with its grid capped (A/B)
+  const int knob = retr_tune_get(RETR_TUNE_UNPACK_GRID);
+  const bool rows = knob == 0;
   int blocks = 0;
+  size_t lds = 0;
   for (int i = 0; i < n; ++i) {
     const retr_conv_unpack_desc& q = d[i];
     RETR_REQUIRE(q.ws && q.grad && q.Ci % 4 == 0 && q.Cp % 4 == 0 && q.Cp >= q.Ci &&
@@ -1729,7 +1812,14 @@ int retr_conv_wgrad_unpack_group(int n, const retr_conv_unpack_desc* d, void* ta
     j.splits = q.splits;
     j.accumulate = q.accumulate;
     j.blk0 = blocks;
-    blocks += (int)cdiv((long)q.Co * j.KHW * (q.Ci / 4), 64);
+    j.pad = ((uintptr_t)q.grad & 15) == 0;        // 16-byte rows for the 1x1 store
+    if (rows) {
+      blocks += q.Co;
+      if (j.KHW > 1 && j.KHW * q.Ci <= kUnpackRowMax)
+        lds = std::max(lds, (size_t)j.KHW * q.Ci * sizeof(float));
+    } else {
+      blocks += (int)cdiv((long)q.Co * j.KHW * (q.Ci / 4), 64);
+    }
   }
   h->nprob = n;
   h->total = blocks;
@@ -1743,11 +1833,17 @@ int retr_conv_wgrad_unpack_group(int n, const retr_conv_unpack_desc* d, void* ta
     hipLaunchKernelGGL(cw_table_put_kernel, dim3(1), dim3(256), 0, st, c, (unsigned*)table);
     if (int e = retr_check_launch("conv_wgrad_unpack_group table")) return e;
   }
-  // RETR_TUNE_UNPACK_GRID: cap the grid (the blocks walk the 64-chunk groups); 0 = one block
-  // per group
+  if (blocks == 0) return 0;
+  if (rows) {
+    if (lds > 65536)
+      (void)hipFuncSetAttribute((const void*)wgrad_unpack_rows_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(wgrad_unpack_rows_kernel, dim3(blocks), dim3(256), lds, st,
+                       (const char*)table);
+    return retr_check_launch("conv_wgrad_unpack_group");
+  }
   int grid = blocks;
-  const int cap = retr_tune_get(RETR_TUNE_UNPACK_GRID);
-  if (cap > 0 && grid > cap) grid = cap;
+  if (knob > 0 && grid > knob) grid = knob;
   hipLaunchKernelGGL(wgrad_unpack_group_kernel, dim3(grid), dim3(256), 0, st,
                      (const char*)table);
   return retr_check_launch("conv_wgrad_unpack_group");

@@ -1437,17 +1437,27 @@ def test_conv_wgrad_group_matches_fp32_and_single_path():
         call("retr_conv_wgrad_unpack", ptr(slabs[i]), ptr(scales[i]), ptr(one), co, c, c, k, k,
              0, arr[i].splits, ops._st())
         assert rel_err(outs[i], one) < 1e-6, (geos[i], rel_err(outs[i], one))
-    # a capped grid (RETR_TUNE_UNPACK_GRID: blocks walk the chunk groups): bitwise the same
+    # round 5's kernel (RETR_TUNE_UNPACK_GRID -1: a block per 64 chunks, four waves' partial
+    # sums through LDS; 37: the same with a capped grid) against the default row kernel (one
+    # block per output channel, the four partials in registers): bitwise the same
     first = [o.clone() for o in outs]
-    for o in outs:
-        o.fill_(float("nan"))
-    try:
-        _lib.load().retr_tune(28, 37)
-        call("retr_conv_wgrad_unpack_group", n, ua, ptr(utab), utab.numel(), ops._st())
-    finally:
-        _lib.load().retr_tune(28, 0)
-    for a, b in zip(first, outs):
-        assert torch.equal(a, b)
+    for knob in (-1, 37):
+        for o in outs:
+            o.fill_(float("nan"))
+        try:
+            _lib.load().retr_tune(28, knob)
+            call("retr_conv_wgrad_unpack_group", n, ua, ptr(utab), utab.numel(), ops._st())
+        finally:
+            _lib.load().retr_tune(28, 0)
+        for a, b in zip(first, outs):
+            assert torch.equal(a, b), knob
+    # accumulate mode: grad += scale * sum (the row kernel's staged and 16-byte paths)
+    for i in range(n):
+        ua[i].accumulate = 1
+    base = [o.clone() for o in outs]
+    call("retr_conv_wgrad_unpack_group", n, ua, ptr(utab), utab.numel(), ops._st())
+    for a, b in zip(base, outs):
+        assert torch.equal(b, a + a)
     torch.cuda.synchronize()
 
 

@@ -80,10 +80,8 @@ VARIANTS = {
     "pos_off": {("ATTR", "POS_DEFER"): False},
     "up2k": {("TUNE", 28): 2048},
     "up8k": {("TUNE", 28): 8192},
-    # round 6: the attention out-projections' next LayerNorm in their epilogue (row-complete
-    # tile) on / off
-    "rowln_off": {("ATTR", "ROWLN_SHORT"): False},
-    "rowln_s3": {("TUNE", 32): 3},
+    # round 6: round 5's conv weight-gradient unpack (block per 64 chunks) vs the row kernel
+    "unpack_old": {("TUNE", 28): -1},
     "cw_w4": {("TUNE", 29): 1},
     "cw_w8": {("TUNE", 29): 2},
     "cw_256": {("TUNE", 29): 3},
@@ -102,7 +100,6 @@ def apply(v):
     ops.FUSE_LN_NEXT = True
     ops.HEAD_WGRAD_DEFER = True
     ops.POS_DEFER = True
-    ops.ROWLN_SHORT = True
     resnet.CONV_WGRAD_GROUP = True
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
