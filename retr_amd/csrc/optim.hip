@@ -52,11 +52,23 @@ __global__ void __launch_bounds__(kThreads)
 adamw_sumsq_kernel(const float4* g, long n4, float* partials, float* step) {
   __shared__ float red[16];
   float s = 0.f;
-  if (g)
-    for (long i = (long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long)gridDim.x * kThreads) {
+  if (g) {
+    // eight loads in flight per thread (one at a time left the ~230 MB pass latency-bound at
+    // ~3 TB/s); the sum runs over the same elements in the same order
+    const long stride = (long)gridDim.x * kThreads;
+    long i = (long)blockIdx.x * kThreads + threadIdx.x;
+    for (; i + 7 * stride < n4; i += 8 * stride) {
+      float4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = g[i + k * stride];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+    }
+    for (; i < n4; i += stride) {
       float4 v = g[i];
       s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
     }
+  }
   s = block_sum(s, red);
   if (threadIdx.x == 0) {
     if (partials) partials[blockIdx.x] = s;
