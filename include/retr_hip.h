@@ -318,6 +318,10 @@ int retr_conv2d_fwd_out(int dtype, const void* x, int Nb, int H, int W, int C, c
 int retr_conv1x1_fwd_cat(int dtype, const void* x1, int C1, const void* x2, int C2, int Nb,
                          int OH, int OW, int H2, int W2, int stride2, const void* w,
                          const float* bias, void* y, int Co, int relu, void* stream);
+/* dx[Nb][H][W][C] = gate(dgrad(dy, W) [+ addend]), gate = (gate > 0).  addend may be dx itself
+ * (in place) when dx already holds gate(addend) at every pixel: a stride-2 conv then rewrites
+ * only the pixels its taps reach (ResNet first blocks: the 1x1 stride-2 downsample's data
+ * gradient added onto conv1's gated one, resnet.py) */
 int retr_conv2d_dgrad(int dtype, const void* dy, int Nb, int H, int W, int C, const void* wt,
                       void* dx, int Co, int KH, int KW, int stride, int pad, int dil,
                       const void* addend, const void* gate, void* stream);

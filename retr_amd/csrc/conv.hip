@@ -829,12 +829,18 @@ int conv_dgrad_t(const void* dy, Geom g, const void* wt, void* dx, const void* a
           zmask |= 1 << (ih0 * 2 + iw0);
         }
       }
-    if (zmask && sizeof(T) == 2 && N % 8 == 0) {
-      const long chunks = (long)M * (N / 8);
-      hipLaunchKernelGGL(dgrad_phase_fill_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256), 0,
-                         st, (bf16*)dx, (const bf16*)addend, (const bf16*)gate, g.H, g.W, N,
-                         chunks, zmask);
-      if (int e = retr_check_launch("conv_dgrad_phase_fill")) return e;
+    // dx == addend (in place): the caller has written gate(addend) at every pixel already (the
+    // block's other branch, ResNet first blocks: resnet.py), so the tap-less phases are final
+    // and only the phases with taps are rewritten -- no fill pass over 3/4 of the map
+    const bool inplace = addend != nullptr && addend == dx;
+    if (zmask && (inplace || (sizeof(T) == 2 && N % 8 == 0))) {
+      if (!inplace) {
+        const long chunks = (long)M * (N / 8);
+        hipLaunchKernelGGL(dgrad_phase_fill_kernel, dim3((unsigned)cdiv(chunks, 256)), dim3(256),
+                           0, st, (bf16*)dx, (const bf16*)addend, (const bf16*)gate, g.H, g.W, N,
+                           chunks, zmask);
+        if (int e = retr_check_launch("conv_dgrad_phase_fill")) return e;
+      }
     } else {
       zmask = 0;
     }

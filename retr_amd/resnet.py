@@ -158,10 +158,15 @@ def _conv_fwd(spec, x, shape, relu, residual=None):
     return y, (n, oh, ow, spec.cout)
 
 
-def _conv_dgrad(spec, g, in_shape, addend=None, gate=None):
+# first blocks' input gradient: the downsample's data gradient accumulated in place onto conv1's
+# gated one (round 6; False: round 5's temporary + elementwise fill of the tap-less phases)
+DS_DGRAD_INPLACE = True
+
+
+def _conv_dgrad(spec, g, in_shape, addend=None, gate=None, out=None):
     n, h, w, c = in_shape
     _, wt, _, _ = PACKS.get(spec, g.dtype)
-    dx = torch.empty(n, h, w, c, dtype=g.dtype, device=g.device)
+    dx = out if out is not None else torch.empty(n, h, w, c, dtype=g.dtype, device=g.device)
     call("retr_conv2d_dgrad", dcode(g.dtype), ptr(g), n, h, w, c, ptr(wt), ptr(dx), spec.cout,
          spec.k, spec.k, spec.s, spec.p, spec.d, ptr(addend), ptr(gate), _st())
     return dx
@@ -460,7 +465,13 @@ class _Backbone(torch.autograd.Function):
             if blk.ds is not None:
                 wgrad(blk.ds, G3, inp, ishape)
             if need_dx:
-                if blk.ds is not None:
+                if blk.ds is not None and DS_DGRAD_INPLACE:
+                    # conv1's gated data gradient, then the stride-2 downsample's added in place
+                    # at the pixels its taps reach: gate(a + b) = gate(a) + b there, and the
+                    # other three phases are final (no fill pass; bitwise the same values)
+                    g = _conv_dgrad(c1, G1, ishape, gate=inp)
+                    g = _conv_dgrad(blk.ds, G3, ishape, addend=g, gate=inp, out=g)
+                elif blk.ds is not None:
                     tmp = _conv_dgrad(c1, G1, ishape)
                     g = _conv_dgrad(blk.ds, G3, ishape, addend=tmp, gate=inp)
                 else:

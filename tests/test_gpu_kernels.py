@@ -627,6 +627,14 @@ def test_conv_dgrad_stride2_addend_gate(H, Ci, Co, k, p):
     call("retr_conv2d_dgrad", ops.dcode(bf), ptr(gn), N, H, H, cp, ptr(wt), ptr(dx), Co, k, k, s,
          p, 1, ptr(add_d), ptr(gate_d), ops._st())
     assert rel_err(dx.float().cpu(), ref) < 1e-2
+    # in place (resnet.py's first blocks): dx already holds gate(addend) everywhere and the
+    # stride-2 data gradient is added at the pixels its taps reach -- bitwise the out-of-place
+    # result (gate(a + b) = gate(a) + b where the gate is 1, 0 elsewhere)
+    dx2 = (add_d.float() * (gate_d.float() > 0)).to(bf)
+    call("retr_conv2d_dgrad", ops.dcode(bf), ptr(gn), N, H, H, cp, ptr(wt), ptr(dx2), Co, k, k, s,
+         p, 1, ptr(dx2), ptr(gate_d), ops._st())
+    torch.cuda.synchronize()
+    assert torch.equal(dx2, dx)
 
 
 @pytest.mark.parametrize("M,N,K", [(6400, 256, 2048), (2048, 256, 2048), (1000, 200, 1536)])

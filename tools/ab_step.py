@@ -82,6 +82,8 @@ VARIANTS = {
     "up8k": {("TUNE", 28): 8192},
     # round 6: round 5's conv weight-gradient unpack (block per 64 chunks) vs the row kernel
     "unpack_old": {("TUNE", 28): -1},
+    # round 6: the first blocks' downsample data gradient out of place (+ phase fill)
+    "ds_fill": {("RESNET", "DS_DGRAD_INPLACE"): False},
     "cw_w4": {("TUNE", 29): 1},
     "cw_w8": {("TUNE", 29): 2},
     "cw_256": {("TUNE", 29): 3},
@@ -101,6 +103,7 @@ def apply(v):
     ops.HEAD_WGRAD_DEFER = True
     ops.POS_DEFER = True
     resnet.CONV_WGRAD_GROUP = True
+    resnet.DS_DGRAD_INPLACE = True
     load().retr_tune(10, 0)
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
