@@ -1552,6 +1552,47 @@ def test_conv3x3_direct_matches_implicit_gemm_and_fp32(nb, H, W, C, Co):
     assert rel_err(res[2][1], res[1][1]) < 5e-3
 
 
+def test_conv3x3_direct_every_tile_variant():
+    """Every RETR_TUNE_C3_TILE variant of the direct 3x3 kernel (tiles, 144 / 160-byte halo
+    rows, two / three weight stages) against the implicit GEMM on a ragged map, forward and
+    data gradient, and each variant bitwise stable over two launches (the weight-stage race of
+    round 6 showed up as run-to-run differences)."""
+    bf = torch.bfloat16
+    nb, H, W, C, Co = 2, 22, 40, 128, 256
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(nb, H, W, C, generator=g).to(DEV, bf)
+    wf = (torch.randn(Co, 3, 3, C, generator=g) / math.sqrt(9 * C)).to(DEV, bf)
+    wt = (torch.randn(C, 3, 3, Co, generator=g) / math.sqrt(9 * Co)).to(DEV, bf)
+    b = torch.randn(Co, generator=g).to(DEV)
+    dy = torch.randn(nb, H, W, Co, generator=g).to(DEV, bf)
+    gate = torch.randn(nb, H, W, C, generator=g).to(DEV, bf)
+
+    def run():
+        y = torch.full((nb, H, W, Co), float("nan"), dtype=bf, device=DEV)
+        call("retr_conv2d_fwd", 1, ptr(x), nb, H, W, C, ptr(wf), ptr(b), None, ptr(y), Co, 3, 3,
+             1, 1, 1, 1, ops._st())
+        dx = torch.full((nb, H, W, C), float("nan"), dtype=bf, device=DEV)
+        call("retr_conv2d_dgrad", 1, ptr(dy), nb, H, W, C, ptr(wt), ptr(dx), Co, 3, 3, 1, 1, 1,
+             None, ptr(gate), ops._st())
+        torch.cuda.synchronize()
+        return y.float(), dx.float()
+
+    lib = _lib.load()
+    try:
+        lib.retr_tune(21, 1)                    # the implicit GEMM
+        ref = run()
+        lib.retr_tune(21, 2)                    # the direct kernel on every map >= 16 wide
+        for v in range(1, 14):
+            lib.retr_tune(22, v)
+            a, a2 = run(), run()
+            for got, again, want in zip(a, a2, ref):
+                assert torch.equal(got, again), v
+                assert rel_err(got, want) < 5e-3, (v, rel_err(got, want))
+    finally:
+        lib.retr_tune(21, 0)
+        lib.retr_tune(22, 0)
+
+
 @pytest.mark.parametrize("M,N,K", [(6400, 2048, 256), (2048, 2048, 256), (1000, 1800, 192),
                                    (640, 1024, 128)])
 def test_panel_gemm_equals_tile_gemm(M, N, K):
