@@ -38,6 +38,13 @@ typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2v;
 // four scores -> elements 4 half .. 4 half + 3 of a bf16x8 MFMA fragment held as u32x4: two
 // v_cvt_pk_bf16_f32 (a per-element (bf16) conversion compiles to one cvt per score + a v_perm
 // per pair)
+// x where the keep mask km (all ones / zero, from __builtin_amdgcn_sbfe of a saved keep word) is
+// set, +0 elsewhere: one v_and instead of a compare + v_cndmask per score, the same bits as
+// `keep ? x : 0.f`
+RETR_DEVICE float keep_and(float x, int km) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(int, x) & km);
+}
+
 RETR_DEVICE void put4(u32x4& w, int half, const float (&v)[4]) {
   const f2v lo = {v[0], v[1]}, hi = {v[2], v[3]};
   w[2 * half] = __builtin_bit_cast(uint32_t, __builtin_convertvector(lo, bf16x2v));
@@ -967,9 +974,11 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
             float p = __builtin_amdgcn_exp2f(S[sub][e] - lq2);
             if constexpr (MASK) p = key_masked(pmlo, pmhi, kl - 4 * hh, diag, mlim) ? 0.f : p;
             float dpv = P[sub][e];
-            if constexpr (DM != 0) {
-              const bool kp = DM == 1 ? ((wm[sub] >> (8 * g + 4 * hh + e4)) & 1u) != 0u
-                                      : attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
+            if constexpr (DM == 1) {
+              dpv = keep_and(dpv * dp.scale,
+                             __builtin_amdgcn_sbfe((int)wm[sub], 8 * g + 4 * hh + e4, 1));
+            } else if constexpr (DM == 2) {
+              const bool kp = attn_keep(e4 < 2 ? b01 : b23, kk + e4, th16);
               dpv = kp ? dpv * dp.scale : 0.f;
             }
             sv[e4] = p * (dpv - Dq);
@@ -1154,11 +1163,14 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
             float p = __builtin_amdgcn_exp2f(S[sub][e] - l4[e4]);
             if constexpr (MASK) p = (qq >= Lq || (causal && kj > qq)) ? 0.f : p;
             float dpv = P[sub][e], pmv = p;
-            if constexpr (DM != 0) {
+            if constexpr (DM == 1) {
               const uint32_t wv = e4 == 0 ? w4.x : e4 == 1 ? w4.y : e4 == 2 ? w4.z : w4.w;
-              const bool kp = DM == 1 ? ((wv >> r) & 1u) != 0u
-                                      : attn_keep(attn_pair_bits(ek[ql + e4], (uint32_t)kj),
-                                                  (uint32_t)kj, th16);
+              const int km = __builtin_amdgcn_sbfe((int)wv, r, 1);
+              dpv = keep_and(dpv * dp.scale, km);
+              pmv = keep_and(p * dp.scale, km);
+            } else if constexpr (DM == 2) {
+              const bool kp = attn_keep(attn_pair_bits(ek[ql + e4], (uint32_t)kj), (uint32_t)kj,
+                                        th16);
               dpv = kp ? dpv * dp.scale : 0.f;
               pmv = kp ? p * dp.scale : 0.f;
             }
