@@ -45,6 +45,15 @@ RETR_DEVICE float keep_and(float x, int km) {
   return __builtin_bit_cast(float, __builtin_bit_cast(int, x) & km);
 }
 
+// bits j of [lo, hi) within a 32-bit word (empty when hi <= lo)
+RETR_DEVICE uint32_t range_bits(int lo, int hi) {
+  lo = lo < 0 ? 0 : lo;
+  hi = hi > 32 ? 32 : hi;
+  if (hi <= lo) return 0u;
+  const uint32_t up = hi >= 32 ? ~0u : ((1u << hi) - 1u);
+  return up & ~((1u << lo) - 1u);
+}
+
 RETR_DEVICE void put4(u32x4& w, int half, const float (&v)[4]) {
   const f2v lo = {v[0], v[1]}, hi = {v[2], v[3]};
   w[2 * half] = __builtin_bit_cast(uint32_t, __builtin_convertvector(lo, bf16x2v));
@@ -930,9 +939,17 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
     const unsigned long long pmask = pm[t];
     const bool diag = causal && (key0 + 63 > q0);
     const bool anym = pmask != 0ull || diag;      // wave-uniform: masking needed on this tile
+    // keep words of the tile's two sub-tiles (bit j: key 32 sub + 8 g + 4 hh + e4 with
+    // j = 8 g + e4 is neither padding nor past the causal diagonal): a bfe + and per score
     const unsigned long long pml = pmask >> (4 * hh);
-    const uint32_t pmlo = (uint32_t)pml, pmhi = (uint32_t)(pml >> 32);
     const int mlim = qi - key0 - 4 * hh;
+    uint32_t kw[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const int L = mlim - 32 * sub;                  // key j masked when j > L (causal)
+      const uint32_t cm = diag ? (L < 0 ? ~0u : (L >= 31 ? 0u : (~0u << (L + 1)))) : 0u;
+      kw[sub] = ~((uint32_t)(pml >> (32 * sub)) | cm);
+    }
     uint32_t wm[2] = {0u, 0u};                     // saved keep bits of the tile's two sub-tiles
     if constexpr (DM == 1) {
 #pragma unroll
@@ -972,7 +989,8 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
           for (int e4 = 0; e4 < 4; ++e4) {
             const int e = 4 * g + e4, kl = sub * 32 + 8 * g + 4 * hh + e4;
             float p = __builtin_amdgcn_exp2f(S[sub][e] - lq2);
-            if constexpr (MASK) p = key_masked(pmlo, pmhi, kl - 4 * hh, diag, mlim) ? 0.f : p;
+            if constexpr (MASK)
+              p = keep_and(p, __builtin_amdgcn_sbfe((int)kw[sub], kl - 4 * hh - 32 * sub, 1));
             float dpv = P[sub][e];
             if constexpr (DM == 1) {
               dpv = keep_and(dpv * dp.scale,
@@ -1147,6 +1165,16 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
     u32x4 pw[4], sw[4];
     auto scores = [&](auto maskc) {
       constexpr bool MASK = decltype(maskc)::value;
+      // keep words (bit j = 8 g + e4: query qt + 32 sub + 4 hh + j is a real row and, causal,
+      // not above this lane's key): a bfe + and per score instead of two compares and a select
+      uint32_t rw[2] = {~0u, ~0u};
+      if constexpr (MASK) {
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+          const int base = qt + 32 * sub + 4 * hh;
+          rw[sub] = range_bits(causal ? kj - base : 0, Lq - base);
+        }
+      }
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
@@ -1159,9 +1187,9 @@ attn_bwd_dkdv3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf
           float pv[4], sv[4];
 #pragma unroll
           for (int e4 = 0; e4 < 4; ++e4) {
-            const int e = 4 * g + e4, qq = qt + ql + e4;
+            const int e = 4 * g + e4;
             float p = __builtin_amdgcn_exp2f(S[sub][e] - l4[e4]);
-            if constexpr (MASK) p = (qq >= Lq || (causal && kj > qq)) ? 0.f : p;
+            if constexpr (MASK) p = keep_and(p, __builtin_amdgcn_sbfe((int)rw[sub], 8 * g + e4, 1));
             float dpv = P[sub][e], pmv = p;
             if constexpr (DM == 1) {
               const uint32_t wv = e4 == 0 ? w4.x : e4 == 1 ? w4.y : e4 == 2 ? w4.z : w4.w;

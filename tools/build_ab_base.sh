@@ -1,17 +1,18 @@
 #!/bin/bash
-# Build the committed HEAD's kernel library into tools/_ab/libretr_base.so (A/B timing only:
+# Build a committed revision's kernel library into tools/_ab/libretr_base.so (A/B timing only:
 # RETR_AB_LIB=tools/_ab/libretr_base.so makes retr_amd._lib load it instead of the working tree's).
+# Uses the working tree's Makefile, so both libraries get the same per-file flags (the attention
+# and decode objects' -amdgpu-mfma-vgpr-form: a plain hipcc loop without it gave a base library
+# whose attention kernels were ~10 % slower -- it confounded round 6's first base/tree A/Bs).
+#   usage: bash tools/build_ab_base.sh [rev]        (default HEAD)
 set -e
 REPO=$(cd "$(dirname "$0")/.." && pwd)
+REV=${1:-HEAD}
 TMP=$(mktemp -d)
-git -C "$REPO" archive HEAD retr_amd/csrc include | tar -x -C "$TMP"
-cd "$TMP"
-for f in retr_amd/csrc/*.hip; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics \
-    -Wno-unused-function -c "$f" -o "${f%.hip}.o" &
-done
-wait
+git -C "$REPO" archive "$REV" retr_amd/csrc include | tar -x -C "$TMP"
 mkdir -p "$REPO/tools/_ab"
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 retr_amd/csrc/*.o -o "$REPO/tools/_ab/libretr_base.so"
+(cd "$TMP" && make -s -f "$REPO/Makefile" -j8 LIB="$REPO/tools/_ab/libretr_base.so" \
+   "$REPO/tools/_ab/libretr_base.so" 2>&1 | grep -E "error" || true)
 rm -rf "$TMP"
-echo "built $REPO/tools/_ab/libretr_base.so from $(git -C "$REPO" rev-parse --short HEAD)"
+test -f "$REPO/tools/_ab/libretr_base.so"
+echo "built $REPO/tools/_ab/libretr_base.so from $(git -C "$REPO" rev-parse --short "$REV")"
