@@ -84,6 +84,10 @@ VARIANTS = {
     "unpack_old": {("TUNE", 28): -1},
     # round 6: the first blocks' downsample data gradient out of place (+ phase fill)
     "ds_fill": {("RESNET", "DS_DGRAD_INPLACE"): False},
+    # grouped projection tiles (RETR_TUNE_GROUP_TILE / _STAGES) re-check
+    "grp_t128": {("TUNE", 0): 128},
+    "grp_t128s1": {("TUNE", 0): 128, ("TUNE", 1): 1},
+    "grp_t128s3": {("TUNE", 0): 128, ("TUNE", 1): 3},
     "cw_w4": {("TUNE", 29): 1},
     "cw_w8": {("TUNE", 29): 2},
     "cw_256": {("TUNE", 29): 3},
@@ -108,7 +112,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 32):
+    for k in (0, 1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 32):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
