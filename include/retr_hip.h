@@ -139,7 +139,7 @@ enum {
   RETR_TUNE_SHORTK = 14,        /* short-K (K <= 256, N >= 256) bf16 GEMMs on the single-stage
                                    64x64 LDS-DMA tile: 0 auto (on), 1 off */
   RETR_TUNE_ADAMW_NT = 15,      /* AdamW update streams: 0 (auto) / 1 non-temporal loads and
-                                   stores, 2 plain */
+                                   stores, 2 plain, 3 non-temporal with two groups in flight (A/B) */
   RETR_TUNE_WGRAD_B32 = 16,     /* 1: 3x3 / strided conv weight gradients on the 64-bit-cursor
                                    ConvWgradB loader instead of ConvWgradB32 */
   RETR_TUNE_WGRAD_FUSED = 17,   /* grouped bf16 linear weight gradients: 0 slabs + a separate

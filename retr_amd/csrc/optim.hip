@@ -77,8 +77,10 @@ adamw_sumsq_kernel(const float4* g, long n4, float* partials, float* step) {
 }
 
 // NT: non-temporal loads and stores (every byte is touched once per step, and none of the
-// outputs is read again before the next step's forward / backward)
-template <bool NT>
+// outputs is read again before the next step's forward / backward).  U: float4 groups per
+// thread and iteration, all loaded before any is updated (U = 2: eight loads in flight); the
+// per-element arithmetic is the same either way.
+template <bool NT, int U = 1>
 __global__ void __launch_bounds__(kThreads)
 adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const float* hyper,
                     double beta1, double beta2, float eps, const float* step, float step_offset,
@@ -101,8 +103,8 @@ adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const f
   const float step_size = (float)((double)lr / bc1), decay = (float)(1.0 - (double)lr * wd);
   const float omb1 = (float)(1.0 - beta1), omb2 = (float)(1.0 - beta2), b2f = (float)beta2;
   const bool scale = !(coef >= 1.f);   // also for a NaN coefficient
-  for (long i = (long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long)gridDim.x * kThreads) {
-    float4 pp, gg, mm, vv;
+  typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+  auto load = [&](long i, float4& pp, float4& gg, float4& mm, float4& vv) {
     if constexpr (NT) {
       pp = nt_load(p + i);
       gg = nt_load(g + i);
@@ -111,6 +113,8 @@ adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const f
     } else {
       pp = p[i], gg = g[i], mm = m[i], vv = v[i];
     }
+  };
+  auto update_store = [&](long i, float4& pp, float4& gg, float4& mm, float4& vv) {
     float* pe = &pp.x; float* ge = &gg.x; float* me = &mm.x; float* ve = &vv.x;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -124,7 +128,6 @@ adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const f
       me[e] = mr;
       ve[e] = vr;
     }
-    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
     if constexpr (NT) {
       nt_store(pp, p + i);
       nt_store(mm, m + i);
@@ -142,6 +145,22 @@ adamw_update_kernel(float4* p, float4* g, float4* m, float4* v, long n4, const f
       if (p16)   // bf16 shadow of the parameters: the GEMM weight operands, no cast launches
         *(bf16x4*)(p16 + 4 * i) = bf16x4{(bf16)pp.x, (bf16)pp.y, (bf16)pp.z, (bf16)pp.w};
     }
+  };
+  const long stride = (long)gridDim.x * kThreads;
+  long i = (long)blockIdx.x * kThreads + threadIdx.x;
+  if constexpr (U > 1) {
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+      float4 pp[U], gg[U], mm[U], vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load(i + u * stride, pp[u], gg[u], mm[u], vv[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) update_store(i + u * stride, pp[u], gg[u], mm[u], vv[u]);
+    }
+  }
+  for (; i < n4; i += stride) {
+    float4 pp, gg, mm, vv;
+    load(i, pp, gg, mm, vv);
+    update_store(i, pp, gg, mm, vv);
   }
 }
 
@@ -184,8 +203,10 @@ int retr_adamw_update2(float* param, float* grad, float* exp_avg, float* exp_avg
   int blocks = (int)std::min<long>(2048, (n4 + kThreads - 1) / kThreads);
   // non-temporal streams by default (same-process A/B, profiles/r3_ab_adamw_nt.txt: graphed
   // step 11.190 -> 11.121 ms); knob 2 = plain loads / stores
-  auto kern = retr_tune_get(RETR_TUNE_ADAMW_NT) == 2 ? adamw_update_kernel<false>
-                                                     : adamw_update_kernel<true>;
+  const int mode = retr_tune_get(RETR_TUNE_ADAMW_NT);
+  auto kern = mode == 2 ? adamw_update_kernel<false>
+              : mode == 3 ? adamw_update_kernel<true, 2>   // two groups in flight (A/B)
+                          : adamw_update_kernel<true>;
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(kThreads), 0, (hipStream_t)stream,
                      (float4*)param, (float4*)grad, (float4*)exp_avg, (float4*)exp_avg_sq, n4,
                      hyper, beta1, beta2, eps, step, step_offset, partials, nparts, max_norm,

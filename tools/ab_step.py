@@ -41,6 +41,7 @@ VARIANTS = {
     "cwg_s1": {("TUNE", 9): 3},
     "adamw_nt": {("TUNE", 15): 1},
     "adamw_plain": {("TUNE", 15): 2},
+    "adamw_u2": {("TUNE", 15): 3},
     "gemm_nt": {("TUNE", 7): 1},
     "ce_unfused": {("ATTR", "FUSED_CE"): False},
     "wgrad_b64": {("TUNE", 16): 1},
