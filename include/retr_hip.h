@@ -96,6 +96,11 @@ int retr_linear_dgrad_splitk(int dtype, const void* dy, long lddy, const void* w
                              void* dx, long lddx, int dx_f32, int M, int N, int K,
                              const void* addend, int addend_f32, long lda, const void* gate,
                              long ldg, int w_trans, float* ws, int splits, void* stream);
+/* the slices of retr_linear_dgrad_splitk only (no epilogue): ws[splits][M][K] fp32 partial
+ * products for a consumer that sums them (retr_layernorm_bwd_slabs); splits = a normalised
+ * slice count (retr_linear_splits).  bf16 only. */
+int retr_linear_dgrad_slabs(int dtype, const void* dy, long lddy, const void* w, long ldw, int M,
+                            int N, int K, int w_trans, float* ws, int splits, void* stream);
 /* dw[N][K] (=|+=) dy^T x (fp32); db[N] (=|+=) column sums of dy (fused; db may be NULL).
  * accumulate = 0: dw/db are overwritten (no pre-zeroing needed); 1: added to.
  * N may be ragged when lddy covers N rounded up to the 16-byte vector (padded dy rows). */
@@ -450,6 +455,17 @@ int retr_layernorm_bwd2(int dtype, const void* dy, const void* dy2, long lddy, c
                         int C, float* dx, long lddx, const float* addend, float* dgamma,
                         float* dbeta, float* workspace, void* dxd, long lddxd, float drop_p,
                         unsigned long long seed, int* nparts, void* stream);
+/* retr_layernorm_bwd2 whose incoming gradient is the fp32 split-K slabs of the producing bf16
+ * data gradient (retr_linear_dgrad_slabs): dy = bf16(sum of ws[0..splits) in slice order) --
+ * bitwise the retr_linear_dgrad_splitk + retr_layernorm_bwd2 pair, one launch and the bf16 dy
+ * round trip fewer.  C 256 or 512, 16-byte aligned rows.  Replaces the LayerNorm backward of
+ * the FFN block's pre-norm (models/transformer_modules.py:6-11) after the up-projection's data
+ * gradient. */
+int retr_layernorm_bwd_slabs(const float* ws, int splits, const float* x, long ldx,
+                             const float* gamma, const float* mean, const float* rstd, int M,
+                             int C, float* dx, long lddx, const float* addend, float* dgamma,
+                             float* dbeta, float* workspace, void* dxd, long lddxd, float drop_p,
+                             unsigned long long seed, int* nparts, void* stream);
 
 /* ---- DecoderEmbeddings: word[caps] + pos[t] -> LayerNorm(eps) -> dropout
  * (models/transformer_modules.py:113-129) ------------------------------------------------- */

@@ -122,6 +122,7 @@ _SIGS = {
                                   _U64, _P, _I, ctypes.POINTER(LnOut), _P],
     "retr_linear_dgrad_splitk": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _L, _P, _L,
                                  _I, _P, _I, _P],
+    "retr_linear_dgrad_slabs": [_I, _P, _L, _P, _L, _I, _I, _I, _I, _P, _I, _P],
     "retr_linear_wgrad": [_I, _P, _L, _P, _L, _P, _L, _I, _I, _I, _P, _I, _P],
     "retr_bias_grad": [_I, _P, _L, _I, _I, _P, _P],
     "retr_linear_fwd_group": [_I, _I, _I, _PFD, _P],
@@ -162,6 +163,8 @@ _SIGS = {
     "retr_layernorm_bwd_workspace": [_I, _I],
     "retr_layernorm_bwd2": [_I, _P, _P, _L, _P, _L, _P, _P, _P, _I, _I, _P, _L, _P, _P, _P, _P,
                             _P, _L, _F, _U64, _P, _P],
+    "retr_layernorm_bwd_slabs": [_P, _I, _P, _L, _P, _P, _P, _I, _I, _P, _L, _P, _P, _P, _P, _P,
+                                 _L, _F, _U64, _P, _P],
     "retr_embed_ln_fwd": [_P, _I, _I, _I, _P, _P, _P, _P, _F, _F, _U64, _P, _P, _P, _P],
     "retr_embed_ln_bwd": [_P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _U64, _P, _P, _P, _P, _I,
                           _P, _P],

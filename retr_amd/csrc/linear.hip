@@ -657,6 +657,27 @@ int retr_linear_dgrad_splitk(int dtype, const void* dy, long lddy, const void* w
                                                     lda, gate, ldg, w_trans, ws, splits, st);
 }
 
+// the split-K data gradient's slices only: ws[splits][M][K] = partial dY[:, slice] W[slice, :]
+// (fp32, plain stores) for a consumer that sums them itself (retr_layernorm_bwd_slabs); splits
+// must already be a normalised slice count (retr_linear_splits' result)
+int retr_linear_dgrad_slabs(int dtype, const void* dy, long lddy, const void* w, long ldw, int M,
+                            int N, int K, int w_trans, float* ws, int splits, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (M == 0) return 0;
+  RETR_REQUIRE(dtype == RETR_BF16, "linear_dgrad_slabs: bf16 only");
+  RETR_REQUIRE(N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0 && ldw % 8 == 0 && ws != nullptr,
+               "linear_dgrad_slabs: N/K/ld must be %%8");
+  RETR_REQUIRE(splits >= 1 && norm_splits_k(N, 64, splits) == splits,
+               "linear_dgrad_slabs: splits=%d is not a normalised slice count for N=%d", splits, N);
+  DenseK<bf16> la{(const bf16*)dy, lddy, M, N};
+  if (w_trans) {
+    DenseK<bf16> lb{(const bf16*)w, ldw, K, N};
+    return splitk_slabs<bf16>(la, lb, M, K, N, ws, splits, 1, st, "linear_dgrad_slabs");
+  }
+  DenseT<bf16> lb{(const bf16*)w, ldw, K, N};
+  return splitk_slabs<bf16>(la, lb, M, K, N, ws, splits, 1, st, "linear_dgrad_slabs");
+}
+
 int retr_linear_wgrad(int dtype, const void* dy, long lddy, const void* x, long ldx, float* dw,
                       long lddw, int M, int N, int K, float* db, int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;

@@ -100,13 +100,17 @@ ln_fwd4_kernel(const float* x, long ldx, const float* gamma, const float* beta, 
 }
 
 // NW waves per block, 2 rows per wave in flight; per-column dgamma / dbeta partials summed over
-// the block's waves in wave order (deterministic) -> part[block][2][C]
-template <typename T, int NCH, int NW>
+// the block's waves in wave order (deterministic) -> part[block][2][C].
+// SLAB: the incoming gradient is the fp32 split-K slabs ws[splits][M][C] of the producing data
+// gradient (the FFN up-projection's), summed in slice order and rounded to bf16 exactly as that
+// GEMM's slab epilogue would have stored it -- the epilogue launch and its bf16 round trip are
+// gone, the result is bitwise the same.
+template <typename T, int NCH, int NW, bool SLAB = false>
 __global__ void __launch_bounds__(NW * 64)
 ln_bwd4_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, const float* gamma,
                const float* mean, const float* rstd, int M, float* dx, long lddx,
                const float* addend, float* part, int rows_per_block, bf16* dxd, long lddxd,
-               DropoutParams dpd) {
+               DropoutParams dpd, const float* ws = nullptr, int splits = 0) {
   constexpr int C = 256 * NCH;
   __shared__ f32x4 red[2][NW][64 * NCH];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -131,8 +135,19 @@ ln_bwd4_kernel(const T* dy, const T* dy2, long lddy, const float* x, long ldx, c
 #pragma unroll
       for (int j = 0; j < NCH; ++j) {
         const int c = 4 * lane + 256 * j;
-        f32x4 t = (ok && dy) ? ld4(dy + (long)row * lddy + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-        if (ok && dy2) t += ld4(dy2 + (long)row * lddy + c);
+        f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (SLAB) {
+          if (ok) {
+            const long MC = (long)M * C;
+            const float* sp = ws + (long)row * C + c;
+            for (int sl = 0; sl < splits; ++sl) t += *(const f32x4*)(sp + sl * MC);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] = (float)(bf16)t[e];
+          }
+        } else {
+          if (ok && dy) t = ld4(dy + (long)row * lddy + c);
+          if (ok && dy2) t += ld4(dy2 + (long)row * lddy + c);
+        }
         d[u][j] = t;
         xv[u][j] = ok ? ld4(x + (long)row * ldx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
         ad[u][j] = (ok && addend) ? ld4(addend + (long)row * ldx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -639,6 +654,55 @@ int retr_layernorm_bwd2(int dtype, const void* dy, const void* dy2, long lddy, c
   if (int e = retr_check_launch("layernorm_bwd")) return e;
   if (dxd && retr_dropout_apply(RETR_BF16, dx, lddx, dxd, lddxd, M, C, drop_p, seed, stream))
     return 1;
+  if (!part) return 0;
+  if (nparts) {
+    *nparts = (int)grid.x;
+    return 0;
+  }
+  hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cdiv(2 * C, 64)), dim3(1024), 0, st, part,
+                     (int)grid.x, C, dgamma, dbeta);
+  return retr_check_launch("layernorm_param_reduce");
+}
+
+// retr_layernorm_bwd2 with the incoming gradient given as the fp32 split-K slabs of the bf16
+// data-gradient GEMM that produces it (retr_linear_dgrad_slabs): dy = bf16(sum of ws[0..splits)
+// in slice order), then the same backward -- bitwise the slab epilogue + retr_layernorm_bwd2
+// path, without the epilogue launch and the dy round trip.  The vectorised layouts only (C 256
+// or 512, 16-byte aligned rows, as the bf16 transformer blocks use).
+int retr_layernorm_bwd_slabs(const float* ws, int splits, const float* x, long ldx,
+                             const float* gamma, const float* mean, const float* rstd, int M,
+                             int C, float* dx, long lddx, const float* addend, float* dgamma,
+                             float* dbeta, float* workspace, void* dxd, long lddxd, float drop_p,
+                             unsigned long long seed, int* nparts, void* stream) {
+  if (nparts) *nparts = 0;
+  if (M == 0) return 0;
+  RETR_REQUIRE(ws && splits >= 1 && ((uintptr_t)ws & 15) == 0,
+               "layernorm_bwd_slabs: slabs %p splits %d", (const void*)ws, splits);
+  RETR_REQUIRE((C == 256 || C == 512) && ldx % 4 == 0 && lddx % 4 == 0 &&
+                   (((uintptr_t)x | (uintptr_t)dx | (uintptr_t)gamma |
+                     (uintptr_t)(addend ? addend : x)) & 15) == 0,
+               "layernorm_bwd_slabs: C=%d (256 | 512, 16-byte aligned rows)", C);
+  RETR_REQUIRE(mean && rstd && gamma && dx, "layernorm_bwd_slabs: missing saved statistics");
+  RETR_REQUIRE(!nparts || workspace, "layernorm_bwd_slabs: deferred sums need a workspace");
+  if (nparts) dgamma = dbeta = nullptr;
+  RETR_REQUIRE(!(dgamma || dbeta) || workspace, "layernorm_bwd_slabs: dgamma/dbeta need a workspace");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (dgamma || dbeta || nparts) ? workspace : nullptr;
+  const DropoutParams dpd = make_dp(drop_p, seed);
+  const bool big = M >= 4096;                      // retr_layernorm_bwd2's choice
+  const int rpb = big ? 32 : 8;
+  const dim3 grid(cdiv(M, rpb));
+#define LNBS(NC, NW)                                                                             \
+  hipLaunchKernelGGL((ln_bwd4_kernel<bf16, NC, NW, true>), grid, dim3(NW * 64), 0, st,           \
+                     (const bf16*)nullptr, (const bf16*)nullptr, 0L, x, ldx, gamma, mean, rstd, M, \
+                     dx, lddx, addend, part, rpb, (bf16*)dxd, lddxd, dpd, ws, splits);
+  if (C == 256) {
+    if (big) { LNBS(1, 16) } else { LNBS(1, 4) }
+  } else {
+    if (big) { LNBS(2, 16) } else { LNBS(2, 4) }
+  }
+#undef LNBS
+  if (int e = retr_check_launch("layernorm_bwd_slabs")) return e;
   if (!part) return 0;
   if (nparts) {
     *nparts = (int)grid.x;

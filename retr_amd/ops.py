@@ -843,14 +843,14 @@ def _take_dbr(dout, drop_p, seed, cdtype):
 
 
 def _ln_bwd_fused(x, gamma, beta, mean, rstd, dy, dy2, addend, prev, cdtype, pos=None, period=1,
-                  need_dpos=False):
+                  need_dpos=False, slabs=None):
     """_ln_bwd for the bf16 blocks: returns (dx, dgamma, dbeta, dpos, extra, arena) where
     ``extra`` are the dgamma / dbeta partial-row sums for the block's weight-gradient launch and
     ``arena`` says both parameter gradients are FusedAdamW arena views; with ``prev`` = (drop_p,
     seed) of the block that produced x, also caches bf16 dropout(dx) for that block."""
     import ctypes
     M, C = x.shape
-    ref = dy if dy is not None else dy2
+    ref = dy if dy is not None else (dy2 if dy2 is not None else x)
     if dy is not None and dy2 is not None and dy.dtype != dy2.dtype:
         dy2 = dy2.to(dy.dtype)
     dx = torch.empty(M, C, dtype=torch.float32, device=x.device)
@@ -859,10 +859,19 @@ def _ln_bwd_fused(x, gamma, beta, mean, rstd, dy, dy2, addend, prev, cdtype, pos
     ws = ln_workspace(M, C, x.device)
     dxd = torch.empty(M, C, dtype=cdtype, device=x.device) if prev is not None else None
     nparts = ctypes.c_int(0)
-    call("retr_layernorm_bwd2", dcode(ref.dtype), ptr(dy), ptr(dy2), C, ptr(x), x.stride(0),
-         ptr(gamma), ptr(mean), ptr(rstd), M, C, ptr(dx), dx.stride(0), ptr(addend),
-         ptr(dgamma), ptr(dbeta), ptr(ws), ptr(dxd), C, prev[0] if prev else 0.0,
-         prev[1] if prev else 0, ctypes.addressof(nparts) if FUSE_LN_PARAMS else None, _st())
+    if slabs is not None:
+        # dy = bf16(sum of the producing data gradient's split-K slabs), summed here
+        sws, nsl = slabs
+        call("retr_layernorm_bwd_slabs", ptr(sws), nsl, ptr(x), x.stride(0), ptr(gamma),
+             ptr(mean), ptr(rstd), M, C, ptr(dx), dx.stride(0), ptr(addend), ptr(dgamma),
+             ptr(dbeta), ptr(ws), ptr(dxd), C, prev[0] if prev else 0.0, prev[1] if prev else 0,
+             ctypes.addressof(nparts) if FUSE_LN_PARAMS else None, _st())
+    else:
+        call("retr_layernorm_bwd2", dcode(ref.dtype), ptr(dy), ptr(dy2), C, ptr(x),
+             x.stride(0), ptr(gamma), ptr(mean), ptr(rstd), M, C, ptr(dx), dx.stride(0),
+             ptr(addend), ptr(dgamma), ptr(dbeta), ptr(ws), ptr(dxd), C,
+             prev[0] if prev else 0.0, prev[1] if prev else 0,
+             ctypes.addressof(nparts) if FUSE_LN_PARAMS else None, _st())
     if dxd is not None:
         _DBR[dx.data_ptr()] = (prev, dx._version, dxd)
     n = nparts.value
@@ -1162,6 +1171,11 @@ class _CrossAttnBlock(torch.autograd.Function):
                 dmem if l_m else None, dw_in, db_in, dw_out, db_out) + (None,) * 9
 
 
+# the FFN block's pre-norm LayerNorm backward reads the up-projection's data-gradient slabs
+# directly (retr_layernorm_bwd_slabs: one slab-epilogue launch and the bf16 dn round trip
+# fewer, bitwise the same; round 6)
+LN_BWD_SLABS = True
+
 # bf16 FFN blocks at d_model 256 as one fused launch per direction (csrc/ffn.hip: the hidden
 # activation chunk goes from the first GEMM's accumulators into the second GEMM's LDS operand;
 # same bits as the two-launch path).  Off by default: measured slower than linear_fwd +
@@ -1247,6 +1261,7 @@ class _FFNBlock(torch.autograd.Function):
         arena = a0 and a1 and a2 and a3
         dh = torch.empty(M, F, dtype=cdtype, device=dev)
         dn = torch.empty(M, C, dtype=cdtype, device=dev)
+        slabs = None
         if ctx.splits:
             # one fused launch: dh = [h > 0] dbr W2 (written for the weight gradients), dn = dh W1
             w1c, w2c = WEIGHTS.get(w1, cdtype), WEIGHTS.get(w2, cdtype)
@@ -1256,11 +1271,25 @@ class _FFNBlock(torch.autograd.Function):
                  ctx.splits, _st())
         else:
             k_linear_dgrad(dbr, w2t, dh, gate=h)
-            k_linear_dgrad(dh, w1t, dn)
+            sp = _splits(cdtype, M, C, F)
+            if fused and LN_BWD_SLABS and sp > 1 and C in (256, 512):
+                # the up-projection's data gradient as split-K slabs only, summed (in slice
+                # order, rounded to bf16 as its epilogue would) by the LayerNorm backward
+                sws = torch.empty(sp, M, C, dtype=torch.float32, device=dev)
+                if isinstance(w1t, _TView):
+                    w1p, w1tr = w1t.w, 0
+                else:
+                    w1p, w1tr = w1t, 1
+                call("retr_linear_dgrad_slabs", dcode(cdtype), ptr(dh), dh.stride(0), ptr(w1p),
+                     w1p.stride(0), M, F, C, w1tr, ptr(sws), sp, _st())
+                slabs = (sws, sp)
+            else:
+                k_linear_dgrad(dh, w1t, dn)
         wg = [(dbr, h, dw2, db2, True), (dh, n, dw1, db1, True)]
         if fused:
-            dx, dlw, dlb, _, extra, la = _ln_bwd_fused(x, ln_w, ctx.ln_b, mean, rstd, dn, None,
-                                                       dout, ctx.prev, cdtype)
+            dx, dlw, dlb, _, extra, la = _ln_bwd_fused(x, ln_w, ctx.ln_b, mean, rstd,
+                                                       dn if slabs is None else None, None,
+                                                       dout, ctx.prev, cdtype, slabs=slabs)
             _wgrad(wg, extra, arena and la)
         else:
             k_linear_wgrad_group(wg)

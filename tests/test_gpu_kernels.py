@@ -307,6 +307,59 @@ def test_layernorm(dtype, tol, M, C):
     assert rel_err(norm.bias.grad, bt.grad) < 5 * tol
 
 
+@pytest.mark.parametrize("M,C,F,prev", [(6400, 256, 2048, True), (2048, 256, 2048, False),
+                                        (600, 512, 2048, True)])
+def test_layernorm_bwd_from_dgrad_slabs_bitwise(M, C, F, prev):
+    """The FFN block's pre-norm LayerNorm backward fed by the up-projection's split-K data
+    gradient slabs (retr_linear_dgrad_slabs + retr_layernorm_bwd_slabs) against the split-K
+    data gradient with its bf16 slab epilogue + retr_layernorm_bwd2: dx, the previous block's
+    dropout(dx) and the dgamma / dbeta partial rows bitwise equal."""
+    import ctypes
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(M + C)
+    dh = torch.randn(M, F, generator=g).to(DEV, bf)
+    w1 = (torch.randn(F, C, generator=g) / math.sqrt(F)).to(DEV, bf)     # W1 [F][C]
+    x = (torch.randn(M, C, generator=g) * 2 + 0.5).to(DEV)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(DEV)
+    mean = x.mean(1)
+    rstd = torch.rsqrt(x.var(1, unbiased=False) + 1e-5)
+    addend = torch.randn(M, C, generator=g).to(DEV)
+    lib = _lib.load()
+    sp = int(lib.retr_linear_splits(1, M, C, F))
+    assert sp > 1
+    nws = int(lib.retr_layernorm_bwd_workspace(M, C))
+    outs = []
+    for slab in (False, True):
+        dx = torch.full((M, C), float("nan"), device=DEV)
+        dxd = torch.full((M, C), float("nan"), device=DEV, dtype=bf) if prev else None
+        ws = torch.zeros(nws // 4 + 64, device=DEV)
+        sws = torch.empty(sp, M, C, device=DEV)
+        nparts = ctypes.c_int(0)
+        pdrop = (0.1, 4321) if prev else (0.0, 0)
+        if slab:
+            call("retr_linear_dgrad_slabs", 1, ptr(dh), F, ptr(w1), C, M, F, C, 0, ptr(sws), sp,
+                 ops._st())
+            call("retr_layernorm_bwd_slabs", ptr(sws), sp, ptr(x), C, ptr(gamma), ptr(mean),
+                 ptr(rstd), M, C, ptr(dx), C, ptr(addend), None, None, ptr(ws), ptr(dxd), C,
+                 pdrop[0], pdrop[1], ctypes.addressof(nparts), ops._st())
+        else:
+            dn = torch.empty(M, C, device=DEV, dtype=bf)
+            call("retr_linear_dgrad_splitk", 1, ptr(dh), F, ptr(w1), C, ptr(dn), C, 0, M, F, C,
+                 None, 0, 0, None, 0, 0, ptr(sws), sp, ops._st())
+            call("retr_layernorm_bwd2", 1, ptr(dn), None, C, ptr(x), C, ptr(gamma), ptr(mean),
+                 ptr(rstd), M, C, ptr(dx), C, ptr(addend), None, None, ptr(ws), ptr(dxd), C,
+                 pdrop[0], pdrop[1], ctypes.addressof(nparts), ops._st())
+        torch.cuda.synchronize()
+        n = nparts.value
+        outs.append((dx, dxd, ws[: 2 * C * n].clone(), n))
+    (a, ad, ap, an), (b, bd, bp, bn) = outs
+    assert an == bn and an > 0
+    assert not torch.isnan(a).any() and torch.equal(a, b)
+    if prev:
+        assert torch.equal(ad, bd)
+    assert torch.equal(ap, bp)
+
+
 def _attn_ref(q, k, v, H, kpm, causal):
     B, Lq, C = q.shape
     Lk = k.shape[1]

@@ -85,6 +85,7 @@ VARIANTS = {
     "unpack_old": {("TUNE", 28): -1},
     # round 6: the first blocks' downsample data gradient out of place (+ phase fill)
     "ds_fill": {("RESNET", "DS_DGRAD_INPLACE"): False},
+    "lnslab_off": {("ATTR", "LN_BWD_SLABS"): False},
     # grouped projection tiles (RETR_TUNE_GROUP_TILE / _STAGES) re-check
     "grp_t128": {("TUNE", 0): 128},
     "grp_t128s1": {("TUNE", 0): 128, ("TUNE", 1): 1},
@@ -107,6 +108,7 @@ def apply(v):
     ops.FUSE_LN_NEXT = True
     ops.HEAD_WGRAD_DEFER = True
     ops.POS_DEFER = True
+    ops.LN_BWD_SLABS = True
     resnet.CONV_WGRAD_GROUP = True
     resnet.DS_DGRAD_INPLACE = True
     load().retr_tune(10, 0)
