@@ -195,6 +195,10 @@ enum {
                                    slabs + slab_epilogue_ln path, 2 / 3 / 4 the row-complete
                                    32 x 256 tile with the LayerNorm in its epilogue (2 / 3 / 4
                                    stage ring), 5 its 64 x 256 8-wave variant (csrc/linear.hip) */
+  RETR_TUNE_LIN_K256 = 33,      /* bf16 linears with K = 256 on the register-staged tiles (few
+                                   output tiles: M 2048 / 6400 x N 256): 0 / 2 every K-step
+                                   fetched at once (gemm2.hpp gemm_short_kernel), 1 the
+                                   double-buffered K loop (gemm.hpp gemm_kernel) */
   RETR_TUNE_COUNT = 40
 };
 int retr_tune(int knob, int value);

@@ -551,6 +551,133 @@ int launch_gemm2(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, 
   return retr_check_launch(what);
 }
 
+// Short-reduction GEMMs (K = NKS x 64, no split: the d_model-256 projections of the
+// transformer at M 2048 / 6400 and N 256, whose few tiles leave the chip latency-bound).
+// gemm_kernel's register-staged loop pays one memory round trip per 64-deep K-step (fetch the
+// next step, compute this one, store, barrier); here every K-step of the A / B tiles is fetched
+// at once, together with the epilogue operands (residual / addend / gate), then stored to LDS
+// behind one barrier: one round trip per tile.  The MFMA chain (K ascending in 32-deep steps,
+// 2 x 2 waves of TM x TN 16x16 sub-tiles) and the epilogue are gemm_kernel's, so the output is
+// the same bits.
+template <int FAM, int BM, int BN, int NKS, class LA, class LB, class EP>
+__global__ void __launch_bounds__(256)
+gemm_short_kernel(LA la, LB lb, EP ep, int M, int N, int tiles_n) {
+  using T = bf16;
+  constexpr int TM = BM / 32, TN = BN / 32;
+  constexpr int kBuf = (BM + BN) * kBKBytes;
+  using SA = Stager<T, BM, LA>;
+  using SB = Stager<T, BN, LB>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+
+  SA sa;
+  SB sb;
+  sa.init(la, m0, tid, 0);
+  sb.init(lb, n0, tid, 0);
+  u32x4 ra[NKS][SA::NCH], rb[NKS][SB::NCH];
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    sa.fetch(la);
+    sb.fetch(lb);
+#pragma unroll
+    for (int i = 0; i < SA::NCH; ++i) ra[s][i] = sa.reg[i];
+#pragma unroll
+    for (int i = 0; i < SB::NCH; ++i) rb[s][i] = sb.reg[i];
+  }
+  constexpr int CH = BN / 8;
+  constexpr int IT = BM * CH / 256;             // 8-column epilogue chunks per thread
+  static_assert(BM * CH % 256 == 0, "short GEMM epilogue chunks");
+  constexpr bool kPre = has_prefetch<EP>::value;
+  typename PreOf<EP>::type pre[IT];
+  if constexpr (kPre) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int q = tid + it * 256;
+      const int m = m0 + q / CH, n = n0 + (q % CH) * 8;
+      if (m < M && n + 8 <= N) ep.fetch8(m, n, pre[it]);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+#pragma unroll
+    for (int i = 0; i < SA::NCH; ++i) sa.reg[i] = ra[s][i];
+#pragma unroll
+    for (int i = 0; i < SB::NCH; ++i) sb.reg[i] = rb[s][i];
+    sa.store(smem + s * kBuf, tid);
+    sb.store(smem + s * kBuf + BM * kBKBytes, tid);
+  }
+  __syncthreads();
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    const char* A = smem + s * kBuf;
+    const char* B = A + BM * kBKBytes;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      u32x4 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = SA::frag(A, wm * (BM / 2) + 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = SB::frag(B, wn * (BN / 2) + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mfma_step<T>(acc[i][j], af[i], bfr[j]);
+    }
+  }
+  __syncthreads();
+  // epilogue through LDS as gemm_kernel's: fp32 [BM][BN + 4], 8 consecutive columns per thread
+  constexpr int CS = BN + 4;
+  float* ct = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        ct[(wm * (BM / 2) + 16 * i + 4 * (lane >> 4) + e) * CS + wn * (BN / 2) + 16 * j +
+           (lane & 15)] = acc[i][j][e];
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int q = tid + it * 256;
+    const int r = q / CH, c = (q % CH) * 8;
+    const int m = m0 + r, n = n0 + c;
+    if (m >= M || n >= N) continue;
+    const f32x4 lo = *(const f32x4*)(ct + r * CS + c);
+    const f32x4 hi = *(const f32x4*)(ct + r * CS + c + 4);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if (n + 8 <= N) {
+      if constexpr (kPre) ep.apply8p(m, n, v, pre[it]);
+      else ep.apply8(m, n, v);
+    } else {
+      for (int e = 0; e < 8 && n + e < N; ++e) ep.apply(m, n + e, v[e]);
+    }
+  }
+}
+
+template <int FAM, int BM, int BN, class LA, class LB, class EP>
+int launch_short(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, hipStream_t st,
+                 const char* what) {
+  constexpr int NKS = 4;
+  RETR_REQUIRE(K == NKS * 64, "%s: short-K GEMM needs K = %d (K = %d)", what, NKS * 64, K);
+  const int tn = cdiv(N, BN), tiles = cdiv(M, BM) * tn;
+  constexpr size_t stage = (size_t)NKS * (BM + BN) * kBKBytes, epi = (size_t)BM * (BN + 4) * 4;
+  constexpr size_t lds = stage > epi ? stage : epi;
+  static_assert(lds <= 65536, "short GEMM LDS");
+  hipLaunchKernelGGL((gemm_short_kernel<FAM, BM, BN, NKS, LA, LB, EP>), dim3(tiles), dim3(256), lds,
+                     st, la, lb, ep, M, N, tn);
+  return retr_check_launch(what);
+}
+
 // Tile choice for the large bf16 GEMMs (convolutions, big linears), from the tools/gemm_tune
 // sweep on MI355X (profiles/r2_gemm_tune.txt): the 4-wave 128x128 LDS-DMA tile with a 2-stage
 // ring (2 blocks per CU) is the fastest on every conv-shaped GEMM; 128x64 (3 stages) for N=64;

@@ -59,6 +59,15 @@ int launch_linear(const LA& la, const LB& lb, const EP& ep, int M, int N, int K,
     if ((long)cdiv(M, 128) * cdiv(N, 128) >= 160 && K >= 128)
       return launch_big<FAM>(la, lb, ep, M, N, K, 1, st, what,
                              K <= 256 && N <= 4096 && retr_tune_get(RETR_TUNE_BIG_TILE) == 0);
+    // K = 256 on few output tiles (the d_model-256 projections): every K-step fetched at once
+    // (same bits as the double-buffered loop; graphed cfg2 step 9.405 -> 9.344 ms,
+    // profiles/r6_ab_lin_k256.txt); knob 1 keeps the loop
+    if (K == 256 && (long)cdiv(M, 128) * cdiv(N, 128) < 240 &&
+        retr_tune_get(RETR_TUNE_LIN_K256) != 1) {
+      if ((long)cdiv(M, 64) * cdiv(N, 64) >= 192 || N < 64)
+        return launch_short<FAM, 64, 64>(la, lb, ep, M, N, K, st, what);
+      return launch_short<FAM, 32, 64>(la, lb, ep, M, N, K, st, what);
+    }
   }
   return launch_sized<FAM, T>(la, lb, ep, M, N, K, st, what);
 }

@@ -1764,3 +1764,54 @@ def test_pos_grad_multi_equals_per_item_launches(n, acc, ld_pad):
     ref = (init if acc else torch.zeros_like(init)) + sum(
         d[:, :C].float().view(B, T, C).sum(0) for d in items)
     assert rel_err(b, ref) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,kind", [(2048, 256, "fwd_res"), (6400, 256, "fwd_res"),
+                                      (2048, 256, "fwd_relu"), (1000, 200, "fwd_res"),
+                                      (2048, 256, "dgrad"), (6400, 256, "dgrad_t"),
+                                      (777, 256, "dgrad")])
+def test_linear_k256_all_steps_at_once_equals_loop(M, N, kind):
+    """K = 256 linears on few output tiles: gemm_short_kernel (every K-step fetched at once,
+    RETR_TUNE_LIN_K256 = 0 / 2) gives the bits of gemm_kernel's double-buffered loop (1), and
+    both match an fp32 reference (ragged M / N included)."""
+    bf, K, lib = torch.bfloat16, 256, _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    outs = []
+    try:
+        for knob in (1, 0):
+            lib.retr_tune(33, knob)
+            if kind.startswith("fwd"):
+                x = torch.randn(M, K, device=DEV, generator=g).to(bf) if not outs else x
+                w = (torch.randn(N, K, device=DEV, generator=g) * 0.05).to(bf) if not outs else w
+                b = torch.randn(N, device=DEV, generator=g) if not outs else b
+                res = torch.randn(M, N, device=DEV, generator=g) if not outs else res
+                y = torch.zeros(M, N, device=DEV)
+                relu = int(kind == "fwd_relu")
+                call("retr_linear_fwd", 1, ptr(x), K, ptr(w), K, ptr(b), ptr(y), N, 1, M, N, K,
+                     relu, None if relu else ptr(res), N, 0.0, 0, _lib.stream())
+                ref = x.float() @ w.float().t() + b
+                ref = torch.relu(ref) if relu else ref + res
+            else:
+                # dX[M][K'] = dY[M][N'] W (reduction over N' = 256), ReLU gate + bf16 addend
+                Kout = N
+                dy = torch.randn(M, K, device=DEV, generator=g).to(bf) if not outs else dy
+                wt = (torch.randn(K, Kout, device=DEV, generator=g) * 0.05).to(bf) if not outs else wt
+                gate = torch.randn(M, Kout, device=DEV, generator=g).to(bf) if not outs else gate
+                add = torch.randn(M, Kout, device=DEV, generator=g).to(bf) if not outs else add
+                y = torch.zeros(M, Kout, device=DEV, dtype=bf)
+                if kind == "dgrad_t":    # W^T stored [K'][N'] (w_trans 1)
+                    wk = wt.t().contiguous()
+                    call("retr_linear_dgrad", 1, ptr(dy), K, ptr(wk), K, ptr(y), Kout, 0, M, K,
+                         Kout, ptr(add), 0, Kout, ptr(gate), Kout, 1, _lib.stream())
+                else:
+                    call("retr_linear_dgrad", 1, ptr(dy), K, ptr(wt), Kout, ptr(y), Kout, 0, M, K,
+                         Kout, ptr(add), 0, Kout, ptr(gate), Kout, 0, _lib.stream())
+                ref = (dy.float() @ wt.float() + add.float()) * (gate.float() > 0)
+            torch.cuda.synchronize()
+            outs.append(y.clone())
+    finally:
+        lib.retr_tune(33, 0)
+    assert torch.equal(outs[0], outs[1])
+    err = (outs[1].float() - ref).abs().max().item()
+    assert err < 0.05 * max(1.0, ref.abs().max().item()), err

@@ -42,6 +42,8 @@ VARIANTS = {
     "adamw_nt": {("TUNE", 15): 1},
     "adamw_plain": {("TUNE", 15): 2},
     "adamw_u2": {("TUNE", 15): 3},
+    "lin_k256": {("TUNE", 33): 2},
+    "lin_k256_loop": {("TUNE", 33): 1},
     "gemm_nt": {("TUNE", 7): 1},
     "ce_unfused": {("ATTR", "FUSED_CE"): False},
     "wgrad_b64": {("TUNE", 16): 1},
@@ -115,7 +117,7 @@ def apply(v):
     load().retr_tune(12, 0)
     load().retr_tune(13, 0)
     load().retr_tune(14, 0)
-    for k in (0, 1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 32):
+    for k in (0, 1, 2, 3, 4, 7, 9, 15, 16, 17, 18, 19, 20, 21, 23, 24, 25, 26, 27, 28, 29, 32, 33):
         load().retr_tune(k, 0)
     ops._SPLITS.clear()                        # split-K counts are cached per shape
     os.environ["RETR_STEM_POOL"] = "1"
