@@ -559,9 +559,10 @@ int launch_gemm2(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, 
 // behind one barrier: one round trip per tile.  The MFMA chain (K ascending in 32-deep steps,
 // 2 x 2 waves of TM x TN 16x16 sub-tiles) and the epilogue are gemm_kernel's, so the output is
 // the same bits.
-template <int FAM, int BM, int BN, int NKS, class LA, class LB, class EP>
-__global__ void __launch_bounds__(256)
-gemm_short_kernel(LA la, LB lb, EP ep, int M, int N, int tiles_n) {
+template <int BM, int BN, int NKS, class LA, class LB, class EP>
+RETR_DEVICE __attribute__((always_inline)) void short_tile(const LA& la, const LB& lb,
+                                                           const EP& ep, int M, int N,
+                                                           int tiles_n, int tile) {
   using T = bf16;
   constexpr int TM = BM / 32, TN = BN / 32;
   constexpr int kBuf = (BM + BN) * kBKBytes;
@@ -570,8 +571,7 @@ gemm_short_kernel(LA la, LB lb, EP ep, int M, int N, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
 
   SA sa;
   SB sb;
@@ -664,14 +664,25 @@ gemm_short_kernel(LA la, LB lb, EP ep, int M, int N, int tiles_n) {
   }
 }
 
+template <int FAM, int BM, int BN, int NKS, class LA, class LB, class EP>
+__global__ void __launch_bounds__(256)
+gemm_short_kernel(LA la, LB lb, EP ep, int M, int N, int tiles_n) {
+  short_tile<BM, BN, NKS>(la, lb, ep, M, N, tiles_n, xcd_remap(blockIdx.x, gridDim.x));
+}
+
+template <int BM, int BN, int NKS>
+constexpr size_t short_lds_bytes() {
+  constexpr size_t stage = (size_t)NKS * (BM + BN) * kBKBytes, epi = (size_t)BM * (BN + 4) * 4;
+  return stage > epi ? stage : epi;
+}
+
 template <int FAM, int BM, int BN, class LA, class LB, class EP>
 int launch_short(const LA& la, const LB& lb, const EP& ep, int M, int N, int K, hipStream_t st,
                  const char* what) {
   constexpr int NKS = 4;
   RETR_REQUIRE(K == NKS * 64, "%s: short-K GEMM needs K = %d (K = %d)", what, NKS * 64, K);
   const int tn = cdiv(N, BN), tiles = cdiv(M, BM) * tn;
-  constexpr size_t stage = (size_t)NKS * (BM + BN) * kBKBytes, epi = (size_t)BM * (BN + 4) * 4;
-  constexpr size_t lds = stage > epi ? stage : epi;
+  constexpr size_t lds = short_lds_bytes<BM, BN, NKS>();
   static_assert(lds <= 65536, "short GEMM LDS");
   hipLaunchKernelGGL((gemm_short_kernel<FAM, BM, BN, NKS, LA, LB, EP>), dim3(tiles), dim3(256), lds,
                      st, la, lb, ep, M, N, tn);
