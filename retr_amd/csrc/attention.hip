@@ -53,17 +53,17 @@ RETR_DEVICE void mma_row(f32x4& acc, const T* arow, const T* brow, int lane) {
 
 // reduce over the 16 lanes that share a row group (lane bits 0..3)
 RETR_DEVICE float grp_max(float v) {
-  v = fmaxf(v, __shfl_xor(v, 1, 64));
-  v = fmaxf(v, __shfl_xor(v, 2, 64));
-  v = fmaxf(v, __shfl_xor(v, 4, 64));
-  v = fmaxf(v, __shfl_xor(v, 8, 64));
+  v = fmaxf(v, xor_lane(v, 1));
+  v = fmaxf(v, xor_lane(v, 2));
+  v = fmaxf(v, xor_lane(v, 4));
+  v = fmaxf(v, xor_lane(v, 8));
   return v;
 }
 RETR_DEVICE float grp_sum(float v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
+  v += xor_lane(v, 1);
+  v += xor_lane(v, 2);
+  v += xor_lane(v, 4);
+  v += xor_lane(v, 8);
   return v;
 }
 

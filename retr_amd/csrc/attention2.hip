@@ -139,7 +139,7 @@ RETR_DEVICE void mask_tile(f32x16 (&S)[2], unsigned long long pmask, bool diag, 
 // re-hashing every score (~10 VALU per score in the key-on-lane kernel).
 RETR_DEVICE void store_dmask(uint32_t* dmask, uint32_t wbits, int hh, int bh, int Lq, int Lk,
                              int qi, int w) {
-  const uint32_t full = wbits | (uint32_t)__shfl_xor((int)wbits, 32, 64);
+  const uint32_t full = wbits | (uint32_t)xor_lane((int)wbits, 32);
   const int nw = (Lk + 31) / 32;
   if (hh == 0 && qi < Lq && w < nw) dmask[((long)bh * nw + w) * Lq + qi] = full;
 }
@@ -257,7 +257,7 @@ RETR_DEVICE __attribute__((always_inline)) void fwd2_tile(
   for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
     for (int e = 0; e < 16; ++e) mt = fmaxf(mt, S[sub][e]);
-  mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+  mt = fmaxf(mt, xor_lane(mt, 32));
   const float mn = fmaxf(m, mt);
   const float ms = (mn == -INFINITY) ? 0.f : mn;
   const float alpha = __builtin_amdgcn_exp2f(m - ms);
@@ -350,7 +350,7 @@ template <int HD>
 RETR_DEVICE void fwd_finish(const f32x16 (&O)[HD / 32], float m, float l, bf16* o, long ldo,
                             int b, int h, int H, int qi, int Lq, int hh, bool drop, float dscale,
                             float* lse) {
-  l += __shfl_xor(l, 32, 64);
+  l += xor_lane(l, 32);
   if (qi < Lq) {
     // fully masked row: 0 * inf = NaN (torch's all -inf softmax); kept probabilities were left
     // unscaled, the dropout scale is applied here once
@@ -760,7 +760,7 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
     for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
       for (int e = 0; e < 16; ++e) mt = fmaxf(mt, S[sub][e]);
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = fmaxf(mt, xor_lane(mt, 32));
     const float mn = fmaxf(m, mt);
     // a row with no valid key so far keeps m = -inf: exponentiate against 0 instead (every
     // score is -inf then, so every p is 0) -- no per-element select
@@ -819,7 +819,7 @@ attn_fwd3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16* v
     }
   }
 
-  l += __shfl_xor(l, 32, 64);
+  l += xor_lane(l, 32);
   if (qi < Lq) {
     const float inv = (drop ? dp.scale : 1.f) / l;
     bf16* orow = o + ((long)b * Lq + qi) * ldo + h * HD;
@@ -915,7 +915,7 @@ attn_bwd_dq3_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
       for (int j = 0; j < 8; ++j) dpart += (float)d8[j] * (float)o8[j];
     }
   }
-  const float Dq = dpart + __shfl_xor(dpart, 32, 64);
+  const float Dq = dpart + xor_lane(dpart, 32);
   if (hh == 0 && qi < Lq && kh == 0) Dout[srow] = Dq;
   const float lq2 = lse[srow] * kLog2e;
   const bool drop = dp.thresh != 0;
@@ -1553,7 +1553,7 @@ attn_bwd_dq2_kernel(const bf16* q, long ldq, const bf16* k, long ldk, const bf16
       for (int j = 0; j < 8; ++j) dpart += (float)d8[j] * (float)o8[j];
     }
   }
-  const float Dq = dpart + __shfl_xor(dpart, 32, 64);
+  const float Dq = dpart + xor_lane(dpart, 32);
   if (hh == 0 && qi < Lq) Dout[srow] = Dq;
   const float lq2 = lse[srow] * kLog2e;
 

@@ -129,8 +129,8 @@ topk_kernel(const T* x, long ld, int V, int* idx_out, float* lp_out) {
     int who = tid;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      float v2 = __shfl_xor(v, o, 64);
-      int i2 = __shfl_xor(i, o, 64), w2 = __shfl_xor(who, o, 64);
+      float v2 = xor_lane(v, o);
+      int i2 = xor_lane(i, o), w2 = xor_lane(who, o);
       if (better(v2, i2, v, i)) v = v2, i = i2, who = w2;
     }
     __syncthreads();
@@ -287,8 +287,8 @@ topk_reg_kernel(const T* x, long ld, int V, int* idx_out, float* lp_out) {
     int who = tid;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      const float v2 = __shfl_xor(bv, o, 64);
-      const int i2 = __shfl_xor(bi, o, 64), w2 = __shfl_xor(who, o, 64);
+      const float v2 = xor_lane(bv, o);
+      const int i2 = xor_lane(bi, o), w2 = xor_lane(who, o);
       if (better(v2, i2, bv, bi)) bv = v2, bi = i2, who = w2;
     }
     __syncthreads();

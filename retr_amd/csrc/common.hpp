@@ -138,15 +138,59 @@ RETR_DEVICE uint32_t drop_keep4(uint32_t row_key, uint32_t n, uint32_t th16) {
 }
 
 // ---- wave reductions (wave64) ------------------------------------------------------------------
-RETR_DEVICE float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// The xor butterfly v = op(v, v[lane ^ o]) for o = 32, 16, 8, 4, 2, 1 -- the bits of the
+// __shfl_xor loop -- without its six ds_bpermute round trips through the LDS crossbar:
+//   o = 32 / 16: v_permlane32_swap / v_permlane16_swap of v with itself hand every lane the
+//                value of the other half / the neighbouring 16-lane row;
+//   o = 8, 4, 2, 1: DPP row rotations: after the wider steps each value equals (bitwise) its
+//                partners' under those xors, so lane (l + o) mod 16 holds the bits of lane l ^ o.
+// The swaps give the two operands in lane-half order; they are put back in (own, partner)
+// order per lane, so even an operand-order-sensitive op returns the butterfly's bits.
+// v of lane (lane ^ o), o in {1, 2, 4, 8, 16, 32} -- what __shfl_xor(v, o, 64) returns -- from
+// DPP moves / permlane swaps instead of a ds_bpermute through the LDS crossbar (o must fold to
+// a constant; tools/wave_reduce_check.py checks every o against __shfl_xor)
+RETR_DEVICE unsigned xor_lane_u(unsigned v, int o) {
+  const unsigned lane = __lane_id();
+  if (o == 32 || o == 16) {
+    const auto s = o == 32 ? __builtin_amdgcn_permlane32_swap(v, v, false, false)
+                           : __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & o) ? s[0] : s[1];
+  }
+  if (o == 8) return __builtin_amdgcn_update_dpp(0u, v, 0x128, 0xf, 0xf, false);   // row_ror:8
+  if (o == 4) {   // row_shl:4 / row_shr:4 (lane i <- i + 4 / i - 4 within the 16-lane row)
+    const unsigned up = __builtin_amdgcn_update_dpp(0u, v, 0x104, 0xf, 0xf, false);
+    const unsigned dn = __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);
+    return (lane & 4) ? dn : up;
+  }
+  if (o == 2) return __builtin_amdgcn_update_dpp(0u, v, 0x4e, 0xf, 0xf, false);    // quad [2,3,0,1]
+  return __builtin_amdgcn_update_dpp(0u, v, 0xb1, 0xf, 0xf, false);                 // quad [1,0,3,2]
+}
+RETR_DEVICE float xor_lane(float v, int o) { return __uint_as_float(xor_lane_u(__float_as_uint(v), o)); }
+RETR_DEVICE int xor_lane(int v, int o) { return (int)xor_lane_u((unsigned)v, o); }
+
+template <class F>
+RETR_DEVICE float wave_butterfly(float v, F op) {
+  const unsigned lane = __lane_id();
+  const auto s32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v),
+                                                    false, false);
+  float lo = __uint_as_float(s32[0]), hi = __uint_as_float(s32[1]);
+  v = (lane & 32) ? op(hi, lo) : op(lo, hi);
+  const auto s16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v),
+                                                    false, false);
+  lo = __uint_as_float(s16[0]);
+  hi = __uint_as_float(s16[1]);
+  v = (lane & 16) ? op(hi, lo) : op(lo, hi);
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xf, 0xf, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xf, 0xf, false)));
   return v;
 }
+RETR_DEVICE float wave_sum(float v) {
+  return wave_butterfly(v, [](float a, float b) { return a + b; });
+}
 RETR_DEVICE float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_butterfly(v, [](float a, float b) { return fmaxf(a, b); });
 }
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

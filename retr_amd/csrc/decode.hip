@@ -462,7 +462,7 @@ RETR_DEVICE void gemv_rows(const bf16* W, const float* a, float* out, int tid) {
         for (int e = 0; e < 8; ++e) s += (float)wv[u][c][e] * a[k0 + e];
       }
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      for (int o = 16; o > 0; o >>= 1) s += xor_lane(s, o);
       if (hl == 0) out[hw + HW * (r0 + u)] = s;
     }
   }
@@ -494,7 +494,7 @@ struct GemvFrag {
         for (int e = 0; e < 8; ++e) s += (float)wv[u][c][e] * a[k0 + e];
       }
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      for (int o = 16; o > 0; o >>= 1) s += xor_lane(s, o);
       if (hl == 0) out[hw + HW * u] = s;
     }
   }
@@ -702,7 +702,7 @@ dec_attn_row_kernel(AttnRowArgs a, float scale) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
 #pragma unroll
-      for (int o = NG; o < 64; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
+      for (int o = NG; o < 64; o <<= 1) acc[e] += xor_lane(acc[e], o);
     if (part == 0) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) ob[h * HD + 8 * g + e] = (float)(bf16)(acc[e] * inv);
@@ -844,7 +844,7 @@ dec_attn_row2_kernel(AttnRowArgs a, float scale) {
 #pragma unroll
   for (int e = 0; e < 8; ++e)
 #pragma unroll
-    for (int o = NG; o < 64; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
+    for (int o = NG; o < 64; o <<= 1) acc[e] += xor_lane(acc[e], o);
   if (lane == 0) {
     hmx[h][half] = mx;
     hsum[h][half] = sum;

@@ -114,7 +114,7 @@ struct OutF {
     s0 = fdot4(w[2], *(const f4*)(o + 8), s0);
     s1 = fdot4(w[3], *(const f4*)(o + 12), s1);
     float s = s0 + s1;
-    s += __shfl_xor(s, 32, 64);
+    s += xor_lane(s, 32);
     if (lane < 32) slab[32 * wv + lane] = s;
   }
 };
@@ -205,7 +205,7 @@ struct AttnF {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
 #pragma unroll
-      for (int o = 4; o < 64; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
+      for (int o = 4; o < 64; o <<= 1) acc[e] += xor_lane(acc[e], o);
     if (lane == 0) {
       mxs[w] = mx;
       sms[w] = sum;

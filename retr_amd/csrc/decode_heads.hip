@@ -234,7 +234,7 @@ struct WaveAttn {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
 #pragma unroll
-      for (int o = NG; o < 64; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
+      for (int o = NG; o < 64; o <<= 1) acc[e] += xor_lane(acc[e], o);
     if (lane == 0) {
       mxs[w] = mx;
       sms[w] = sum;

@@ -116,6 +116,9 @@ __global__ void slab_epilogue_kernel(const float* ws, int splits, int M, int N, 
   const float* p = ws + (long)m * N + n;
   float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (n + 8 <= N && N % 4 == 0) {
+    // the epilogue's operands (residual / addend / gate) in flight with the slabs
+    typename PreOf<EP>::type pre;
+    if constexpr (has_prefetch<EP>::value) ep.fetch8(m, n, pre);
     int s = 0;
     for (; s + 3 < splits; s += 4) {
       f32x4 a[4], b[4];
@@ -134,7 +137,8 @@ __global__ void slab_epilogue_kernel(const float* ws, int splits, int M, int N, 
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += a[e], v[e + 4] += b[e];
     }
-    ep.apply8(m, n, v);
+    if constexpr (has_prefetch<EP>::value) ep.apply8p(m, n, v, pre);
+    else ep.apply8(m, n, v);
     return;
   }
   for (int e = 0; e < 8 && n + e < N; ++e) {
@@ -188,6 +192,22 @@ slab_epilogue_ln_kernel(const float* ws, int splits, int M, EpiFwd<float, float>
   f32x4 v[NCH];
 #pragma unroll
   for (int j = 0; j < NCH; ++j) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the epilogue's and the LayerNorm's row operands (bias, residual, gamma, beta, position row)
+  // issued up front with the slabs: one memory round trip, not one per operand behind the slab
+  // sum.  No branch around a load (a conditional load drains the load counter at the join): an
+  // absent operand reads the row's first slab instead and is not used.
+  const float* bp = ep.bias ? ep.bias + 4 * lane : p;
+  const float* rp = ep.res ? ep.res + (long)row * ep.ldr + 4 * lane : p;
+  const float* pr = (ln.y2 && ln.pos) ? ln.pos + (long)(row % ln.period) * N + 4 * lane : p;
+  f32x4 ob[NCH], orr[NCH], og[NCH], obe[NCH], opos[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    ob[j] = *(const f32x4*)(bp + 256 * j);
+    orr[j] = *(const f32x4*)(rp + 256 * j);
+    og[j] = *(const f32x4*)(ln.gamma + 4 * lane + 256 * j);
+    obe[j] = *(const f32x4*)(ln.beta + 4 * lane + 256 * j);
+    opos[j] = *(const f32x4*)(pr + 256 * j);
+  }
   // every load of a group of four slices in flight before the adds (slice order kept)
   int s0 = 0;
   for (; s0 + 3 < splits; s0 += 4) {
@@ -217,9 +237,8 @@ slab_epilogue_ln_kernel(const float* ws, int splits, int M, EpiFwd<float, float>
   for (int j = 0; j < NCH; ++j) {
     const int c = 4 * lane + 256 * j;
     if (ep.bias) {
-      const f32x4 b = *(const f32x4*)(ep.bias + c);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[j][e] += b[e];
+      for (int e = 0; e < 4; ++e) v[j][e] += ob[j][e];
     }
     if (ep.relu == 1) {
 #pragma unroll
@@ -231,9 +250,8 @@ slab_epilogue_ln_kernel(const float* ws, int splits, int M, EpiFwd<float, float>
       for (int e = 0; e < 4; ++e) v[j][e] = ((km >> e) & 1u) ? v[j][e] * ep.dp.scale : 0.f;
     }
     if (ep.res) {
-      const f32x4 r = *(const f32x4*)(ep.res + (long)row * ep.ldr + c);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[j][e] += r[e];
+      for (int e = 0; e < 4; ++e) v[j][e] += orr[j][e];
     }
     if (ep.relu == 2) {
 #pragma unroll
@@ -252,12 +270,11 @@ slab_epilogue_ln_kernel(const float* ws, int splits, int M, EpiFwd<float, float>
       q += d * d;
     }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / N + ln.eps);
-  const float* pr = ln.pos ? ln.pos + (long)(row % ln.period) * N + 4 * lane : nullptr;
   typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
     const int c = 4 * lane + 256 * j;
-    const f32x4 g = *(const f32x4*)(ln.gamma + c), b = *(const f32x4*)(ln.beta + c);
+    const f32x4 g = og[j], b = obe[j];
     f32x4 o;
 #pragma unroll
     for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mean) * rstd * g[e] + b[e];
@@ -265,7 +282,7 @@ slab_epilogue_ln_kernel(const float* ws, int splits, int M, EpiFwd<float, float>
       *(bf16x4*)((bf16*)ln.y + (long)row * ln.ldy + c) =
           bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
     if (ln.y2) {
-      const f32x4 o2 = o + *(const f32x4*)(pr + 256 * j);
+      const f32x4 o2 = o + opos[j];
       *(bf16x4*)((bf16*)ln.y2 + (long)row * ln.ldy + c) =
           bf16x4{(bf16)o2[0], (bf16)o2[1], (bf16)o2[2], (bf16)o2[3]};
     }
@@ -605,7 +622,8 @@ int retr_linear_fwd_splitk_ln(int dtype, const void* x, long ldx, const void* w,
                      K % 8 == 0 && ldx % 8 == 0 && ldw % 8 == 0 && ldy % 4 == 0 &&
                      ldr % 4 == 0 && ln->ldy % 4 == 0 && a16(y) && a16(bias) && a16(residual) &&
                      a16(ws) && a16(ln->gamma) && a16(ln->beta) && a16(ln->pos) && a8(ln->y) &&
-                     a8(ln->y2) && (ln->pos == nullptr || ln->period > 0);
+                     a8(ln->y2) && (ln->pos == nullptr || ln->period > 0) &&
+                     ln->gamma != nullptr && ln->beta != nullptr;
   if (!fused) {
     // two launches with the same results: the (split-K) linear, then the LayerNorm
     if (int e = ws ? retr_linear_fwd_splitk(dtype, x, ldx, w, ldw, bias, y, ldy, 1, M, N, K,

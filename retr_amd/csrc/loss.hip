@@ -30,7 +30,7 @@ ce_fwd_kernel(const T* x, long ld, int V, const long long* tgt, float* lse, floa
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
-    float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    float m2 = xor_lane(m, o), s2 = xor_lane(s, o);
     online_merge(m, s, m2, s2);
   }
   int w = threadIdx.x >> 6;
@@ -102,7 +102,7 @@ ce_fused_kernel(const bf16* x, long ld, int V, const long long* tgt, float* lse,
       for (int e = 0; e < 8; ++e)
         if (8 * j + e < V) m = fmaxf(m, (float)c[i][e]);
   }
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, xor_lane(m, o));
   if (lane == 0) red[w] = m;
   __syncthreads();
   m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
@@ -116,7 +116,7 @@ ce_fused_kernel(const bf16* x, long ld, int V, const long long* tgt, float* lse,
       for (int e = 0; e < 8; ++e)
         if (8 * j + e < V) s += __expf((float)c[i][e] - m);
   }
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  for (int o = 32; o > 0; o >>= 1) s += xor_lane(s, o);
   if (lane == 0) red[w] = s;
   __syncthreads();
   const float l = m + logf(red[0] + red[1] + red[2] + red[3]);
@@ -193,8 +193,8 @@ argmax_kernel(const T* x, long ld, int V, long long* out) {
   }
   for (int j = 8 * V8 + threadIdx.x; j < V; j += 256) visit(to_f(xr[j]), j);
   for (int o = 32; o > 0; o >>= 1) {
-    float v2 = __shfl_xor(bv, o, 64);
-    int i2 = __shfl_xor(bi, o, 64);
+    float v2 = xor_lane(bv, o);
+    int i2 = xor_lane(bi, o);
     bool nan2 = v2 != v2, nan1 = bv != bv;
     if ((nan2 && !nan1) || (nan2 == nan1 && (v2 > bv || (v2 == bv && i2 < bi)))) bv = v2, bi = i2;
   }
@@ -253,8 +253,8 @@ argmax_part_kernel(const T* x, long ld, int V, float* pv, int* pi) {
     for (int j = 8 * V8 + threadIdx.x; j < V; j += 256)
       if (am_better(to_f(xr[j]), j, bv, bi)) bv = to_f(xr[j]), bi = j;
   for (int o = 32; o > 0; o >>= 1) {
-    const float v2 = __shfl_xor(bv, o, 64);
-    const int i2 = __shfl_xor(bi, o, 64);
+    const float v2 = xor_lane(bv, o);
+    const int i2 = xor_lane(bi, o);
     if (am_better(v2, i2, bv, bi)) bv = v2, bi = i2;
   }
   const int w = threadIdx.x >> 6;
@@ -275,8 +275,8 @@ __global__ void argmax_final_kernel(const float* pv, const int* pi, int M, long 
   int bi = 0x7fffffff;
   if (row < M) bv = pv[row * kArgSeg + s], bi = pi[row * kArgSeg + s];
   for (int o = kArgSeg / 2; o > 0; o >>= 1) {
-    const float v2 = __shfl_xor(bv, o, 64);
-    const int i2 = __shfl_xor(bi, o, 64);
+    const float v2 = xor_lane(bv, o);
+    const int i2 = xor_lane(bi, o);
     if (am_better(v2, i2, bv, bi)) bv = v2, bi = i2;
   }
   if (row < M && s == 0) out[row] = bi;
@@ -427,8 +427,8 @@ greedy_select_kernel(const float* pv, const int* pi, int B, int T, int i, long l
     int bi = 0x7fffffff;
     if (row < B) bv = pv[row * kArgSeg + s], bi = pi[row * kArgSeg + s];
     for (int o = kArgSeg / 2; o > 0; o >>= 1) {
-      const float v2 = __shfl_xor(bv, o, 64);
-      const int i2 = __shfl_xor(bi, o, 64);
+      const float v2 = xor_lane(bv, o);
+      const int i2 = xor_lane(bi, o);
       if (am_better(v2, i2, bv, bi)) bv = v2, bi = i2;
     }
     if (row < B && s == 0) {

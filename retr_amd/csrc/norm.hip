@@ -65,13 +65,23 @@ ln_fwd4_kernel(const float* x, long ldx, const float* gamma, const float* beta, 
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= M) return;
   const float* xr = x + (long)row * ldx + 4 * lane;
-  f32x4 v[NCH];
-  float s = 0.f;
+  // the row, gamma / beta and the position row in one round trip, issued behind one another
+  // before the reductions (the compiler had left gamma / beta behind the row's reductions and
+  // the position row behind the first stores); without y2 the position loads re-read gamma
+  // (no branch around them: a conditional load drains the load counter at the join)
+  const float* pr = (y2 && pos) ? pos + (long)(row % period) * C + 4 * lane : gamma + 4 * lane;
+  f32x4 v[NCH], g[NCH], b[NCH], pv[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) v[j] = ld4(xr + 256 * j);
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
-    v[j] = ld4(xr + 256 * j);
-    s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    g[j] = ld4(gamma + 4 * lane + 256 * j);
+    b[j] = ld4(beta + 4 * lane + 256 * j);
+    pv[j] = ld4(pr + 256 * j);
   }
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) s += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
   const float mean = wave_sum(s) / C;
   float q = 0.f;
 #pragma unroll
@@ -82,16 +92,14 @@ ln_fwd4_kernel(const float* x, long ldx, const float* gamma, const float* beta, 
       q += d * d;
     }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
-  const float* pr = pos ? pos + (long)(row % period) * C + 4 * lane : nullptr;
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
     const int c = 4 * lane + 256 * j;
-    const f32x4 g = ld4(gamma + c), b = ld4(beta + c);
     f32x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mean) * rstd * g[e] + b[e];
+    for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mean) * rstd * g[j][e] + b[j][e];
     if (y) st4(y + (long)row * ldy + c, o);
-    if (y2) st4(y2 + (long)row * ldy + c, o + ld4(pr + 256 * j));
+    if (y2) st4(y2 + (long)row * ldy + c, o + pv[j]);
   }
   if (lane == 0) {
     if (mean_out) mean_out[row] = mean;
