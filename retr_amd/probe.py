@@ -244,8 +244,8 @@ TRACKED = ("retr_conv2d_fwd", "retr_conv2d_fwd_out", "retr_conv1x1_fwd_cat",
            "retr_attention_fwd_dm", "retr_attention_bwd_dm")
 
 
-FAMILY_SYMBOL = {"linear_fwd": "gemm{,2,2_group}_kernel<0,",
-                 "linear_dgrad": "gemm{,2,2_group}_kernel<1,",
+FAMILY_SYMBOL = {"linear_fwd": "gemm{,2,2_group,_short}_kernel<0,",
+                 "linear_dgrad": "gemm{,2,2_group,_short}_kernel<1,",
                  "linear_wgrad": "gemm{,2,2_group}_kernel<2, + wgrad_batch_kernel",
                  "conv_fwd": "gemm{,2}_kernel<3, + conv3x3_kernel<..., false> + bottleneck_s1_kernel + stem_pool_kernel",
                  "conv_dgrad": "gemm{,2}_kernel<4, + conv3x3_kernel<..., true>",
@@ -258,8 +258,8 @@ def family_of_symbol(name):
     """Family key of a rocprof kernel name (mangled ``_ZN4retr11gemm_kernelILi3E...`` or
     demangled ``retr::gemm_kernel<3, ...>``), or None."""
     import re
-    m = re.search(r"gemm2?(?:_group)?_kernelILi(\d+)E", name) or \
-        re.search(r"gemm2?(?:_group)?_kernel<(\d+),", name)
+    m = re.search(r"gemm(?:2|_short)?(?:_group)?_kernelILi(\d+)E", name) or \
+        re.search(r"gemm(?:2|_short)?(?:_group)?_kernel<(\d+),", name)
     if m:
         return ("linear_fwd", "linear_dgrad", "linear_wgrad", "conv_fwd", "conv_dgrad",
                 "conv_wgrad")[int(m.group(1))]

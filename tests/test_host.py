@@ -166,5 +166,7 @@ def test_kernel_family_classifier_covers_current_kernel_names():
     assert family_of_symbol("void (anonymous namespace)::conv3x3_kernel<8, 20, 128, 2, 4, 160, 3, "
                             "true, retr::EpiDgrad<bf16, bf16, bf16> >(...)") == "conv_dgrad"
     assert family_of_symbol("_ZN4retr12gemm2_kernelILi3ELi64ELi64E") == "conv_fwd"
+    assert family_of_symbol("_ZN4retr17gemm_short_kernelILi0ELi64ELi64ELi4E") == "linear_fwd"
+    assert family_of_symbol("retr::gemm_short_kernel<1, 32, 64, 4, x>(...)") == "linear_dgrad"
     assert family_of_symbol("conv_wgrad_group_kernel<1, 8, 128>") == "conv_wgrad"
     assert family_of_symbol("adamw_update_kernel<true>") is None
